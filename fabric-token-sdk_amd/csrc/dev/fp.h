@@ -1,0 +1,283 @@
+// BN254 prime-field arithmetic for CDNA4 (gfx950): 8 x 32-bit limbs, Montgomery
+// form (R = 2^256), CIOS multiplication written as u32 x u32 -> u64 MAD chains
+// (lowered to v_mad_u64_u32 + carry adds).  One field element per lane.
+//
+// The same header compiles for the host (FTS_HD expands to `inline`) so the
+// test-only emulation library can check every formula against the Python
+// oracle on CPU; the product library only ever runs it on the GPU.
+//
+// Replaces the Fp/Fr arithmetic mathlib obtains from gnark-crypto v0.6.0
+// (ecc/bn254/fp, fr) -- SURVEY.md Appendix C.
+#pragma once
+#include <stdint.h>
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+#define FTS_HD __host__ __device__ __forceinline__
+#define FTS_HDN __host__ __device__ __noinline__
+#else
+#define FTS_HD inline
+#define FTS_HDN
+#endif
+#include "constants.h"
+
+namespace fts {
+
+struct ModP {
+  static constexpr const uint32_t* m = P_MOD;
+  static constexpr uint32_t inv = P_INV;
+  static constexpr const uint32_t* r2 = P_R2;
+  static constexpr const uint32_t* one = P_ONE;
+};
+struct ModR {
+  static constexpr const uint32_t* m = R_MOD;
+  static constexpr uint32_t inv = R_INV;
+  static constexpr const uint32_t* r2 = R_R2;
+  static constexpr const uint32_t* one = R_ONE;
+};
+
+template <class M>
+struct Fe {
+  uint32_t v[8];
+};
+typedef Fe<ModP> fp;
+typedef Fe<ModR> fr;
+
+template <class M>
+FTS_HD Fe<M> fe_zero() {
+  Fe<M> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = 0;
+  return r;
+}
+
+template <class M>
+FTS_HD Fe<M> fe_one() {
+  Fe<M> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = M::one[i];
+  return r;
+}
+
+template <class M>
+FTS_HD Fe<M> fe_const(const uint32_t* c) {
+  Fe<M> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = c[i];
+  return r;
+}
+
+// a >= m ?  (plain integer compare with the modulus)
+template <class M>
+FTS_HD bool fe_geq_mod(const uint32_t a[8]) {
+  bool gt = false, eq = true;
+#pragma unroll
+  for (int i = 7; i >= 0; i--) {
+    bool lt_i = a[i] < M::m[i];
+    bool gt_i = a[i] > M::m[i];
+    gt = gt || (eq && gt_i);
+    eq = eq && !lt_i && !gt_i;
+    (void)lt_i;
+  }
+  return gt || eq;
+}
+
+// r = a - m (borrow discarded); returns borrow
+FTS_HD uint32_t sub8(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint32_t borrow = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = (uint64_t)a[i] - b[i] - borrow;
+    r[i] = (uint32_t)d;
+    borrow = (uint32_t)(d >> 63);
+  }
+  return borrow;
+}
+
+FTS_HD uint32_t add8(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c = (uint64_t)a[i] + b[i] + (c >> 32);
+    r[i] = (uint32_t)c;
+  }
+  return (uint32_t)(c >> 32);
+}
+
+template <class M>
+FTS_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> r, t;
+  add8(r.v, a.v, b.v);  // < 2m < 2^256: no carry out
+  uint32_t mm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) mm[i] = M::m[i];
+  uint32_t br = sub8(t.v, r.v, mm);
+  return br ? r : t;
+}
+
+template <class M>
+FTS_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> r, t;
+  uint32_t br = sub8(r.v, a.v, b.v);
+  uint32_t mm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) mm[i] = M::m[i];
+  add8(t.v, r.v, mm);
+  return br ? t : r;
+}
+
+template <class M>
+FTS_HD Fe<M> fe_neg(const Fe<M>& a) {
+  return fe_zero<M>() - a;
+}
+
+template <class M>
+FTS_HD Fe<M> fe_dbl(const Fe<M>& a) {
+  return a + a;
+}
+
+// Montgomery multiplication, CIOS, 32-bit limbs.  Inputs < m, output < m.
+template <class M>
+FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t t[10];
+#pragma unroll
+  for (int i = 0; i < 10; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      c = (uint64_t)a.v[j] * b.v[i] + t[j] + (c >> 32);
+      t[j] = (uint32_t)c;
+    }
+    uint64_t s = (uint64_t)t[8] + (c >> 32);
+    t[8] = (uint32_t)s;
+    t[9] = (uint32_t)(s >> 32);
+    uint32_t m = t[0] * M::inv;
+    c = (uint64_t)m * M::m[0] + t[0];
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      c = (uint64_t)m * M::m[j] + t[j] + (c >> 32);
+      t[j - 1] = (uint32_t)c;
+    }
+    s = (uint64_t)t[8] + (c >> 32);
+    t[7] = (uint32_t)s;
+    t[8] = t[9] + (uint32_t)(s >> 32);
+  }
+  Fe<M> r, u;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  uint32_t mm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) mm[i] = M::m[i];
+  uint32_t br = sub8(u.v, r.v, mm);
+  // t < 2m and m < 2^254, so t[8] == 0 here
+  return br ? r : u;
+}
+
+template <class M>
+FTS_HD Fe<M> fe_sqr(const Fe<M>& a) {
+  return a * a;
+}
+
+template <class M>
+FTS_HD bool fe_is_zero(const Fe<M>& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.v[i];
+  return o == 0;
+}
+
+template <class M>
+FTS_HD bool fe_eq(const Fe<M>& a, const Fe<M>& b) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i];
+  return o == 0;
+}
+
+// canonical integer (little-endian limbs, any value < 2^256) -> Montgomery
+template <class M>
+FTS_HD Fe<M> fe_from_int(const uint32_t a[8]) {
+  // reduce a < 2^256 to < m by conditional subtractions (m > 2^253: at most 7)
+  Fe<M> x;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x.v[i] = a[i];
+  uint32_t mm[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) mm[i] = M::m[i];
+  for (int k = 0; k < 7; k++) {
+    uint32_t t[8];
+    uint32_t br = sub8(t, x.v, mm);
+    if (!br) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) x.v[i] = t[i];
+    }
+  }
+  return x * fe_const<M>(M::r2);
+}
+
+// Montgomery -> canonical integer limbs
+template <class M>
+FTS_HD void fe_to_int(uint32_t out[8], const Fe<M>& a) {
+  Fe<M> one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) one.v[i] = (i == 0);
+  Fe<M> r = a * one;
+#pragma unroll
+  for (int i = 0; i < 8; i++) out[i] = r.v[i];
+}
+
+// big-endian 32 bytes <-> limbs
+FTS_HD void be32_to_limbs(uint32_t out[8], const uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint8_t* q = b + 28 - 4 * i;
+    out[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+  }
+}
+
+FTS_HD void limbs_to_be32(uint8_t* b, const uint32_t in[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint8_t* q = b + 28 - 4 * i;
+    q[0] = (uint8_t)(in[i] >> 24);
+    q[1] = (uint8_t)(in[i] >> 16);
+    q[2] = (uint8_t)(in[i] >> 8);
+    q[3] = (uint8_t)in[i];
+  }
+}
+
+// a^e for a fixed 256-bit exponent (left-to-right, 4-bit windows)
+template <class M>
+FTS_HDN Fe<M> fe_pow(const Fe<M>& a, const uint32_t* e) {
+  Fe<M> tab[16];
+  tab[0] = fe_one<M>();
+  tab[1] = a;
+  for (int i = 2; i < 16; i++) tab[i] = tab[i - 1] * a;
+  Fe<M> r = fe_one<M>();
+  for (int w = 63; w >= 0; w--) {
+    r = fe_sqr(r);
+    r = fe_sqr(r);
+    r = fe_sqr(r);
+    r = fe_sqr(r);
+    uint32_t d = (e[w >> 3] >> ((w & 7) * 4)) & 15;
+    // constant-time-ish select to keep registers bounded
+    Fe<M> s = tab[0];
+    for (int k = 1; k < 16; k++)
+      if (d == (uint32_t)k) s = tab[k];
+    r = r * s;
+  }
+  return r;
+}
+
+FTS_HD fp fp_inv(const fp& a) { return fe_pow<ModP>(a, P_MINUS_2); }
+FTS_HD fr fr_inv(const fr& a) { return fe_pow<ModR>(a, R_MINUS_2); }
+
+// square root for p = 3 mod 4; returns false if a is not a square
+FTS_HD bool fp_sqrt(fp& out, const fp& a) {
+  fp s = fe_pow<ModP>(a, P_SQRT_EXP);
+  out = s;
+  return fe_eq(fe_sqr(s), a);
+}
+
+}  // namespace fts

@@ -1,0 +1,216 @@
+// Optimal-ate pairing on BN254 (loop 6x+2 in NAF, two Frobenius lines) and the
+// final exponentiation, per lane.  Replaces mathlib Curve.Pairing2 / FExp
+// (gnark bn254 MillerLoop / FinalExponentiation), reference call sites
+// sigproof/pok.go:199-203, sigproof/membership.go:246-247.
+//
+// Line formulas: homogeneous projective doubling / mixed addition on the
+// D-type twist; the line through T (and Q) evaluated at P is
+//   l(P) = r0*yP + (r1*xP) w + r2 v w        (sparse "034" element)
+// which differs from the affine line by an Fp2 factor -- annihilated by the
+// final exponentiation, so the reduced pairing is exactly gnark's.
+#pragma once
+#include "curve.h"
+
+namespace fts {
+
+struct LineCoef {
+  fp2 r0, r1, r2;
+};
+
+struct g2p {
+  fp2 x, y, z;  // homogeneous projective point on E'
+};
+
+FTS_HD fp fp_half(const fp& a) {
+  uint32_t t[9];
+  uint64_t c = 0;
+  bool odd = a.v[0] & 1;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c = (uint64_t)a.v[i] + (odd ? P_MOD[i] : 0u) + (c >> 32);
+    t[i] = (uint32_t)c;
+  }
+  t[8] = (uint32_t)(c >> 32);
+  fp r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = (t[i] >> 1) | (t[i + 1] << 31);
+  return r;
+}
+FTS_HD fp2 f2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
+
+// T <- 2T; returns the tangent line coefficients
+FTS_HD LineCoef dbl_step(g2p& T) {
+  fp2 A = f2_half(T.x * T.y);
+  fp2 B = f2_sqr(T.y);
+  fp2 C = f2_sqr(T.z);
+  fp2 E = (C + C + C) * f2_const(TWIST_B);  // 3 b' Z^2
+  fp2 F = E + E + E;
+  fp2 G = f2_half(B + F);
+  fp2 H = f2_sqr(T.y + T.z) - (B + C);
+  fp2 I = E - B;
+  fp2 J = f2_sqr(T.x);
+  fp2 EE = f2_sqr(E);
+  fp2 K = EE + EE + EE;
+  T.x = A * (B - F);
+  T.y = f2_sqr(G) - K;
+  T.z = B * H;
+  LineCoef l;
+  l.r0 = f2_neg(H);
+  l.r1 = J + J + J;
+  l.r2 = I;
+  return l;
+}
+
+// T <- T + Q (Q affine); returns the chord line coefficients
+FTS_HD LineCoef add_step(g2p& T, const g2a& Q) {
+  fp2 O = T.y - Q.y * T.z;
+  fp2 L = T.x - Q.x * T.z;
+  fp2 C = f2_sqr(O);
+  fp2 D = f2_sqr(L);
+  fp2 E = L * D;
+  fp2 F = T.z * C;
+  fp2 G = T.x * D;
+  fp2 H = E + F - (G + G);
+  fp2 t1 = T.y * E;
+  T.x = L * H;
+  T.y = (G - H) * O - t1;
+  T.z = E * T.z;
+  LineCoef l;
+  l.r0 = L;
+  l.r1 = f2_neg(O);
+  l.r2 = Q.x * O - L * Q.y;
+  return l;
+}
+
+FTS_HD fp12 line_mul(const fp12& f, const LineCoef& l, const g1a& P) {
+  return f12_mul_034(f, f2_mul_fp(l.r0, P.y), f2_mul_fp(l.r1, P.x), l.r2);
+}
+
+// pi(Q) and -pi^2(Q) on the twist
+FTS_HD g2a tw_frob(const g2a& q) {
+  g2a r;
+  r.x = f2_conj(q.x) * f2_const(TW_FROB_X);
+  r.y = f2_conj(q.y) * f2_const(TW_FROB_Y);
+  r.inf = q.inf;
+  return r;
+}
+FTS_HD g2a tw_frob2_neg(const g2a& q) {
+  g2a r;
+  r.x = f2_mul_fp(q.x, fe_const<ModP>(TW_FROB2_X));
+  r.y = f2_neg(f2_mul_fp(q.y, fe_const<ModP>(TW_FROB2_Y)));
+  r.inf = q.inf;
+  return r;
+}
+
+FTS_HD int naf_digit(int i) {
+  if ((ATE_NAF_POS >> i) & 1) return 1;
+  if ((ATE_NAF_NEG >> i) & 1) return -1;
+  return 0;
+}
+
+static constexpr int MILLER_LINES = 65 + 21 + 2;  // doublings + NAF additions + 2 Frobenius lines
+
+// Line coefficients of a fixed G2 point, in consumption order (host precompute
+// at context creation; consumed by miller_2 for the PP generator Q).
+FTS_HD int precompute_lines(LineCoef* out, const g2a& Q) {
+  g2p T = {Q.x, Q.y, f2_one()};
+  g2a Qn = aff_neg(Q);
+  int n = 0;
+  for (int i = 64; i >= 0; i--) {
+    out[n++] = dbl_step(T);
+    int d = naf_digit(i);
+    if (d == 1) out[n++] = add_step(T, Q);
+    if (d == -1) out[n++] = add_step(T, Qn);
+  }
+  out[n++] = add_step(T, tw_frob(Q));
+  out[n++] = add_step(T, tw_frob2_neg(Q));
+  return n;
+}
+
+// Miller loop of the 2-pair product  f(P1, Qfix) * f(P2, Q2)  where Qfix is
+// given by precomputed lines.  Pairs with an infinity point contribute 1
+// (gnark MillerLoop skips them).
+template <class LinePtr>
+FTS_HD fp12 miller_2(const LinePtr qlines, const g1a& P1, const g1a& P2, const g2a& Q2) {
+  fp12 f = f12_one();
+  bool use1 = !P1.inf;
+  bool use2 = !(P2.inf || Q2.inf);
+  g2p T = {Q2.x, Q2.y, f2_one()};
+  g2a Qn = aff_neg(Q2);
+  int n = 0;
+  for (int i = 64; i >= 0; i--) {
+    if (i != 64) f = f12_sqr(f);
+    if (use1) f = line_mul(f, qlines[n], P1);
+    n++;
+    if (use2) f = line_mul(f, dbl_step(T), P2);
+    int d = naf_digit(i);
+    if (d != 0) {
+      if (use1) f = line_mul(f, qlines[n], P1);
+      n++;
+      if (use2) f = line_mul(f, add_step(T, d == 1 ? Q2 : Qn), P2);
+    }
+  }
+  if (use1) {
+    f = line_mul(f, qlines[n], P1);
+    f = line_mul(f, qlines[n + 1], P1);
+  }
+  if (use2) {
+    f = line_mul(f, add_step(T, tw_frob(Q2)), P2);
+    f = line_mul(f, add_step(T, tw_frob2_neg(Q2)), P2);
+  }
+  return f;
+}
+
+// Miller loop for one pair with on-the-fly lines (used for tests / prover).
+FTS_HD fp12 miller_1(const g1a& P, const g2a& Q) {
+  fp12 f = f12_one();
+  if (P.inf || Q.inf) return f;
+  g2p T = {Q.x, Q.y, f2_one()};
+  g2a Qn = aff_neg(Q);
+  for (int i = 64; i >= 0; i--) {
+    if (i != 64) f = f12_sqr(f);
+    f = line_mul(f, dbl_step(T), P);
+    int d = naf_digit(i);
+    if (d == 1) f = line_mul(f, add_step(T, Q), P);
+    if (d == -1) f = line_mul(f, add_step(T, Qn), P);
+  }
+  f = line_mul(f, add_step(T, tw_frob(Q)), P);
+  f = line_mul(f, add_step(T, tw_frob2_neg(Q)), P);
+  return f;
+}
+
+// cyclotomic-subgroup squaring (Granger-Scott): valid after the easy part
+FTS_HD fp12 f12_cyclo_sqr(const fp12& a) { return f12_sqr(a); }
+
+// a^x, x = BN parameter (positive), a in the cyclotomic subgroup
+FTS_HDN fp12 f12_expt(const fp12& a) {
+  fp12 r = a;
+  for (int i = 61; i >= 0; i--) {
+    r = f12_cyclo_sqr(r);
+    if ((BN_X >> i) & 1) r = r * a;
+  }
+  return r;
+}
+
+// final exponentiation: easy part (p^6-1)(p^2+1), hard part
+//   FUENTES: 2x(6x^2+3x+1)(p^4-p^2+1)/r  via f^(l0 + l1 p + l2 p^2 + l3 p^3),
+//   l0 = 1+6x+12x^2+12x^3, l1 = 4x+6x^2+12x^3, l2 = 6x+6x^2+12x^3,
+//   l3 = -1+4x+6x^2+12x^3   (Fuentes-Castaneda et al.; [EXT] gnark variant).
+FTS_HDN fp12 final_exp(const fp12& f) {
+  fp12 t = f12_conj(f) * f12_inv(f);
+  t = f12_frob2(t) * t;
+  fp12 a = f12_expt(t);                 // t^x
+  fp12 a2 = f12_cyclo_sqr(a);           // t^2x
+  fp12 a6 = f12_cyclo_sqr(a2) * a2;     // t^6x
+  fp12 b = f12_expt(a6);                // t^6x^2
+  fp12 c = f12_expt(f12_cyclo_sqr(b));  // t^12x^3
+  fp12 A = a6 * b * c;                  // l2
+  fp12 B = A * f12_conj(a2);            // l1
+  fp12 res = f12_frob2(A);
+  res = res * (A * b * t);              // l0
+  res = res * f12_frob(B);
+  res = res * f12_frob3(B * f12_conj(t));  // l3
+  return res;
+}
+
+}  // namespace fts

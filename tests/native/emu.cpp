@@ -1,0 +1,103 @@
+// TEST-ONLY host build of the product's device arithmetic headers
+// (fabric-token-sdk_amd/csrc/dev/*.h compiled with g++, FTS_HD = inline).
+// Lets the CPU test tier check every formula the HIP kernels run against the
+// independent Python oracle without a GPU.  Never loaded by the product.
+#include <string.h>
+#include "../../fabric-token-sdk_amd/csrc/dev/pairing.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/sha256.h"
+
+using namespace fts;
+
+static fp ld_fp(const uint8_t* b) {
+  uint32_t t[8];
+  be32_to_limbs(t, b);
+  return fe_from_int<ModP>(t);
+}
+static void st_fp(uint8_t* b, const fp& a) {
+  uint32_t t[8];
+  fe_to_int(t, a);
+  limbs_to_be32(b, t);
+}
+static g1a ld_g1(const uint8_t* b) {
+  g1a a;
+  a.x = ld_fp(b);
+  a.y = ld_fp(b + 32);
+  a.inf = is_zero(a.x) && is_zero(a.y);
+  return a;
+}
+// G2 in gnark RawBytes order X.A1|X.A0|Y.A1|Y.A0
+static g2a ld_g2(const uint8_t* b) {
+  g2a a;
+  a.x.c1 = ld_fp(b);
+  a.x.c0 = ld_fp(b + 32);
+  a.y.c1 = ld_fp(b + 64);
+  a.y.c0 = ld_fp(b + 96);
+  a.inf = f2_is_zero(a.x) && f2_is_zero(a.y);
+  return a;
+}
+
+extern "C" {
+
+int emu_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  st_fp(out, ld_fp(a) * ld_fp(b));
+  return 0;
+}
+int emu_fp_inv(const uint8_t* a, uint8_t* out) {
+  st_fp(out, fp_inv(ld_fp(a)));
+  return 0;
+}
+int emu_fr_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  uint32_t t[8];
+  be32_to_limbs(t, a);
+  fr x = fe_from_int<ModR>(t);
+  be32_to_limbs(t, b);
+  fr y = fe_from_int<ModR>(t);
+  fe_to_int(t, x * y);
+  limbs_to_be32(out, t);
+  return 0;
+}
+int emu_g1_mul(const uint8_t* p64, const uint8_t* k32, uint8_t* out64) {
+  uint32_t k[8];
+  be32_to_limbs(k, k32);
+  g1a r = jac_to_aff(aff_mul(ld_g1(p64), k));
+  g1_to_bytes(out64, r);
+  return g1_on_curve(r) ? 0 : 1;
+}
+int emu_g2_mul(const uint8_t* p128, const uint8_t* k32, uint8_t* out128) {
+  uint32_t k[8];
+  be32_to_limbs(k, k32);
+  g2a r = jac_to_aff(aff_mul(ld_g2(p128), k));
+  g2_to_bytes(out128, r);
+  return g2_on_curve(r) ? 0 : 1;
+}
+int emu_pairing(const uint8_t* p64, const uint8_t* q128, uint8_t* out384) {
+  fp12 f = final_exp(miller_1(ld_g1(p64), ld_g2(q128)));
+  f12_to_bytes(out384, f);
+  return 0;
+}
+// e(P1, Qfix) * e(P2, Q2) with precomputed lines for Qfix
+int emu_pairing2_fixed(const uint8_t* qfix128, const uint8_t* p1, const uint8_t* p2, const uint8_t* q2,
+                       uint8_t* out384) {
+  static LineCoef lines[MILLER_LINES];
+  int n = precompute_lines(lines, ld_g2(qfix128));
+  if (n != MILLER_LINES) return -1;
+  fp12 f = final_exp(miller_2(lines, ld_g1(p1), ld_g1(p2), ld_g2(q2)));
+  f12_to_bytes(out384, f);
+  return 0;
+}
+int emu_miller_raw(const uint8_t* p64, const uint8_t* q128, uint8_t* out384) {
+  fp12 f = miller_1(ld_g1(p64), ld_g2(q128));
+  f12_to_bytes(out384, f);
+  return 0;
+}
+int emu_sha256(const uint8_t* data, uint32_t n, uint8_t* out32, uint8_t* modr32) {
+  Sha256 s;
+  s.init();
+  s.update(data, n);
+  s.final(out32);
+  uint32_t t[8];
+  digest_mod_r(t, out32);
+  limbs_to_be32(modr32, t);
+  return 0;
+}
+}
