@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Build libftsamd.so (HIP kernels for gfx950 + C++ host planner + C ABI).
+
+One hipcc process per translation unit, run in parallel, incremental on
+source/header mtimes.  Output: zkatdlog/_lib/libftsamd.so (in-tree, so it
+travels to the GPU box with the repo snapshot).
+
+    python fabric-token-sdk_amd/build.py [-j N] [--force]
+"""
+import argparse
+import glob
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "build", "obj")
+LIB = os.path.join(HERE, "zkatdlog", "_lib", "libftsamd.so")
+ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH]
+
+SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip"))) + [os.path.join(CSRC, "runtime.hip")]
+           + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))))
+
+
+def headers():
+    return (glob.glob(os.path.join(CSRC, "dev", "*.h")) + glob.glob(os.path.join(CSRC, "host", "*.h"))
+            + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(HERE, "..", "include", "ftsamd.h")])
+
+
+def newest(paths):
+    return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
+
+
+def compile_one(src, force, hdr_time):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_time):
+        return obj, None
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, "%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr)
+    return obj, None
+
+
+def build(jobs=8, force=False, verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    hdr_time = newest(headers())
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(lambda s: compile_one(s, force, hdr_time), SOURCES))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < newest(objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-j", type=int, default=8)
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    try:
+        build(a.j, a.force)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -62,7 +62,7 @@ FTS_HD Jac<F> jac_neg(const Jac<F>& a) {
 
 // dbl-2009-l (a = 0): 2M + 5S
 template <class F>
-FTS_HD Jac<F> jac_dbl(const Jac<F>& p) {
+FTS_HDN Jac<F> jac_dbl(const Jac<F>& p) {
   F A = sqr(p.x);
   F B = sqr(p.y);
   F C = sqr(B);
@@ -83,7 +83,7 @@ FTS_HD Jac<F> jac_dbl(const Jac<F>& p) {
 
 // madd-2007-bl: Jacobian + affine, 7M + 4S, with the exceptional cases
 template <class F>
-FTS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+FTS_HDN Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   if (q.inf) return p;
   if (is_zero(p.z)) return {q.x, q.y, one_of<F>()};
   F Z1Z1 = sqr(p.z);
@@ -111,7 +111,7 @@ FTS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
 
 // add-2007-bl: Jacobian + Jacobian, 11M + 5S
 template <class F>
-FTS_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+FTS_HDN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   if (is_zero(p.z)) return q;
   if (is_zero(q.z)) return p;
   F Z1Z1 = sqr(p.z);
@@ -140,7 +140,7 @@ FTS_HD Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 }
 
 template <class F>
-FTS_HD Aff<F> jac_to_aff(const Jac<F>& p) {
+FTS_HDN Aff<F> jac_to_aff(const Jac<F>& p) {
   Aff<F> r;
   if (is_zero(p.z)) {
     r.x = zero_of<F>();
@@ -160,10 +160,11 @@ FTS_HD Aff<F> jac_to_aff(const Jac<F>& p) {
 // (any value < 2^256; points have order r so no reduction is needed).
 // Left-to-right double-and-add with mixed additions.
 template <class F>
-FTS_HD Jac<F> aff_mul(const Aff<F>& p, const uint32_t k[8]) {
+FTS_HDN Jac<F> aff_mul(const Aff<F>& p, const uint32_t k[8]) {
   Jac<F> acc = jac_inf<F>();
   if (p.inf) return acc;
   bool started = false;
+#pragma nounroll
   for (int i = 255; i >= 0; i--) {
     if (started) acc = jac_dbl(acc);
     if ((k[i >> 5] >> (i & 31)) & 1) {
@@ -176,10 +177,11 @@ FTS_HD Jac<F> aff_mul(const Aff<F>& p, const uint32_t k[8]) {
 
 // small (<= 64-bit) scalar multiplication
 template <class F>
-FTS_HD Jac<F> aff_mul_u64(const Aff<F>& p, uint64_t k) {
+FTS_HDN Jac<F> aff_mul_u64(const Aff<F>& p, uint64_t k) {
   Jac<F> acc = jac_inf<F>();
   if (p.inf) return acc;
   bool started = false;
+#pragma nounroll
   for (int i = 63; i >= 0; i--) {
     if (started) acc = jac_dbl(acc);
     if ((k >> i) & 1) {

@@ -13,10 +13,10 @@
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>
 #define FTS_HD __host__ __device__ __forceinline__
-#define FTS_HDN __host__ __device__ __noinline__
+#define FTS_HDN __host__ __device__ __noinline__ inline
 #else
 #define FTS_HD inline
-#define FTS_HDN
+#define FTS_HDN inline
 #endif
 #include "constants.h"
 
@@ -205,6 +205,7 @@ FTS_HD Fe<M> fe_from_int(const uint32_t a[8]) {
   uint32_t mm[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) mm[i] = M::m[i];
+#pragma nounroll
   for (int k = 0; k < 7; k++) {
     uint32_t t[8];
     uint32_t br = sub8(t, x.v, mm);
@@ -253,8 +254,10 @@ FTS_HDN Fe<M> fe_pow(const Fe<M>& a, const uint32_t* e) {
   Fe<M> tab[16];
   tab[0] = fe_one<M>();
   tab[1] = a;
+#pragma nounroll
   for (int i = 2; i < 16; i++) tab[i] = tab[i - 1] * a;
   Fe<M> r = fe_one<M>();
+#pragma nounroll
   for (int w = 63; w >= 0; w--) {
     r = fe_sqr(r);
     r = fe_sqr(r);

@@ -1,0 +1,496 @@
+// Batch job model shared by the host planner (host/planner.cpp) and the HIP
+// kernels (kernels.hip).  A batch of zkatdlog proofs is compiled on the host
+// into flat, typed job arrays; each kernel runs one job per lane:
+//
+//   decode   wire G1 bytes -> Montgomery affine, on-curve check, canonical
+//            RawBytes (+ base64 for the hashed signature JSON)
+//   zr       wire Zr bytes (any length) -> canonical scalar mod r
+//   scalar   derived scalars: a*b mod r, a*k mod r, sum mod r
+//   g1       sum_i fixedbase_i * s_i  (-)  s * (sum_j w_j P_j)      -> G1 + bytes
+//   g2       sum_i fixedbase_i * s_i  (PK0, PK1, PK2)                -> G2
+//   miller   ML(P1, Q_pp) * ML(P2, Q2)  (Q_pp lines precomputed)    -> Fp12
+//   fexp     final exponentiation -> GT bytes (gnark E12.Bytes order)
+//   hash     SHA-256 over arena segments, mod r, compare with challenge
+//   verdict  per proof: first failing check in reference order -> code
+//
+// Reference seams: transfer.Verifier.Verify (transfer/transfer.go:124),
+// issue.Verifier.Verify (issue/issue.go:202), TransferZKProofValidate
+// (validator/validator_transfer.go:84-98).
+#pragma once
+#include "pairing.h"
+#include "sha256.h"
+
+namespace fts {
+
+static constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+struct G1Dev {
+  uint32_t x[8], y[8];  // Montgomery affine; all-zero = infinity
+};
+struct G2Dev {
+  uint32_t x0[8], x1[8], y0[8], y1[8];
+};
+struct F12Dev {
+  uint32_t w[96];
+};
+
+enum G1Base : uint8_t { G1B_PED0 = 0, G1B_PED1, G1B_PED2, G1B_PEDGEN, G1B_GEN, G1B_COUNT };
+enum G2Base : uint8_t { G2B_PK0 = 0, G2B_PK1, G2B_PK2, G2B_Q, G2B_COUNT };
+static constexpr int TAB_WINDOWS = 32;  // 8-bit windows over 256-bit scalars
+static constexpr int TAB_DIGITS = 256;
+
+struct DecodeJob {
+  uint32_t raw;       // offset of the element bytes in the wire pool
+  uint32_t len;       // element length as received
+  uint32_t out;       // pts index
+  uint32_t bytes;     // arena offset for canonical RawBytes (NONE: skip)
+  uint32_t b64;       // arena offset for 88 base64 chars (NONE: skip)
+};
+
+struct ZrJob {
+  uint32_t raw, len;  // big-endian bytes in the wire pool (len <= ZR_MAX_LEN)
+  uint32_t out;       // scalar index
+};
+static constexpr uint32_t ZR_MAX_LEN = 256;
+
+enum ScalOp : uint32_t { SOP_MUL = 0, SOP_MULK = 1, SOP_SUM = 2 };
+struct ScalJob {
+  uint32_t op, a, b, out;  // MUL: a*b; MULK: a*(uint32)b; SUM: sum of list[a .. a+b)
+};
+
+struct VTerm {
+  uint32_t pt;        // pts index
+  uint32_t w_lo, w_hi;
+  uint32_t pad;
+};
+
+struct G1Job {
+  uint32_t fscal[3];
+  uint8_t fbase[3];
+  uint8_t nfix;
+  uint32_t vstart, vcount;  // VTerm range (variable points with small weights)
+  uint32_t vscal;           // scalar of the variable part (NONE: no variable part)
+  uint32_t vneg;            // 1: subtract the variable part
+  uint32_t out;             // g1out index
+  uint32_t bytes;           // arena offset for RawBytes (NONE: skip)
+};
+
+struct G2Job {
+  uint32_t fscal[3];
+  uint8_t fbase[3];
+  uint8_t nfix;
+  uint32_t out;
+};
+
+struct PairJob {
+  uint32_t p1;     // g1out index, paired with the PP generator Q (precomputed lines)
+  uint32_t p2;     // pts index (signature R)
+  uint32_t q2;     // g2out index
+  uint32_t bytes;  // arena offset for the 384 GT bytes
+};
+
+struct Seg {
+  uint32_t off, len;  // arena byte range
+};
+
+struct HashJob {
+  uint32_t seg_start, seg_count;
+  uint32_t expect;    // scalar index of the claimed challenge (NONE: no compare)
+  uint32_t out_scal;  // write HashToZr(data) to this scalar (NONE: skip)
+};
+
+enum CheckKind : uint8_t { CK_STATIC = 0, CK_PTS = 1, CK_HASH = 2 };
+struct Check {
+  uint8_t kind;
+  uint8_t code;  // error class reported if this check fails
+  uint16_t pad;
+  uint32_t a, b;  // CK_PTS: pts range [a, a+b); CK_HASH: hash job a
+};
+struct TxChecks {
+  uint32_t wf_start, wf_count;  // first part ("well-formedness" / issue WF)
+  uint32_t rg_start, rg_count;  // second part (range proof), may be empty
+  uint32_t mode;                // 0: transfer precedence, 1: issue (sequential)
+};
+
+// error classes (mirror include/ftsamd.h)
+enum : int32_t { E_OK = 0, E_PARSE = 1, E_MALFORMED = 2, E_WF = 3, E_RANGE = 4, E_MEMBERSHIP = 5, E_PANIC = 6 };
+
+// ------------------------------------------------------------------ helpers
+FTS_HD g1a g1_load(const G1Dev& d) {
+  g1a a;
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.x.v[i] = d.x[i];
+    a.y.v[i] = d.y[i];
+    o |= d.x[i] | d.y[i];
+  }
+  a.inf = (o == 0);
+  return a;
+}
+FTS_HD void g1_store(G1Dev& d, const g1a& a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.x[i] = a.inf ? 0u : a.x.v[i];
+    d.y[i] = a.inf ? 0u : a.y.v[i];
+  }
+}
+FTS_HD g2a g2_load(const G2Dev& d) {
+  g2a a;
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.x.c0.v[i] = d.x0[i];
+    a.x.c1.v[i] = d.x1[i];
+    a.y.c0.v[i] = d.y0[i];
+    a.y.c1.v[i] = d.y1[i];
+    o |= d.x0[i] | d.x1[i] | d.y0[i] | d.y1[i];
+  }
+  a.inf = (o == 0);
+  return a;
+}
+FTS_HD void g2_store(G2Dev& d, const g2a& a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.x0[i] = a.inf ? 0u : a.x.c0.v[i];
+    d.x1[i] = a.inf ? 0u : a.x.c1.v[i];
+    d.y0[i] = a.inf ? 0u : a.y.c0.v[i];
+    d.y1[i] = a.inf ? 0u : a.y.c1.v[i];
+  }
+}
+FTS_HD void f12_store(F12Dev& d, const fp12& f) {
+  const fp* p = &f.c0.c0.c0;
+  for (int k = 0; k < 12; k++)
+    for (int i = 0; i < 8; i++) d.w[8 * k + i] = p[k].v[i];
+}
+FTS_HD fp12 f12_load(const F12Dev& d) {
+  fp12 f;
+  fp* p = &f.c0.c0.c0;
+  for (int k = 0; k < 12; k++)
+    for (int i = 0; i < 8; i++) p[k].v[i] = d.w[8 * k + i];
+  return f;
+}
+
+FTS_HD void b64_encode_64(uint8_t* out, const uint8_t* in) {
+  const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  int o = 0;
+  for (int k = 0; k < 63; k += 3) {
+    uint32_t v = ((uint32_t)in[k] << 16) | ((uint32_t)in[k + 1] << 8) | in[k + 2];
+    out[o++] = a[v >> 18];
+    out[o++] = a[(v >> 12) & 63];
+    out[o++] = a[(v >> 6) & 63];
+    out[o++] = a[v & 63];
+  }
+  uint32_t v = (uint32_t)in[63] << 16;
+  out[o++] = a[v >> 18];
+  out[o++] = a[(v >> 12) & 63];
+  out[o++] = '=';
+  out[o++] = '=';
+}
+
+// ------------------------------------------------------------------ jobs
+// gnark G1Affine.SetBytes via mathlib NewG1FromBytes:
+// flags 00 uncompressed (coordinates reduced mod p, (0,0) = infinity, must be
+// on the curve), 01 infinity, 10/11 compressed (smallest/largest root).
+FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, uint8_t* arena) {
+  const uint8_t* b = wire + j.raw;
+  g1a a;
+  a.inf = false;
+  bool ok = true;
+  uint8_t m = j.len >= 1 ? (b[0] & 0xC0) : 0;
+  if (j.len < 32) {
+    ok = false;
+    a.inf = true;
+  } else if (m == 0x40) {
+    a.inf = true;
+  } else if (m == 0x00) {
+    if (j.len < 64) {
+      ok = false;
+      a.inf = true;
+    } else {
+      uint32_t t[8];
+      be32_to_limbs(t, b);
+      a.x = fe_from_int<ModP>(t);
+      be32_to_limbs(t, b + 32);
+      a.y = fe_from_int<ModP>(t);
+      if (is_zero(a.x) && is_zero(a.y)) {
+        a.inf = true;
+      } else {
+        ok = g1_on_curve(a);
+      }
+    }
+  } else {
+    uint8_t xb[32];
+    for (int k = 0; k < 32; k++) xb[k] = b[k];
+    xb[0] &= 0x3F;
+    uint32_t t[8];
+    be32_to_limbs(t, xb);
+    uint32_t mm[8];
+    for (int k = 0; k < 8; k++) mm[k] = P_MOD[k];
+    uint32_t tmp[8];
+    if (!sub8(tmp, t, mm)) {
+      ok = false;  // X >= p
+      a.inf = true;
+    } else {
+      a.x = fe_from_int<ModP>(t);
+      fp three = fe_one<ModP>() + fe_one<ModP>() + fe_one<ModP>();
+      fp rhs = sqr(a.x) * a.x + three;
+      fp y;
+      if (!fp_sqrt(y, rhs)) {
+        ok = false;
+        a.inf = true;
+      } else {
+        // gnark LexicographicallyLargest: y > (p-1)/2 as integers
+        fp ny = fe_neg(y);
+        uint32_t yi[8], nyi[8], d[8];
+        fe_to_int(yi, y);
+        fe_to_int(nyi, ny);
+        bool largest = sub8(d, nyi, yi) != 0;  // y > -y
+        bool want_largest = (m == 0xC0);
+        a.y = (largest == want_largest) ? y : ny;
+      }
+    }
+  }
+  G1Dev d;
+  g1_store(d, a);
+  pts[j.out] = d;
+  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, a);
+  if (j.b64 != NONE) {
+    uint8_t tmp[64];
+    g1_to_bytes(tmp, a);
+    b64_encode_64(arena + j.b64, tmp);
+  }
+  return ok ? 1 : 0;
+}
+
+// G2 RawBytes (X.A1|X.A0|Y.A1|Y.A0), uncompressed only (public parameters)
+FTS_HD uint8_t decode_g2(const uint8_t* b, uint32_t len, G2Dev& out, uint8_t* bytes_out) {
+  g2a a;
+  a.inf = true;
+  bool ok = len >= 128 && (b[0] & 0xC0) == 0;
+  if (ok) {
+    uint32_t t[8];
+    be32_to_limbs(t, b);
+    a.x.c1 = fe_from_int<ModP>(t);
+    be32_to_limbs(t, b + 32);
+    a.x.c0 = fe_from_int<ModP>(t);
+    be32_to_limbs(t, b + 64);
+    a.y.c1 = fe_from_int<ModP>(t);
+    be32_to_limbs(t, b + 96);
+    a.y.c0 = fe_from_int<ModP>(t);
+    a.inf = f2_is_zero(a.x) && f2_is_zero(a.y);
+    ok = g2_on_curve(a);
+  }
+  g2_store(out, a);
+  if (bytes_out) g2_to_bytes(bytes_out, a);
+  return ok ? 1 : 0;
+}
+
+// table entry: digit * 2^(8 window) * B
+FTS_HD void job_tab_g1(uint32_t idx, const G1Dev* bases, G1Dev* tab) {
+  uint32_t d = idx % TAB_DIGITS, w = (idx / TAB_DIGITS) % TAB_WINDOWS, b = idx / (TAB_DIGITS * TAB_WINDOWS);
+  uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  k[w >> 2] = d << ((w & 3) * 8);
+  g1a r = jac_to_aff(aff_mul(g1_load(bases[b]), k));
+  G1Dev o;
+  g1_store(o, r);
+  tab[idx] = o;
+}
+FTS_HD void job_tab_g2(uint32_t idx, const G2Dev* bases, G2Dev* tab) {
+  uint32_t d = idx % TAB_DIGITS, w = (idx / TAB_DIGITS) % TAB_WINDOWS, b = idx / (TAB_DIGITS * TAB_WINDOWS);
+  uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  k[w >> 2] = d << ((w & 3) * 8);
+  g2a r = jac_to_aff(aff_mul(g2_load(bases[b]), k));
+  G2Dev o;
+  g2_store(o, r);
+  tab[idx] = o;
+}
+
+// big.Int SetBytes then mod r (scalar use) + "raw value < r" flag (Zr.Equals
+// compares raw big integers, so a claimed challenge >= r never matches).
+FTS_HD void job_zr(const ZrJob& j, const uint8_t* wire, uint32_t (*scal)[8], uint8_t* canon) {
+  const uint8_t* b = wire + j.raw;
+  uint32_t len = j.len;
+  // strip leading zeros
+  uint32_t s = 0;
+  while (s < len && b[s] == 0) s++;
+  uint32_t sig = len - s;
+  // Horner over 32-byte chunks from the most significant end:
+  // v_m = v_m * 2^256 + chunk   (Montgomery domain: mont(v*2^256) = v_m * R2 / R * R ...)
+  fr acc = fe_zero<ModR>();
+  fr r2 = fe_const<ModR>(R_R2);
+  uint32_t first = sig % 32 == 0 ? 32 : sig % 32;
+  uint32_t pos = s;
+  bool firstc = true;
+  while (pos < len) {
+    uint32_t take = firstc ? first : 32;
+    uint8_t chunk[32];
+    for (int k = 0; k < 32; k++) chunk[k] = 0;
+    for (uint32_t k = 0; k < take; k++) chunk[32 - take + k] = b[pos + k];
+    pos += take;
+    firstc = false;
+    uint32_t t[8];
+    be32_to_limbs(t, chunk);
+    fr c = fe_from_int<ModR>(t);
+    // acc * 2^256 in Montgomery form = acc_m * R2 (mont_mul divides by R once)
+    acc = acc * r2 + c;
+  }
+  uint32_t out[8];
+  fe_to_int(out, acc);
+  for (int k = 0; k < 8; k++) scal[j.out][k] = out[k];
+  // canonical: at most 32 significant bytes and value < r
+  bool c = sig <= 32;
+  if (c && sig > 0) {
+    uint8_t full[32];
+    for (int k = 0; k < 32; k++) full[k] = 0;
+    for (uint32_t k = 0; k < sig; k++) full[32 - sig + k] = b[s + k];
+    uint32_t t[8], d[8], mm[8];
+    be32_to_limbs(t, full);
+    for (int k = 0; k < 8; k++) mm[k] = R_MOD[k];
+    c = sub8(d, t, mm) != 0;  // t < r
+  }
+  canon[j.out] = c ? 1 : 0;
+}
+
+FTS_HD void job_scalar(const ScalJob& j, uint32_t (*scal)[8], const uint32_t* list) {
+  fr r;
+  if (j.op == SOP_SUM) {
+    r = fe_zero<ModR>();
+    for (uint32_t k = 0; k < j.b; k++) r = r + fe_from_int<ModR>(scal[list[j.a + k]]);
+  } else {
+    fr x = fe_from_int<ModR>(scal[j.a]);
+    fr y;
+    if (j.op == SOP_MUL) {
+      y = fe_from_int<ModR>(scal[j.b]);
+    } else {
+      uint32_t k[8] = {j.b, 0, 0, 0, 0, 0, 0, 0};
+      y = fe_from_int<ModR>(k);
+    }
+    r = x * y;
+  }
+  uint32_t out[8];
+  fe_to_int(out, r);
+  for (int k = 0; k < 8; k++) scal[j.out][k] = out[k];
+}
+
+// fixed-base table entry T[base][window][digit] = digit * 2^(8 window) * B
+template <class Dev>
+FTS_HD const Dev& tab_at(const Dev* tab, int base, int window, int digit) {
+  return tab[((size_t)base * TAB_WINDOWS + window) * TAB_DIGITS + digit];
+}
+
+FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]) {
+#pragma nounroll
+  for (int w = 0; w < TAB_WINDOWS; w++) {
+    uint32_t d = (s[w >> 2] >> ((w & 3) * 8)) & 0xFF;
+    if (d) acc = jac_add_aff(acc, g1_load(tab_at(tab, base, w, (int)d)));
+  }
+  return acc;
+}
+
+FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]) {
+#pragma nounroll
+  for (int w = 0; w < TAB_WINDOWS; w++) {
+    uint32_t d = (s[w >> 2] >> ((w & 3) * 8)) & 0xFF;
+    if (d) acc = jac_add_aff(acc, g2_load(tab_at(tab, base, w, (int)d)));
+  }
+  return acc;
+}
+
+FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const uint32_t (*scal)[8],
+                   const G1Dev* tab, G1Dev* g1out, uint8_t* arena) {
+  g1j acc = jac_inf<fp>();
+  if (j.vscal != NONE) {
+    g1j V = jac_inf<fp>();
+    for (uint32_t t = 0; t < j.vcount; t++) {
+      const VTerm& vt = vterms[j.vstart + t];
+      g1a P = g1_load(pts[vt.pt]);
+      uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
+      if (w == 1) {
+        V = jac_add_aff(V, P);
+      } else {
+        V = jac_add(V, aff_mul_u64(P, w));
+      }
+    }
+    g1a Va = jac_to_aff(V);
+    if (j.vneg) Va = aff_neg(Va);
+    acc = aff_mul(Va, scal[j.vscal]);
+  }
+  for (int f = 0; f < j.nfix; f++) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
+  g1a r = jac_to_aff(acc);
+  G1Dev d;
+  g1_store(d, r);
+  g1out[j.out] = d;
+  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+}
+
+FTS_HD void job_g2(const G2Job& j, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out) {
+  g2j acc = jac_inf<fp2>();
+  for (int f = 0; f < j.nfix; f++) acc = g2_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
+  G2Dev d;
+  g2_store(d, jac_to_aff(acc));
+  g2out[j.out] = d;
+}
+
+FTS_HD void job_miller(const PairJob& j, const LineCoef* qlines, const G1Dev* g1out, const G1Dev* pts,
+                       const G2Dev* g2out, F12Dev* fout, uint32_t idx) {
+  fp12 f = miller_2(qlines, g1_load(g1out[j.p1]), g1_load(pts[j.p2]), g2_load(g2out[j.q2]));
+  f12_store(fout[idx], f);
+}
+
+FTS_HD void job_fexp(const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena) {
+  fp12 g = final_exp(f12_load(fin[idx]));
+  f12_to_bytes(arena + j.bytes, g);
+}
+
+FTS_HD uint8_t job_hash(const HashJob& j, const Seg* segs, const uint8_t* arena, uint32_t (*scal)[8],
+                        const uint8_t* canon) {
+  Sha256 s;
+  s.init();
+  for (uint32_t k = 0; k < j.seg_count; k++) {
+    const Seg& g = segs[j.seg_start + k];
+    s.update(arena + g.off, g.len);
+  }
+  uint8_t dg[32];
+  s.final(dg);
+  uint32_t h[8];
+  digest_mod_r(h, dg);
+  if (j.out_scal != NONE)
+    for (int k = 0; k < 8; k++) scal[j.out_scal][k] = h[k];
+  if (j.expect == NONE) return 1;
+  uint32_t o = 0;
+  for (int k = 0; k < 8; k++) o |= h[k] ^ scal[j.expect][k];
+  return (o == 0 && canon[j.expect]) ? 1 : 0;
+}
+
+FTS_HD int32_t eval_part(const Check* ck, uint32_t start, uint32_t count, const uint8_t* pt_ok,
+                         const uint8_t* hash_ok) {
+  for (uint32_t k = 0; k < count; k++) {
+    const Check& c = ck[start + k];
+    bool fail = false;
+    if (c.kind == CK_STATIC) {
+      fail = true;
+    } else if (c.kind == CK_PTS) {
+      for (uint32_t q = 0; q < c.b; q++) fail = fail || !pt_ok[c.a + q];
+    } else {
+      fail = !hash_ok[c.a];
+    }
+    if (fail) return c.code;
+  }
+  return E_OK;
+}
+
+// transfer.Verifier.Verify precedence (transfer/transfer.go:124-154): a panic
+// in either part wins (the WF part runs first, synchronously); otherwise the
+// WF error, then the range error.
+// issue.Verifier.Verify (issue/issue.go:202-223) runs the parts sequentially:
+// a WF error returns before the range proof is looked at.
+FTS_HD int32_t job_verdict(const TxChecks& t, const Check* ck, const uint8_t* pt_ok, const uint8_t* hash_ok) {
+  int32_t wf = eval_part(ck, t.wf_start, t.wf_count, pt_ok, hash_ok);
+  if (wf == E_PANIC || (t.mode == 1 && wf != E_OK)) return wf;
+  int32_t rg = eval_part(ck, t.rg_start, t.rg_count, pt_ok, hash_ok);
+  if (rg == E_PANIC) return E_PANIC;
+  return wf != E_OK ? wf : rg;
+}
+
+}  // namespace fts

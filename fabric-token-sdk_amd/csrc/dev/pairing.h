@@ -39,7 +39,7 @@ FTS_HD fp fp_half(const fp& a) {
 FTS_HD fp2 f2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
 // T <- 2T; returns the tangent line coefficients
-FTS_HD LineCoef dbl_step(g2p& T) {
+FTS_HDN LineCoef dbl_step(g2p& T) {
   fp2 A = f2_half(T.x * T.y);
   fp2 B = f2_sqr(T.y);
   fp2 C = f2_sqr(T.z);
@@ -62,7 +62,7 @@ FTS_HD LineCoef dbl_step(g2p& T) {
 }
 
 // T <- T + Q (Q affine); returns the chord line coefficients
-FTS_HD LineCoef add_step(g2p& T, const g2a& Q) {
+FTS_HDN LineCoef add_step(g2p& T, const g2a& Q) {
   fp2 O = T.y - Q.y * T.z;
   fp2 L = T.x - Q.x * T.z;
   fp2 C = f2_sqr(O);
@@ -82,7 +82,7 @@ FTS_HD LineCoef add_step(g2p& T, const g2a& Q) {
   return l;
 }
 
-FTS_HD fp12 line_mul(const fp12& f, const LineCoef& l, const g1a& P) {
+FTS_HDN fp12 line_mul(const fp12& f, const LineCoef& l, const g1a& P) {
   return f12_mul_034(f, f2_mul_fp(l.r0, P.y), f2_mul_fp(l.r1, P.x), l.r2);
 }
 
@@ -112,10 +112,11 @@ static constexpr int MILLER_LINES = 65 + 21 + 2;  // doublings + NAF additions +
 
 // Line coefficients of a fixed G2 point, in consumption order (host precompute
 // at context creation; consumed by miller_2 for the PP generator Q).
-FTS_HD int precompute_lines(LineCoef* out, const g2a& Q) {
+FTS_HDN int precompute_lines(LineCoef* out, const g2a& Q) {
   g2p T = {Q.x, Q.y, f2_one()};
   g2a Qn = aff_neg(Q);
   int n = 0;
+#pragma nounroll
   for (int i = 64; i >= 0; i--) {
     out[n++] = dbl_step(T);
     int d = naf_digit(i);
@@ -131,13 +132,14 @@ FTS_HD int precompute_lines(LineCoef* out, const g2a& Q) {
 // given by precomputed lines.  Pairs with an infinity point contribute 1
 // (gnark MillerLoop skips them).
 template <class LinePtr>
-FTS_HD fp12 miller_2(const LinePtr qlines, const g1a& P1, const g1a& P2, const g2a& Q2) {
+FTS_HDN fp12 miller_2(const LinePtr qlines, const g1a& P1, const g1a& P2, const g2a& Q2) {
   fp12 f = f12_one();
   bool use1 = !P1.inf;
   bool use2 = !(P2.inf || Q2.inf);
   g2p T = {Q2.x, Q2.y, f2_one()};
   g2a Qn = aff_neg(Q2);
   int n = 0;
+#pragma nounroll
   for (int i = 64; i >= 0; i--) {
     if (i != 64) f = f12_sqr(f);
     if (use1) f = line_mul(f, qlines[n], P1);
@@ -162,11 +164,12 @@ FTS_HD fp12 miller_2(const LinePtr qlines, const g1a& P1, const g1a& P2, const g
 }
 
 // Miller loop for one pair with on-the-fly lines (used for tests / prover).
-FTS_HD fp12 miller_1(const g1a& P, const g2a& Q) {
+FTS_HDN fp12 miller_1(const g1a& P, const g2a& Q) {
   fp12 f = f12_one();
   if (P.inf || Q.inf) return f;
   g2p T = {Q.x, Q.y, f2_one()};
   g2a Qn = aff_neg(Q);
+#pragma nounroll
   for (int i = 64; i >= 0; i--) {
     if (i != 64) f = f12_sqr(f);
     f = line_mul(f, dbl_step(T), P);
@@ -185,6 +188,7 @@ FTS_HD fp12 f12_cyclo_sqr(const fp12& a) { return f12_sqr(a); }
 // a^x, x = BN parameter (positive), a in the cyclotomic subgroup
 FTS_HDN fp12 f12_expt(const fp12& a) {
   fp12 r = a;
+#pragma nounroll
   for (int i = 61; i >= 0; i--) {
     r = f12_cyclo_sqr(r);
     if ((BN_X >> i) & 1) r = r * a;

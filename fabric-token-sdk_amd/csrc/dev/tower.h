@@ -53,7 +53,7 @@ FTS_HD fp2 f2_mul_xi(const fp2& a) {
   return {a0_9 - a.c1, a.c0 + a1_9};
 }
 
-FTS_HD fp2 f2_inv(const fp2& a) {
+FTS_HDN fp2 f2_inv(const fp2& a) {
   fp n = fe_sqr(a.c0) + fe_sqr(a.c1);
   fp ni = fp_inv(n);
   return {a.c0 * ni, fe_neg(a.c1 * ni)};
@@ -67,7 +67,7 @@ FTS_HD fp6 operator-(const fp6& a, const fp6& b) { return {a.c0 - b.c0, a.c1 - b
 FTS_HD fp6 f6_neg(const fp6& a) { return {f2_neg(a.c0), f2_neg(a.c1), f2_neg(a.c2)}; }
 
 // Karatsuba-style: 6 Fp2 multiplications
-FTS_HD fp6 operator*(const fp6& a, const fp6& b) {
+FTS_HDN fp6 operator*(const fp6& a, const fp6& b) {
   fp2 t0 = a.c0 * b.c0;
   fp2 t1 = a.c1 * b.c1;
   fp2 t2 = a.c2 * b.c2;
@@ -86,7 +86,7 @@ FTS_HD fp6 f6_mul_v(const fp6& a) { return {f2_mul_xi(a.c2), a.c0, a.c1}; }
 FTS_HD fp6 f6_mul_f2(const fp6& a, const fp2& s) { return {a.c0 * s, a.c1 * s, a.c2 * s}; }
 
 // a * (b0 + b1 v)
-FTS_HD fp6 f6_mul_01(const fp6& a, const fp2& b0, const fp2& b1) {
+FTS_HDN fp6 f6_mul_01(const fp6& a, const fp2& b0, const fp2& b1) {
   fp2 t0 = a.c0 * b0;
   fp2 t1 = a.c1 * b1;
   fp2 c0 = f2_mul_xi((a.c1 + a.c2) * b1 - t1) + t0;
@@ -95,7 +95,7 @@ FTS_HD fp6 f6_mul_01(const fp6& a, const fp2& b0, const fp2& b1) {
   return {c0, c1, c2};
 }
 
-FTS_HD fp6 f6_inv(const fp6& a) {
+FTS_HDN fp6 f6_inv(const fp6& a) {
   fp2 t0 = f2_sqr(a.c0) - f2_mul_xi(a.c1 * a.c2);
   fp2 t1 = f2_mul_xi(f2_sqr(a.c2)) - a.c0 * a.c1;
   fp2 t2 = f2_sqr(a.c1) - a.c0 * a.c2;
@@ -107,7 +107,7 @@ FTS_HD fp6 f6_inv(const fp6& a) {
 // ----------------------------------------------------------------- Fp12
 FTS_HD fp12 f12_one() { return {f6_one(), f6_zero()}; }
 
-FTS_HD fp12 operator*(const fp12& a, const fp12& b) {
+FTS_HDN fp12 operator*(const fp12& a, const fp12& b) {
   fp6 t0 = a.c0 * b.c0;
   fp6 t1 = a.c1 * b.c1;
   fp6 c1 = (a.c0 + a.c1) * (b.c0 + b.c1) - t0 - t1;
@@ -116,7 +116,7 @@ FTS_HD fp12 operator*(const fp12& a, const fp12& b) {
 }
 
 // complex squaring: 2 Fp6 multiplications
-FTS_HD fp12 f12_sqr(const fp12& a) {
+FTS_HDN fp12 f12_sqr(const fp12& a) {
   fp6 ab = a.c0 * a.c1;
   fp6 c0 = (a.c0 + a.c1) * (a.c0 + f6_mul_v(a.c1)) - ab - f6_mul_v(ab);
   return {c0, ab + ab};
@@ -124,7 +124,7 @@ FTS_HD fp12 f12_sqr(const fp12& a) {
 
 FTS_HD fp12 f12_conj(const fp12& a) { return {a.c0, f6_neg(a.c1)}; }
 
-FTS_HD fp12 f12_inv(const fp12& a) {
+FTS_HDN fp12 f12_inv(const fp12& a) {
   fp6 den = f6_sqr(a.c0) - f6_mul_v(f6_sqr(a.c1));
   fp6 di = f6_inv(den);
   return {a.c0 * di, f6_neg(a.c1 * di)};
@@ -136,7 +136,7 @@ FTS_HD bool f12_eq(const fp12& a, const fp12& b) {
 }
 
 // f * (c0 + c3 w + c4 v w): sparse line multiplication (gnark "MulBy034")
-FTS_HD fp12 f12_mul_034(const fp12& f, const fp2& c0, const fp2& c3, const fp2& c4) {
+FTS_HDN fp12 f12_mul_034(const fp12& f, const fp2& c0, const fp2& c3, const fp2& c4) {
   fp6 a = f6_mul_f2(f.c0, c0);
   fp6 b = f6_mul_01(f.c1, c3, c4);
   fp2 d0 = c0 + c3;
@@ -147,7 +147,7 @@ FTS_HD fp12 f12_mul_034(const fp12& f, const fp2& c0, const fp2& c3, const fp2& 
 }
 
 // Frobenius maps: coefficient of w^k (k = 2i + j for v^i w^j) scaled by gamma_{n,k}
-FTS_HD fp12 f12_frob(const fp12& a) {
+FTS_HDN fp12 f12_frob(const fp12& a) {
   fp12 r;
   r.c0.c0 = f2_conj(a.c0.c0);
   r.c0.c1 = f2_conj(a.c0.c1) * f2_const(FROB1[2]);
@@ -158,7 +158,7 @@ FTS_HD fp12 f12_frob(const fp12& a) {
   return r;
 }
 
-FTS_HD fp12 f12_frob2(const fp12& a) {
+FTS_HDN fp12 f12_frob2(const fp12& a) {
   fp12 r;
   r.c0.c0 = a.c0.c0;
   r.c0.c1 = f2_mul_fp(a.c0.c1, fe_const<ModP>(FROB2[2][0]));
@@ -169,7 +169,7 @@ FTS_HD fp12 f12_frob2(const fp12& a) {
   return r;
 }
 
-FTS_HD fp12 f12_frob3(const fp12& a) {
+FTS_HDN fp12 f12_frob3(const fp12& a) {
   fp12 r;
   r.c0.c0 = f2_conj(a.c0.c0);
   r.c0.c1 = f2_conj(a.c0.c1) * f2_const(FROB3[2]);
@@ -181,7 +181,7 @@ FTS_HD fp12 f12_frob3(const fp12& a) {
 }
 
 // gnark E12.Bytes(): 12 canonical big-endian Fp words, C1.B2.A1 first.
-FTS_HD void f12_to_bytes(uint8_t* out, const fp12& a) {
+FTS_HDN void f12_to_bytes(uint8_t* out, const fp12& a) {
   const fp2* cs[6] = {&a.c1.c2, &a.c1.c1, &a.c1.c0, &a.c0.c2, &a.c0.c1, &a.c0.c0};
   for (int k = 0; k < 6; k++) {
     uint32_t t[8];

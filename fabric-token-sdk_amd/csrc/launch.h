@@ -1,0 +1,28 @@
+// Kernel declarations (definitions live in k_*.hip, one TU per kernel family,
+// so the heavy pairing TUs compile in parallel).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev/jobs.h"
+
+using namespace fts;
+
+__global__ void k_decode(const DecodeJob* jobs, uint32_t n, const uint8_t* wire, G1Dev* pts, uint8_t* pt_ok,
+                         uint8_t* arena);
+__global__ void k_zr(const ZrJob* jobs, uint32_t n, const uint8_t* wire, uint32_t (*scal)[8], uint8_t* canon);
+__global__ void k_scalar(const ScalJob* jobs, uint32_t n, uint32_t (*scal)[8], const uint32_t* list);
+__global__ void k_hash(const HashJob* jobs, uint32_t n, const Seg* segs, const uint8_t* arena, uint32_t (*scal)[8],
+                       const uint8_t* canon, uint8_t* ok);
+__global__ void k_verdict(const TxChecks* tx, uint32_t n, const Check* ck, const uint8_t* pt_ok,
+                          const uint8_t* hash_ok, int32_t* codes, uint32_t* bitmap);
+__global__ void k_pp_decode(const uint8_t* raw, const uint32_t* g1off, uint32_t n1, const uint32_t* g2off,
+                            uint32_t n2, G1Dev* g1, G2Dev* g2, uint8_t* g1bytes, uint8_t* g2bytes, uint8_t* ok);
+__global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts, const uint32_t (*scal)[8],
+                     const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
+__global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
+__global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out);
+__global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
+__global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines, const G1Dev* g1out,
+                         const G1Dev* pts, const G2Dev* g2out, F12Dev* fbuf);
+__global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
+__global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);

@@ -1,0 +1,455 @@
+// ftsamd: HIP runtime + kernels + C ABI (include/ftsamd.h).
+//
+// One context per GPU holds the public parameters in device form: fixed-base
+// tables (8-bit windows) for Ped0..2, PedGen, the G1 generator and PK0..2, Q;
+// the precomputed Miller lines of Q; and the canonical RawBytes of the PP
+// points that every transcript hashes.  A batch is planned on the host
+// (host/planner.cpp), uploaded once, and executed as a fixed sequence of
+// job kernels on one HIP stream (see dev/jobs.h for the job model).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ftsamd.h"
+#include "dev/jobs.h"
+#include "host/planner.h"
+#include "launch.h"
+
+using namespace fts;
+using namespace ftsh;
+
+// ------------------------------------------------------------------ host runtime
+static thread_local std::string g_err;
+static int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HC(expr)                                                                                    \
+  do {                                                                                              \
+    hipError_t e_ = (expr);                                                                         \
+    if (e_ != hipSuccess)                                                                           \
+      return set_err(FTZ_E_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_));        \
+  } while (0)
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t alloc(size_t cnt) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = cnt;
+    if (cnt == 0) return hipSuccess;
+    return hipMalloc(&p, cnt * sizeof(T));
+  }
+  hipError_t upload(const std::vector<T>& v, hipStream_t s) {
+    hipError_t e = alloc(v.size());
+    if (e != hipSuccess || v.empty()) return e;
+    return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+};
+
+struct ftz_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  PPInfo pp;
+  std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
+  DBuf<G1Dev> g1tab;
+  DBuf<G2Dev> g2tab;
+  DBuf<LineCoef> qlines;
+  int threads = 8;
+  std::mutex mu;
+};
+
+struct ftz_batch {
+  ftz_ctx* ctx = nullptr;
+  size_t n = 0;
+  Plan plan;
+  DBuf<uint8_t> wire, arena, pt_ok, canon, hash_ok_pre, hash_ok;
+  DBuf<DecodeJob> dec;
+  DBuf<ZrJob> zr;
+  DBuf<ScalJob> sc;
+  DBuf<uint32_t> sclist;
+  DBuf<VTerm> vt;
+  DBuf<G1Job> g1;
+  DBuf<G2Job> g2;
+  DBuf<PairJob> pr;
+  DBuf<Seg> seg;
+  DBuf<HashJob> hpre, hmain;
+  DBuf<Check> ck;
+  DBuf<TxChecks> tx;
+  DBuf<G1Dev> pts, g1out;
+  DBuf<G2Dev> g2out;
+  DBuf<uint32_t> scal;  // 8 limbs per scalar
+  DBuf<F12Dev> fbuf;
+  DBuf<int32_t> codes;
+  DBuf<uint32_t> bitmap;
+  hipEvent_t ev[FTZ_NKERNELS + 1];
+  bool ev_init = false;
+  ftz_stats stats;
+};
+
+static int blocks_for(uint32_t n, int bs) { return (int)((n + bs - 1) / bs); }
+
+extern "C" const char* ftz_last_error(void) { return g_err.c_str(); }
+
+extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {
+  if (!pp || !out) return set_err(FTZ_E_INVALID, "null argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return set_err(FTZ_E_DEVICE, "no HIP device available (ftsamd requires an MI355X / gfx950 GPU)");
+  if (device < 0 || device >= ndev) return set_err(FTZ_E_DEVICE, "device ordinal out of range");
+  HC(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HC(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(FTZ_E_DEVICE, std::string("unsupported GPU architecture ") + prop.gcnArchName +
+                                     " (code objects are built for gfx950)");
+  ftz_ctx* c = new ftz_ctx();
+  c->device = device;
+  unsigned hc = std::thread::hardware_concurrency();
+  c->threads = (int)std::max(1u, std::min(16u, hc ? hc : 8u));
+  std::string e = parse_pp(pp, pp_len, "zkatdlog", c->pp);
+  if (!e.empty()) {
+    delete c;
+    return set_err(FTZ_E_PP, e);
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
+  }
+  // decode PP points on the GPU: G1 [PedGen, Ped0, Ped1, Ped2, G1 generator], G2 [PK0, PK1, PK2, Q]
+  std::vector<uint8_t> raw;
+  std::vector<uint32_t> g1off, g2off;
+  auto push = [&](const std::vector<uint8_t>& v, size_t need, std::vector<uint32_t>& offs) {
+    offs.push_back((uint32_t)raw.size());
+    std::vector<uint8_t> t = v;
+    t.resize(std::max(need, v.size()), 0);
+    raw.insert(raw.end(), t.begin(), t.end());
+  };
+  push(c->pp.pedgen, 64, g1off);
+  for (int k = 0; k < 3; k++) push(c->pp.ped[k], 64, g1off);
+  std::vector<uint8_t> gen(64, 0);
+  gen[31] = 1;
+  gen[63] = 2;
+  push(gen, 64, g1off);
+  for (int k = 0; k < 3; k++) push(c->pp.pk[k], 128, g2off);
+  push(c->pp.q, 128, g2off);
+  raw.resize(raw.size() + 128, 0);
+  DBuf<uint8_t> d_raw, d_g1b, d_g2b, d_ok;
+  DBuf<uint32_t> d_g1off, d_g2off;
+  DBuf<G1Dev> d_g1;
+  DBuf<G2Dev> d_g2;
+  int rc = FTZ_SUCCESS;
+  auto fail = [&](int code, const std::string& m) {
+    rc = set_err(code, m);
+    return rc;
+  };
+  do {
+    if (d_raw.upload(raw, c->stream) != hipSuccess || d_g1off.upload(g1off, c->stream) != hipSuccess ||
+        d_g2off.upload(g2off, c->stream) != hipSuccess || d_g1.alloc(5) != hipSuccess ||
+        d_g2.alloc(4) != hipSuccess || d_g1b.alloc(64 * 5) != hipSuccess || d_g2b.alloc(128 * 4) != hipSuccess ||
+        d_ok.alloc(9) != hipSuccess) {
+      fail(FTZ_E_NOMEM, "device allocation failed");
+      break;
+    }
+    k_pp_decode<<<1, 64, 0, c->stream>>>(d_raw.p, d_g1off.p, 5, d_g2off.p, 4, d_g1.p, d_g2.p, d_g1b.p, d_g2b.p,
+                                         d_ok.p);
+    uint8_t ok[9];
+    std::vector<uint8_t> g1b(64 * 5), g2b(128 * 4);
+    if (hipMemcpyAsync(ok, d_ok.p, 9, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(g1b.data(), d_g1b.p, g1b.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(g2b.data(), d_g2b.p, g2b.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      fail(FTZ_E_DEVICE, std::string("public-parameter decode failed: ") + hipGetErrorString(hipGetLastError()));
+      break;
+    }
+    bool allok = true;
+    for (int k = 0; k < 9; k++) allok = allok && ok[k];
+    if (!allok) {
+      fail(FTZ_E_PP, "public parameters hold an invalid curve point");
+      break;
+    }
+    c->const_bytes.assign(C_SIZE, 0);
+    memcpy(&c->const_bytes[C_PEDGEN], &g1b[0], 64);
+    memcpy(&c->const_bytes[C_PED0], &g1b[64], 192);
+    memcpy(&c->const_bytes[C_Q_PK], &g2b[384], 128);        // Q
+    memcpy(&c->const_bytes[C_Q_PK + 128], &g2b[0], 384);    // PK0..2
+    memcpy(&c->const_bytes[C_PK_Q + 384], &g2b[384], 128);  // Q again (PK0..2 shared)
+    // fixed-base tables: G1 base order must follow G1Base: PED0, PED1, PED2, PEDGEN, GEN
+    std::vector<G1Dev> hb(5);
+    std::vector<G1Dev> got(5);
+    if (hipMemcpy(got.data(), d_g1.p, 5 * sizeof(G1Dev), hipMemcpyDeviceToHost) != hipSuccess) {
+      fail(FTZ_E_DEVICE, "copy failed");
+      break;
+    }
+    hb[G1B_PED0] = got[1];
+    hb[G1B_PED1] = got[2];
+    hb[G1B_PED2] = got[3];
+    hb[G1B_PEDGEN] = got[0];
+    hb[G1B_GEN] = got[4];
+    DBuf<G1Dev> d_b1;
+    if (d_b1.upload(hb, c->stream) != hipSuccess) {
+      fail(FTZ_E_NOMEM, "alloc");
+      break;
+    }
+    uint32_t n1 = G1B_COUNT * TAB_WINDOWS * TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
+    if (c->g1tab.alloc(n1) != hipSuccess || c->g2tab.alloc(n2) != hipSuccess ||
+        c->qlines.alloc(MILLER_LINES) != hipSuccess) {
+      fail(FTZ_E_NOMEM, "table allocation failed");
+      break;
+    }
+    k_tab_g1<<<blocks_for(n1, 64), 64, 0, c->stream>>>(d_b1.p, n1, c->g1tab.p);
+    k_tab_g2<<<blocks_for(n2, 64), 64, 0, c->stream>>>(d_g2.p, n2, c->g2tab.p);  // PK0, PK1, PK2, Q
+    DBuf<int> d_n;
+    if (d_n.alloc(1) != hipSuccess) {
+      fail(FTZ_E_NOMEM, "alloc");
+      break;
+    }
+    k_qlines<<<1, 64, 0, c->stream>>>(d_g2.p + 3, c->qlines.p, d_n.p);
+    int nl = 0;
+    if (hipMemcpyAsync(&nl, d_n.p, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess || nl != MILLER_LINES) {
+      fail(FTZ_E_DEVICE, std::string("context setup kernels failed: ") + hipGetErrorString(hipGetLastError()));
+      break;
+    }
+  } while (0);
+  if (rc != FTZ_SUCCESS) {
+    ftz_ctx_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return FTZ_SUCCESS;
+}
+
+extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->g1tab.alloc(0);
+  c->g2tab.alloc(0);
+  c->qlines.alloc(0);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" int ftz_ctx_set_threads(ftz_ctx* c, int threads) {
+  if (!c || threads < 1) return set_err(FTZ_E_INVALID, "bad argument");
+  c->threads = threads;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_ctx_info(const ftz_ctx* c, uint32_t* base, uint32_t* exponent) {
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  if (base) *base = c->pp.base;
+  if (exponent) *exponent = (uint32_t)c->pp.exponent;
+  return FTZ_SUCCESS;
+}
+
+static int batch_upload(ftz_batch* b) {
+  ftz_ctx* c = b->ctx;
+  Plan& p = b->plan;
+  hipStream_t s = c->stream;
+  memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
+  std::vector<uint8_t> wire = p.wire;
+  wire.resize(wire.size() + 64, 0);  // decode jobs may look at 64 bytes past a short element
+  HC(b->wire.upload(wire, s));
+  HC(b->arena.upload(p.arena, s));
+  HC(b->dec.upload(p.dec, s));
+  HC(b->zr.upload(p.zr, s));
+  HC(b->sc.upload(p.sc, s));
+  HC(b->sclist.upload(p.sclist, s));
+  HC(b->vt.upload(p.vt, s));
+  HC(b->g1.upload(p.g1, s));
+  HC(b->g2.upload(p.g2, s));
+  HC(b->pr.upload(p.pr, s));
+  HC(b->seg.upload(p.seg, s));
+  HC(b->hpre.upload(p.hpre, s));
+  HC(b->hmain.upload(p.hmain, s));
+  HC(b->ck.upload(p.ck, s));
+  HC(b->tx.upload(p.tx, s));
+  HC(b->pts.alloc(std::max<uint32_t>(p.n_pts, 1)));
+  HC(b->pt_ok.alloc(std::max<uint32_t>(p.n_pts, 1)));
+  HC(b->scal.alloc(8 * (size_t)std::max<uint32_t>(p.n_scal, 1)));
+  HC(b->canon.alloc(std::max<uint32_t>(p.n_scal, 1)));
+  HC(b->g1out.alloc(std::max<uint32_t>(p.n_g1out, 1)));
+  HC(b->g2out.alloc(std::max<uint32_t>(p.n_g2out, 1)));
+  HC(b->fbuf.alloc(std::max<size_t>(p.pr.size(), 1)));
+  HC(b->hash_ok.alloc(std::max<size_t>(p.hmain.size(), 1)));
+  HC(b->hash_ok_pre.alloc(std::max<size_t>(p.hpre.size(), 1)));
+  HC(b->codes.alloc(std::max<size_t>(b->n, 1)));
+  HC(b->bitmap.alloc((b->n + 31) / 32 + 1));
+  HC(hipMemsetAsync(b->pt_ok.p, 1, std::max<uint32_t>(p.n_pts, 1), s));
+  HC(hipStreamSynchronize(s));
+  if (!b->ev_init) {
+    for (int k = 0; k <= FTZ_NKERNELS; k++) HC(hipEventCreate(&b->ev[k]));
+    b->ev_init = true;
+  }
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_load_transfers(ftz_ctx* c, size_t n, const ftz_transfer* tx, ftz_batch** out) {
+  if (!c || !out || (n && !tx)) return set_err(FTZ_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if ((tx[i].n_in && !tx[i].inputs) || (tx[i].n_out && !tx[i].outputs) || (tx[i].proof_len && !tx[i].proof))
+      return set_err(FTZ_E_INVALID, "null buffer in transfer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  ftz_batch* b = new ftz_batch();
+  b->ctx = c;
+  b->n = n;
+  std::vector<TransferIn> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+  plan_transfers(c->pp, n, t.data(), b->plan, c->threads);
+  int rc = batch_upload(b);
+  if (rc != FTZ_SUCCESS) {
+    ftz_batch_destroy(b);
+    return rc;
+  }
+  *out = b;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, ftz_batch** out) {
+  if (!c || !out || (n && !is)) return set_err(FTZ_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if ((is[i].n_out && !is[i].outputs) || (is[i].proof_len && !is[i].proof))
+      return set_err(FTZ_E_INVALID, "null buffer in issue");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  ftz_batch* b = new ftz_batch();
+  b->ctx = c;
+  b->n = n;
+  std::vector<IssueIn> t(n);
+  for (size_t i = 0; i < n; i++) t[i] = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
+  plan_issues(c->pp, n, t.data(), b->plan, c->threads);
+  int rc = batch_upload(b);
+  if (rc != FTZ_SUCCESS) {
+    ftz_batch_destroy(b);
+    return rc;
+  }
+  *out = b;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_run(ftz_batch* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+  ftz_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  Plan& p = b->plan;
+  hipStream_t s = c->stream;
+  uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
+  uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
+  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g2 = (uint32_t)p.g2.size(), n_pr = (uint32_t)p.pr.size();
+  uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
+  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1, n_g2, n_pr, n_pr, n_hm, n_tx, 0};
+  HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
+  HC(hipEventRecord(b->ev[0], s));
+  if (n_dec) k_decode<<<blocks_for(n_dec, 256), 256, 0, s>>>(b->dec.p, n_dec, b->wire.p, b->pts.p, b->pt_ok.p, b->arena.p);
+  HC(hipEventRecord(b->ev[1], s));
+  if (n_zr) k_zr<<<blocks_for(n_zr, 256), 256, 0, s>>>(b->zr.p, n_zr, b->wire.p, scal, b->canon.p);
+  HC(hipEventRecord(b->ev[2], s));
+  if (n_hp)
+    k_hash<<<blocks_for(n_hp, 128), 128, 0, s>>>(b->hpre.p, n_hp, b->seg.p, b->arena.p, scal, b->canon.p,
+                                                 b->hash_ok_pre.p);
+  HC(hipEventRecord(b->ev[3], s));
+  if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
+  HC(hipEventRecord(b->ev[4], s));
+  if (n_g1)
+    k_g1<<<blocks_for(n_g1, 128), 128, 0, s>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
+                                               b->arena.p);
+  HC(hipEventRecord(b->ev[5], s));
+  if (n_g2) k_g2<<<blocks_for(n_g2, 128), 128, 0, s>>>(b->g2.p, n_g2, scal, c->g2tab.p, b->g2out.p);
+  HC(hipEventRecord(b->ev[6], s));
+  if (n_pr)
+    k_miller<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->g1out.p, b->pts.p, b->g2out.p,
+                                                 b->fbuf.p);
+  HC(hipEventRecord(b->ev[7], s));
+  if (n_pr) k_fexp<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
+  HC(hipEventRecord(b->ev[8], s));
+  if (n_hm)
+    k_hash<<<blocks_for(n_hm, 128), 128, 0, s>>>(b->hmain.p, n_hm, b->seg.p, b->arena.p, scal, b->canon.p,
+                                                 b->hash_ok.p);
+  HC(hipEventRecord(b->ev[9], s));
+  if (n_tx)
+    k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
+                                                    b->bitmap.p);
+  HC(hipEventRecord(b->ev[10], s));
+  HC(hipGetLastError());
+  HC(hipStreamSynchronize(s));
+  for (int k = 0; k < 10; k++) {
+    float ms = 0;
+    HC(hipEventElapsedTime(&ms, b->ev[k], b->ev[k + 1]));
+    b->stats.ms[k] = ms;
+    b->stats.jobs[k] = jobs[k];
+  }
+  float tot = 0;
+  HC(hipEventElapsedTime(&tot, b->ev[0], b->ev[10]));
+  b->stats.ms[10] = tot;
+  b->stats.jobs[10] = n_tx;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_codes(ftz_batch* b, int32_t* codes) {
+  if (!b || (b->n && !codes)) return set_err(FTZ_E_INVALID, "null argument");
+  HC(hipSetDevice(b->ctx->device));
+  if (b->n) HC(hipMemcpy(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits) {
+  if (!b || (b->n && !bits)) return set_err(FTZ_E_INVALID, "null argument");
+  HC(hipSetDevice(b->ctx->device));
+  std::vector<uint32_t> w((b->n + 31) / 32);
+  if (!w.empty()) HC(hipMemcpy(w.data(), b->bitmap.p, w.size() * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < (b->n + 7) / 8; i++) bits[i] = (uint8_t)(w[i / 4] >> (8 * (i % 4)));
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_batch_stats(const ftz_batch* b, ftz_stats* out) {
+  if (!b || !out) return set_err(FTZ_E_INVALID, "null argument");
+  *out = b->stats;
+  return FTZ_SUCCESS;
+}
+
+extern "C" size_t ftz_batch_size(const ftz_batch* b) { return b ? b->n : 0; }
+
+extern "C" void ftz_batch_destroy(ftz_batch* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->ctx->device);
+  if (b->ev_init)
+    for (int k = 0; k <= FTZ_NKERNELS; k++) (void)hipEventDestroy(b->ev[k]);
+  delete b;
+}
+
+extern "C" int ftz_verify_transfers(ftz_ctx* c, size_t n, const ftz_transfer* tx, int32_t* codes) {
+  if (n == 0) return FTZ_SUCCESS;
+  ftz_batch* b = nullptr;
+  int rc = ftz_batch_load_transfers(c, n, tx, &b);
+  if (rc == FTZ_SUCCESS) rc = ftz_batch_run(b);
+  if (rc == FTZ_SUCCESS) rc = ftz_batch_codes(b, codes);
+  ftz_batch_destroy(b);
+  return rc;
+}
+
+extern "C" int ftz_verify_issues(ftz_ctx* c, size_t n, const ftz_issue* is, int32_t* codes) {
+  if (n == 0) return FTZ_SUCCESS;
+  ftz_batch* b = nullptr;
+  int rc = ftz_batch_load_issues(c, n, is, &b);
+  if (rc == FTZ_SUCCESS) rc = ftz_batch_run(b);
+  if (rc == FTZ_SUCCESS) rc = ftz_batch_codes(b, codes);
+  ftz_batch_destroy(b);
+  return rc;
+}

@@ -1,0 +1,177 @@
+"""zkatdlog -- MI355X batch verifier for the Fabric Token SDK zkatdlog (nogh) driver.
+
+Host-side mirror of the reference's verifier interfaces (Go, paths relative to
+/root/reference/token/core/zkatdlog/crypto/):
+
+    transfer.NewVerifier(inputs, outputs, pp).Verify(proof)   transfer/transfer.go:66,124
+    issue.NewVerifier(tokens, anonymous, pp).Verify(proof)    issue/issue.go:194,202
+    validator TransferZKProofValidate(ctx)                    validator/validator_transfer.go:232
+
+backed by libftsamd.so (include/ftsamd.h): every proof is parsed on the host
+and verified by HIP kernels on the GPU.  There is no CPU fallback: without
+the library or without an MI355X the constructors raise.
+
+Batch form (the point of the port):
+
+    ctx = Context(pp_bytes, device=0)
+    codes = ctx.verify_transfers([(inputs64, outputs64, proof), ...])   # 0 = accept
+"""
+import ctypes
+
+from . import _abi
+from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_PANIC, FTZ_ERR_PARSE, FTZ_ERR_RANGE,  # noqa: F401
+                   FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
+
+__all__ = ["Context", "Batch", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
+           "FTZ_OK", "MESSAGES"]
+
+
+class ZKError(Exception):
+    """A rejected proof; ``code`` is the FTZ_ERR_* class, the message carries
+    the reference's error text for that class."""
+
+    def __init__(self, code):
+        super().__init__(MESSAGES.get(code, "verification failed (%d)" % code))
+        self.code = code
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+def _check(rc, lib):
+    if rc != 0:
+        raise DeviceError("ftsamd error %d: %s" % (rc, lib.ftz_last_error().decode(errors="replace")))
+
+
+class Context:
+    """Public parameters resident on one GPU (crypto.PublicParams + the
+    fixed-base tables / Miller lines the kernels use).  The reference builds
+    its validator once per process (token/services/network/fabric/tcc/tcc.go:170-182);
+    so does this."""
+
+    def __init__(self, pp_bytes, device=0, threads=None):
+        self._lib = _abi.load()
+        h = ctypes.c_void_p()
+        pp_bytes = bytes(pp_bytes)
+        _check(self._lib.ftz_ctx_create(pp_bytes, len(pp_bytes), int(device), ctypes.byref(h)), self._lib)
+        self._h = h
+        if threads:
+            _check(self._lib.ftz_ctx_set_threads(h, int(threads)), self._lib)
+        b, e = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(self._lib.ftz_ctx_info(h, ctypes.byref(b), ctypes.byref(e)), self._lib)
+        self.base, self.exponent = b.value, e.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ftz_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def verify_transfers(self, transfers):
+        """transfers: iterable of (inputs, outputs, proof) with inputs/outputs the
+        concatenated 64-byte G1 RawBytes commitments.  Returns a list of codes."""
+        arr, keep = _abi.pack_transfers(transfers)
+        n = len(keep) // 3
+        codes = (ctypes.c_int32 * max(1, n))()
+        _check(self._lib.ftz_verify_transfers(self._h, n, arr, codes), self._lib)
+        return list(codes)[:n]
+
+    def verify_issues(self, issues):
+        """issues: iterable of (outputs, proof, anonymous)."""
+        arr, keep = _abi.pack_issues(issues)
+        n = len(keep) // 2
+        codes = (ctypes.c_int32 * max(1, n))()
+        _check(self._lib.ftz_verify_issues(self._h, n, arr, codes), self._lib)
+        return list(codes)[:n]
+
+    def load_transfers(self, transfers):
+        arr, keep = _abi.pack_transfers(transfers)
+        n = len(keep) // 3
+        h = ctypes.c_void_p()
+        _check(self._lib.ftz_batch_load_transfers(self._h, n, arr, ctypes.byref(h)), self._lib)
+        return Batch(self, h, n)
+
+    def load_issues(self, issues):
+        arr, keep = _abi.pack_issues(issues)
+        n = len(keep) // 2
+        h = ctypes.c_void_p()
+        _check(self._lib.ftz_batch_load_issues(self._h, n, arr, ctypes.byref(h)), self._lib)
+        return Batch(self, h, n)
+
+
+class Batch:
+    """A planned, device-resident batch: run() re-executes the GPU pipeline."""
+
+    def __init__(self, ctx, h, n):
+        self._ctx, self._lib, self._h, self.n = ctx, ctx._lib, h, n
+
+    def run(self):
+        _check(self._lib.ftz_batch_run(self._h), self._lib)
+
+    def codes(self):
+        c = (ctypes.c_int32 * max(1, self.n))()
+        _check(self._lib.ftz_batch_codes(self._h, c), self._lib)
+        return list(c)[:self.n]
+
+    def bitmap(self):
+        b = (ctypes.c_uint8 * max(1, (self.n + 7) // 8))()
+        _check(self._lib.ftz_batch_bitmap(self._h, b), self._lib)
+        return bytes(b)[:(self.n + 7) // 8]
+
+    def stats(self):
+        s = _abi.Stats()
+        _check(self._lib.ftz_batch_stats(self._h, ctypes.byref(s)), self._lib)
+        return {name: (s.ms[k], s.jobs[k]) for k, name in enumerate(KERNEL_NAMES)}
+
+    def close(self):
+        if self._h:
+            self._lib.ftz_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class TransferVerifier:
+    """transfer.NewVerifier(inputs, outputs, pp) (transfer/transfer.go:66-77)."""
+
+    def __init__(self, inputs, outputs, ctx):
+        self.inputs = b"".join(bytes(x) for x in inputs)
+        self.outputs = b"".join(bytes(x) for x in outputs)
+        self.ctx = ctx
+
+    def verify(self, proof):
+        """transfer.Verifier.Verify (transfer/transfer.go:124-154): raises ZKError."""
+        code = self.ctx.verify_transfers([(self.inputs, self.outputs, bytes(proof))])[0]
+        if code != FTZ_OK:
+            raise ZKError(code)
+
+
+class IssueVerifier:
+    """issue.NewVerifier(tokens, anonymous, pp) (issue/issue.go:194-199)."""
+
+    def __init__(self, tokens, anonymous, ctx):
+        self.tokens = b"".join(bytes(x) for x in tokens)
+        self.anonymous = bool(anonymous)
+        self.ctx = ctx
+
+    def verify(self, proof):
+        code = self.ctx.verify_issues([(self.tokens, bytes(proof), self.anonymous)])[0]
+        if code != FTZ_OK:
+            raise ZKError(code)
+
+
+def transfer_zkproof_validate(ctx, input_commitments, output_commitments, proof):
+    """validator.TransferZKProofValidate (validator/validator_transfer.go:232-246):
+    inputs are the commitments of the ledger tokens, not the action's own
+    InputCommitments."""
+    TransferVerifier(input_commitments, output_commitments, ctx).verify(proof)

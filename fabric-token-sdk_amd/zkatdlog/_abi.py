@@ -1,0 +1,115 @@
+"""ctypes mirror of include/ftsamd.h (structs, codes) and the library loader."""
+import ctypes
+import os
+
+FTZ_OK = 0
+FTZ_ERR_PARSE = 1
+FTZ_ERR_MALFORMED = 2
+FTZ_ERR_WF = 3
+FTZ_ERR_RANGE = 4
+FTZ_ERR_MEMBERSHIP = 5
+FTZ_ERR_PANIC = 6
+
+FTZ_SUCCESS = 0
+FTZ_E_INVALID = -1
+FTZ_E_PP = -2
+FTZ_E_DEVICE = -3
+FTZ_E_NOMEM = -4
+
+FTZ_NKERNELS = 11
+KERNEL_NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "hash", "verdict", "total"]
+
+# error strings of the reference for each class (tests match substrings)
+MESSAGES = {
+    FTZ_ERR_PARSE: "invalid transfer proof: cannot parse proof",
+    FTZ_ERR_MALFORMED: "range proof not well formed",
+    FTZ_ERR_WF: "invalid zero-knowledge transfer",
+    FTZ_ERR_RANGE: "invalid range proof",
+    FTZ_ERR_MEMBERSHIP: "invalid membership proof",
+    FTZ_ERR_PANIC: "proof would make the reference verifier panic",
+}
+
+
+class Transfer(ctypes.Structure):
+    _fields_ = [("inputs", ctypes.c_void_p), ("n_in", ctypes.c_uint32),
+                ("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
+                ("proof", ctypes.c_void_p), ("proof_len", ctypes.c_size_t)]
+
+
+class Issue(ctypes.Structure):
+    _fields_ = [("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
+                ("proof", ctypes.c_void_p), ("proof_len", ctypes.c_size_t),
+                ("anonymous", ctypes.c_uint8)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_float * FTZ_NKERNELS), ("jobs", ctypes.c_uint64 * FTZ_NKERNELS)]
+
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libftsamd.so")
+
+# every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
+SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_threads", "ftz_ctx_info",
+           "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
+           "ftz_batch_run", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
+           "ftz_batch_destroy"]
+
+_lib = None
+
+
+def load():
+    """Load libftsamd.so; raises loudly when it is missing (no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libftsamd.so not built (%s); run fabric-token-sdk_amd/build.py "
+                           "-- there is no CPU fallback for the zkatdlog GPU verifier" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32
+    lib.ftz_ctx_create.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
+    lib.ftz_ctx_destroy.argtypes = [vp]
+    lib.ftz_ctx_destroy.restype = None
+    lib.ftz_last_error.restype = ctypes.c_char_p
+    lib.ftz_ctx_set_threads.argtypes = [vp, ctypes.c_int]
+    lib.ftz_ctx_info.argtypes = [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    lib.ftz_verify_transfers.argtypes = [vp, sz, ctypes.POINTER(Transfer), ctypes.POINTER(i32)]
+    lib.ftz_verify_issues.argtypes = [vp, sz, ctypes.POINTER(Issue), ctypes.POINTER(i32)]
+    lib.ftz_batch_load_transfers.argtypes = [vp, sz, ctypes.POINTER(Transfer), ctypes.POINTER(vp)]
+    lib.ftz_batch_load_issues.argtypes = [vp, sz, ctypes.POINTER(Issue), ctypes.POINTER(vp)]
+    lib.ftz_batch_run.argtypes = [vp]
+    lib.ftz_batch_codes.argtypes = [vp, ctypes.POINTER(i32)]
+    lib.ftz_batch_bitmap.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8)]
+    lib.ftz_batch_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.ftz_batch_size.argtypes = [vp]
+    lib.ftz_batch_size.restype = sz
+    lib.ftz_batch_destroy.argtypes = [vp]
+    lib.ftz_batch_destroy.restype = None
+    _lib = lib
+    return lib
+
+
+def pack_transfers(items):
+    """items: iterable of (inputs: bytes (n_in*64), outputs: bytes (n_out*64), proof: bytes).
+    Returns (ctypes array, keepalive list)."""
+    items = list(items)
+    arr = (Transfer * max(1, len(items)))()
+    keep = []
+    for k, (ins, outs, proof) in enumerate(items):
+        bi, bo, bp = (ctypes.create_string_buffer(bytes(x), max(1, len(x))) for x in (ins, outs, proof))
+        keep += [bi, bo, bp]
+        arr[k] = Transfer(ctypes.addressof(bi), len(ins) // 64, ctypes.addressof(bo), len(outs) // 64,
+                          ctypes.addressof(bp), len(proof))
+    return arr, keep
+
+
+def pack_issues(items):
+    """items: iterable of (outputs: bytes, proof: bytes, anonymous: bool)."""
+    items = list(items)
+    arr = (Issue * max(1, len(items)))()
+    keep = []
+    for k, (outs, proof, anon) in enumerate(items):
+        bo, bp = (ctypes.create_string_buffer(bytes(x), max(1, len(x))) for x in (outs, proof))
+        keep += [bo, bp]
+        arr[k] = Issue(ctypes.addressof(bo), len(outs) // 64, ctypes.addressof(bp), len(proof), 1 if anon else 0)
+    return arr, keep

@@ -1,0 +1,107 @@
+/* ftsamd -- MI355X batch verifier for the zkatdlog (nogh) driver of the
+ * Fabric Token SDK.  C ABI: plain pointers and sizes, no torch / HIP types.
+ *
+ * Reference interfaces this boundary replaces (paths relative to
+ * /root/reference/token/core/zkatdlog/):
+ *   ftz_ctx_create        crypto/setup.go:350-367   PublicParams.Deserialize
+ *                         nogh/driver/driver.go:114-124 Driver.NewValidator (PP parsed once per process)
+ *   ftz_verify_transfers  crypto/transfer/transfer.go:66-77,124-154
+ *                         transfer.NewVerifier(inputs, outputs, pp).Verify(proof)
+ *                         as called by crypto/validator/validator_transfer.go:232-246
+ *                         TransferZKProofValidate (inputs = ledger commitments)
+ *   ftz_verify_issues     crypto/issue/issue.go:194-223
+ *                         issue.NewVerifier(tokens, anonymous, pp).Verify(proof)
+ *                         as called by crypto/validator/validator.go:181-191 verifyIssue
+ * The Go error classes map to the FTZ_ERR_* codes below; a proof on which the
+ * reference would panic (nil dereference, foreign curve id) is reported as
+ * FTZ_ERR_PANIC (reject) instead of crashing the process.
+ *
+ * Thread-safety: a context may be used from several threads; calls on one
+ * context are serialised internally.  Every entry point is synchronous.
+ */
+#ifndef FTSAMD_H
+#define FTSAMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-proof verdict codes (0 = accept) */
+#define FTZ_OK 0
+#define FTZ_ERR_PARSE 1      /* json / base64 / element decoding failed            */
+#define FTZ_ERR_MALFORMED 2  /* "not well formed", nil fields, length mismatches    */
+#define FTZ_ERR_WF 3         /* "invalid zero-knowledge transfer" / issue WF        */
+#define FTZ_ERR_RANGE 4      /* "invalid range proof"                               */
+#define FTZ_ERR_MEMBERSHIP 5 /* "invalid membership proof"                          */
+#define FTZ_ERR_PANIC 6      /* the reference would panic on this proof             */
+
+/* API return codes */
+#define FTZ_SUCCESS 0
+#define FTZ_E_INVALID (-1) /* bad argument                                         */
+#define FTZ_E_PP (-2)      /* public parameters rejected                            */
+#define FTZ_E_DEVICE (-3)  /* no usable MI355X / HIP error (see ftz_last_error)     */
+#define FTZ_E_NOMEM (-4)
+
+typedef struct ftz_ctx ftz_ctx;
+typedef struct ftz_batch ftz_batch;
+
+/* One transfer action: commitments are 64-byte gnark G1 RawBytes (X||Y). */
+typedef struct {
+  const uint8_t* inputs; /* n_in  x 64 bytes: input token commitments (ledger)   */
+  uint32_t n_in;
+  const uint8_t* outputs; /* n_out x 64 bytes: output token commitments          */
+  uint32_t n_out;
+  const uint8_t* proof; /* json(transfer.Proof) as carried in TransferAction.Proof */
+  size_t proof_len;
+} ftz_transfer;
+
+typedef struct {
+  const uint8_t* outputs; /* n_out x 64 bytes: issued token commitments          */
+  uint32_t n_out;
+  const uint8_t* proof; /* json(issue.Proof)                                      */
+  size_t proof_len;
+  uint8_t anonymous; /* IssueAction.Anonymous                                     */
+} ftz_issue;
+
+/* Per-kernel timing of the last ftz_batch_run (HIP events on the batch stream). */
+#define FTZ_NKERNELS 11
+typedef struct {
+  float ms[FTZ_NKERNELS];     /* decode, zr, hash_pre, scalar, g1, g2, miller, fexp, hash, verdict, total */
+  uint64_t jobs[FTZ_NKERNELS];
+} ftz_stats;
+
+/* pp: json(driver.SerializedPublicParameters{Identifier:"zkatdlog", Raw}) as
+ * produced by crypto.PublicParams.Serialize (setup.go:335-344).
+ * device: HIP device ordinal (the local rank in a multi-GPU job). */
+int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out);
+void ftz_ctx_destroy(ftz_ctx* ctx);
+/* last error message of the calling thread (empty string if none) */
+const char* ftz_last_error(void);
+/* number of host threads used to plan a batch (default: min(16, cores)) */
+int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
+/* PP properties: base (len(SignedValues)) and exponent */
+int ftz_ctx_info(const ftz_ctx* ctx, uint32_t* base, uint32_t* exponent);
+
+/* Verify n proofs; codes[i] receives FTZ_OK or an FTZ_ERR_* class. */
+int ftz_verify_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, int32_t* codes);
+int ftz_verify_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, int32_t* codes);
+
+/* Staged form: plan + upload once, then run the GPU pipeline on resident
+ * inputs any number of times (used by bench.py to time the device path). */
+int ftz_batch_load_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, ftz_batch** out);
+int ftz_batch_load_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, ftz_batch** out);
+int ftz_batch_run(ftz_batch* b);
+int ftz_batch_codes(ftz_batch* b, int32_t* codes);
+/* verdict bitmap: bit i set <=> proof i accepted; (n+7)/8 bytes */
+int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits);
+int ftz_batch_stats(const ftz_batch* b, ftz_stats* out);
+size_t ftz_batch_size(const ftz_batch* b);
+void ftz_batch_destroy(ftz_batch* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FTSAMD_H */

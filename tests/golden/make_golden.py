@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ with the CPU oracle.
+
+The reference (Go) cannot run here, so the fixtures come from the build's own
+restatement (oracle/py/ftsoracle).  Every expected verdict is the oracle's
+answer; the cases reproduce the reference's own test classes
+(transfer/transfer_test.go:61-84, transfer/wellformedness_test.go:90-151,
+sigproof/membership_test.go:34-47, range/proof_test.go) plus the tamper corpus
+of SURVEY.md Appendix C.3.
+
+    python tests/golden/make_golden.py            # writes tests/golden/*.json
+"""
+import base64
+import copy
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle", "py"))
+from ftsoracle import bn254 as C  # noqa: E402
+from ftsoracle import zkat as Z  # noqa: E402
+
+R = C.R
+
+
+def g1cat(pts):
+    return b"".join(C.g1_bytes(p) for p in pts)
+
+
+def jload(b):
+    return json.loads(b)
+
+
+def jdump(o):
+    return json.dumps(o, separators=(",", ":")).encode()
+
+
+def b64(b):
+    return base64.b64encode(b).decode()
+
+
+def unb64(s):
+    return base64.b64decode(s)
+
+
+def zr_elem(v, length=32):
+    return {"curve": 1, "element": b64(v.to_bytes(length, "big"))}
+
+
+def zr_val(e):
+    return int.from_bytes(unb64(e["element"]), "big")
+
+
+def split_transfer(proof):
+    top = jload(proof)
+    wf = jload(unb64(top["WellFormedness"]))
+    rc = jload(unb64(top["RangeCorrectness"])) if top["RangeCorrectness"] is not None else None
+    return top, wf, rc
+
+
+def join_transfer(top, wf, rc, raw_wf=None, raw_rc=None):
+    top = dict(top)
+    top["WellFormedness"] = b64(raw_wf if raw_wf is not None else jdump(wf))
+    if raw_rc is not None:
+        top["RangeCorrectness"] = b64(raw_rc)
+    elif rc is not None:
+        top["RangeCorrectness"] = b64(jdump(rc))
+    return jdump(top)
+
+
+def other_point(seed):
+    return C.g1_bytes(C.g1_mul(C.G1_GEN, seed))
+
+
+def make_pp(base, exponent, seed):
+    rnd = Z.Rand(seed)
+    return Z.setup(base, exponent, rnd), rnd
+
+
+def transfer_case(pp, rnd, tag, in_vals, out_vals, ttype="ABC"):
+    inw = [(v, rnd.zr(tag + "/inbf/%d" % i)) for i, v in enumerate(in_vals)]
+    outw = [(v, rnd.zr(tag + "/outbf/%d" % i)) for i, v in enumerate(out_vals)]
+    ins = [Z.token_commitment(pp, ttype, v, b) for v, b in inw]
+    outs = [Z.token_commitment(pp, ttype, v, b) for v, b in outw]
+    proof = Z.transfer_prove(pp, rnd, ins, outs, inw, outw, ttype, tag=tag)
+    return ins, outs, proof
+
+
+def main():
+    out = {}
+    # ---------------------------------------------------------------- PP-A
+    pp, rnd = make_pp(100, 2, b"golden-pp-A")
+    cases = []
+
+    def add(name, ins, outs, proof, kind="transfer", anonymous=False):
+        if kind == "transfer":
+            ok, code, msg = Z.transfer_verify(pp, ins, outs, proof)
+        else:
+            ok, code, msg = Z.issue_verify(pp, outs, proof, anonymous)
+        cases.append({"name": name, "kind": kind, "inputs": g1cat(ins).hex(), "outputs": g1cat(outs).hex(),
+                      "proof": b64(proof), "anonymous": anonymous, "expect": code, "message": msg})
+        print("%-40s code=%d %s" % (name, code, msg), flush=True)
+
+    # valid transfers (transfer/transfer_test.go:53-59 uses in (90,60) / out (50,100))
+    ins, outs, proof = transfer_case(pp, rnd, "t0", [90, 60], [50, 100])
+    add("valid_2in_2out", ins, outs, proof)
+    for k, (iv, ov) in enumerate([([1, 2], [3, 0]), ([9999, 0], [5000, 4999]), ([500, 500], [999, 1])]):
+        i2, o2, p2 = transfer_case(pp, rnd, "tv%d" % k, iv, ov)
+        add("valid_2in_2out_%d" % k, i2, o2, p2)
+    i3, o3, p3 = transfer_case(pp, rnd, "t3", [77, 23, 100], [200])
+    add("valid_3in_1out", i3, o3, p3)
+    i4, o4, p4 = transfer_case(pp, rnd, "t4", [1000], [1, 2, 997])
+    add("valid_1in_3out", i4, o4, p4)
+    i5, o5, p5 = transfer_case(pp, rnd, "t5", [90], [90])
+    add("valid_ownership_1in_1out", i5, o5, p5)
+
+    # reference negative: sum mismatch (transfer_test.go:61-73, data :208-241)
+    ib, ob, pb = transfer_case(pp, rnd, "tbad", [90, 60], [110, 45])
+    add("ref_wrong_sum", ib, ob, pb)
+
+    top, wf, rc = split_transfer(proof)
+    # WF tampers (wellformedness_test.go:90-151 classes)
+    w = copy.deepcopy(wf); w["Challenge"] = zr_elem(zr_val(w["Challenge"]) ^ 1)
+    add("wf_challenge_bitflip", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["InputValues"][0] = zr_elem((zr_val(w["InputValues"][0]) + 1) % R)
+    add("wf_wrong_value", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Type"] = zr_elem((zr_val(w["Type"]) + 1) % R)
+    add("wf_wrong_type", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["OutputBlindingFactors"][1] = zr_elem((zr_val(w["OutputBlindingFactors"][1]) + 5) % R)
+    add("wf_wrong_blinding_factor", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Challenge"] = zr_elem(zr_val(w["Challenge"]) + R)
+    add("wf_challenge_plus_r", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["InputValues"][1] = zr_elem(zr_val(w["InputValues"][1]) + R)
+    add("wf_response_plus_r_accepts", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Sum"] = zr_elem(zr_val(w["Sum"]) + 3 * R, 33)
+    add("wf_response_33_bytes_plus_3r", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Sum"] = {"curve": 1, "element": b64(b"\x00" * 5 + zr_val(w["Sum"]).to_bytes(32, "big"))}
+    add("wf_response_leading_zeros", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); del w["Type"]
+    add("wf_missing_type_panics", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Sum"] = None
+    add("wf_null_sum", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["InputValues"] = w["InputValues"][:1]
+    add("wf_length_mismatch", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Type"]["curve"] = 0
+    add("wf_foreign_curve_panics", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Type"]["element"] = "!!notbase64"
+    add("wf_bad_base64", ins, outs, join_transfer(top, w, rc))
+    w = copy.deepcopy(wf); w["Type"]["curve"] = 1.0
+    add("wf_curve_not_int", ins, outs, join_transfer(top, w, rc))
+    w = {("challenge" if k == "Challenge" else ("TYPE" if k == "Type" else k)): v for k, v in wf.items()}
+    add("wf_case_insensitive_keys", ins, outs, join_transfer(top, w, rc))
+    raw = jdump(wf)
+    dup = raw[:-1] + b',"Challenge":' + jdump(zr_elem(12345)) + b"}"
+    add("wf_duplicate_key_last_wins_bad", ins, outs, join_transfer(top, None, rc, raw_wf=dup))
+    dup2 = b'{"Challenge":' + jdump(zr_elem(12345)) + b"," + raw[1:]
+    add("wf_duplicate_key_last_wins_good", ins, outs, join_transfer(top, None, rc, raw_wf=dup2))
+    w = dict(wf); w["Extra"] = [1, 2, {"x": None}]
+    add("wf_unknown_field", ins, outs, join_transfer(top, w, rc))
+    add("wf_pretty_printed", ins, outs,
+        join_transfer(top, None, rc, raw_wf=json.dumps(wf, indent=2).encode()))
+    add("swapped_outputs", ins, list(reversed(outs)), proof)
+    add("swapped_inputs", list(reversed(ins)), outs, proof)
+    add("truncated_proof_json", ins, outs, proof[:-7])
+    add("empty_proof", ins, outs, b"")
+
+    # range tampers
+    r = copy.deepcopy(rc); r["Challenge"] = zr_elem(zr_val(r["Challenge"]) ^ 4)
+    add("range_challenge_bitflip", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["EqualityProofs"]["Value"][0] = zr_elem((zr_val(r["EqualityProofs"]["Value"][0]) + 1) % R)
+    add("range_equality_value", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["EqualityProofs"] = None
+    add("range_null_equality", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["EqualityProofs"]["CommitmentBlindingFactor"] = r["EqualityProofs"]["CommitmentBlindingFactor"][:1]
+    add("range_equality_length", ins, outs, join_transfer(top, wf, r))
+    mp = lambda rr, k, i: rr["MembershipProofs"][k]["SignatureProofs"][i]
+    r = copy.deepcopy(rc); mp(r, 0, 1)["Challenge"] = zr_elem(zr_val(mp(r, 0, 1)["Challenge"]) ^ 2)
+    add("membership_challenge_bitflip", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 1, 0)["Value"] = zr_elem((zr_val(mp(r, 1, 0)["Value"]) + 1) % R)
+    add("membership_value", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 1, 1)["Hash"] = zr_elem((zr_val(mp(r, 1, 1)["Hash"]) + 1) % R)
+    add("membership_hash", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 0)["SigBlindingFactor"] = zr_elem((zr_val(mp(r, 0, 0)["SigBlindingFactor"]) + 1) % R)
+    add("membership_sig_bf", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 0)["Commitment"] = {"curve": 1, "element": b64(other_point(777))}
+    add("membership_commitment_field_replaced", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["MembershipProofs"][0]["Commitments"][1] = {"curve": 1, "element": b64(other_point(778))}
+    add("range_commitment_replaced", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 0)["Signature"]["R"] = {"curve": 1, "element": b64(other_point(779))}
+    add("membership_signature_R_replaced", ins, outs, join_transfer(top, wf, r))
+    bad = bytearray(unb64(mp(rc, 0, 0)["Commitment"]["element"])); bad[63] ^= 1
+    r = copy.deepcopy(rc); mp(r, 0, 0)["Commitment"]["element"] = b64(bytes(bad))
+    add("g1_off_curve", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 1, 0)["Commitment"]["element"] = b64(b"\x40" + bytes(63))
+    add("g1_infinity_flag", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 1, 0)["Commitment"]["element"] = b64(bytes(64))
+    add("g1_all_zero_is_infinity", ins, outs, join_transfer(top, wf, r))
+    cb = unb64(mp(rc, 0, 1)["Commitment"]["element"])
+    y = int.from_bytes(cb[32:], "big")
+    r = copy.deepcopy(rc); mp(r, 0, 1)["Commitment"]["element"] = b64(cb[:32] + (y + C.P).to_bytes(32, "big"))
+    add("g1_noncanonical_y_accepts", ins, outs, join_transfer(top, wf, r))
+    x = int.from_bytes(cb[:32], "big")
+    ny = (-y) % C.P
+    flag = 0xC0 if y > ny else 0x80
+    comp = bytes([flag | cb[0]]) + cb[1:32]
+    r = copy.deepcopy(rc); mp(r, 0, 1)["Commitment"]["element"] = b64(comp)
+    add("g1_compressed_accepts", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 1)["Commitment"]["element"] = b64(bytes([cb[0] | (0xC0 if flag == 0x80 else 0x80)]) + cb[1:32])
+    add("g1_compressed_wrong_root", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); del r["MembershipProofs"][0]["SignatureProofs"][1]
+    add("range_sigproofs_length", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc)
+    for k in range(2):
+        del r["MembershipProofs"][k]["SignatureProofs"][1]
+        del r["MembershipProofs"][k]["Commitments"][1]
+    add("range_exponent_mismatch", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["MembershipProofs"][1]["SignatureProofs"][0] = None
+    add("range_null_sigproof_panics", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["MembershipProofs"][1] = None
+    add("range_null_membership", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); r["MembershipProofs"] = r["MembershipProofs"][:1]
+    add("range_too_few_membership", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 0)["Value"] = None
+    add("membership_null_value", ins, outs, join_transfer(top, wf, r))
+    r = copy.deepcopy(rc); mp(r, 0, 0)["Value"] = {"curve": 1}
+    add("membership_value_missing_element_is_zero", ins, outs, join_transfer(top, wf, r))
+    t2 = dict(top); t2["RangeCorrectness"] = None
+    add("range_null_for_2out", ins, outs, jdump(t2))
+    # ownership transfer ignores the range proof (transfer.go:70-72)
+    t5, w5, _ = split_transfer(p5)
+    t5b = dict(t5); t5b["RangeCorrectness"] = b64(b"garbage{{")
+    add("ownership_ignores_garbage_range", i5, o5, jdump(t5b))
+    add("ownership_wrong_output", i5, [C.g1_mul(C.G1_GEN, 99)], p5)
+
+    # issues (issue/issue_test.go:26-35)
+    for k, (vals, anon) in enumerate([([10, 20], False), ([9999], False), ([5, 6, 7], True)]):
+        wit = [(v, rnd.zr("is%d/bf/%d" % (k, i))) for i, v in enumerate(vals)]
+        toks = [Z.token_commitment(pp, "ABC", v, b) for v, b in wit]
+        ip = Z.issue_prove(pp, rnd, toks, wit, "ABC", anonymous=anon, tag="issue%d" % k)
+        add("issue_valid_%d%s" % (k, "_anon" if anon else ""), [], toks, ip, kind="issue", anonymous=anon)
+        if k == 0:
+            top_i = jload(ip)
+            wfi = jload(unb64(top_i["WellFormedness"]))
+            wfi["TypeInTheClear"] = "XYZ"
+            ti = dict(top_i); ti["WellFormedness"] = b64(jdump(wfi))
+            add("issue_wrong_type_in_clear", [], toks, jdump(ti), kind="issue")
+            rci = jload(unb64(top_i["RangeCorrectness"]))
+            rci["Challenge"] = zr_elem(zr_val(rci["Challenge"]) ^ 1)
+            ti = dict(top_i); ti["RangeCorrectness"] = b64(jdump(rci))
+            add("issue_range_challenge", [], toks, jdump(ti), kind="issue")
+            add("issue_as_anonymous_mismatch", [], toks, ip, kind="issue", anonymous=True)
+    # value out of range: the prover refuses (transfer_test.go:74-84)
+    try:
+        transfer_case(pp, rnd, "toor", [10000, 0], [10000, 0])
+        raise AssertionError("prover accepted an out-of-range value")
+    except ValueError:
+        pass
+    out["pp_a"] = {"base": 100, "exponent": 2, "pp": pp.to_json().decode(), "cases": cases}
+
+    # ---------------------------------------------------------------- PP-B (64-bit-class)
+    if os.environ.get("GOLDEN_PPB", "1") == "1":
+        ppb, rndb = make_pp(16, 16, b"golden-pp-B")
+        pp_save = pp
+        pp = ppb
+        cases = []
+        ib_, ob_, pb_ = transfer_case(ppb, rndb, "b0", [2 ** 62, 12345], [2 ** 61, 2 ** 61 + 12345])
+        add("ppb_valid_2in_2out", ib_, ob_, pb_)
+        top_b, wf_b, rc_b = split_transfer(pb_)
+        r = copy.deepcopy(rc_b)
+        r["MembershipProofs"][1]["SignatureProofs"][15]["Challenge"] = zr_elem(
+            zr_val(r["MembershipProofs"][1]["SignatureProofs"][15]["Challenge"]) ^ 1)
+        add("ppb_membership_last_digit", ib_, ob_, join_transfer(top_b, wf_b, r))
+        out["pp_b"] = {"base": 16, "exponent": 16, "pp": ppb.to_json().decode(), "cases": cases}
+        pp = pp_save
+
+    path = os.path.join(HERE, "zkatdlog_golden.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

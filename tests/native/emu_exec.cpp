@@ -1,0 +1,155 @@
+// TEST-ONLY: runs the product's planner (host/planner.cpp) and the device job
+// functions (dev/jobs.h) on the CPU, in the same order as the HIP kernels in
+// runtime.hip, so the CPU test tier can check the complete verification
+// pipeline against the Python oracle without a GPU.  The product library
+// (libftsamd.so) contains no CPU execution path; this file is never part of it.
+#include <string.h>
+
+#include <thread>
+#include <vector>
+
+#include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
+#include "../../fabric-token-sdk_amd/csrc/host/planner.h"
+#include "../../include/ftsamd.h"
+
+using namespace fts;
+using namespace ftsh;
+
+struct EmuCtx {
+  PPInfo pp;
+  std::vector<uint8_t> const_bytes;
+  std::vector<G1Dev> g1tab;
+  std::vector<G2Dev> g2tab;
+  std::vector<LineCoef> qlines;
+};
+
+template <class F>
+static void par_for(uint32_t n, F f) {
+  unsigned t = std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  for (unsigned k = 0; k < t; k++)
+    th.emplace_back([&, k]() {
+      for (uint32_t i = k; i < n; i += t) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+extern "C" {
+
+void* emu_ctx_create(const uint8_t* pp, size_t len, char* err, size_t errlen) {
+  EmuCtx* c = new EmuCtx();
+  std::string e = parse_pp(pp, len, "zkatdlog", c->pp);
+  if (!e.empty()) {
+    snprintf(err, errlen, "%s", e.c_str());
+    delete c;
+    return nullptr;
+  }
+  std::vector<uint8_t> raw;
+  std::vector<uint32_t> g1off, g2off;
+  auto push = [&](const std::vector<uint8_t>& v, size_t need, std::vector<uint32_t>& offs) {
+    offs.push_back((uint32_t)raw.size());
+    std::vector<uint8_t> t = v;
+    t.resize(std::max(need, v.size()), 0);
+    raw.insert(raw.end(), t.begin(), t.end());
+  };
+  push(c->pp.pedgen, 64, g1off);
+  for (int k = 0; k < 3; k++) push(c->pp.ped[k], 64, g1off);
+  std::vector<uint8_t> gen(64, 0);
+  gen[31] = 1;
+  gen[63] = 2;
+  push(gen, 64, g1off);
+  for (int k = 0; k < 3; k++) push(c->pp.pk[k], 128, g2off);
+  push(c->pp.q, 128, g2off);
+  std::vector<G1Dev> g1(5);
+  std::vector<G2Dev> g2(4);
+  std::vector<uint8_t> g1b(64 * 5), g2b(128 * 4);
+  for (int i = 0; i < 5; i++) {
+    DecodeJob j{g1off[i], 64, (uint32_t)i, NONE, NONE};
+    if (!job_decode(j, raw.data(), g1.data(), nullptr)) {
+      snprintf(err, errlen, "bad G1 in PP");
+      delete c;
+      return nullptr;
+    }
+    g1_to_bytes(&g1b[64 * i], g1_load(g1[i]));
+  }
+  for (int k = 0; k < 4; k++)
+    if (!decode_g2(&raw[g2off[k]], 128, g2[k], &g2b[128 * k])) {
+      snprintf(err, errlen, "bad G2 in PP");
+      delete c;
+      return nullptr;
+    }
+  c->const_bytes.assign(C_SIZE, 0);
+  memcpy(&c->const_bytes[C_PEDGEN], &g1b[0], 64);
+  memcpy(&c->const_bytes[C_PED0], &g1b[64], 192);
+  memcpy(&c->const_bytes[C_Q_PK], &g2b[384], 128);
+  memcpy(&c->const_bytes[C_Q_PK + 128], &g2b[0], 384);
+  memcpy(&c->const_bytes[C_PK_Q + 384], &g2b[384], 128);
+  std::vector<G1Dev> hb(5);
+  hb[G1B_PED0] = g1[1];
+  hb[G1B_PED1] = g1[2];
+  hb[G1B_PED2] = g1[3];
+  hb[G1B_PEDGEN] = g1[0];
+  hb[G1B_GEN] = g1[4];
+  uint32_t n1 = G1B_COUNT * TAB_WINDOWS * TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
+  c->g1tab.resize(n1);
+  c->g2tab.resize(n2);
+  par_for(n1, [&](uint32_t i) { job_tab_g1(i, hb.data(), c->g1tab.data()); });
+  par_for(n2, [&](uint32_t i) { job_tab_g2(i, g2.data(), c->g2tab.data()); });
+  c->qlines.resize(MILLER_LINES);
+  precompute_lines(c->qlines.data(), g2_load(g2[3]));
+  return c;
+}
+
+void emu_ctx_destroy(void* c) { delete (EmuCtx*)c; }
+
+static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
+  memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
+  std::vector<uint8_t> wire = p.wire;
+  wire.resize(wire.size() + 64, 0);
+  std::vector<G1Dev> pts(std::max<uint32_t>(p.n_pts, 1));
+  std::vector<uint8_t> pt_ok(std::max<uint32_t>(p.n_pts, 1), 1);
+  std::vector<uint32_t> scalv(8 * (size_t)std::max<uint32_t>(p.n_scal, 1));
+  uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(scalv.data());
+  std::vector<uint8_t> canon(std::max<uint32_t>(p.n_scal, 1));
+  std::vector<G1Dev> g1out(std::max<uint32_t>(p.n_g1out, 1));
+  std::vector<G2Dev> g2out(std::max<uint32_t>(p.n_g2out, 1));
+  std::vector<F12Dev> fbuf(std::max<size_t>(p.pr.size(), 1));
+  std::vector<uint8_t> hok(std::max<size_t>(p.hmain.size(), 1)), hpok(std::max<size_t>(p.hpre.size(), 1));
+  // same order as ftz_batch_run
+  par_for((uint32_t)p.dec.size(), [&](uint32_t i) { pt_ok[p.dec[i].out] = job_decode(p.dec[i], wire.data(), pts.data(), p.arena.data()); });
+  par_for((uint32_t)p.zr.size(), [&](uint32_t i) { job_zr(p.zr[i], wire.data(), scal, canon.data()); });
+  par_for((uint32_t)p.hpre.size(), [&](uint32_t i) { hpok[i] = job_hash(p.hpre[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  par_for((uint32_t)p.sc.size(), [&](uint32_t i) { job_scalar(p.sc[i], scal, p.sclist.data()); });
+  par_for((uint32_t)p.g1.size(), [&](uint32_t i) {
+    job_g1(p.g1[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
+  });
+  par_for((uint32_t)p.g2.size(), [&](uint32_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
+    job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), i);
+  });
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data()); });
+  par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  for (size_t i = 0; i < n; i++) codes[i] = job_verdict(p.tx[i], p.ck.data(), pt_ok.data(), hok.data());
+}
+
+int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* codes) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<TransferIn> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+  Plan p;
+  plan_transfers(c->pp, n, t.data(), p, 4);
+  run_plan(c, p, n, codes);
+  return 0;
+}
+
+int emu_verify_issues(void* ctx, size_t n, const ftz_issue* is, int32_t* codes) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<IssueIn> t(n);
+  for (size_t i = 0; i < n; i++) t[i] = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
+  Plan p;
+  plan_issues(c->pp, n, t.data(), p, 4);
+  run_plan(c, p, n, codes);
+  return 0;
+}
+}

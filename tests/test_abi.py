@@ -1,0 +1,46 @@
+"""CPU: the C-ABI library loads and exports every symbol include/ftsamd.h
+declares (no compute calls here -- there is no GPU in the CPU tier)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from zkatdlog import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    src = open(os.path.join(ROOT, "include", "ftsamd.h")).read()
+    return sorted(set(re.findall(r"\b(ftz_[a-z_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_list():
+    assert declared() == sorted(_abi.SYMBOLS)
+
+
+def test_library_exports_all_symbols():
+    if not os.path.exists(_abi.LIB_PATH):
+        pytest.skip("libftsamd.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_abi.LIB_PATH)
+    missing = [s for s in declared() if not hasattr(lib, s)]
+    assert not missing
+
+
+def test_codes_match_header():
+    src = open(os.path.join(ROOT, "include", "ftsamd.h")).read()
+    for name in ("FTZ_OK", "FTZ_ERR_PARSE", "FTZ_ERR_MALFORMED", "FTZ_ERR_WF", "FTZ_ERR_RANGE",
+                 "FTZ_ERR_MEMBERSHIP", "FTZ_ERR_PANIC"):
+        m = re.search(r"#define %s (\d+)" % name, src)
+        assert m and int(m.group(1)) == getattr(_abi, name)
+    from ftsoracle import zkat as Z
+    assert (Z.OK, Z.ERR_PARSE, Z.ERR_MALFORMED, Z.ERR_WF, Z.ERR_RANGE, Z.ERR_MEMBERSHIP, Z.ERR_PANIC) == \
+        (0, 1, 2, 3, 4, 5, 6)
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(_abi, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(_abi, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _abi.load()

@@ -1,0 +1,106 @@
+"""CPU: the product's device code (dev/*.h job functions) and host planner,
+compiled for the host by the TEST-ONLY emulation library, against the oracle.
+This is how the CPU tier checks the GPU formulas; the product library itself
+has no CPU path."""
+import ctypes
+import hashlib
+import random
+
+import pytest
+
+from conftest import case_tuple
+from ftsoracle import bn254 as C
+from zkatdlog import _abi as A
+
+
+def buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def test_field_ops(emu):
+    rng = random.Random(7)
+    for _ in range(100):
+        x, y = rng.randrange(C.P), rng.randrange(C.P)
+        o = buf(32)
+        emu.emu_fp_mul(x.to_bytes(32, "big"), y.to_bytes(32, "big"), o)
+        assert int.from_bytes(o.raw, "big") == x * y % C.P
+        emu.emu_fp_inv(x.to_bytes(32, "big"), o)
+        assert int.from_bytes(o.raw, "big") == pow(x, C.P - 2, C.P)
+        a, b = rng.randrange(1 << 256), rng.randrange(C.R)
+        emu.emu_fr_mul(a.to_bytes(32, "big"), b.to_bytes(32, "big"), o)
+        assert int.from_bytes(o.raw, "big") == a * b % C.R
+
+
+def test_group_ops(emu):
+    rng = random.Random(8)
+    for _ in range(8):
+        k = rng.randrange(1 << 256)
+        P = C.g1_mul(C.G1_GEN, rng.randrange(C.R))
+        o = buf(64)
+        assert emu.emu_g1_mul(C.g1_bytes(P), k.to_bytes(32, "big"), o) == 0
+        assert o.raw == C.g1_bytes(C.g1_mul(P, k))
+    for _ in range(3):
+        k = rng.randrange(1 << 256)
+        Q = C.g2_mul(C.G2_GEN, rng.randrange(C.R))
+        o = buf(128)
+        assert emu.emu_g2_mul(C.g2_bytes(Q), k.to_bytes(32, "big"), o) == 0
+        assert o.raw == C.g2_bytes(C.g2_mul(Q, k))
+
+
+def test_sha256_and_hash_to_zr(emu):
+    for data in [b"", b"abc", bytes(range(256)) * 3, b"a" * 55, b"a" * 56, b"a" * 64, b"x" * 1451]:
+        o, m = buf(32), buf(32)
+        emu.emu_sha256(data, len(data), o, m)
+        assert o.raw == hashlib.sha256(data).digest()
+        assert int.from_bytes(m.raw, "big") == C.hash_to_zr(data)
+
+
+def test_pairing_gt_bytes(emu):
+    P, Q = C.g1_mul(C.G1_GEN, 12345), C.g2_mul(C.G2_GEN, 6789)
+    o = buf(384)
+    emu.emu_pairing(C.g1_bytes(P), C.g2_bytes(Q), o)
+    assert o.raw == C.gt_bytes(C.pairing(P, Q))
+    P2, Q2, Qf = C.g1_mul(C.G1_GEN, 7), C.g2_mul(C.G2_GEN, 9), C.g2_mul(C.G2_GEN, 31337)
+    emu.emu_pairing2_fixed(C.g2_bytes(Qf), C.g1_bytes(P), C.g1_bytes(P2), C.g2_bytes(Q2), o)
+    assert o.raw == C.gt_bytes(C.final_exp(C.miller_loop([(P, Qf), (P2, Q2)])))
+    # infinity on the fixed pair contributes 1
+    emu.emu_pairing2_fixed(C.g2_bytes(Qf), bytes(64), C.g1_bytes(P2), C.g2_bytes(Q2), o)
+    assert o.raw == C.gt_bytes(C.pairing(P2, Q2))
+
+
+def _run(emu, pp_json, cases):
+    err = ctypes.create_string_buffer(256)
+    ctx = emu.emu_ctx_create(pp_json, len(pp_json), err, 256)
+    assert ctx, err.value
+    try:
+        got = {}
+        tr = [c for c in cases if c["kind"] == "transfer"]
+        iss = [c for c in cases if c["kind"] == "issue"]
+        if tr:
+            arr, keep = A.pack_transfers([case_tuple(c) for c in tr])
+            codes = (ctypes.c_int32 * len(tr))()
+            emu.emu_verify_transfers(ctx, len(tr), arr, codes)
+            got.update({c["name"]: v for c, v in zip(tr, codes)})
+        if iss:
+            arr, keep = A.pack_issues([case_tuple(c) for c in iss])
+            codes = (ctypes.c_int32 * len(iss))()
+            emu.emu_verify_issues(ctx, len(iss), arr, codes)
+            got.update({c["name"]: v for c, v in zip(iss, codes)})
+        return got
+    finally:
+        emu.emu_ctx_destroy(ctx)
+
+
+def test_pipeline_golden_pp_a(emu, golden):
+    cases = golden["pp_a"]["cases"]
+    got = _run(emu, golden["pp_a"]["pp"].encode(), cases)
+    bad = {c["name"]: (got[c["name"]], c["expect"]) for c in cases if got[c["name"]] != c["expect"]}
+    assert not bad, bad
+
+
+def test_pipeline_golden_pp_b(emu, golden):
+    if "pp_b" not in golden:
+        pytest.skip("no PP-B fixtures")
+    cases = golden["pp_b"]["cases"]
+    got = _run(emu, golden["pp_b"]["pp"].encode(), cases)
+    assert got == {c["name"]: c["expect"] for c in cases}
