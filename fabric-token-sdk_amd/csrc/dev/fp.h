@@ -20,6 +20,14 @@
 #endif
 #include "constants.h"
 
+// Test-only instrumentation (host emulation build): counts Montgomery products.
+#ifdef FTS_COUNT_OPS
+extern thread_local unsigned long long fts_mont_count;
+#define FTS_COUNT_MUL() (++fts_mont_count)
+#else
+#define FTS_COUNT_MUL() ((void)0)
+#endif
+
 namespace fts {
 
 struct ModP {
@@ -138,6 +146,7 @@ FTS_HD Fe<M> fe_dbl(const Fe<M>& a) {
 // Montgomery multiplication, CIOS, 32-bit limbs.  Inputs < m, output < m.
 template <class M>
 FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  FTS_COUNT_MUL();
   uint32_t t[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) t[i] = 0;

@@ -141,12 +141,23 @@ class Batch:
         self.close()
 
 
+def _commitments(xs):
+    """A list of 64-byte G1 RawBytes, or their concatenation."""
+    if isinstance(xs, (bytes, bytearray, memoryview)):
+        b = bytes(xs)
+    else:
+        b = b"".join(bytes(x) for x in xs)
+    if len(b) % 64:
+        raise ValueError("commitments must be 64-byte G1 RawBytes")
+    return b
+
+
 class TransferVerifier:
     """transfer.NewVerifier(inputs, outputs, pp) (transfer/transfer.go:66-77)."""
 
     def __init__(self, inputs, outputs, ctx):
-        self.inputs = b"".join(bytes(x) for x in inputs)
-        self.outputs = b"".join(bytes(x) for x in outputs)
+        self.inputs = _commitments(inputs)
+        self.outputs = _commitments(outputs)
         self.ctx = ctx
 
     def verify(self, proof):
@@ -160,7 +171,7 @@ class IssueVerifier:
     """issue.NewVerifier(tokens, anonymous, pp) (issue/issue.go:194-199)."""
 
     def __init__(self, tokens, anonymous, ctx):
-        self.tokens = b"".join(bytes(x) for x in tokens)
+        self.tokens = _commitments(tokens)
         self.anonymous = bool(anonymous)
         self.ctx = ctx
 

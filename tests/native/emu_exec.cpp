@@ -15,6 +15,10 @@
 using namespace fts;
 using namespace ftsh;
 
+#ifdef FTS_COUNT_OPS
+thread_local unsigned long long fts_mont_count = 0;
+#endif
+
 struct EmuCtx {
   PPInfo pp;
   std::vector<uint8_t> const_bytes;
@@ -131,6 +135,50 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   for (size_t i = 0; i < n; i++) codes[i] = job_verdict(p.tx[i], p.ck.data(), pt_ok.data(), hok.data());
 }
+
+#ifdef FTS_COUNT_OPS
+// Montgomery products per pipeline stage (decode, zr, hash_pre, scalar, g1,
+// g2, miller, fexp, hash, verdict) for a batch, single-threaded.
+int emu_opcount_transfers(void* ctx, size_t n, const ftz_transfer* tx, unsigned long long* per_stage,
+                          unsigned long long* jobs) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<TransferIn> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+  Plan p;
+  plan_transfers(c->pp, n, t.data(), p, 1);
+  memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
+  std::vector<uint8_t> wire = p.wire;
+  wire.resize(wire.size() + 64, 0);
+  std::vector<G1Dev> pts(std::max<uint32_t>(p.n_pts, 1));
+  std::vector<uint8_t> pt_ok(std::max<uint32_t>(p.n_pts, 1), 1);
+  std::vector<uint32_t> scalv(8 * (size_t)std::max<uint32_t>(p.n_scal, 1));
+  uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(scalv.data());
+  std::vector<uint8_t> canon(std::max<uint32_t>(p.n_scal, 1));
+  std::vector<G1Dev> g1out(std::max<uint32_t>(p.n_g1out, 1));
+  std::vector<G2Dev> g2out(std::max<uint32_t>(p.n_g2out, 1));
+  std::vector<F12Dev> fbuf(std::max<size_t>(p.pr.size(), 1));
+  std::vector<uint8_t> hok(std::max<size_t>(p.hmain.size(), 1));
+  auto stage = [&](int k, size_t nj, auto fn) {
+    unsigned long long c0 = fts_mont_count;
+    for (size_t i = 0; i < nj; i++) fn(i);
+    per_stage[k] = fts_mont_count - c0;
+    jobs[k] = nj;
+  };
+  stage(0, p.dec.size(), [&](size_t i) { pt_ok[p.dec[i].out] = job_decode(p.dec[i], wire.data(), pts.data(), p.arena.data()); });
+  stage(1, p.zr.size(), [&](size_t i) { job_zr(p.zr[i], wire.data(), scal, canon.data()); });
+  stage(2, p.hpre.size(), [&](size_t i) { job_hash(p.hpre[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  stage(3, p.sc.size(), [&](size_t i) { job_scalar(p.sc[i], scal, p.sclist.data()); });
+  stage(4, p.g1.size(), [&](size_t i) { job_g1(p.g1[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data()); });
+  stage(5, p.g2.size(), [&](size_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
+  stage(6, p.pr.size(), [&](size_t i) { job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), (uint32_t)i); });
+  stage(7, p.pr.size(), [&](size_t i) { job_fexp(p.pr[i], fbuf.data(), (uint32_t)i, p.arena.data()); });
+  stage(8, p.hmain.size(), [&](size_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  per_stage[9] = 0;
+  jobs[9] = n;
+  return 0;
+}
+#endif
 
 int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* codes) {
   EmuCtx* c = (EmuCtx*)ctx;

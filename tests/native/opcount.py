@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""TEST-ONLY: count Montgomery products per GPU job type with the host
+emulation build (-DFTS_COUNT_OPS) on the bench workload; writes
+profiles/opcounts.json (the algorithmic-work figure bench.py's roofline uses)."""
+import base64
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
+from zkatdlog import _abi as A  # noqa: E402
+
+NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "hash", "verdict"]
+
+
+def main():
+    lib = "/tmp/libftsemu_count.so"
+    srcs = ["tests/native/emu.cpp", "tests/native/emu_exec.cpp", "fabric-token-sdk_amd/csrc/host/planner.cpp",
+            "fabric-token-sdk_amd/csrc/host/gojson.cpp"]
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-pthread",
+                    "-DFTS_COUNT_OPS"] + [os.path.join(ROOT, s) for s in srcs] + ["-o", lib], check=True)
+    L = ctypes.CDLL(lib)
+    L.emu_ctx_create.restype = ctypes.c_void_p
+    L.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))
+    out = {}
+    for key, sel in (("pp_a", None), ("pp_b", "ppb_valid_2in_2out")):
+        pp = g[key]["pp"].encode()
+        err = ctypes.create_string_buffer(200)
+        ctx = L.emu_ctx_create(pp, len(pp), err, 200)
+        if key == "pp_a":
+            bs = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_transfers.json")))["transfers"]
+            items = [(bytes.fromhex(t["inputs"]), bytes.fromhex(t["outputs"]), base64.b64decode(t["proof"]))
+                     for t in bs]
+        else:
+            c = [x for x in g[key]["cases"] if x["name"] == sel][0]
+            items = [(bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"]))]
+        arr, keep = A.pack_transfers(items)
+        ps, js = (ctypes.c_ulonglong * 10)(), (ctypes.c_ulonglong * 10)()
+        L.emu_opcount_transfers(ctypes.c_void_p(ctx), len(items), arr, ps, js)
+        out[key] = {"transfers": len(items),
+                    "m_per_tx": sum(ps) / len(items),
+                    "m_per_job": {n: (ps[i] / js[i] if js[i] else 0) for i, n in enumerate(NAMES)},
+                    "jobs_per_tx": {n: js[i] / len(items) for i, n in enumerate(NAMES)}}
+        print(key, json.dumps(out[key]))
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "profiles", "opcounts.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
