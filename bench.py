@@ -55,7 +55,7 @@ def cpu_baseline(pp_json, items, expect, seconds=15.0):
     same workload on all host cores (one process per core)."""
     from concurrent.futures import ProcessPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
-    cores = min(os.cpu_count() or 1, int(os.environ.get("FTS_CPU_BASELINE_CORES", "64")))
+    cores = min(os.cpu_count() or 1, int(os.environ.get("FTS_CPU_BASELINE_CORES", "16")))
     # one proof takes ~1-1.5 s in the pure-Python oracle: size the sample to ~seconds * cores
     n = max(cores, int(seconds * cores / 1.3))
     sample = [(pp_json, items[i], expect[i]) for i in range(min(n, len(items)))]
