@@ -19,6 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build", "obj")
 LIB = os.path.join(HERE, "zkatdlog", "_lib", "libftsamd.so")
 MADPEAK = os.path.join(HERE, "zkatdlog", "_lib", "libftsmadpeak.so")
+FPCHECK = os.path.join(HERE, "zkatdlog", "_lib", "libftsfpcheck.so")
 ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH]
@@ -64,11 +65,12 @@ def build(jobs=8, force=False, verbose=True):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
-    src = os.path.join(CSRC, "tools", "madpeak.hip")
-    if force or not os.path.exists(MADPEAK) or os.path.getmtime(MADPEAK) < os.path.getmtime(src):
-        r = subprocess.run([HIPCC] + FLAGS + ["-shared", src, "-o", MADPEAK], capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError("madpeak build failed:\n" + r.stderr)
+    for src, out in ((os.path.join(CSRC, "tools", "madpeak.hip"), MADPEAK),
+                     (os.path.join(CSRC, "tools", "fpcheck.hip"), FPCHECK)):
+        if force or not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(src), hdr_time):
+            r = subprocess.run([HIPCC] + FLAGS + ["-shared", src, "-o", out], capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError("tool build failed:\n" + r.stderr)
     if verbose:
         print("built", LIB)
     return LIB

@@ -143,10 +143,24 @@ FTS_HD Fe<M> fe_dbl(const Fe<M>& a) {
   return a + a;
 }
 
+#include "fp_fips.h"
+
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class M>
+__device__ __forceinline__ Fe<M> mont_mul_fips(const Fe<M>& a, const Fe<M>& b) {
+  Fe<M> x, y;
+  mont_mul_fips_limbs<M>(x.v, a.v, b.v);
+  uint32_t pm[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) pm[j] = M::m[j];
+  uint32_t br = sub8(y.v, x.v, pm);
+  return br ? x : y;
+}
+#endif
+
 // Montgomery multiplication, CIOS, 32-bit limbs.  Inputs < m, output < m.
 template <class M>
-FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
-  FTS_COUNT_MUL();
+FTS_HD Fe<M> mont_mul_cios(const Fe<M>& a, const Fe<M>& b) {
   uint32_t t[10];
 #pragma unroll
   for (int i = 0; i < 10; i++) t[i] = 0;
@@ -181,6 +195,20 @@ FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
   uint32_t br = sub8(u.v, r.v, mm);
   // t < 2m and m < 2^254, so t[8] == 0 here
   return br ? r : u;
+}
+
+#ifndef FTS_MUL_IMPL
+#define FTS_MUL_IMPL 1  // 0: CIOS in C, 1: FIPS with inline v_mad_u64_u32 (device)
+#endif
+
+template <class M>
+FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
+  FTS_COUNT_MUL();
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_MUL_IMPL == 1
+  return mont_mul_fips(a, b);
+#else
+  return mont_mul_cios(a, b);
+#endif
 }
 
 template <class M>

@@ -1,0 +1,105 @@
+// Device self-check and microbenchmark of the two Montgomery multipliers
+// (C CIOS vs inline-asm FIPS), used by tests/test_gpu.py and for tuning.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../dev/fp.h"
+
+using namespace fts;
+
+__device__ uint32_t xorshift(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return s;
+}
+
+template <class M>
+__device__ Fe<M> rnd_fe(uint32_t& s) {
+  Fe<M> x;
+  for (int i = 0; i < 8; i++) x.v[i] = xorshift(s);
+  x.v[7] &= 0x1FFFFFFFu;  // < 2^253 < m
+  return x;
+}
+
+template <class M>
+__global__ void k_fpcheck(uint32_t seed, uint32_t* bad) {
+  uint32_t s = seed ^ (blockIdx.x * blockDim.x + threadIdx.x) * 2654435761u;
+  if (!s) s = 1;
+  for (int it = 0; it < 64; it++) {
+    Fe<M> a = rnd_fe<M>(s), b = rnd_fe<M>(s);
+    if (it == 0) {  // edge: m-1 times m-1
+      for (int i = 0; i < 8; i++) a.v[i] = M::m[i];
+      a.v[0] -= 1;
+      b = a;
+    }
+    Fe<M> x = mont_mul_cios(a, b);
+#if defined(__HIP_DEVICE_COMPILE__)
+    Fe<M> y = mont_mul_fips(a, b);
+#else
+    Fe<M> y = x;  // host pass only parses the kernel body
+#endif
+    if (!fe_eq(x, y)) atomicAdd(bad, 1u);
+  }
+}
+
+template <int IMPL>
+__global__ void k_fpbench(fp* io, int iters) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  fp x = io[i], y = io[i + 1];
+  fp z = io[i + 2], w = io[i + 3];
+#pragma nounroll
+  for (int k = 0; k < iters; k++) {
+    if (IMPL == 0) {
+      x = mont_mul_cios(x, y);
+      z = mont_mul_cios(z, w);
+    } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+      x = mont_mul_fips(x, y);
+      z = mont_mul_fips(z, w);
+#endif
+    }
+  }
+  io[i] = x + z;
+}
+
+extern "C" int ftz_fpcheck(int device, uint32_t seed) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  uint32_t* bad;
+  if (hipMalloc(&bad, 8) != hipSuccess) return -1;
+  (void)hipMemset(bad, 0, 8);
+  k_fpcheck<ModP><<<256, 256>>>(seed, bad);
+  k_fpcheck<ModR><<<256, 256>>>(seed + 1, bad + 1);
+  uint32_t h[2] = {0, 0};
+  (void)hipMemcpy(h, bad, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(bad);
+  return (int)(h[0] + h[1]);
+}
+
+// returns Montgomery products per second for implementation impl (0 C, 1 asm)
+extern "C" double ftz_fpbench(int device, int impl, int iters, int waves_per_simd) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  int threads = 256, blocks = 256 * waves_per_simd;
+  size_t n = (size_t)threads * blocks + 4;
+  fp* io;
+  if (hipMalloc(&io, n * sizeof(fp)) != hipSuccess) return -1;
+  (void)hipMemset(io, 1, n * sizeof(fp));
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  for (int rep = 0; rep < 2; rep++) {
+    (void)hipEventRecord(e0);
+    if (impl == 0)
+      k_fpbench<0><<<blocks, threads>>>(io, iters);
+    else
+      k_fpbench<1><<<blocks, threads>>>(io, iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+  }
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipFree(io);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 2.0 * threads * blocks * (double)iters / (ms * 1e-3);
+}

@@ -91,3 +91,14 @@ def test_batch_4096_verdict_positions(zk, ctx_a, golden):
     st = b.stats()
     assert st["total"][0] > 0 and st["miller"][1] > 0
     b.close()
+
+
+def test_fp_multiplier_self_check():
+    """Inline-asm FIPS Montgomery product == C CIOS product on 2 x 4M random
+    inputs per field (p and r), including (m-1)^2."""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsfpcheck.so"))
+    lib.ftz_fpcheck.argtypes = [ctypes.c_int, ctypes.c_uint32]
+    assert lib.ftz_fpcheck(0, 12345) == 0
