@@ -182,16 +182,47 @@ FTS_HDN fp12 miller_1(const g1a& P, const g2a& Q) {
   return f;
 }
 
-// cyclotomic-subgroup squaring (Granger-Scott): valid after the easy part
-FTS_HD fp12 f12_cyclo_sqr(const fp12& a) { return f12_sqr(a); }
+// Cyclotomic-subgroup squaring (Granger-Scott, ePrint 2009/565 section 3.2):
+// valid only for elements of order dividing p^4 - p^2 + 1 (after the easy
+// part of the final exponentiation).  9 Fp2 squarings instead of 12 Fp2
+// multiplications.  Viewing Fp12 as three Fp4 = Fp2[t]/(t^2 - xi) pairs
+// (c0.c0, c1.c1), (c1.c0, c0.c2), (c0.c1, c1.c2).
+FTS_HDN fp12 f12_cyclo_sqr(const fp12& x) {
+  fp2 t0 = f2_sqr(x.c1.c1);
+  fp2 t1 = f2_sqr(x.c0.c0);
+  fp2 t6 = f2_sqr(x.c1.c1 + x.c0.c0) - t0 - t1;  // 2 x4 x0
+  fp2 t2 = f2_sqr(x.c0.c2);
+  fp2 t3 = f2_sqr(x.c1.c0);
+  fp2 t7 = f2_sqr(x.c0.c2 + x.c1.c0) - t2 - t3;  // 2 x2 x3
+  fp2 t4 = f2_sqr(x.c1.c2);
+  fp2 t5 = f2_sqr(x.c0.c1);
+  fp2 t8 = f2_mul_xi(f2_sqr(x.c1.c2 + x.c0.c1) - t4 - t5);  // 2 x5 x1 xi
+  t0 = f2_mul_xi(t0) + t1;  // x4^2 xi + x0^2
+  t2 = f2_mul_xi(t2) + t3;  // x2^2 xi + x3^2
+  t4 = f2_mul_xi(t4) + t5;  // x5^2 xi + x1^2
+  fp12 z;
+  z.c0.c0 = f2_dbl(t0 - x.c0.c0) + t0;
+  z.c0.c1 = f2_dbl(t2 - x.c0.c1) + t2;
+  z.c0.c2 = f2_dbl(t4 - x.c0.c2) + t4;
+  z.c1.c0 = f2_dbl(t8 + x.c1.c0) + t8;
+  z.c1.c1 = f2_dbl(t6 + x.c1.c1) + t6;
+  z.c1.c2 = f2_dbl(t7 + x.c1.c2) + t7;
+  return z;
+}
 
-// a^x, x = BN parameter (positive), a in the cyclotomic subgroup
+// BN parameter x in non-adjacent form (24 non-zero digits over 63 positions)
+static constexpr uint64_t BN_X_NAF_POS = 0x450a14044a890a01ull;
+static constexpr uint64_t BN_X_NAF_NEG = 0x0020815000200010ull;
+
+// a^x, x = BN parameter, a in the cyclotomic subgroup (a^-1 = conj(a))
 FTS_HDN fp12 f12_expt(const fp12& a) {
   fp12 r = a;
+  fp12 ai = f12_conj(a);
 #pragma nounroll
   for (int i = 61; i >= 0; i--) {
     r = f12_cyclo_sqr(r);
-    if ((BN_X >> i) & 1) r = r * a;
+    if ((BN_X_NAF_POS >> i) & 1) r = r * a;
+    if ((BN_X_NAF_NEG >> i) & 1) r = r * ai;
   }
   return r;
 }

@@ -31,6 +31,7 @@ void Plan::clear() {
   sclist.clear();
   vt.clear();
   g1.clear();
+  g1p.clear();
   g2.clear();
   pr.clear();
   seg.clear();
@@ -211,7 +212,7 @@ class Builder {
     return (uint32_t)pl.seg.size() - 1;
   }
   uint32_t g1job(std::initializer_list<std::pair<uint8_t, uint32_t>> fixed, const std::vector<VTerm>& var,
-                 uint32_t vscal, uint32_t bytes) {
+                 uint32_t vscal, uint32_t bytes, bool feeds_pairing = false) {
     G1Job j;
     memset(&j, 0, sizeof(j));
     j.nfix = 0;
@@ -227,7 +228,7 @@ class Builder {
     j.vneg = 1;
     j.out = pl.n_g1out++;
     j.bytes = bytes;
-    pl.g1.push_back(j);
+    (feeds_pairing ? pl.g1p : pl.g1).push_back(j);
     return j.out;
   }
   static VTerm vterm(uint32_t pt, uint64_t w = 1) {
@@ -506,7 +507,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
       // G1 commitment: v*Ped0 + cb*Ped1 - c*Commitments[k][i]
       g1job({{G1B_PED0, sc_v}, {G1B_PED1, sc_cb}}, {vterm(com_pt[k][i])}, sc_ch, d.slot + 64);
       // P1 = sigbf*P - c*S   (pairs with Q)
-      uint32_t p1 = g1job({{G1B_PEDGEN, sc_sb}}, {vterm(d.S)}, sc_ch, NONE);
+      uint32_t p1 = g1job({{G1B_PEDGEN, sc_sb}}, {vterm(d.S)}, sc_ch, NONE, true);
       // t' = c*PK0 + v*PK1 + h*PK2   (pairs with R)
       G2Job g2;
       memset(&g2, 0, sizeof(g2));
@@ -815,13 +816,15 @@ void merge(Plan& a, const Plan& b) {
     v.pt += o_pts;
     a.vt.push_back(v);
   }
-  for (G1Job j : b.g1) {
-    for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
-    j.vstart += o_vt;
-    j.vscal = rel(j.vscal, o_scal);
-    j.out += o_g1;
-    j.bytes = rel(j.bytes, o_arena);
-    a.g1.push_back(j);
+  for (int side = 0; side < 2; side++) {
+    for (G1Job j : (side ? b.g1p : b.g1)) {
+      for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
+      j.vstart += o_vt;
+      j.vscal = rel(j.vscal, o_scal);
+      j.out += o_g1;
+      j.bytes = rel(j.bytes, o_arena);
+      (side ? a.g1p : a.g1).push_back(j);
+    }
   }
   for (G2Job j : b.g2) {
     for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;

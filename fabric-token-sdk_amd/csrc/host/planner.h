@@ -45,7 +45,8 @@ struct Plan {
   std::vector<ScalJob> sc;
   std::vector<uint32_t> sclist;
   std::vector<VTerm> vt;
-  std::vector<G1Job> g1;
+  std::vector<G1Job> g1;   // G1 jobs independent of the pairings
+  std::vector<G1Job> g1p;  // G1 jobs whose outputs feed the Miller loops
   std::vector<G2Job> g2;
   std::vector<PairJob> pr;
   std::vector<Seg> seg;

@@ -60,7 +60,7 @@ struct DBuf {
 
 struct ftz_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr, stream2 = nullptr;
   PPInfo pp;
   std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
   DBuf<G1Dev> g1tab;
@@ -80,7 +80,7 @@ struct ftz_batch {
   DBuf<ScalJob> sc;
   DBuf<uint32_t> sclist;
   DBuf<VTerm> vt;
-  DBuf<G1Job> g1;
+  DBuf<G1Job> g1, g1p;
   DBuf<G2Job> g2;
   DBuf<PairJob> pr;
   DBuf<Seg> seg;
@@ -93,7 +93,7 @@ struct ftz_batch {
   DBuf<F12Dev> fbuf;
   DBuf<int32_t> codes;
   DBuf<uint32_t> bitmap;
-  hipEvent_t ev[FTZ_NKERNELS + 1];
+  hipEvent_t ev[14];
   bool ev_init = false;
   ftz_stats stats;
 };
@@ -124,7 +124,8 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
     delete c;
     return set_err(FTZ_E_PP, e);
   }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
   }
@@ -239,6 +240,7 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   c->g1tab.alloc(0);
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -271,6 +273,7 @@ static int batch_upload(ftz_batch* b) {
   HC(b->sclist.upload(p.sclist, s));
   HC(b->vt.upload(p.vt, s));
   HC(b->g1.upload(p.g1, s));
+  HC(b->g1p.upload(p.g1p, s));
   HC(b->g2.upload(p.g2, s));
   HC(b->pr.upload(p.pr, s));
   HC(b->seg.upload(p.seg, s));
@@ -292,7 +295,7 @@ static int batch_upload(ftz_batch* b) {
   HC(hipMemsetAsync(b->pt_ok.p, 1, std::max<uint32_t>(p.n_pts, 1), s));
   HC(hipStreamSynchronize(s));
   if (!b->ev_init) {
-    for (int k = 0; k <= FTZ_NKERNELS; k++) HC(hipEventCreate(&b->ev[k]));
+    for (int k = 0; k < 14; k++) HC(hipEventCreate(&b->ev[k]));
     b->ev_init = true;
   }
   return FTZ_SUCCESS;
@@ -343,62 +346,78 @@ extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, 
   return FTZ_SUCCESS;
 }
 
+// Two streams: the chain that feeds the pairings (G1 jobs of P1 = sbf*P - c*S,
+// G2, Miller, final exponentiation) runs on the main stream while the G1 jobs
+// that do not feed a pairing (well-formedness, range equality, membership
+// Schnorr commitments) run concurrently on a side stream, filling the SIMDs the
+// pairing kernels leave idle; the transcript hashes wait for both.
 extern "C" int ftz_batch_run(ftz_batch* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null batch");
   ftz_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
-  hipStream_t s = c->stream;
+  hipStream_t s = c->stream, s2 = c->stream2;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
-  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g2 = (uint32_t)p.g2.size(), n_pr = (uint32_t)p.pr.size();
+  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
+  uint32_t n_pr = (uint32_t)p.pr.size();
   uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
-  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1, n_g2, n_pr, n_pr, n_hm, n_tx, 0};
+  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1, n_hm, n_tx, n_tx};
+  hipEvent_t* e = b->ev;
   HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
-  HC(hipEventRecord(b->ev[0], s));
+  HC(hipEventRecord(e[0], s));
   if (n_dec) k_decode<<<blocks_for(n_dec, 256), 256, 0, s>>>(b->dec.p, n_dec, b->wire.p, b->pts.p, b->pt_ok.p, b->arena.p);
-  HC(hipEventRecord(b->ev[1], s));
+  HC(hipEventRecord(e[1], s));
   if (n_zr) k_zr<<<blocks_for(n_zr, 256), 256, 0, s>>>(b->zr.p, n_zr, b->wire.p, scal, b->canon.p);
-  HC(hipEventRecord(b->ev[2], s));
+  HC(hipEventRecord(e[2], s));
   if (n_hp)
     k_hash<<<blocks_for(n_hp, 128), 128, 0, s>>>(b->hpre.p, n_hp, b->seg.p, b->arena.p, scal, b->canon.p,
                                                  b->hash_ok_pre.p);
-  HC(hipEventRecord(b->ev[3], s));
+  HC(hipEventRecord(e[3], s));
   if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
-  HC(hipEventRecord(b->ev[4], s));
+  HC(hipEventRecord(e[4], s));
+  // side stream: pairing-independent G1 jobs
+  HC(hipStreamWaitEvent(s2, e[4], 0));
+  HC(hipEventRecord(e[11], s2));
   if (n_g1)
-    k_g1<<<blocks_for(n_g1, 128), 128, 0, s>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
-                                               b->arena.p);
-  HC(hipEventRecord(b->ev[5], s));
+    k_g1<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
+                                                b->arena.p);
+  HC(hipEventRecord(e[12], s2));
+  // main stream: pairing chain
+  if (n_g1p)
+    k_g1<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
+                                                b->arena.p);
+  HC(hipEventRecord(e[5], s));
   if (n_g2) k_g2<<<blocks_for(n_g2, 128), 128, 0, s>>>(b->g2.p, n_g2, scal, c->g2tab.p, b->g2out.p);
-  HC(hipEventRecord(b->ev[6], s));
+  HC(hipEventRecord(e[6], s));
   if (n_pr)
     k_miller<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->g1out.p, b->pts.p, b->g2out.p,
                                                  b->fbuf.p);
-  HC(hipEventRecord(b->ev[7], s));
+  HC(hipEventRecord(e[7], s));
   if (n_pr) k_fexp<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
-  HC(hipEventRecord(b->ev[8], s));
+  HC(hipEventRecord(e[8], s));
+  HC(hipStreamWaitEvent(s, e[12], 0));
+  HC(hipEventRecord(e[9], s));
   if (n_hm)
     k_hash<<<blocks_for(n_hm, 128), 128, 0, s>>>(b->hmain.p, n_hm, b->seg.p, b->arena.p, scal, b->canon.p,
                                                  b->hash_ok.p);
-  HC(hipEventRecord(b->ev[9], s));
+  HC(hipEventRecord(e[10], s));
   if (n_tx)
     k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
                                                     b->bitmap.p);
-  HC(hipEventRecord(b->ev[10], s));
+  HC(hipEventRecord(e[13], s));
   HC(hipGetLastError());
   HC(hipStreamSynchronize(s));
-  for (int k = 0; k < 10; k++) {
+  // stats order: decode zr hash_pre scalar g1p g2 miller fexp g1(side) hash verdict total
+  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 5, 6, 7, 11, 9, 10, 0};
+  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 6, 7, 8, 12, 10, 13, 13};
+  for (int k = 0; k < FTZ_NKERNELS; k++) {
     float ms = 0;
-    HC(hipEventElapsedTime(&ms, b->ev[k], b->ev[k + 1]));
+    HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
     b->stats.ms[k] = ms;
     b->stats.jobs[k] = jobs[k];
   }
-  float tot = 0;
-  HC(hipEventElapsedTime(&tot, b->ev[0], b->ev[10]));
-  b->stats.ms[10] = tot;
-  b->stats.jobs[10] = n_tx;
   return FTZ_SUCCESS;
 }
 
@@ -430,7 +449,7 @@ extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
   if (b->ev_init)
-    for (int k = 0; k <= FTZ_NKERNELS; k++) (void)hipEventDestroy(b->ev[k]);
+    for (int k = 0; k < 14; k++) (void)hipEventDestroy(b->ev[k]);
   delete b;
 }
 

@@ -16,8 +16,8 @@ FTZ_E_PP = -2
 FTZ_E_DEVICE = -3
 FTZ_E_NOMEM = -4
 
-FTZ_NKERNELS = 11
-KERNEL_NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "hash", "verdict", "total"]
+FTZ_NKERNELS = 12
+KERNEL_NAMES = ["decode", "zr", "hash_pre", "scalar", "g1p", "g2", "miller", "fexp", "g1", "hash", "verdict", "total"]
 
 # error strings of the reference for each class (tests match substrings)
 MESSAGES = {

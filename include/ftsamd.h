@@ -67,9 +67,11 @@ typedef struct {
 } ftz_issue;
 
 /* Per-kernel timing of the last ftz_batch_run (HIP events on the batch stream). */
-#define FTZ_NKERNELS 11
+#define FTZ_NKERNELS 12
 typedef struct {
-  float ms[FTZ_NKERNELS];     /* decode, zr, hash_pre, scalar, g1, g2, miller, fexp, hash, verdict, total */
+  /* decode, zr, hash_pre, scalar, g1_pairing, g2, miller, fexp, g1_side (concurrent stream), hash,
+   * verdict, total */
+  float ms[FTZ_NKERNELS];
   uint64_t jobs[FTZ_NKERNELS];
 } ftz_stats;
 

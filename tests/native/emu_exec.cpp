@@ -127,6 +127,9 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   par_for((uint32_t)p.g1.size(), [&](uint32_t i) {
     job_g1(p.g1[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
   });
+  par_for((uint32_t)p.g1p.size(), [&](uint32_t i) {
+    job_g1(p.g1p[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
+  });
   par_for((uint32_t)p.g2.size(), [&](uint32_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
   par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
     job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), i);
@@ -169,7 +172,9 @@ int emu_opcount_transfers(void* ctx, size_t n, const ftz_transfer* tx, unsigned 
   stage(1, p.zr.size(), [&](size_t i) { job_zr(p.zr[i], wire.data(), scal, canon.data()); });
   stage(2, p.hpre.size(), [&](size_t i) { job_hash(p.hpre[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   stage(3, p.sc.size(), [&](size_t i) { job_scalar(p.sc[i], scal, p.sclist.data()); });
-  stage(4, p.g1.size(), [&](size_t i) { job_g1(p.g1[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data()); });
+  std::vector<G1Job> all = p.g1;
+  all.insert(all.end(), p.g1p.begin(), p.g1p.end());
+  stage(4, all.size(), [&](size_t i) { job_g1(all[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data()); });
   stage(5, p.g2.size(), [&](size_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
   stage(6, p.pr.size(), [&](size_t i) { job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), (uint32_t)i); });
   stage(7, p.pr.size(), [&](size_t i) { job_fexp(p.pr[i], fbuf.data(), (uint32_t)i, p.arena.data()); });
