@@ -166,7 +166,7 @@ def main():
         peak = madpeak(local)
         if os.path.exists(opc_path):
             opc = json.load(open(opc_path))["pp_a"]
-            m_per_job = opc["m_per_job"].get(dom)
+            m_per_job = opc["m_per_job"].get("g1" if dom == "g1p" else dom)
             if m_per_job and kern[dom][0] > 0:
                 achieved = m_per_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
                 roof = {"bound": "valu", "kernel": "k_" + dom, "achieved": round(achieved / 1e12, 4),
