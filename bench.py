@@ -132,25 +132,14 @@ def main():
         batch.run()  # synchronous: returns after the stream drained
     barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
     # verdicts: exact per-proof codes, and the gathered accept bitmap
     codes = batch.codes()
     ok_local = codes == expect
     bits = batch.bitmap()
     if dist is not None:
-        import torch
-        bt = torch.frombuffer(bytearray(bits), dtype=torch.uint8).cuda()
-        gathered = [torch.empty_like(bt) for _ in range(world)]
-        dist.all_gather(gathered, bt)  # verdict bitmaps over RCCL
-        okt = torch.tensor([1 if ok_local else 0], device="cuda")
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        verdict_ok = bool(okt.item())
-        n_accept = sum(bin(b).count("1") for g in gathered for b in g.cpu().tolist())
+        from zkatdlog.dist import gather_verdicts, max_elapsed
+        elapsed = max_elapsed(elapsed, dist)
+        _, n_accept, verdict_ok = gather_verdicts(bits, len(items), ok_local, dist)  # RCCL over xGMI
     else:
         verdict_ok = ok_local
         n_accept = sum(bin(b).count("1") for b in bits)

@@ -182,7 +182,7 @@ class IssueVerifier:
 
 
 def transfer_zkproof_validate(ctx, input_commitments, output_commitments, proof):
-    """validator.TransferZKProofValidate (validator/validator_transfer.go:232-246):
+    """validator.TransferZKProofValidate (validator/validator_transfer.go:84-98):
     inputs are the commitments of the ledger tokens, not the action's own
     InputCommitments."""
     TransferVerifier(input_commitments, output_commitments, ctx).verify(proof)

@@ -1,0 +1,59 @@
+"""Multi-GPU sharding of a verification job.
+
+Transfers are independent, so a job of N transfers is cut into contiguous
+slices, one per rank (one process per GPU).  There is no data-path collective:
+each rank verifies its slice on its own GPU; the only exchange is the gather
+of the per-rank verdict bitmaps (RCCL all-gather over xGMI when the process
+group backend is "nccl", gloo on CPU in the tests) and a MIN all-reduce of the
+per-rank "verdicts matched the expected codes" flag.
+"""
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous [start, stop) slice of n_total transfers owned by rank."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    base, extra = divmod(n_total, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def _device(dist):
+    import torch
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def gather_verdicts(bits, n_local, ok_local, dist):
+    """All-gather rank-local verdict bitmaps (bit i of rank r <=> transfer
+    shard_start(r)+i accepted).  Returns (list of per-rank bitmaps as bytes,
+    total accepted, all ranks matched their expected codes)."""
+    import torch
+    dev = _device(dist)
+    world = dist.get_world_size()
+    # ranks may hold different slice sizes: exchange sizes first, pad to max
+    nb = torch.tensor([len(bits), n_local], dtype=torch.int64, device=dev)
+    sizes = [torch.empty_like(nb) for _ in range(world)]
+    dist.all_gather(sizes, nb)
+    width = max(int(s[0].item()) for s in sizes) or 1
+    bt = torch.zeros(width, dtype=torch.uint8, device=dev)
+    if bits:
+        bt[:len(bits)] = torch.frombuffer(bytearray(bits), dtype=torch.uint8).to(dev)
+    gathered = [torch.empty_like(bt) for _ in range(world)]
+    dist.all_gather(gathered, bt)
+    okt = torch.tensor([1 if ok_local else 0], dtype=torch.int64, device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    out, n_accept = [], 0
+    for g, s in zip(gathered, sizes):
+        b = bytes(g.cpu().tolist())[:int(s[0].item())]
+        n = int(s[1].item())
+        n_accept += sum(((b[i // 8] >> (i % 8)) & 1) for i in range(n))
+        out.append(b)
+    return out, n_accept, bool(okt.item())
+
+
+def max_elapsed(elapsed, dist):
+    """Max over ranks of a wall-clock interval (the job ends with the slowest rank)."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=_device(dist))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

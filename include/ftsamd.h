@@ -3,11 +3,11 @@
  *
  * Reference interfaces this boundary replaces (paths relative to
  * /root/reference/token/core/zkatdlog/):
- *   ftz_ctx_create        crypto/setup.go:350-367   PublicParams.Deserialize
+ *   ftz_ctx_create        crypto/setup.go:134-151   PublicParams.Deserialize (+ Validate :238-273)
  *                         nogh/driver/driver.go:114-124 Driver.NewValidator (PP parsed once per process)
  *   ftz_verify_transfers  crypto/transfer/transfer.go:66-77,124-154
  *                         transfer.NewVerifier(inputs, outputs, pp).Verify(proof)
- *                         as called by crypto/validator/validator_transfer.go:232-246
+ *                         as called by crypto/validator/validator_transfer.go:84-98
  *                         TransferZKProofValidate (inputs = ledger commitments)
  *   ftz_verify_issues     crypto/issue/issue.go:194-223
  *                         issue.NewVerifier(tokens, anonymous, pp).Verify(proof)
