@@ -20,13 +20,15 @@
 #endif
 #include "constants.h"
 
-// Test-only instrumentation (host emulation build): counts Montgomery products.
+// Test-only instrumentation (host emulation build): counts u32 x u32 -> u64
+// MADs (a Montgomery product = 136; M = MADs / 136 in profiles/opcounts.json).
 #ifdef FTS_COUNT_OPS
 extern thread_local unsigned long long fts_mont_count;
-#define FTS_COUNT_MUL() (++fts_mont_count)
+#define FTS_COUNT_MAD(n) (fts_mont_count += (n))
 #else
-#define FTS_COUNT_MUL() ((void)0)
+#define FTS_COUNT_MAD(n) ((void)0)
 #endif
+#define FTS_COUNT_MUL() FTS_COUNT_MAD(136)
 
 namespace fts {
 

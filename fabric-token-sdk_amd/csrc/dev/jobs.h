@@ -494,3 +494,43 @@ FTS_HD int32_t job_verdict(const TxChecks& t, const Check* ck, const uint8_t* pt
 }
 
 }  // namespace fts
+
+// ------------------------------------------------------------------ sextet jobs
+// Pairing jobs in the sextet layout (dev/sextet.h): lane k of the sextet of
+// job idx holds coefficient k of the Miller-loop value.  F12Dev keeps gnark's
+// E12 word order (C0.B0, C0.B1, C0.B2, C1.B0, C1.B1, C1.B2), so coefficient k
+// lives at Fp2 index (k odd ? 3 + k/2 : k/2).
+#include "sextet.h"
+
+namespace fts {
+
+FTS_HD int sx_f12_index(int k) { return (k & 1) ? 3 + (k >> 1) : (k >> 1); }
+
+template <class X>
+FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, const G1Dev* g1out,
+                          const G1Dev* pts, const G2Dev* g2out, F12Dev* fout, uint32_t idx, bool valid) {
+  fp2 f = sx_miller_2(x, qlines, g1_load(g1out[j.p1]), g1_load(pts[j.p2]), g2_load(g2out[j.q2]));
+  if (valid) {
+    uint32_t* o = &fout[idx].w[16 * sx_f12_index(x.k)];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      o[i] = f.c0.v[i];
+      o[8 + i] = f.c1.v[i];
+    }
+  }
+}
+
+template <class X>
+FTS_HD void sx_job_fexp(const X& x, const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena, bool valid) {
+  const uint32_t* w = &fin[idx].w[16 * sx_f12_index(x.k)];
+  fp2 f;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    f.c0.v[i] = w[i];
+    f.c1.v[i] = w[8 + i];
+  }
+  fp2 g = sx_final_exp(x, f);
+  if (valid) sx_gt_bytes(arena + j.bytes, x.k, g);
+}
+
+}  // namespace fts

@@ -6,12 +6,10 @@
 
 using namespace fts;
 
-#define JOB_KERNEL_PROLOGUE(n)                          \
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; \
-  if (i >= (n)) return;
-
-__global__ void __launch_bounds__(64) k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf,
+// Final exponentiations, sextet layout (see k_miller).
+__global__ void __launch_bounds__(64, 2) k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf,
                                              uint8_t* arena) {
-  JOB_KERNEL_PROLOGUE(n);
-  job_fexp(jobs[i], fbuf, i, arena);
+  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_FEXP];
+  SX_KERNEL_PROLOGUE(n);
+  sx_job_fexp(x, jobs[jc], fbuf, jc, arena, valid);
 }

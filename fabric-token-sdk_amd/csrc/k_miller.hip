@@ -6,15 +6,14 @@
 
 using namespace fts;
 
-#define JOB_KERNEL_PROLOGUE(n)                          \
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; \
-  if (i >= (n)) return;
-
-__global__ void __launch_bounds__(64) k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines,
+// 2-pair Miller loops, sextet layout: 10 jobs per 64-lane wave (lanes 60..63
+// shadow the last sextet read-only), one wave per workgroup.
+__global__ void __launch_bounds__(64, 2) k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines,
                                                const G1Dev* g1out, const G1Dev* pts, const G2Dev* g2out,
                                                F12Dev* fbuf) {
-  JOB_KERNEL_PROLOGUE(n);
-  job_miller(jobs[i], qlines, g1out, pts, g2out, fbuf, i);
+  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_MILLER];
+  SX_KERNEL_PROLOGUE(n);
+  sx_job_miller(x, jobs[jc], qlines, g1out, pts, g2out, fbuf, jc, valid);
 }
 
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n) {

@@ -7,6 +7,23 @@
 
 using namespace fts;
 
+// Sextet kernels (dev/sextet.h): 10 jobs per one-wave workgroup.
+static constexpr uint32_t SX_JOBS_PER_WAVE = 10;
+struct SyncWave {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+// Lane -> (sextet, role); lanes 60..63 are ghosts that shadow sextet 9 without
+// writing its slots.  Every lane runs the whole program (barriers inside).
+#define SX_KERNEL_PROLOGUE(n)                                           \
+  uint32_t lane_ = threadIdx.x, sx_ = lane_ / 6;                        \
+  bool ghost_ = sx_ >= SX_JOBS_PER_WAVE;                                \
+  int k_ = ghost_ ? (int)(lane_ - 6 * SX_JOBS_PER_WAVE) : (int)(lane_ - 6 * sx_); \
+  if (ghost_) sx_ = SX_JOBS_PER_WAVE - 1;                               \
+  uint32_t job_ = blockIdx.x * SX_JOBS_PER_WAVE + sx_;                  \
+  bool valid = !ghost_ && job_ < (n);                                   \
+  uint32_t jc = job_ < (n) ? job_ : (n) - 1;                            \
+  Sx<SyncWave> x{k_, (SlotT*)(slots[sx_]), !ghost_, {}};
+
 __global__ void k_decode(const DecodeJob* jobs, uint32_t n, const uint8_t* wire, G1Dev* pts, uint8_t* pt_ok,
                          uint8_t* arena);
 __global__ void k_zr(const ZrJob* jobs, uint32_t n, const uint8_t* wire, uint32_t (*scal)[8], uint8_t* canon);

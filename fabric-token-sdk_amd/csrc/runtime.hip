@@ -392,10 +392,10 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   if (n_g2) k_g2<<<blocks_for(n_g2, 128), 128, 0, s>>>(b->g2.p, n_g2, scal, c->g2tab.p, b->g2out.p);
   HC(hipEventRecord(e[6], s));
   if (n_pr)
-    k_miller<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->g1out.p, b->pts.p, b->g2out.p,
+    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->g1out.p, b->pts.p, b->g2out.p,
                                                  b->fbuf.p);
   HC(hipEventRecord(e[7], s));
-  if (n_pr) k_fexp<<<blocks_for(n_pr, 64), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
+  if (n_pr) k_fexp<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
   HC(hipEventRecord(e[8], s));
   HC(hipStreamWaitEvent(s, e[12], 0));
   HC(hipEventRecord(e[9], s));

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""TEST-ONLY: count Montgomery products per GPU job type with the host
+"""TEST-ONLY: count MADs (reported as M = MADs/136 Montgomery-product equivalents) per GPU job type with the host
 emulation build (-DFTS_COUNT_OPS) on the bench workload; writes
 profiles/opcounts.json (the algorithmic-work figure bench.py's roofline uses)."""
 import base64
@@ -42,8 +42,8 @@ def main():
         ps, js = (ctypes.c_ulonglong * 10)(), (ctypes.c_ulonglong * 10)()
         L.emu_opcount_transfers(ctypes.c_void_p(ctx), len(items), arr, ps, js)
         out[key] = {"transfers": len(items),
-                    "m_per_tx": sum(ps) / len(items),
-                    "m_per_job": {n: (ps[i] / js[i] if js[i] else 0) for i, n in enumerate(NAMES)},
+                    "m_per_tx": sum(ps) / 136 / len(items),
+                    "m_per_job": {n: (ps[i] / 136 / js[i] if js[i] else 0) for i, n in enumerate(NAMES)},
                     "jobs_per_tx": {n: js[i] / len(items) for i, n in enumerate(NAMES)}}
         print(key, json.dumps(out[key]))
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)

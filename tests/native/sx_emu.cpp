@@ -1,0 +1,165 @@
+// TEST-ONLY host emulation of the sextet pairing code (dev/sextet.h): the six
+// lanes of a sextet run as six host threads sharing a slot array, with a
+// pthread barrier standing in for the wave's __syncthreads.  Each routine is
+// compared with the one-lane tower/pairing code (dev/tower.h, dev/pairing.h),
+// which tests/test_emu.py checks against the Python oracle.
+#include <pthread.h>
+#include <string.h>
+
+#include <functional>
+#include <thread>
+#include <vector>
+
+#include "../../fabric-token-sdk_amd/csrc/dev/sextet.h"
+
+using namespace fts;
+
+namespace {
+
+struct SyncHost {
+  pthread_barrier_t* b;
+  void operator()() const { pthread_barrier_wait(b); }
+};
+typedef Sx<SyncHost> SxH;
+
+// run body(x) on six threads (lanes 0..5) sharing one slot region
+void run6(const std::function<void(const SxH&)>& body) {
+  std::vector<F2Slot> slots(SX_SLOTS_MILLER > SX_SLOTS_FEXP ? SX_SLOTS_MILLER : SX_SLOTS_FEXP);
+  memset(slots.data(), 0xA5, slots.size() * sizeof(F2Slot));  // garbage: nothing may read unwritten slots
+  pthread_barrier_t b;
+  pthread_barrier_init(&b, nullptr, 6);
+  std::vector<std::thread> th;
+  for (int k = 0; k < 6; k++)
+    th.emplace_back([&, k] {
+      SxH x{k, slots.data(), true, {&b}};
+      body(x);
+    });
+  for (auto& t : th) t.join();
+  pthread_barrier_destroy(&b);
+}
+
+uint32_t xs(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return s;
+}
+fp rnd_fp(uint32_t& s) {
+  uint32_t t[8];
+  for (int i = 0; i < 8; i++) t[i] = xs(s);
+  t[7] &= 0x1FFFFFFF;
+  return fe_from_int<ModP>(t);
+}
+fp12 rnd_f12(uint32_t& s) {
+  fp12 f;
+  fp* p = &f.c0.c0.c0;
+  for (int i = 0; i < 12; i++) p[i] = rnd_fp(s);
+  return f;
+}
+fp12 from_coefs(const fp2 c[6]) {
+  fp12 f;
+  f.c0.c0 = c[0];
+  f.c1.c0 = c[1];
+  f.c0.c1 = c[2];
+  f.c1.c1 = c[3];
+  f.c0.c2 = c[4];
+  f.c1.c2 = c[5];
+  return f;
+}
+
+fp ld_fp(const uint8_t* b) {
+  uint32_t t[8];
+  be32_to_limbs(t, b);
+  return fe_from_int<ModP>(t);
+}
+g1a ld_g1(const uint8_t* b) {
+  g1a a;
+  a.x = ld_fp(b);
+  a.y = ld_fp(b + 32);
+  a.inf = is_zero(a.x) && is_zero(a.y);
+  return a;
+}
+g2a ld_g2(const uint8_t* b) {
+  g2a a;
+  a.x.c1 = ld_fp(b);
+  a.x.c0 = ld_fp(b + 32);
+  a.y.c1 = ld_fp(b + 64);
+  a.y.c0 = ld_fp(b + 96);
+  a.inf = f2_is_zero(a.x) && f2_is_zero(a.y);
+  return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns a bitmask of mismatching operations (0 = all sextet ops equal the
+// one-lane tower ops) over `iters` random inputs:
+// 1 mul, 2 sqr, 4 line, 8 cyc, 16 frob1, 32 frob2, 64 frob3, 128 inv, 256 conj, 512 expt
+int sxe_ops(uint32_t seed, int iters) {
+  int bad = 0;
+  uint32_t s = seed | 1;
+  for (int it = 0; it < iters; it++) {
+    fp12 a = rnd_f12(s), b = rnd_f12(s);
+    fp2 l0 = {rnd_fp(s), rnd_fp(s)}, l1 = {rnd_fp(s), rnd_fp(s)}, l3 = {rnd_fp(s), rnd_fp(s)};
+    // a cyclotomic element for cyc / expt: easy part of the final exponentiation
+    fp12 c = f12_conj(a) * f12_inv(a);
+    c = f12_frob2(c) * c;
+    fp2 r[10][6];
+    run6([&](const SxH& x) {
+      int k = x.k;
+      fp2 ak = f12_coef(a, k), bk = f12_coef(b, k), ck = f12_coef(c, k);
+      r[0][k] = sx_mulv(x, ak, bk);
+      r[1][k] = sx_sqr(x, ak);
+      if (k == 0) {
+        x.put(SX_L + 0, l0);
+        x.put(SX_L + 1, l1);
+        x.put(SX_L + 2, l3);
+      }
+      x.sync();
+      r[2][k] = sx_mul_line(x, ak, SX_L);
+      r[3][k] = sx_cyc_sqr(x, ck);
+      r[4][k] = sx_frob1(k, ak);
+      r[5][k] = sx_frob2(k, ak);
+      r[6][k] = sx_frob3(k, ak);
+      r[7][k] = sx_inv(x, ak);
+      r[8][k] = sx_conj(k, ak);
+      r[9][k] = it == 0 ? sx_expt(x, ck) : ck;
+    });
+    fp12 want[10] = {a * b,        f12_sqr(a),   f12_mul_034(a, l0, l1, l3), f12_cyclo_sqr(c), f12_frob(a),
+                     f12_frob2(a), f12_frob3(a), f12_inv(a),                 f12_conj(a),      it == 0 ? f12_expt(c) : c};
+    for (int o = 0; o < 10; o++)
+      if (!f12_eq(from_coefs(r[o]), want[o])) bad |= 1 << o;
+  }
+  return bad;
+}
+
+// final exponentiation of a random Fp12: sextet vs one-lane (GT bytes)
+int sxe_fexp(uint32_t seed, uint8_t* out_sx, uint8_t* out_ref) {
+  uint32_t s = seed | 1;
+  fp12 f = rnd_f12(s);
+  f12_to_bytes(out_ref, final_exp(f));
+  run6([&](const SxH& x) {
+    fp2 g = sx_final_exp(x, f12_coef(f, x.k));
+    sx_gt_bytes(out_sx, x.k, g);
+  });
+  return memcmp(out_sx, out_ref, 384) != 0;
+}
+
+// 2-pair Miller loop: sextet vs one-lane, raw Fp12 (same formulas => equal).
+// p1, p2: G1 RawBytes (64); q2, qfix: G2 RawBytes (128, X.A1|X.A0|Y.A1|Y.A0).
+int sxe_miller(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2, const uint8_t* qfix, uint8_t* out_sx,
+               uint8_t* out_ref) {
+  std::vector<LineCoef> ql(MILLER_LINES);
+  precompute_lines(ql.data(), ld_g2(qfix));
+  g1a P1 = ld_g1(p1), P2 = ld_g1(p2);
+  g2a Q2 = ld_g2(q2);
+  fp12 want = miller_2(ql.data(), P1, P2, Q2);
+  fp2 got[6];
+  run6([&](const SxH& x) { got[x.k] = sx_miller_2(x, ql.data(), P1, P2, Q2); });
+  f12_to_bytes(out_ref, want);
+  f12_to_bytes(out_sx, from_coefs(got));
+  return memcmp(out_sx, out_ref, 384) != 0;
+}
+
+}  // extern "C"

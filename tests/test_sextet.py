@@ -1,0 +1,44 @@
+"""Sextet (6 lanes per pairing job) arithmetic, host-emulated with six threads
+and a barrier: every operation must equal the one-lane tower / pairing code
+bit for bit (which test_emu.py pins to the Python oracle)."""
+import ctypes
+import random
+
+import pytest
+from conftest import build_emu
+
+from ftsoracle import bn254 as C
+
+
+@pytest.fixture(scope="module")
+def sx():
+    return ctypes.CDLL(build_emu())
+
+
+def test_sextet_field_ops(sx):
+    # mul, sqr, sparse line mul, cyclotomic sqr, frobenius 1/2/3, inverse, conj, expt
+    assert sx.sxe_ops(20241016, 4) == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_sextet_final_exp(sx, seed):
+    a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
+    assert sx.sxe_fexp(seed, a, b) == 0
+    assert bytes(a) == bytes(b)
+
+
+@pytest.mark.parametrize("case", ["both", "p2_inf", "p1_inf", "q2_inf"])
+def test_sextet_miller(sx, case):
+    rng = random.Random(case)
+    p1 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)))
+    p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)))
+    q2 = C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R)))
+    qf = C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R)))
+    if case == "p2_inf":
+        p2 = bytes(64)
+    if case == "p1_inf":
+        p1 = bytes(64)
+    if case == "q2_inf":
+        q2 = bytes(128)
+    a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
+    assert sx.sxe_miller(p1, p2, q2, qf, a, b) == 0
