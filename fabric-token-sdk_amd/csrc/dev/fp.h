@@ -91,26 +91,42 @@ FTS_HD bool fe_geq_mod(const uint32_t a[8]) {
   return gt || eq;
 }
 
-// r = a - m (borrow discarded); returns borrow
+// 32-bit add/subtract with carry.  On the device these are clang's
+// __builtin_addc/__builtin_subc, which lower to v_add_co_u32 / v_addc_co_u32
+// (v_sub_co_u32 / v_subb_co_u32) chains: one instruction per limb.  (Plain C
+// on uint64_t becomes 64-bit v_lshl_add_u64 sequences with twice the registers.)
+FTS_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_addc(a, b, cin, cout);
+#else
+  uint64_t s = (uint64_t)a + b + cin;
+  *cout = (uint32_t)(s >> 32);
+  return (uint32_t)s;
+#endif
+}
+FTS_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t bin, uint32_t* bout) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_subc(a, b, bin, bout);
+#else
+  uint64_t d = (uint64_t)a - b - bin;
+  *bout = (uint32_t)(d >> 63);
+  return (uint32_t)d;
+#endif
+}
+
+// r = a - b (borrow discarded); returns borrow
 FTS_HD uint32_t sub8(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   uint32_t borrow = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t d = (uint64_t)a[i] - b[i] - borrow;
-    r[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 8; i++) r[i] = subb32(a[i], b[i], borrow, &borrow);
   return borrow;
 }
 
 FTS_HD uint32_t add8(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c = (uint64_t)a[i] + b[i] + (c >> 32);
-    r[i] = (uint32_t)c;
-  }
-  return (uint32_t)(c >> 32);
+  for (int i = 0; i < 8; i++) r[i] = addc32(a[i], b[i], c, &c);
+  return c;
 }
 
 template <class M>
@@ -287,27 +303,24 @@ FTS_HD void limbs_to_be32(uint8_t* b, const uint32_t in[8]) {
   }
 }
 
-// a^e for a fixed 256-bit exponent (left-to-right, 4-bit windows)
+// a^e for a fixed 256-bit exponent (left-to-right, 2-bit windows: 3 table
+// entries keep the register footprint small; 256 squarings + <= 128 products)
 template <class M>
 FTS_HDN Fe<M> fe_pow(const Fe<M>& a, const uint32_t* e) {
-  Fe<M> tab[16];
-  tab[0] = fe_one<M>();
-  tab[1] = a;
-#pragma nounroll
-  for (int i = 2; i < 16; i++) tab[i] = tab[i - 1] * a;
+  Fe<M> a2 = fe_sqr(a);
+  Fe<M> a3 = a2 * a;
   Fe<M> r = fe_one<M>();
 #pragma nounroll
-  for (int w = 63; w >= 0; w--) {
+  for (int w = 127; w >= 0; w--) {
     r = fe_sqr(r);
     r = fe_sqr(r);
-    r = fe_sqr(r);
-    r = fe_sqr(r);
-    uint32_t d = (e[w >> 3] >> ((w & 7) * 4)) & 15;
-    // constant-time-ish select to keep registers bounded
-    Fe<M> s = tab[0];
-    for (int k = 1; k < 16; k++)
-      if (d == (uint32_t)k) s = tab[k];
-    r = r * s;
+    uint32_t d = (e[w >> 4] >> ((w & 15) * 2)) & 3;
+    if (d) {
+      Fe<M> s;
+#pragma unroll
+      for (int i = 0; i < 8; i++) s.v[i] = d == 1 ? a.v[i] : (d == 2 ? a2.v[i] : a3.v[i]);
+      r = r * s;
+    }
   }
   return r;
 }

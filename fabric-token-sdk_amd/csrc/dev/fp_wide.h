@@ -91,23 +91,25 @@ FTS_HD fp redc_wide(const uint32_t t[16]) {
 }
 
 FTS_HD void add16(uint32_t r[16], const uint32_t a[16]) {
-  uint64_t c = 0;
+  uint32_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    c = (uint64_t)r[i] + a[i] + (c >> 32);
-    r[i] = (uint32_t)c;
-  }
+  for (int i = 0; i < 16; i++) r[i] = addc32(r[i], a[i], c, &c);
 }
 
 FTS_HD void sub16(uint32_t r[16], const uint32_t a[16]) {
-  uint32_t borrow = 0;
+  uint32_t b = 0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    uint64_t d = (uint64_t)r[i] - a[i] - borrow;
-    r[i] = (uint32_t)d;
-    borrow = (uint32_t)(d >> 63);
-  }
+  for (int i = 0; i < 16; i++) r[i] = subb32(r[i], a[i], b, &b);
 }
+
+// Scheduling fence (device): keeps the compiler from hoisting the next term's
+// operand loads above the current term's multiply chains, which otherwise
+// doubles the live registers and spills.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define FTS_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define FTS_SCHED_FENCE() ((void)0)
+#endif
 
 // Lazily reduced Fp2 accumulator (up to 6 products of reduced operands).
 struct Wide2 {
@@ -127,6 +129,7 @@ FTS_HD void w2_init(Wide2& w) {
 // non-negative between "- t0 - t1" and "+ t2" (multiples of p vanish in REDC).
 FTS_HD void w2_mac(Wide2& w, const fp2& a, const fp2& b) {
   FTS_COUNT_MAD(192);  // 3 full-width 8x8 products
+  FTS_SCHED_FENCE();
   uint32_t t[16], sa[8], sb[8];
   mul_wide(t, a.c0.v, b.c0.v);
   add16(w.re, t);

@@ -506,10 +506,46 @@ namespace fts {
 
 FTS_HD int sx_f12_index(int k) { return (k & 1) ? 3 + (k >> 1) : (k >> 1); }
 
+// Miller-loop lines of Q in consumption order (precompute_lines), each
+// evaluated at P, stored at lines[n * njobs + idx].  A pair with an infinity
+// point contributes 1 (gnark MillerLoop skips it): its lines are written as 1.
+FTS_HD void g2lines_emit(const g2a& Q, const g1a& P, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+  bool use = !(P.inf || Q.inf);
+  g2p T = {Q.x, Q.y, f2_one()};
+  g2a Qn = aff_neg(Q);
+  uint32_t n = 0;
+  auto emit = [&](const LineCoef& l) {
+    fp2 c0 = use ? f2_mul_fp(l.r0, P.y) : f2_one();
+    fp2 c3 = use ? f2_mul_fp(l.r1, P.x) : f2_zero();
+    fp2 c4 = use ? l.r2 : f2_zero();
+    evline_store(lines[(size_t)n * njobs + idx], c0, c3, c4);
+    n++;
+  };
+#pragma nounroll
+  for (int i = 64; i >= 0; i--) {
+    emit(dbl_step(T));
+    int d = naf_digit(i);
+    if (d == 1) emit(add_step(T, Q));
+    if (d == -1) emit(add_step(T, Qn));
+  }
+  emit(add_step(T, tw_frob(Q)));
+  emit(add_step(T, tw_frob2_neg(Q)));
+}
+
+// Pair 2 of membership job idx (one lane): t' = c PK0 + v PK1 + h PK2 (the G2
+// job with the same index; pok.go:175-183 folded), then its lines evaluated at
+// P2 = R.  Layout [line][job]: a wave writes, and the sextet Miller kernel
+// reads, consecutive jobs.
+FTS_HD void job_g2lines(const G2Job& g, const PairJob& j, const uint32_t (*scal)[8], const G2Dev* tab,
+                        G2Dev* g2out, const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+  job_g2(g, scal, tab, g2out);
+  g2lines_emit(g2_load(g2out[g.out]), g1_load(pts[j.p2]), lines, idx, njobs);
+}
+
 template <class X>
-FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, const G1Dev* g1out,
-                          const G1Dev* pts, const G2Dev* g2out, F12Dev* fout, uint32_t idx, bool valid) {
-  fp2 f = sx_miller_2(x, qlines, g1_load(g1out[j.p1]), g1_load(pts[j.p2]), g2_load(g2out[j.q2]));
+FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, const EvLineDev* lines2,
+                          const G1Dev* g1out, F12Dev* fout, uint32_t idx, uint32_t njobs, bool valid) {
+  fp2 f = sx_miller_f(x, qlines, g1_load(g1out[j.p1]), lines2 + idx, njobs);
   if (valid) {
     uint32_t* o = &fout[idx].w[16 * sx_f12_index(x.k)];
 #pragma unroll

@@ -22,18 +22,15 @@ struct g2p {
 };
 
 FTS_HD fp fp_half(const fp& a) {
-  uint32_t t[9];
-  uint64_t c = 0;
-  bool odd = a.v[0] & 1;
+  uint32_t t[8], mm[8];
+  uint32_t odd = a.v[0] & 1;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    c = (uint64_t)a.v[i] + (odd ? P_MOD[i] : 0u) + (c >> 32);
-    t[i] = (uint32_t)c;
-  }
-  t[8] = (uint32_t)(c >> 32);
+  for (int i = 0; i < 8; i++) mm[i] = odd ? P_MOD[i] : 0u;
+  uint32_t top = add8(t, a.v, mm);
   fp r;
 #pragma unroll
-  for (int i = 0; i < 8; i++) r.v[i] = (t[i] >> 1) | (t[i + 1] << 31);
+  for (int i = 0; i < 7; i++) r.v[i] = (t[i] >> 1) | (t[i + 1] << 31);
+  r.v[7] = (t[7] >> 1) | (top << 31);
   return r;
 }
 FTS_HD fp2 f2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
@@ -103,6 +100,7 @@ FTS_HD g2a tw_frob2_neg(const g2a& q) {
 }
 
 FTS_HD int naf_digit(int i) {
+  if (i >= 64) return 0;  // position 64: the leading digit, consumed by T = Q
   if ((ATE_NAF_POS >> i) & 1) return 1;
   if ((ATE_NAF_NEG >> i) & 1) return -1;
   return 0;

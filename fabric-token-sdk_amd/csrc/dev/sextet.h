@@ -71,6 +71,7 @@ enum : int {
   SX_PC = 23,  // (yP2, xP2), (yP1, xP1) packed as Fp2 slots
   SX_L = 25,   // lines at P: pair 2 (l0, l1, l3), pair 1 (l0, l1, l3)
   SX_SLOTS_MILLER = 31,
+  SX_SLOTS_MILLER_F = 18,  // f-chain only Miller loop (pair-2 lines precomputed)
 };
 
 // Sextet context, passed by value.  Sync is a callable barrier across the
@@ -169,14 +170,20 @@ static constexpr TermRow SX_SQR_TAB[4] = {
     term_row(SQ_(2, 4, 1, 1), SQZ, SQ_(3, 5, 1, 1), SQZ, SQ_(1, 3, 0, 1), SQZ),
 };
 
+// (The symmetric 4-term form above is kept as a table for reference; the
+// 6-term schoolbook loop runs faster on the device: no per-term selects.)
 template <class X>
 FTS_HD fp2 sx_sqr(X x, fp2 a) {
   sx_pub(x, SX_A, a);
   x.sync();
   Wide2 w;
   w2_init(w);
-#pragma unroll
-  for (int t = 0; t < 4; t++) sx_term(x, w, term_at(SX_SQR_TAB[t], x.k));
+#pragma nounroll
+  for (int i = 0; i < 6; i++) {
+    int j = x.k - i;
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w2_mac(w, x.get(SX_A + i), x.get(sb));
+  }
   x.sync();
   return w2_reduce(w);
 }
@@ -193,17 +200,27 @@ static constexpr TermRow SX_CYC_TAB[2] = {
 
 template <class X>
 FTS_HD fp2 sx_cyc_sqr(X x, fp2 a) {
+  const int k = x.k, m = k >> 1;
   sx_pub(x, SX_A, a);
   x.sync();
+  // even k = 2m: a_m * a_m + a_(m+3) * (xi a_(m+3));  odd: one product
+  // k=1: a_5 (xi a_2), k=3: a_3 a_0, k=5: a_4 a_1 (the factor 2 goes into the final 6r)
+  bool odd = (k & 1) != 0;
+  int i1 = odd ? (k == 1 ? 5 : (k == 3 ? 3 : 4)) : m;
+  int j1 = odd ? (k == 1 ? SX_AX + 2 : (k == 3 ? SX_A + 0 : SX_A + 1)) : SX_A + m;
   Wide2 w;
   w2_init(w);
-  sx_term(x, w, term_at(SX_CYC_TAB[0], x.k));
-  sx_term(x, w, term_at(SX_CYC_TAB[1], x.k));
+#pragma nounroll
+  for (int t = 0; t < 2; t++) {
+    fp2 u = x.get(t == 0 ? SX_A + i1 : SX_A + m + 3);
+    fp2 v = x.get(t == 0 ? j1 : SX_AX + m + 3);
+    w2_mac(w, f2_sel(odd && t == 1, f2_zero(), u), v);
+  }
   x.sync();
   fp2 r = w2_reduce(w);
   fp2 r3 = f2_dbl(r) + r;
-  fp2 a2 = f2_dbl(a);
-  return f2_sel((x.k & 1) == 0, r3 - a2, r3 + a2);
+  fp2 ad = f2_dbl(a);
+  return f2_sel(odd, f2_dbl(r3) + ad, r3 - ad);
 }
 
 // f * l with l = l0 + l1 w + l3 w^3 (gnark MulBy034 shape), l in slots lb..lb+2
@@ -213,10 +230,12 @@ FTS_HD fp2 sx_mul_line(X x, fp2 f, int lb) {
   x.sync();
   Wide2 w;
   w2_init(w);
-  w2_mac(w, x.get(lb), f);
-  int j1 = x.k - 1, j3 = x.k - 3;
-  w2_mac(w, x.get(lb + 1), x.get(j1 < 0 ? SX_AX + j1 + 6 : SX_A + j1));
-  w2_mac(w, x.get(lb + 2), x.get(j3 < 0 ? SX_AX + j3 + 6 : SX_A + j3));
+#pragma nounroll
+  for (int t = 0; t < 3; t++) {
+    int j = x.k - (t == 0 ? 0 : (t == 1 ? 1 : 3));
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w2_mac(w, x.get(lb + t), x.get(sb));
+  }
   x.sync();
   return w2_reduce(w);
 }
@@ -246,17 +265,16 @@ FTS_HD fp2 sx_inv(X x, fp2 f) {
   // t0 = d0^2 - xi d1 d2, t1 = xi d2^2 - d0 d1, t2 = d1^2 - d0 d2 (lanes 0..2)
   Wide2 w;
   w2_init(w);
-  sx_term(x, w, term_at(SX_INV_TAB[0], x.k));
-  sx_term(x, w, term_at(SX_INV_TAB[1], x.k));
+#pragma nounroll
+  for (int t = 0; t < 2; t++) sx_term(x, w, term_at(SX_INV_TAB[t], x.k));
   fp2 t = w2_reduce(w);
   x.put(SX_P + x.k, t);
   x.sync();
   // den6 = d0 t0 + xi d2 t1 + xi d1 t2  (every lane)
   Wide2 v;
   w2_init(v);
-  w2_mac(v, x.get(SX_A + 0), x.get(SX_P + 0));
-  w2_mac(v, x.get(SX_AX + 4), x.get(SX_P + 1));
-  w2_mac(v, x.get(SX_AX + 2), x.get(SX_P + 2));
+#pragma nounroll
+  for (int t = 0; t < 3; t++) w2_mac(v, x.get(t == 0 ? SX_A + 0 : (t == 1 ? SX_AX + 4 : SX_AX + 2)), x.get(SX_P + t));
   fp2 tk = x.get(SX_P + (x.k >> 1));
   x.sync();
   fp2 di = f2_inv(w2_reduce(v));
@@ -278,17 +296,28 @@ FTS_HD fp2 sx_expt(X x, fp2 a) {
   return r;
 }
 
-// final exponentiation (same sequence as final_exp)
+// final exponentiation (same sequence as final_exp).  The three x-powers run
+// as one loop so the expt body is emitted once.
 template <class X>
 FTS_HD fp2 sx_final_exp(const X& x, const fp2& f) {
   const int k = x.k;
   fp2 t = sx_mulv(x, sx_conj(k, f), sx_inv(x, f));
   t = sx_mulv(x, sx_frob2(k, t), t);
-  fp2 a = sx_expt(x, t);
-  fp2 a2 = sx_cyc_sqr(x, a);
-  fp2 a6 = sx_mulv(x, sx_cyc_sqr(x, a2), a2);
-  fp2 b = sx_expt(x, a6);
-  fp2 c = sx_expt(x, sx_cyc_sqr(x, b));
+  fp2 in = t, a2, a6, b, c;
+#pragma nounroll
+  for (int e = 0; e < 3; e++) {
+    fp2 r = sx_expt(x, in);
+    if (e == 0) {  // a = t^x, a2 = a^2, a6 = a2^3
+      a2 = sx_cyc_sqr(x, r);
+      a6 = sx_mulv(x, sx_cyc_sqr(x, a2), a2);
+      in = a6;
+    } else if (e == 1) {  // b = a6^x, then c = (b^2)^x
+      b = r;
+      in = sx_cyc_sqr(x, b);
+    } else {
+      c = r;
+    }
+  }
   fp2 A = sx_mulv(x, sx_mulv(x, a6, b), c);
   fp2 B = sx_mulv(x, A, sx_conj(k, a2));
   fp2 res = sx_frob2(k, A);
@@ -309,6 +338,30 @@ FTS_HD void sx_gt_bytes(uint8_t* out, int k, const fp2& a) {
   limbs_to_be32(o, t);
   fe_to_int(t, a.c0);
   limbs_to_be32(o + 32, t);
+}
+
+// Evaluated line of pair 2: l = c0 + c3 w + c4 w^3 (sx_mul_line_r operands).
+struct EvLineDev {
+  uint32_t w[48];  // c0, c3, c4 as Fp2 (Montgomery, 16 words each)
+};
+FTS_HD void evline_store(EvLineDev& d, const fp2& c0, const fp2& c3, const fp2& c4) {
+  const fp2* v[3] = {&c0, &c3, &c4};
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      d.w[16 * m + i] = v[m]->c0.v[i];
+      d.w[16 * m + 8 + i] = v[m]->c1.v[i];
+    }
+}
+FTS_HD fp2 evline_ld(const EvLineDev& d, int m) {
+  fp2 a;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.c0.v[i] = d.w[16 * m + i];
+    a.c1.v[i] = d.w[16 * m + 8 + i];
+  }
+  return a;
 }
 
 // ----------------------------------------------------------------- Miller loop
@@ -442,6 +495,80 @@ FTS_HD fp2 sx_miller_2(const X& x, const LineCoef* qlines, const g1a& P1, const 
     sx_add_step(x, qlines + n + e, use, 0);
     f = sx_mul_line(x, f, SX_L + 3);
     f = sx_mul_line(x, f, SX_L + 0);
+  }
+  return f;
+}
+
+// f * l, l = l0 + l1 w + l3 w^3 held in registers of every lane
+template <class X>
+FTS_HD fp2 sx_mul_line_r(const X& x, const fp2& f, const fp2& l0, const fp2& l1, const fp2& l3) {
+  sx_pub(x, SX_A, f);
+  x.sync();
+  Wide2 w;
+  w2_init(w);
+#pragma nounroll
+  for (int t = 0; t < 3; t++) {
+    int j = x.k - (t == 0 ? 0 : (t == 1 ? 1 : 3));
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w2_mac(w, t == 0 ? l0 : (t == 1 ? l1 : l3), x.get(sb));
+  }
+  x.sync();
+  return w2_reduce(w);
+}
+
+// f <- f * (line lq of the fixed Q evaluated at P1): lanes 0..3 compute the
+// four Fp products r0.c0 yP, r0.c1 yP, r1.c0 xP, r1.c1 xP and exchange them.
+// A pair-1 point at infinity contributes 1.
+template <class X>
+FTS_HD fp2 sx_fixed_line(const X& x, const fp2& f, const LineCoef* lq, const g1a& P1) {
+  const int k = x.k;
+  const LineCoef& q = *lq;
+  fp a = (k == 0) ? q.r0.c0 : (k == 1) ? q.r0.c1 : (k == 2) ? q.r1.c0 : q.r1.c1;
+  fp b = (k < 2) ? P1.y : P1.x;
+  x.put(SX_P + k, f2_of_fp(a * b));
+  x.sync();
+  fp2 l0 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
+  fp2 l1 = {x.get(SX_P + 2).c0, x.get(SX_P + 3).c0};
+  fp2 l3 = q.r2;
+  l0 = f2_sel(P1.inf, f2_one(), l0);
+  l1 = f2_sel(P1.inf, f2_zero(), l1);
+  l3 = f2_sel(P1.inf, f2_zero(), l3);
+  return sx_mul_line_r(x, f, l0, l1, l3);
+}
+
+// Which of the MILLER_LINES lines is preceded by a squaring of f: the first
+// line of every loop iteration i < 64 (miller_2 order).
+struct SqrMask {
+  uint64_t lo, hi;
+};
+constexpr SqrMask miller_sqr_mask() {
+  SqrMask m{0, 0};
+  int n = 0;
+  for (int i = 64; i >= 0; i--) {
+    if (i != 64) {
+      if (n < 64)
+        m.lo |= 1ull << n;
+      else
+        m.hi |= 1ull << (n - 64);
+    }
+    n += 1 + ((i < 64 && (((ATE_NAF_POS >> i) & 1) || ((ATE_NAF_NEG >> i) & 1))) ? 1 : 0);
+  }
+  return m;
+}
+static constexpr SqrMask MILLER_SQR = miller_sqr_mask();
+
+// 2-pair Miller loop with pair 2's lines precomputed per job (job_g2lines,
+// layout [line][job]): same factors, same order as miller_2.
+template <class X>
+FTS_HD fp2 sx_miller_f(const X& x, const LineCoef* qlines, const g1a& P1, const EvLineDev* l2, uint32_t njobs) {
+  fp2 f = f2_sel(x.k == 0, f2_one(), f2_zero());
+#pragma nounroll
+  for (int s = 0; s < MILLER_LINES; s++) {
+    bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
+    if (sq) f = sx_sqr(x, f);
+    f = sx_fixed_line(x, f, qlines + s, P1);
+    const EvLineDev& e = l2[(size_t)s * njobs];
+    f = sx_mul_line_r(x, f, evline_ld(e, 0), evline_ld(e, 1), evline_ld(e, 2));
   }
   return f;
 }

@@ -16,6 +16,14 @@ __global__ void __launch_bounds__(128) k_g2(const G2Job* jobs, uint32_t n, const
   job_g2(jobs[i], scal, tab, g2out);
 }
 
+// t' of every membership job and its 88 Miller lines evaluated at R (one lane per job).
+__global__ void __launch_bounds__(64) k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n,
+                                                const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out,
+                                                const G1Dev* pts, EvLineDev* lines) {
+  JOB_KERNEL_PROLOGUE(n);
+  job_g2lines(g2[i], pr[i], scal, tab, g2out, pts, lines, i, n);
+}
+
 __global__ void __launch_bounds__(64) k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab) {
   JOB_KERNEL_PROLOGUE(n);
   job_tab_g2(i, bases, tab);

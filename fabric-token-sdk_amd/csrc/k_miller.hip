@@ -9,11 +9,10 @@ using namespace fts;
 // 2-pair Miller loops, sextet layout: 10 jobs per 64-lane wave (lanes 60..63
 // shadow the last sextet read-only), one wave per workgroup.
 __global__ void __launch_bounds__(64, 2) k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines,
-                                               const G1Dev* g1out, const G1Dev* pts, const G2Dev* g2out,
-                                               F12Dev* fbuf) {
-  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_MILLER];
+                                                  const EvLineDev* lines2, const G1Dev* g1out, F12Dev* fbuf) {
+  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_MILLER_F];
   SX_KERNEL_PROLOGUE(n);
-  sx_job_miller(x, jobs[jc], qlines, g1out, pts, g2out, fbuf, jc, valid);
+  sx_job_miller(x, jobs[jc], qlines, lines2, g1out, fbuf, jc, n, valid);
 }
 
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n) {

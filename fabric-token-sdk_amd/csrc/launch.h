@@ -38,8 +38,10 @@ __global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev
                      const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
 __global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
 __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out);
+__global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
+                          G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
-__global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines, const G1Dev* g1out,
-                         const G1Dev* pts, const G2Dev* g2out, F12Dev* fbuf);
+__global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines, const EvLineDev* lines2,
+                         const G1Dev* g1out, F12Dev* fbuf);
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);

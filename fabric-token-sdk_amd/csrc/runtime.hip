@@ -60,7 +60,7 @@ struct DBuf {
 
 struct ftz_ctx {
   int device = 0;
-  hipStream_t stream = nullptr, stream2 = nullptr;
+  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
   PPInfo pp;
   std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
   DBuf<G1Dev> g1tab;
@@ -91,9 +91,10 @@ struct ftz_batch {
   DBuf<G2Dev> g2out;
   DBuf<uint32_t> scal;  // 8 limbs per scalar
   DBuf<F12Dev> fbuf;
+  DBuf<EvLineDev> lines2;  // pair-2 Miller lines, [line][pair job]
   DBuf<int32_t> codes;
   DBuf<uint32_t> bitmap;
-  hipEvent_t ev[14];
+  hipEvent_t ev[16];
   bool ev_init = false;
   ftz_stats stats;
 };
@@ -124,8 +125,13 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
     delete c;
     return set_err(FTZ_E_PP, e);
   }
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess) {
+  // The pairing chain (stream, stream3) gets the higher priority: the G1 jobs
+  // no pairing depends on (stream2) fill the SIMDs the chain leaves idle.
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
     delete c;
     return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
   }
@@ -241,6 +247,7 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
   if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -288,6 +295,10 @@ static int batch_upload(ftz_batch* b) {
   HC(b->g1out.alloc(std::max<uint32_t>(p.n_g1out, 1)));
   HC(b->g2out.alloc(std::max<uint32_t>(p.n_g2out, 1)));
   HC(b->fbuf.alloc(std::max<size_t>(p.pr.size(), 1)));
+  HC(b->lines2.alloc(std::max<size_t>(p.pr.size(), 1) * MILLER_LINES));
+  if (p.g2.size() != p.pr.size()) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
+  for (size_t i = 0; i < p.pr.size(); i++)
+    if (p.pr[i].q2 != p.g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   HC(b->hash_ok.alloc(std::max<size_t>(p.hmain.size(), 1)));
   HC(b->hash_ok_pre.alloc(std::max<size_t>(p.hpre.size(), 1)));
   HC(b->codes.alloc(std::max<size_t>(b->n, 1)));
@@ -295,7 +306,7 @@ static int batch_upload(ftz_batch* b) {
   HC(hipMemsetAsync(b->pt_ok.p, 1, std::max<uint32_t>(p.n_pts, 1), s));
   HC(hipStreamSynchronize(s));
   if (!b->ev_init) {
-    for (int k = 0; k < 14; k++) HC(hipEventCreate(&b->ev[k]));
+    for (int k = 0; k < 16; k++) HC(hipEventCreate(&b->ev[k]));
     b->ev_init = true;
   }
   return FTZ_SUCCESS;
@@ -346,18 +357,20 @@ extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, 
   return FTZ_SUCCESS;
 }
 
-// Two streams: the chain that feeds the pairings (G1 jobs of P1 = sbf*P - c*S,
-// G2, Miller, final exponentiation) runs on the main stream while the G1 jobs
-// that do not feed a pairing (well-formedness, range equality, membership
-// Schnorr commitments) run concurrently on a side stream, filling the SIMDs the
-// pairing kernels leave idle; the transcript hashes wait for both.
+// Three streams after the light decode/scalar kernels:
+//   stream3: G2 jobs t' and the pair-2 Miller lines evaluated at R (k_g2lines)
+//   stream : G1 jobs feeding the pairings (P1 = sbf*P - c*S), then, after
+//            stream3, the sextet Miller loops and final exponentiations
+//   stream2: the G1 jobs no pairing depends on (well-formedness, range
+//            equality, membership Schnorr commitments)
+// The transcript hashes wait for all three.
 extern "C" int ftz_batch_run(ftz_batch* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null batch");
   ftz_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
-  hipStream_t s = c->stream, s2 = c->stream2;
+  hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
   uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
@@ -377,7 +390,14 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   HC(hipEventRecord(e[3], s));
   if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
   HC(hipEventRecord(e[4], s));
-  // side stream: pairing-independent G1 jobs
+  // stream3: G2 jobs + pair-2 lines
+  HC(hipStreamWaitEvent(s3, e[4], 0));
+  HC(hipEventRecord(e[14], s3));
+  if (n_g2)
+    k_g2lines<<<blocks_for(n_g2, 64), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p, b->g2out.p, b->pts.p,
+                                                   b->lines2.p);
+  HC(hipEventRecord(e[15], s3));
+  // stream2: pairing-independent G1 jobs
   HC(hipStreamWaitEvent(s2, e[4], 0));
   HC(hipEventRecord(e[11], s2));
   if (n_g1)
@@ -389,11 +409,11 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
     k_g1<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
                                                 b->arena.p);
   HC(hipEventRecord(e[5], s));
-  if (n_g2) k_g2<<<blocks_for(n_g2, 128), 128, 0, s>>>(b->g2.p, n_g2, scal, c->g2tab.p, b->g2out.p);
+  HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (n_pr)
-    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->g1out.p, b->pts.p, b->g2out.p,
-                                                 b->fbuf.p);
+    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->lines2.p, b->g1out.p,
+                                                               b->fbuf.p);
   HC(hipEventRecord(e[7], s));
   if (n_pr) k_fexp<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
   HC(hipEventRecord(e[8], s));
@@ -409,9 +429,9 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   HC(hipEventRecord(e[13], s));
   HC(hipGetLastError());
   HC(hipStreamSynchronize(s));
-  // stats order: decode zr hash_pre scalar g1p g2 miller fexp g1(side) hash verdict total
-  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 5, 6, 7, 11, 9, 10, 0};
-  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 6, 7, 8, 12, 10, 13, 13};
+  // stats order: decode zr hash_pre scalar g1p g2+lines miller fexp g1(side) hash verdict total
+  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 14, 6, 7, 11, 9, 10, 0};
+  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
   for (int k = 0; k < FTZ_NKERNELS; k++) {
     float ms = 0;
     HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
@@ -449,7 +469,7 @@ extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
   if (b->ev_init)
-    for (int k = 0; k < 14; k++) (void)hipEventDestroy(b->ev[k]);
+    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev[k]);
   delete b;
 }
 

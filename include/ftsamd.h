@@ -69,7 +69,7 @@ typedef struct {
 /* Per-kernel timing of the last ftz_batch_run (HIP events on the batch stream). */
 #define FTZ_NKERNELS 12
 typedef struct {
-  /* decode, zr, hash_pre, scalar, g1_pairing, g2, miller, fexp, g1_side (concurrent stream), hash,
+  /* decode, zr, hash_pre, scalar, g1_pairing, g2 + pair-2 lines (stream 3), miller, fexp, g1_side (stream 2), hash,
    * verdict, total */
   float ms[FTZ_NKERNELS];
   uint64_t jobs[FTZ_NKERNELS];

@@ -10,7 +10,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../fabric-token-sdk_amd/csrc/dev/sextet.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 
 using namespace fts;
 
@@ -157,6 +157,12 @@ int sxe_miller(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2, const ui
   fp12 want = miller_2(ql.data(), P1, P2, Q2);
   fp2 got[6];
   run6([&](const SxH& x) { got[x.k] = sx_miller_2(x, ql.data(), P1, P2, Q2); });
+  // the production path: pair-2 lines precomputed (g2lines_emit), f-chain only
+  std::vector<EvLineDev> l2(MILLER_LINES);
+  g2lines_emit(Q2, P2, l2.data(), 0, 1);
+  fp2 got2[6];
+  run6([&](const SxH& x) { got2[x.k] = sx_miller_f(x, ql.data(), P1, l2.data(), 1); });
+  if (!f12_eq(from_coefs(got2), want)) return 2;
   f12_to_bytes(out_ref, want);
   f12_to_bytes(out_sx, from_coefs(got));
   return memcmp(out_sx, out_ref, 384) != 0;
