@@ -17,6 +17,7 @@
 // issue.Verifier.Verify (issue/issue.go:202), TransferZKProofValidate
 // (validator/validator_transfer.go:84-98).
 #pragma once
+#include "fp_wide.h"
 #include "pairing.h"
 #include "sha256.h"
 
@@ -397,24 +398,113 @@ FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]
   return acc;
 }
 
+// ---- GLV variable-base multiplication on G1 (phi(x, y) = (beta x, y) = [lambda]).
+// r[na + nb] = a[na] * b[nb]  (schoolbook, small operands)
+FTS_HD void mul_small(uint32_t* r, const uint32_t* a, int na, const uint32_t* b, int nb) {
+  for (int i = 0; i < na + nb; i++) r[i] = 0;
+  for (int i = 0; i < na; i++) {
+    uint32_t c = 0;
+    for (int j = 0; j < nb; j++) {
+      uint64_t t = (uint64_t)a[i] * b[j] + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = (uint32_t)(t >> 32);
+    }
+    r[i + nb] = c;
+  }
+}
+
+// k = k1 + k2 lambda (mod r) with |k1|, |k2| < 2^128 (constants from
+// gen_constants.py: c1 = (k g1) >> 256, c2 = (k g2) >> 256, k2 = c1 |b1| - c2 b2,
+// k1 = k - k2 lambda mod r taken in (-r/2, r/2]).
+FTS_HD void glv_split(const uint32_t k[8], uint32_t k1[4], bool& n1, uint32_t k2[4], bool& n2) {
+  uint32_t g[8], w[16], c1[4], c2[4];
+  for (int i = 0; i < 8; i++) g[i] = GLV_G1[i];
+  mul_wide(w, k, g);
+  for (int i = 0; i < 4; i++) c1[i] = w[8 + i];
+  for (int i = 0; i < 8; i++) g[i] = GLV_G2[i];
+  mul_wide(w, k, g);
+  for (int i = 0; i < 4; i++) c2[i] = w[8 + i];
+  uint32_t b1[2] = {GLV_B1ABS[0], GLV_B1ABS[1]}, b2[4] = {GLV_B2[0], GLV_B2[1], GLV_B2[2], GLV_B2[3]};
+  uint32_t t1[6], t2[6], d[6];
+  mul_small(t1, c1, 4, b1, 2);
+  mul_small(t2, c2, 2, b2, 4);
+  uint32_t br = 0;
+  for (int i = 0; i < 6; i++) d[i] = subb32(t1[i], t2[i], br, &br);
+  n2 = br != 0;  // |t1 - t2| < 2^128 <<< 2^192: the borrow is the sign
+  if (n2) {
+    uint32_t c = 1;
+    for (int i = 0; i < 6; i++) d[i] = addc32(~d[i], 0, c, &c);
+  }
+  for (int i = 0; i < 4; i++) k2[i] = d[i];
+  // k1 = k - k2 lambda  (mod r)
+  uint32_t k2f[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
+  fr t = fe_from_int<ModR>(k2f) * fe_const<ModR>(GLV_LAMBDA);
+  fr K = fe_from_int<ModR>(k);
+  fr r1 = n2 ? K + t : K - t;
+  uint32_t v[8], u[8], h[8], rm[8];
+  fe_to_int(v, r1);
+  for (int i = 0; i < 8; i++) {
+    h[i] = R_HALF[i];
+    rm[i] = R_MOD[i];
+  }
+  n1 = sub8(u, h, v) != 0;  // v > (r-1)/2
+  if (n1) sub8(v, rm, v);
+  for (int i = 0; i < 4; i++) k1[i] = v[i];
+}
+
+// k P for affine P and a scalar k < r.  Joint double-and-add over the two
+// 128-bit GLV halves (Shamir): one mixed addition per bit with the operand
+// chosen among P', phi(P)', P' + phi(P)' -- uniform across the wave.
+FTS_HDN g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
+  g1j acc = jac_inf<fp>();
+  if (p.inf) return acc;
+  uint32_t k1[4], k2[4];
+  bool n1, n2;
+  glv_split(k, k1, n1, k2, n2);
+  g1a P1 = n1 ? aff_neg(p) : p;
+  g1a P2;
+  P2.x = p.x * fe_const<ModP>(GLV_BETA);
+  P2.y = n2 ? fe_neg(p.y) : p.y;
+  P2.inf = false;
+  g1a S = jac_to_aff(jac_add_aff(jac_from_aff(P1), P2));  // P1 != +-P2 for points of order r
+#pragma nounroll
+  for (int i = 127; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1, b2 = (k2[i >> 5] >> (i & 31)) & 1;
+    g1a T;
+    T.x = b1 ? (b2 ? S.x : P1.x) : P2.x;
+    T.y = b1 ? (b2 ? S.y : P1.y) : P2.y;
+    T.inf = false;
+    g1j nacc = jac_add_aff(acc, T);
+    if (b1 | b2) acc = nacc;
+  }
+  return acc;
+}
+
 FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const uint32_t (*scal)[8],
                    const G1Dev* tab, G1Dev* g1out, uint8_t* arena) {
   g1j acc = jac_inf<fp>();
   if (j.vscal != NONE) {
-    g1j V = jac_inf<fp>();
-    for (uint32_t t = 0; t < j.vcount; t++) {
-      const VTerm& vt = vterms[j.vstart + t];
-      g1a P = g1_load(pts[vt.pt]);
-      uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
-      if (w == 1) {
-        V = jac_add_aff(V, P);
-      } else {
-        V = jac_add(V, aff_mul_u64(P, w));
+    g1a Va;
+    const VTerm& v0 = vterms[j.vstart];
+    if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
+      Va = g1_load(pts[v0.pt]);  // a single unit-weight point is already affine
+    } else {
+      g1j V = jac_inf<fp>();
+      for (uint32_t t = 0; t < j.vcount; t++) {
+        const VTerm& vt = vterms[j.vstart + t];
+        g1a P = g1_load(pts[vt.pt]);
+        uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
+        if (w == 1) {
+          V = jac_add_aff(V, P);
+        } else {
+          V = jac_add(V, aff_mul_u64(P, w));
+        }
       }
+      Va = jac_to_aff(V);
     }
-    g1a Va = jac_to_aff(V);
     if (j.vneg) Va = aff_neg(Va);
-    acc = aff_mul(Va, scal[j.vscal]);
+    acc = g1_mul_glv(Va, scal[j.vscal]);
   }
   for (int f = 0; f < j.nfix; f++) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
   g1a r = jac_to_aff(acc);
