@@ -62,7 +62,7 @@ FTS_HD Jac<F> jac_neg(const Jac<F>& a) {
 
 // dbl-2009-l (a = 0): 2M + 5S
 template <class F>
-FTS_HDN Jac<F> jac_dbl(const Jac<F>& p) {
+FTS_HD Jac<F> jac_dbl(const Jac<F>& p) {
   F A = sqr(p.x);
   F B = sqr(p.y);
   F C = sqr(B);
@@ -83,7 +83,7 @@ FTS_HDN Jac<F> jac_dbl(const Jac<F>& p) {
 
 // madd-2007-bl: Jacobian + affine, 7M + 4S, with the exceptional cases
 template <class F>
-FTS_HDN Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
+FTS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   if (q.inf) return p;
   if (is_zero(p.z)) return {q.x, q.y, one_of<F>()};
   F Z1Z1 = sqr(p.z);

@@ -455,7 +455,7 @@ FTS_HD void glv_split(const uint32_t k[8], uint32_t k1[4], bool& n1, uint32_t k2
 // k P for affine P and a scalar k < r.  Joint double-and-add over the two
 // 128-bit GLV halves (Shamir): one mixed addition per bit with the operand
 // chosen among P', phi(P)', P' + phi(P)' -- uniform across the wave.
-FTS_HDN g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
+FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
   g1j acc = jac_inf<fp>();
   if (p.inf) return acc;
   uint32_t k1[4], k2[4];
@@ -467,10 +467,22 @@ FTS_HDN g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
   P2.y = n2 ? fe_neg(p.y) : p.y;
   P2.inf = false;
   g1a S = jac_to_aff(jac_add_aff(jac_from_aff(P1), P2));  // P1 != +-P2 for points of order r
+  // the scalars are consumed from the top bit by shifting them left (a
+  // dynamically indexed limb array would live in scratch memory)
+  uint32_t u0 = k1[0], u1 = k1[1], u2 = k1[2], u3 = k1[3];
+  uint32_t v0 = k2[0], v1 = k2[1], v2 = k2[2], v3 = k2[3];
 #pragma nounroll
   for (int i = 127; i >= 0; i--) {
     acc = jac_dbl(acc);
-    uint32_t b1 = (k1[i >> 5] >> (i & 31)) & 1, b2 = (k2[i >> 5] >> (i & 31)) & 1;
+    uint32_t b1 = u3 >> 31, b2 = v3 >> 31;
+    u3 = (u3 << 1) | (u2 >> 31);
+    u2 = (u2 << 1) | (u1 >> 31);
+    u1 = (u1 << 1) | (u0 >> 31);
+    u0 <<= 1;
+    v3 = (v3 << 1) | (v2 >> 31);
+    v2 = (v2 << 1) | (v1 >> 31);
+    v1 = (v1 << 1) | (v0 >> 31);
+    v0 <<= 1;
     g1a T;
     T.x = b1 ? (b2 ? S.x : P1.x) : P2.x;
     T.y = b1 ? (b2 ? S.y : P1.y) : P2.y;
@@ -630,6 +642,139 @@ FTS_HD void job_g2lines(const G2Job& g, const PairJob& j, const uint32_t (*scal)
                         G2Dev* g2out, const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
   job_g2(g, scal, tab, g2out);
   g2lines_emit(g2_load(g2out[g.out]), g1_load(pts[j.p2]), lines, idx, njobs);
+}
+
+// Sextet form of job_g2lines (same values): six lanes per membership digit.
+//  phase A  t' = sum over (base, window) of table points: lane k takes the
+//           pairs k, k+6, ... (16 mixed additions), then a 3-level tree of
+//           Jacobian additions through LDS and one affine conversion;
+//  phase B  the 88 Miller lines of t': each doubling / addition step runs as
+//           layers of one reduced Fp2 product per lane (dbl_step / add_step
+//           formulas), the running point T held identically by every lane;
+//           lanes 0..2 write the three evaluated coefficients of each line.
+template <class X>
+FTS_HD void sx_job_g2lines(const X& x, const G2Job& g, const PairJob& j, const uint32_t (*scal)[8],
+                           const G2Dev* tab, G2Dev* g2out, const G1Dev* pts, EvLineDev* lines, uint32_t idx,
+                           uint32_t njobs, bool valid) {
+  const int k = x.k;
+  // ---- phase A
+  g2j acc = jac_inf<fp2>();
+#pragma nounroll
+  for (int p = k; p < 3 * TAB_WINDOWS; p += 6) {
+    int f = p / TAB_WINDOWS, w = p % TAB_WINDOWS;
+    if (f < g.nfix) {
+      uint32_t d = (scal[g.fscal[f]][w >> 2] >> ((w & 3) * 8)) & 0xFF;
+      if (d) acc = jac_add_aff(acc, g2_load(tab_at(tab, g.fbase[f], w, (int)d)));
+    }
+  }
+  x.put(3 * k + 0, acc.x);
+  x.put(3 * k + 1, acc.y);
+  x.put(3 * k + 2, acc.z);
+  x.sync();
+  if (k < 3) acc = jac_add(acc, g2j{x.get(3 * k + 9), x.get(3 * k + 10), x.get(3 * k + 11)});
+  x.sync();
+  if (k < 3) {
+    x.put(3 * k + 0, acc.x);
+    x.put(3 * k + 1, acc.y);
+    x.put(3 * k + 2, acc.z);
+  }
+  x.sync();
+  acc = jac_add(g2j{x.get(0), x.get(1), x.get(2)}, g2j{x.get(3), x.get(4), x.get(5)});
+  acc = jac_add(acc, g2j{x.get(6), x.get(7), x.get(8)});
+  x.sync();
+  g2a Q = jac_to_aff(acc);
+  if (valid && k == 0) {
+    G2Dev d;
+    g2_store(d, Q);
+    g2out[g.out] = d;
+  }
+  // ---- phase B
+  g1a P = g1_load(pts[j.p2]);
+  bool use = !(P.inf || Q.inf);
+  const fp2 yP = f2_of_fp(P.y), xP = f2_of_fp(P.x), b3 = f2_const(TWIST_B);
+  fp2 TX = Q.x, TY = Q.y, TZ = f2_one();
+  int i = 64, sign = 0;
+  bool pend = false;
+#pragma nounroll
+  for (int s = 0; s < MILLER_LINES; s++) {
+    // line type: doubling, addition of +-Q (NAF digit), or a Frobenius line
+    bool dbl = false;
+    g2a Qa = Q;
+    if (s >= MILLER_LINES - 2) {
+      Qa = (s == MILLER_LINES - 2) ? tw_frob(Q) : tw_frob2_neg(Q);
+    } else if (!pend) {
+      dbl = true;
+      sign = naf_digit(i);
+      pend = sign != 0;
+      if (!pend) i--;
+    } else {
+      if (sign < 0) Qa = aff_neg(Q);
+      pend = false;
+      i--;
+    }
+    fp2 l0, l1, l3;
+    if (dbl) {
+      // dbl_step: A = XY/2, B = Y^2, C = Z^2, E = 3C b', F = 3E, G = (B+F)/2,
+      // H = (Y+Z)^2 - (B+C), I = E - B, J = X^2; line (-H, 3J, I)
+      fp2 YZ = TY + TZ;
+      x.put(SX_P + k, f2_pick(k, TX, TY, TZ, YZ, TX, TX) * f2_pick(k, TY, TY, TZ, YZ, TX, TX));
+      x.sync();
+      fp2 A = f2_half(x.get(SX_P + 0)), B = x.get(SX_P + 1), C = x.get(SX_P + 2);
+      fp2 H = x.get(SX_P + 3) - (B + C), J = x.get(SX_P + 4);
+      x.sync();
+      x.put(SX_P + k, f2_pick(k, C + C + C, f2_neg(H), J + J + J, C, C, C) * f2_pick(k, b3, yP, xP, b3, b3, b3));
+      x.sync();
+      fp2 E = x.get(SX_P + 0);
+      l0 = x.get(SX_P + 1);
+      l1 = x.get(SX_P + 2);
+      x.sync();
+      l3 = E - B;
+      fp2 F = E + E + E, G = f2_half(B + F);
+      x.put(SX_P + k, f2_pick(k, A, G, E, B, A, A) * f2_pick(k, B - F, G, E, H, B, B));
+      x.sync();
+      TX = x.get(SX_P + 0);
+      fp2 EE = x.get(SX_P + 2);
+      TY = x.get(SX_P + 1) - (EE + EE + EE);
+      TZ = x.get(SX_P + 3);
+      x.sync();
+    } else {
+      // add_step: O = Y - Qy Z, L = X - Qx Z, C = O^2, D = L^2, E = L D, F = Z C,
+      // G = X D, H = E + F - 2G; X3 = L H, Y3 = (G - H) O - Y E, Z3 = E Z;
+      // line (L, -O, Qx O - L Qy)
+      x.put(SX_P + k, f2_pick(k, Qa.y, Qa.x, Qa.y, Qa.y, Qa.y, Qa.y) * TZ);
+      x.sync();
+      fp2 O = TY - x.get(SX_P + 0), Lc = TX - x.get(SX_P + 1);
+      x.sync();
+      x.put(SX_P + k, f2_pick(k, O, Lc, Qa.x, Lc, Lc, f2_neg(O)) * f2_pick(k, O, Lc, O, Qa.y, yP, xP));
+      x.sync();
+      fp2 C = x.get(SX_P + 0), D = x.get(SX_P + 1);
+      l3 = x.get(SX_P + 2) - x.get(SX_P + 3);
+      l0 = x.get(SX_P + 4);
+      l1 = x.get(SX_P + 5);
+      x.sync();
+      x.put(SX_P + k, f2_pick(k, Lc, TZ, TX, Lc, Lc, Lc) * f2_pick(k, D, C, D, D, D, D));
+      x.sync();
+      fp2 E = x.get(SX_P + 0), F = x.get(SX_P + 1), G = x.get(SX_P + 2);
+      x.sync();
+      fp2 H = E + F - (G + G);
+      x.put(SX_P + k, f2_pick(k, TY, Lc, G - H, E, E, E) * f2_pick(k, E, H, O, TZ, TZ, TZ));
+      x.sync();
+      fp2 t1 = x.get(SX_P + 0);
+      TX = x.get(SX_P + 1);
+      TY = x.get(SX_P + 2) - t1;
+      TZ = x.get(SX_P + 3);
+      x.sync();
+    }
+    if (valid && k < 3) {
+      fp2 v = f2_pick(k, use ? l0 : f2_one(), use ? l1 : f2_zero(), use ? l3 : f2_zero(), l0, l0, l0);
+      uint32_t* o = &lines[(size_t)s * njobs + idx].w[16 * k];
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        o[q] = v.c0.v[q];
+        o[8 + q] = v.c1.v[q];
+      }
+    }
+  }
 }
 
 template <class X>

@@ -8,6 +8,7 @@
 // job kernels on one HIP stream (see dev/jobs.h for the job model).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -371,6 +372,10 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
   hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
+  // FTZ_SERIAL=1: run every kernel on one stream (per-kernel timings without
+  // overlap, for profiling)
+  static const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';
+  if (serial) s2 = s3 = s;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
   uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
@@ -394,7 +399,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   HC(hipStreamWaitEvent(s3, e[4], 0));
   HC(hipEventRecord(e[14], s3));
   if (n_g2)
-    k_g2lines<<<blocks_for(n_g2, 64), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p, b->g2out.p, b->pts.p,
+    k_g2lines<<<blocks_for(n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p, b->g2out.p, b->pts.p,
                                                    b->lines2.p);
   HC(hipEventRecord(e[15], s3));
   // stream2: pairing-independent G1 jobs

@@ -168,4 +168,40 @@ int sxe_miller(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2, const ui
   return memcmp(out_sx, out_ref, 384) != 0;
 }
 
+// G2 job + pair-2 lines: sextet (sx_job_g2lines) vs one lane (job_g2lines).
+// bases: 3 G2 RawBytes (PK0..2), p2: G1 RawBytes (R), scalars: 3 x 32 bytes BE.
+// Only the table entries the scalars touch are built.
+int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars) {
+  std::vector<G2Dev> b(4);
+  for (int i = 0; i < 3; i++) g2_store(b[i], ld_g2(bases + 128 * i));
+  std::vector<uint32_t> sc(8 * 3);
+  for (int i = 0; i < 3; i++) be32_to_limbs(&sc[8 * i], scalars + 32 * i);
+  std::vector<G2Dev> tab((size_t)G2B_COUNT * TAB_WINDOWS * TAB_DIGITS);
+  for (int f = 0; f < 3; f++)
+    for (int w = 0; w < TAB_WINDOWS; w++) {
+      uint32_t d = (sc[8 * f + (w >> 2)] >> ((w & 3) * 8)) & 0xFF;
+      if (d) job_tab_g2((uint32_t)((f * TAB_WINDOWS + w) * TAB_DIGITS + d), b.data(), tab.data());
+    }
+  G2Job g;
+  memset(&g, 0, sizeof(g));
+  g.nfix = 3;
+  for (int f = 0; f < 3; f++) {
+    g.fbase[f] = (uint8_t)f;
+    g.fscal[f] = (uint32_t)f;
+  }
+  g.out = 0;
+  G1Dev pt;
+  g1_store(pt, ld_g1(p2));
+  PairJob j = {0, 0, 0, 0};
+  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(sc.data());
+  std::vector<G2Dev> o1(1), o2(1);
+  std::vector<EvLineDev> l1(MILLER_LINES), l2(MILLER_LINES);
+  job_g2lines(g, j, scal, tab.data(), o1.data(), &pt, l1.data(), 0, 1);
+  run6([&](const SxH& x) { sx_job_g2lines(x, g, j, scal, tab.data(), o2.data(), &pt, l2.data(), 0, 1, true); });
+  if (memcmp(o1.data(), o2.data(), sizeof(G2Dev))) return 1;
+  for (int s = 0; s < MILLER_LINES; s++)
+    if (memcmp(&l1[s], &l2[s], sizeof(EvLineDev))) return 2 + s;
+  return 0;
+}
+
 }  // extern "C"

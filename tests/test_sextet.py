@@ -42,3 +42,16 @@ def test_sextet_miller(sx, case):
         q2 = bytes(128)
     a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
     assert sx.sxe_miller(p1, p2, q2, qf, a, b) == 0
+
+
+@pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar"])
+def test_sextet_g2_lines(sx, case):
+    """G2 fixed-base combination + the 88 evaluated pair-2 lines, six lanes vs one."""
+    rng = random.Random("g2" + case)
+    bases = b"".join(C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))) for _ in range(3))
+    p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "r_infinity" else bytes(64)
+    ks = [rng.randrange(C.R) for _ in range(3)]
+    if case == "zero_scalar":
+        ks[1] = 0
+    scal = b"".join(k.to_bytes(32, "big") for k in ks)
+    assert sx.sxe_g2lines(bases, p2, scal) == 0
