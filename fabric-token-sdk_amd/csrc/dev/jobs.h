@@ -526,6 +526,75 @@ FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const 
   if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
 }
 
+// ---- G1 jobs split into uniform parts (device path): item i of [0, 4n) is
+// fixed-base slot f = i / n (0..2) or the variable part (f = 3) of job i % n;
+// job_g1_combine adds the parts and converts to affine.  Same point as job_g1.
+struct G1JDev {
+  uint32_t x[8], y[8], z[8];  // Jacobian (Montgomery); z = 0: infinity
+};
+FTS_HD void g1j_store(G1JDev& d, const g1j& p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.x[i] = p.x.v[i];
+    d.y[i] = p.y.v[i];
+    d.z[i] = p.z.v[i];
+  }
+}
+FTS_HD g1j g1j_load(const G1JDev& d) {
+  g1j p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p.x.v[i] = d.x[i];
+    p.y.v[i] = d.y[i];
+    p.z.v[i] = d.z[i];
+  }
+  return p;
+}
+
+FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* vterms, const G1Dev* pts,
+                        const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part) {
+  uint32_t f = i / n, jb = i - f * n;
+  const G1Job& j = jobs[jb];
+  g1j acc = jac_inf<fp>();
+  if (f < 3) {
+    if (f < j.nfix) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
+  } else if (j.vscal != NONE) {
+    g1a Va;
+    const VTerm& v0 = vterms[j.vstart];
+    if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
+      Va = g1_load(pts[v0.pt]);
+    } else {
+      g1j V = jac_inf<fp>();
+      for (uint32_t t = 0; t < j.vcount; t++) {
+        const VTerm& vt = vterms[j.vstart + t];
+        g1a P = g1_load(pts[vt.pt]);
+        uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
+        if (w == 1) {
+          V = jac_add_aff(V, P);
+        } else {
+          V = jac_add(V, aff_mul_u64(P, w));
+        }
+      }
+      Va = jac_to_aff(V);
+    }
+    if (j.vneg) Va = aff_neg(Va);
+    acc = g1_mul_glv(Va, scal[j.vscal]);
+  }
+  g1j_store(part[i], acc);
+}
+
+FTS_HD void job_g1_combine(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev* part, G1Dev* g1out,
+                           uint8_t* arena) {
+  g1j acc = g1j_load(part[3 * (size_t)n + jb]);
+  for (uint32_t f = 0; f < 3; f++)
+    if (f < j.nfix) acc = jac_add(acc, g1j_load(part[(size_t)f * n + jb]));
+  g1a r = jac_to_aff(acc);
+  G1Dev d;
+  g1_store(d, r);
+  g1out[j.out] = d;
+  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+}
+
 FTS_HD void job_g2(const G2Job& j, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out) {
   g2j acc = jac_inf<fp2>();
   for (int f = 0; f < j.nfix; f++) acc = g2_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);

@@ -36,6 +36,9 @@ __global__ void k_pp_decode(const uint8_t* raw, const uint32_t* g1off, uint32_t 
                             uint32_t n2, G1Dev* g1, G2Dev* g2, uint8_t* g1bytes, uint8_t* g2bytes, uint8_t* ok);
 __global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts, const uint32_t (*scal)[8],
                      const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
+__global__ void k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
+                          const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part);
+__global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena);
 __global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
 __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out);
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,

@@ -93,6 +93,7 @@ struct ftz_batch {
   DBuf<uint32_t> scal;  // 8 limbs per scalar
   DBuf<F12Dev> fbuf;
   DBuf<EvLineDev> lines2;  // pair-2 Miller lines, [line][pair job]
+  DBuf<G1JDev> part1, part1p;  // G1 job parts (4 per job) of the side / pairing G1 jobs
   DBuf<int32_t> codes;
   DBuf<uint32_t> bitmap;
   hipEvent_t ev[16];
@@ -297,6 +298,8 @@ static int batch_upload(ftz_batch* b) {
   HC(b->g2out.alloc(std::max<uint32_t>(p.n_g2out, 1)));
   HC(b->fbuf.alloc(std::max<size_t>(p.pr.size(), 1)));
   HC(b->lines2.alloc(std::max<size_t>(p.pr.size(), 1) * MILLER_LINES));
+  HC(b->part1.alloc(4 * std::max<size_t>(p.g1.size(), 1)));
+  HC(b->part1p.alloc(4 * std::max<size_t>(p.g1p.size(), 1)));
   if (p.g2.size() != p.pr.size()) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   for (size_t i = 0; i < p.pr.size(); i++)
     if (p.pr[i].q2 != p.g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
@@ -405,14 +408,18 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   // stream2: pairing-independent G1 jobs
   HC(hipStreamWaitEvent(s2, e[4], 0));
   HC(hipEventRecord(e[11], s2));
-  if (n_g1)
-    k_g1<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
-                                                b->arena.p);
+  if (n_g1) {
+    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
+                                                         b->part1.p);
+    k_g1_combine<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+  }
   HC(hipEventRecord(e[12], s2));
   // main stream: pairing chain
-  if (n_g1p)
-    k_g1<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p, b->g1out.p,
-                                                b->arena.p);
+  if (n_g1p) {
+    k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
+                                                         b->part1p.p);
+    k_g1_combine<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
+  }
   HC(hipEventRecord(e[5], s));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));

@@ -124,9 +124,15 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   par_for((uint32_t)p.zr.size(), [&](uint32_t i) { job_zr(p.zr[i], wire.data(), scal, canon.data()); });
   par_for((uint32_t)p.hpre.size(), [&](uint32_t i) { hpok[i] = job_hash(p.hpre[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   par_for((uint32_t)p.sc.size(), [&](uint32_t i) { job_scalar(p.sc[i], scal, p.sclist.data()); });
-  par_for((uint32_t)p.g1.size(), [&](uint32_t i) {
-    job_g1(p.g1[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
-  });
+  // side G1 jobs through the device's split path (parts + combine), pairing G1 jobs whole (job_g1)
+  {
+    uint32_t n1 = (uint32_t)p.g1.size();
+    std::vector<G1JDev> part(4 * (size_t)std::max<uint32_t>(n1, 1));
+    par_for(4 * n1, [&](uint32_t i) {
+      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data());
+    });
+    par_for(n1, [&](uint32_t i) { job_g1_combine(p.g1[i], i, n1, part.data(), g1out.data(), p.arena.data()); });
+  }
   par_for((uint32_t)p.g1p.size(), [&](uint32_t i) {
     job_g1(p.g1p[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
   });
