@@ -91,6 +91,34 @@ def madpeak(device):
     return max(lib.ftz_madpeak(device, 20000) for _ in range(3))
 
 
+def msm_latency(ctx, lg, reps=5, seed=7):
+    """BASELINE configs[2]: latency of one BN254 G1 MSM of 2^lg points resident
+    in HBM (P_i = (i + 1) G generated on the device, random 256-bit scalars),
+    median wall-clock of `reps` synchronous runs after one warm-up; the result
+    must be identical on every run (tests/test_msm.py checks it bit-exactly)."""
+    import zkatdlog
+    n = 1 << lg
+    import numpy as np
+    scal = np.random.default_rng(seed + lg).bytes(32 * n)
+    m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
+    try:
+        first = m.run()
+        wall, dev = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = m.run()
+            wall.append((time.perf_counter() - t0) * 1e3)
+            dev.append(m.info()["last_ms"])
+            assert out == first, "MSM result changed between runs"
+        info = m.info()
+    finally:
+        m.close()
+    wall.sort()
+    dev.sort()
+    return {"n": n, "ms": round(wall[reps // 2], 3), "device_ms": round(dev[reps // 2], 3),
+            "window_bits": info["window_bits"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -99,6 +127,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096, help="transfers per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,6 +192,8 @@ def main():
                         "traffic": None,
                         "note": "integer VALU roofline (v_mad_u64_u32); work = counted Montgomery products "
                                 "x 136 MAD; HBM traffic ~2 KB/tx is not a bound"}
+        msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
+        msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(pp_json, items, expect, args.cpu_seconds)
@@ -179,7 +210,7 @@ def main():
             "kernel_ms": {k: round(v[0], 3) for k, v in stats.items()},
             "plan_upload_s": round(t_plan, 3),
             "roofline": roof, "cpu_baseline": cpu,
-            "msm_2^20_latency_ms": None,
+            "msm_2^20_latency_ms": msm20, "msm": msm,
         }
         print(json.dumps(line), flush=True)
     batch.close()

@@ -24,7 +24,7 @@ ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH]
 
-SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip"))) + [os.path.join(CSRC, "runtime.hip")]
+SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip"))) + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "msm_rt.hip")]
            + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))))
 
 

@@ -109,9 +109,10 @@ FTS_HD Jac<F> jac_add_aff(const Jac<F>& p, const Aff<F>& q) {
   return {X3, Y3, Z3};
 }
 
-// add-2007-bl: Jacobian + Jacobian, 11M + 5S
+// add-2007-bl: Jacobian + Jacobian, 11M + 5S (inline body; jac_add below is
+// the out-of-line call most sites use to keep code size down)
 template <class F>
-FTS_HDN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+FTS_HD Jac<F> jac_add_inl(const Jac<F>& p, const Jac<F>& q) {
   if (is_zero(p.z)) return q;
   if (is_zero(q.z)) return p;
   F Z1Z1 = sqr(p.z);
@@ -137,6 +138,11 @@ FTS_HDN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
   F t = p.z + q.z;
   F Z3 = (sqr(t) - Z1Z1 - Z2Z2) * H;
   return {X3, Y3, Z3};
+}
+
+template <class F>
+FTS_HDN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
+  return jac_add_inl(p, q);
 }
 
 template <class F>

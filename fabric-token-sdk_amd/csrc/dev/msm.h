@@ -1,0 +1,176 @@
+// BN254 G1 multi-scalar multiplication  sum_i k_i P_i  (Pippenger, signed
+// c-bit windows), the standalone MSM of BASELINE.json configs[2].  The
+// reference path has no MSM; the operation is what
+// mathlib exposes from gnark-crypto v0.6.0 as G1Jac.MultiExp [EXT]: the result
+// is the unique group element, so any correct bucket order gives the same bytes.
+//
+// Pipeline (k_msm.hip; every stage one lane per item):
+//   digits    k_i -> W signed digits d in [-2^(c-1), 2^(c-1)]; bucket |d|-1,
+//             counted per (window, bucket)
+//   scan      exclusive prefix sums of the bucket counts
+//   slots     bucket b gets m_b = max(1, ceil(count_b / T)) slots of at most T
+//             points (scan of m_b -> slot offsets, slot -> bucket owner map), so
+//             that heavy buckets (the top window's few buckets, skewed scalars)
+//             are spread over several lanes
+//   scatter   (window, bucket)-sorted list of point indices (sign in bit 31)
+//   bucket    one lane per slot: Jacobian sum of its <= T points
+//   segment   one lane per run of S consecutive slots of one window: running
+//             sums give sum (b+1) S_b restricted to the run
+//   window    tree sum of the segments through LDS
+//   final     Horner over the windows, affine, gnark RawBytes
+#pragma once
+#include "jobs.h"
+
+namespace fts {
+
+struct MsmPlan {
+  uint32_t n;          // points
+  uint32_t c;          // window bits
+  uint32_t windows;    // W = ceil(255 / c)
+  uint32_t buckets;    // B = 2^(c-1) per window
+  uint32_t slot_cap;   // T: points per bucket slot
+  uint32_t seg_len;    // S: slots per segment
+  uint32_t max_slots;  // per window: B + ceil(n / T) bounds sum_b m_b
+  uint32_t segs;       // segments per window: ceil(max_slots / S)
+};
+
+FTS_HD uint32_t msm_window_bits(uint64_t n) {
+  uint32_t lg = 0;
+  while ((1ull << (lg + 1)) <= n) lg++;
+  uint32_t c = lg > 4 ? lg - 4 : 1;
+  if (c < 8) c = 8;
+  if (c > 20) c = 20;
+  return c;
+}
+
+// plan for n points with c-bit windows (0: msm_window_bits(n)), slot cap T
+// (0: twice the mean bucket load, at least 4) and S slots per segment (0: sized
+// for >= 16k segment lanes, in [4, 64])
+inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, uint32_t seg_len = 0) {
+  MsmPlan p;
+  p.n = (uint32_t)n;
+  p.c = c ? c : msm_window_bits(n);
+  p.windows = (255 + p.c - 1) / p.c;
+  p.buckets = 1u << (p.c - 1);
+  if (!slot_cap) {
+    uint64_t mean = (n + p.buckets - 1) / p.buckets;
+    slot_cap = (uint32_t)(2 * mean < 4 ? 4 : 2 * mean);
+  }
+  p.slot_cap = slot_cap;
+  p.max_slots = p.buckets + (uint32_t)((n + slot_cap - 1) / slot_cap);
+  if (!seg_len) {
+    uint64_t tot = (uint64_t)p.windows * p.max_slots;
+    seg_len = 4;
+    while (seg_len < 64 && tot / (2 * seg_len) >= 16384) seg_len *= 2;
+  }
+  p.seg_len = seg_len;
+  p.segs = (p.max_slots + seg_len - 1) / seg_len;
+  return p;
+}
+
+// Signed digits of k (8 limbs, k < 2^255) for window w: raw c-bit chunk plus the
+// carry of the window below.  Returns d in [-2^(c-1), 2^(c-1)].
+FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& carry) {
+  uint32_t bit = c * w, limb = bit >> 5, sh = bit & 31;
+  uint64_t lo = limb < 8 ? k[limb] : 0, hi = limb + 1 < 8 ? k[limb + 1] : 0;
+  uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1ull << c) - 1)) + carry;
+  if (raw > (1u << (c - 1))) {
+    carry = 1;
+    return (int32_t)raw - (int32_t)(1u << c);
+  }
+  carry = 0;
+  return (int32_t)raw;
+}
+
+// digits of point i: key[w * n + i] = bucket | sign << 31, or NONE for a zero digit
+FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key,
+                           uint32_t* count, bool atomic_count) {
+  uint32_t carry = 0;
+  for (uint32_t w = 0; w < p.windows; w++) {
+    int32_t d = msm_digit(scal[i], p.c, w, carry);
+    uint32_t kk = NONE;
+    if (d != 0) {
+      uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+      kk = b | (d < 0 ? 0x80000000u : 0u);
+      uint32_t* ct = &count[(size_t)w * p.buckets + b];
+#if defined(__HIP_DEVICE_COMPILE__)
+      (void)atomic_count;
+      atomicAdd(ct, 1u);
+#else
+      if (atomic_count)
+        __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
+      else
+        (*ct)++;
+#endif
+    }
+    key[(size_t)w * p.n + i] = kk;
+  }
+}
+
+// bucket g = w B + b: its slot count and, once the counts are scanned into
+// soff, the slot -> bucket owner map and the window slot ranges [wlo, whi)
+FTS_HD uint32_t msm_bucket_slots(const MsmPlan& p, uint32_t count) {
+  uint32_t m = (count + p.slot_cap - 1) / p.slot_cap;
+  return m ? m : 1;
+}
+
+FTS_HD void msm_job_owner(const MsmPlan& p, uint32_t g, const uint32_t* count, const uint32_t* soff,
+                          uint32_t* owner, uint32_t* wlo, uint32_t* whi) {
+  uint32_t m = msm_bucket_slots(p, count[g]), o = soff[g];
+  for (uint32_t s = 0; s < m; s++) owner[o + s] = g;
+  uint32_t w = g / p.buckets, b = g - w * p.buckets;
+  if (b == 0) wlo[w] = o;
+  if (b == p.buckets - 1) whi[w] = o + m;
+}
+
+// Jacobian sum of slot j: points [s T, s T + T) of its bucket's sorted list
+// (negated where bit 31 of the entry is set)
+FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, const uint32_t* soff,
+                        const uint32_t* start, const uint32_t* count, const uint32_t* perm, const G1Dev* pts) {
+  uint32_t g = owner[j], s = j - soff[g];
+  uint32_t lo = s * p.slot_cap, hi = lo + p.slot_cap;
+  if (hi > count[g]) hi = count[g];
+  const uint32_t* e = perm + start[g];
+  g1j acc = jac_inf<fp>();
+  for (uint32_t q = lo; q < hi; q++) {
+    uint32_t v = e[q];
+    g1a P = g1_load(pts[v & 0x7FFFFFFFu]);
+    if (v >> 31) P = aff_neg(P);
+    acc = jac_add_aff(acc, P);
+  }
+  return acc;
+}
+
+// small-scalar multiple of a Jacobian point (k < 2^32), from the top set bit
+FTS_HD g1j jac_mul_small(const g1j& p, uint32_t k) {
+  g1j acc = jac_inf<fp>();
+  if (!k) return acc;
+  acc = p;
+  int top = 31;
+  while (!((k >> top) & 1)) top--;
+  for (int i = top - 1; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    if ((k >> i) & 1) acc = jac_add_inl(acc, p);
+  }
+  return acc;
+}
+
+// Segment s of window w: slots [lo, hi) of the window's slot range, covering
+// consecutive buckets bl..bh (every bucket owns >= 1 slot).  Returns
+//   sum_slots (b + 1) P_slot = sum (b - bl + 1) P + bl sum P,
+// the first term by the running-sum trick from the top slot down.
+FTS_HD g1j msm_job_segment(const MsmPlan& p, uint32_t w, uint32_t s, const uint32_t* wlo, const uint32_t* whi,
+                           const uint32_t* owner, const G1JDev* slot_sum) {
+  uint32_t lo = wlo[w] + s * p.seg_len, hi = lo + p.seg_len;
+  if (hi > whi[w]) hi = whi[w];
+  g1j run = jac_inf<fp>(), acc = jac_inf<fp>();
+  if (lo >= hi) return acc;
+  for (uint32_t j = hi; j > lo; j--) {
+    run = jac_add_inl(run, g1j_load(slot_sum[j - 1]));
+    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = jac_add_inl(acc, run);
+  }
+  uint32_t bl = owner[lo] - w * p.buckets;
+  return jac_add_inl(acc, jac_mul_small(run, bl));
+}
+
+}  // namespace fts

@@ -1,0 +1,173 @@
+// Kernels of the standalone G1 MSM (dev/msm.h): one lane per item.
+#include <hip/hip_runtime.h>
+
+#include "dev/msm.h"
+#include "launch.h"
+
+using namespace fts;
+
+#define LANE_PROLOGUE(n)                                  \
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;     \
+  if (i >= (n)) return;
+
+// 64-byte gnark RawBytes (uncompressed, big-endian) -> Montgomery affine;
+// ok[i] = 0 for a point off the curve or not in canonical form.
+__global__ void __launch_bounds__(256) k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok) {
+  LANE_PROLOGUE(n);
+  const uint8_t* b = raw_pts + 64 * (size_t)i;
+  uint32_t x[8], y[8], t[8], mm[8];
+  be32_to_limbs(x, b);
+  be32_to_limbs(y, b + 32);
+  for (int q = 0; q < 8; q++) mm[q] = P_MOD[q];
+  bool canon = ((b[0] & 0xC0) == 0) && sub8(t, x, mm) && sub8(t, y, mm);
+  g1a a;
+  a.x = fe_from_int<ModP>(x);
+  a.y = fe_from_int<ModP>(y);
+  a.inf = is_zero(a.x) && is_zero(a.y);
+  ok[i] = (canon && g1_on_curve(a)) ? 1 : 0;
+  G1Dev d;
+  g1_store(d, a);
+  pts[i] = d;
+}
+
+// 32-byte big-endian scalars -> 8 limbs reduced mod r
+__global__ void __launch_bounds__(256) k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]) {
+  LANE_PROLOGUE(n);
+  uint32_t k[8];
+  be32_to_limbs(k, raw_scal + 32 * (size_t)i);
+  fe_to_int(scal[i], fe_from_int<ModR>(k));
+}
+
+__global__ void __launch_bounds__(256) k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
+                                                    uint32_t* count) {
+  LANE_PROLOGUE(p.n);
+  msm_job_digits(p, i, scal, key, count, true);
+}
+
+// exclusive scan, 1024 elements per workgroup; block totals to `tot`
+__global__ void __launch_bounds__(1024) k_scan_block(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tot) {
+  __shared__ uint32_t s[1024];
+  uint32_t t = threadIdx.x, i = blockIdx.x * 1024 + t;
+  uint32_t v = i < n ? in[i] : 0;
+  s[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    uint32_t a = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  if (i < n) out[i] = s[t] - v;
+  if (t == 1023) tot[blockIdx.x] = s[1023];
+}
+
+__global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add) {
+  uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  if (i < n) out[i] += add[blockIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor,
+                                                     uint32_t* perm) {
+  LANE_PROLOGUE(p.n);
+  for (uint32_t w = 0; w < p.windows; w++) {
+    uint32_t k = key[(size_t)w * p.n + i];
+    if (k == NONE) continue;
+    uint32_t pos = atomicAdd(&cursor[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)], 1u);
+    perm[pos] = i | (k & 0x80000000u);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m) {
+  LANE_PROLOGUE(p.windows * p.buckets);
+  m[i] = msm_bucket_slots(p, count[i]);
+}
+
+__global__ void __launch_bounds__(256) k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff,
+                                                   uint32_t* owner, uint32_t* wlo, uint32_t* whi) {
+  LANE_PROLOGUE(p.windows * p.buckets);
+  msm_job_owner(p, i, count, soff, owner, wlo, whi);
+}
+
+// one lane per bucket slot; the grid covers the bound W * max_slots, lanes past
+// the last window's end exit
+__global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* owner,
+                                                    const uint32_t* soff, const uint32_t* start,
+                                                    const uint32_t* count, const uint32_t* perm, const G1Dev* pts,
+                                                    G1JDev* slot_sum) {
+  LANE_PROLOGUE(whi[p.windows - 1]);
+  g1j_store(slot_sum[i], msm_job_slot(p, i, owner, soff, start, count, perm, pts));
+}
+
+__global__ void __launch_bounds__(128) k_msm_segment(MsmPlan p, const uint32_t* wlo, const uint32_t* whi,
+                                                     const uint32_t* owner, const G1JDev* slot_sum, G1JDev* part) {
+  LANE_PROLOGUE(p.windows * p.segs);
+  uint32_t w = i / p.segs, s = i - w * p.segs;
+  g1j_store(part[i], msm_job_segment(p, w, s, wlo, whi, owner, slot_sum));
+}
+
+// tree sum of m consecutive parts per window in chunks of 256: out[w][ceil(m/256)]
+__global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out) {
+  __shared__ G1JDev s[256];
+  uint32_t chunks = (m + 255) / 256;
+  uint32_t w = blockIdx.x / chunks, ch = blockIdx.x - w * chunks, t = threadIdx.x;
+  uint32_t i = ch * 256 + t;
+  g1j v = i < m ? g1j_load(in[(size_t)w * m + i]) : jac_inf<fp>();
+  g1j_store(s[t], v);
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (t < o) g1j_store(s[t], jac_add(g1j_load(s[t]), g1j_load(s[t + o])));
+    __syncthreads();
+  }
+  if (t == 0) out[(size_t)w * chunks + ch] = s[0];
+}
+
+// Horner over the window sums: sum_w 2^(c w) W_w; affine + RawBytes
+__global__ void k_msm_final(MsmPlan p, const G1JDev* wsum, G1Dev* res, uint8_t* bytes) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  g1j acc = jac_inf<fp>();
+  for (int w = (int)p.windows - 1; w >= 0; w--) {
+    for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
+    acc = jac_add_inl(acc, g1j_load(wsum[w]));
+  }
+  g1a r = jac_to_aff(acc);
+  G1Dev d;
+  g1_store(d, r);
+  *res = d;
+  g1_to_bytes(bytes, r);
+}
+
+// test points with known logs: P_i = (i + off) G from the generator's fixed-base
+// table, chunks of `chunk` consecutive points per lane made affine together
+// (Montgomery batch inversion; zs is chunk * lanes Fp of scratch)
+__global__ void __launch_bounds__(128) k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const G1Dev* gtab,
+                                                       G1JDev* jtmp, uint32_t (*zs)[8], G1Dev* pts) {
+  uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t i0 = lane * chunk;
+  if (i0 >= n) return;
+  uint32_t cnt = n - i0 < chunk ? n - i0 : chunk;
+  uint32_t k[8] = {i0 + off, 0, 0, 0, 0, 0, 0, 0};
+  g1j acc = g1_fixed_acc(jac_inf<fp>(), gtab, G1B_GEN, k);
+  g1a G = g1_load(gtab[((size_t)G1B_GEN * TAB_WINDOWS + 0) * TAB_DIGITS + 1]);
+  fp prod = fe_one<ModP>();
+  for (uint32_t e = 0; e < cnt; e++) {
+    if (e) acc = jac_add_aff(acc, G);
+    g1j_store(jtmp[i0 + e], acc);
+    prod = prod * acc.z;
+    for (int q = 0; q < 8; q++) zs[i0 + e][q] = prod.v[q];
+  }
+  fp inv = fp_inv(prod);
+  for (int e = (int)cnt - 1; e >= 0; e--) {
+    g1j pj = g1j_load(jtmp[i0 + e]);
+    fp prev = e ? fe_const<ModP>(zs[i0 + e - 1]) : fe_one<ModP>();
+    fp zi = inv * prev;
+    inv = inv * pj.z;
+    fp zi2 = zi * zi;
+    g1a a;
+    a.x = pj.x * zi2;
+    a.y = pj.y * zi2 * zi;
+    a.inf = false;
+    G1Dev d;
+    g1_store(d, a);
+    pts[i0 + e] = d;
+  }
+}

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "dev/jobs.h"
+#include "dev/msm.h"
 
 using namespace fts;
 
@@ -48,3 +49,23 @@ __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines
                          const G1Dev* g1out, F12Dev* fbuf);
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
+
+// standalone MSM (k_msm.hip)
+__global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok);
+__global__ void k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]);
+__global__ void k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* count);
+__global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tot);
+__global__ void k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add);
+__global__ void k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor, uint32_t* perm);
+__global__ void k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m);
+__global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
+                            uint32_t* whi);
+__global__ void k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* owner, const uint32_t* soff,
+                             const uint32_t* start, const uint32_t* count, const uint32_t* perm, const G1Dev* pts,
+                             G1JDev* slot_sum);
+__global__ void k_msm_segment(MsmPlan p, const uint32_t* wlo, const uint32_t* whi, const uint32_t* owner,
+                              const G1JDev* slot_sum, G1JDev* part);
+__global__ void k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out);
+__global__ void k_msm_final(MsmPlan p, const G1JDev* wsum, G1Dev* res, uint8_t* bytes);
+__global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const G1Dev* gtab, G1JDev* jtmp,
+                                uint32_t (*zs)[8], G1Dev* pts);

@@ -1,0 +1,228 @@
+// C ABI of the standalone G1 MSM (include/ftsamd.h, dev/msm.h).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "launch.h"
+#include "rt_internal.h"
+
+struct ftz_msm {
+  ftz_ctx* ctx = nullptr;
+  MsmPlan p{};
+  DBuf<G1Dev> pts;
+  DBuf<uint32_t> scal, key, count, start, cursor, perm, tot, nsl, soff, owner, wlo, whi;
+  DBuf<G1JDev> slot_sum, part, tree;
+  DBuf<G1Dev> res;
+  DBuf<uint8_t> bytes, ok;
+  hipEvent_t ev[2];
+  bool ev_init = false;
+  float last_ms = 0;
+};
+
+static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
+
+static int msm_alloc(ftz_msm* m, size_t n) {
+  const MsmPlan& p = m->p;
+  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * n, ws = (size_t)p.windows * p.max_slots;
+  HC(m->pts.alloc(n));
+  HC(m->scal.alloc(8 * n));
+  HC(m->key.alloc(wn));
+  HC(m->perm.alloc(wn));
+  HC(m->count.alloc(wb));
+  HC(m->start.alloc(wb));
+  HC(m->cursor.alloc(wb));
+  HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
+  HC(m->nsl.alloc(wb));
+  HC(m->soff.alloc(wb));
+  HC(m->owner.alloc(ws));
+  HC(m->wlo.alloc(p.windows));
+  HC(m->whi.alloc(p.windows));
+  HC(m->slot_sum.alloc(ws));
+  HC(m->part.alloc((size_t)p.windows * p.segs));
+  HC(m->tree.alloc((size_t)p.windows * ((p.segs + 255) / 256) * 2));
+  HC(m->res.alloc(1));
+  HC(m->bytes.alloc(64));
+  HC(m->ok.alloc(n));
+  for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
+  m->ev_init = true;
+  return FTZ_SUCCESS;
+}
+
+// exclusive scan of n counters in place of `out` (recursive over block totals)
+static int scan(uint32_t* in, uint32_t* out, size_t n, uint32_t* tmp, hipStream_t s) {
+  uint32_t nb = (uint32_t)((n + 1023) / 1024);
+  k_scan_block<<<nb, 1024, 0, s>>>(in, out, (uint32_t)n, tmp);
+  if (nb > 1) {
+    uint32_t* sums = tmp + nb;
+    int rc = scan(tmp, sums, nb, sums + nb + 1, s);
+    if (rc != FTZ_SUCCESS) return rc;
+    k_scan_add<<<nb, 1024, 0, s>>>(out, (uint32_t)n, sums);
+  }
+  return FTZ_SUCCESS;
+}
+
+static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
+  if (!c || !out) return set_err(FTZ_E_INVALID, "null argument");
+  if (n == 0 || n > (1u << 28)) return set_err(FTZ_E_INVALID, "MSM size must be in [1, 2^28]");
+  HC(hipSetDevice(c->device));
+  ftz_msm* m = new ftz_msm();
+  m->ctx = c;
+  m->p = msm_make_plan(n);
+  int rc = msm_alloc(m, n);
+  if (rc != FTZ_SUCCESS) {
+    ftz_msm_destroy(m);
+    return rc;
+  }
+  *out = m;
+  return FTZ_SUCCESS;
+}
+
+static int upload_scalars(ftz_msm* m, const uint8_t* scalars) {
+  hipStream_t s = m->ctx->stream;
+  size_t n = m->p.n;
+  DBuf<uint8_t> raw;
+  HC(raw.alloc(32 * n));
+  HC(hipMemcpyAsync(raw.p, scalars, 32 * n, hipMemcpyHostToDevice, s));
+  k_msm_load_scal<<<blocks(n, 256), 256, 0, s>>>((uint32_t)n, raw.p, reinterpret_cast<uint32_t (*)[8]>(m->scal.p));
+  HC(hipStreamSynchronize(s));
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_msm_load(ftz_ctx* c, size_t n, const uint8_t* points, const uint8_t* scalars, ftz_msm** out) {
+  if (!points || !scalars) return set_err(FTZ_E_INVALID, "null argument");
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  std::lock_guard<std::mutex> lk(c->mu);
+  ftz_msm* m = nullptr;
+  int rc = msm_new(c, n, &m);
+  if (rc != FTZ_SUCCESS) return rc;
+  hipStream_t s = c->stream;
+  {
+    DBuf<uint8_t> raw;
+    if (raw.alloc(64 * n) != hipSuccess ||
+        hipMemcpyAsync(raw.p, points, 64 * n, hipMemcpyHostToDevice, s) != hipSuccess) {
+      ftz_msm_destroy(m);
+      return set_err(FTZ_E_NOMEM, "point upload failed");
+    }
+    k_msm_load_pts<<<blocks(n, 256), 256, 0, s>>>((uint32_t)n, raw.p, m->pts.p, m->ok.p);
+    std::vector<uint8_t> ok(n);
+    if (hipMemcpyAsync(ok.data(), m->ok.p, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      ftz_msm_destroy(m);
+      return set_err(FTZ_E_DEVICE, "point decode failed");
+    }
+    for (size_t i = 0; i < n; i++)
+      if (!ok[i]) {
+        ftz_msm_destroy(m);
+        return set_err(FTZ_E_INVALID, "point " + std::to_string(i) + " is not a canonical BN254 G1 point");
+      }
+  }
+  rc = upload_scalars(m, scalars);
+  if (rc != FTZ_SUCCESS) {
+    ftz_msm_destroy(m);
+    return rc;
+  }
+  *out = m;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_msm_load_gen(ftz_ctx* c, size_t n, uint32_t offset, const uint8_t* scalars, ftz_msm** out) {
+  if (!scalars) return set_err(FTZ_E_INVALID, "null argument");
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  if ((uint64_t)offset + n >= (1ull << 32) || offset == 0) return set_err(FTZ_E_INVALID, "bad point offset");
+  std::lock_guard<std::mutex> lk(c->mu);
+  ftz_msm* m = nullptr;
+  int rc = msm_new(c, n, &m);
+  if (rc != FTZ_SUCCESS) return rc;
+  hipStream_t s = c->stream;
+  {
+    const uint32_t chunk = 64;
+    DBuf<G1JDev> jtmp;
+    DBuf<uint32_t> zs;
+    if (jtmp.alloc(n) != hipSuccess || zs.alloc(8 * n) != hipSuccess) {
+      ftz_msm_destroy(m);
+      return set_err(FTZ_E_NOMEM, "scratch allocation failed");
+    }
+    k_msm_genpoints<<<blocks((n + chunk - 1) / chunk, 128), 128, 0, s>>>(
+        (uint32_t)n, offset, chunk, c->g1tab.p, jtmp.p, reinterpret_cast<uint32_t (*)[8]>(zs.p), m->pts.p);
+    if (hipStreamSynchronize(s) != hipSuccess) {
+      ftz_msm_destroy(m);
+      return set_err(FTZ_E_DEVICE, "point generation failed");
+    }
+  }
+  rc = upload_scalars(m, scalars);
+  if (rc != FTZ_SUCCESS) {
+    ftz_msm_destroy(m);
+    return rc;
+  }
+  *out = m;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
+  if (!m || !out) return set_err(FTZ_E_INVALID, "null argument");
+  ftz_ctx* c = m->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const MsmPlan& p = m->p;
+  size_t wb = (size_t)p.windows * p.buckets;
+  HC(hipEventRecord(m->ev[0], s));
+  HC(hipMemsetAsync(m->count.p, 0, wb * sizeof(uint32_t), s));
+  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
+  k_msm_digits<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->count.p);
+  int rc = scan(m->count.p, m->start.p, wb, m->tot.p, s);
+  if (rc != FTZ_SUCCESS) return rc;
+  HC(hipMemcpyAsync(m->cursor.p, m->start.p, wb * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  k_msm_nslots<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->nsl.p);
+  rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
+  if (rc != FTZ_SUCCESS) return rc;
+  k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
+  k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
+  k_msm_bucket<<<blocks((size_t)p.windows * p.max_slots, 128), 128, 0, s>>>(
+      p, m->whi.p, m->owner.p, m->soff.p, m->start.p, m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
+  k_msm_segment<<<blocks((size_t)p.windows * p.segs, 128), 128, 0, s>>>(p, m->wlo.p, m->whi.p, m->owner.p,
+                                                                       m->slot_sum.p, m->part.p);
+  // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
+  G1JDev* in = m->part.p;
+  uint32_t cnt = p.segs;
+  G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.windows * ((p.segs + 255) / 256)};
+  int which = 0;
+  do {
+    uint32_t chunks = (cnt + 255) / 256;
+    k_msm_tree<<<p.windows * chunks, 256, 0, s>>>(in, cnt, bufs[which]);
+    in = bufs[which];
+    which ^= 1;
+    cnt = chunks;
+  } while (cnt > 1);
+  k_msm_final<<<1, 64, 0, s>>>(p, in, m->res.p, m->bytes.p);
+  HC(hipEventRecord(m->ev[1], s));
+  HC(hipGetLastError());
+  HC(hipMemcpyAsync(out, m->bytes.p, 64, hipMemcpyDeviceToHost, s));
+  HC(hipStreamSynchronize(s));
+  HC(hipEventElapsedTime(&m->last_ms, m->ev[0], m->ev[1]));
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits) {
+  if (!m) return set_err(FTZ_E_INVALID, "null argument");
+  if (last_ms) *last_ms = m->last_ms;
+  if (window_bits) *window_bits = m->p.c;
+  return FTZ_SUCCESS;
+}
+
+extern "C" void ftz_msm_destroy(ftz_msm* m) {
+  if (!m) return;
+  (void)hipSetDevice(m->ctx->device);
+  if (m->ev_init)
+    for (int k = 0; k < 2; k++) (void)hipEventDestroy(m->ev[k]);
+  delete m;
+}
+
+extern "C" int ftz_msm_g1(ftz_ctx* c, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[64]) {
+  ftz_msm* m = nullptr;
+  int rc = ftz_msm_load(c, n, points, scalars, &m);
+  if (rc == FTZ_SUCCESS) rc = ftz_msm_run(m, out);
+  ftz_msm_destroy(m);
+  return rc;
+}

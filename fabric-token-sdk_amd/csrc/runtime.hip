@@ -25,51 +25,13 @@
 using namespace fts;
 using namespace ftsh;
 
-// ------------------------------------------------------------------ host runtime
-static thread_local std::string g_err;
-static int set_err(int code, const std::string& msg) {
+#include "rt_internal.h"
+
+thread_local std::string g_err;
+int set_err(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-#define HC(expr)                                                                                    \
-  do {                                                                                              \
-    hipError_t e_ = (expr);                                                                         \
-    if (e_ != hipSuccess)                                                                           \
-      return set_err(FTZ_E_DEVICE, std::string(#expr " failed: ") + hipGetErrorString(e_));        \
-  } while (0)
-
-template <class T>
-struct DBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  ~DBuf() {
-    if (p) (void)hipFree(p);
-  }
-  hipError_t alloc(size_t cnt) {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = cnt;
-    if (cnt == 0) return hipSuccess;
-    return hipMalloc(&p, cnt * sizeof(T));
-  }
-  hipError_t upload(const std::vector<T>& v, hipStream_t s) {
-    hipError_t e = alloc(v.size());
-    if (e != hipSuccess || v.empty()) return e;
-    return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
-  }
-};
-
-struct ftz_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
-  PPInfo pp;
-  std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
-  DBuf<G1Dev> g1tab;
-  DBuf<G2Dev> g2tab;
-  DBuf<LineCoef> qlines;
-  int threads = 8;
-  std::mutex mu;
-};
 
 struct ftz_batch {
   ftz_ctx* ctx = nullptr;

@@ -22,7 +22,7 @@ from . import _abi
 from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_PANIC, FTZ_ERR_PARSE, FTZ_ERR_RANGE,  # noqa: F401
                    FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
 
-__all__ = ["Context", "Batch", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
+__all__ = ["Context", "Batch", "Msm", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
            "FTZ_OK", "MESSAGES"]
 
 
@@ -93,6 +93,15 @@ class Context:
         _check(self._lib.ftz_verify_issues(self._h, n, arr, codes), self._lib)
         return list(codes)[:n]
 
+    def msm_g1(self, points, scalars):
+        """sum_i k_i P_i (gnark G1Jac.MultiExp semantics): points n x 64-byte
+        RawBytes, scalars n x 32 bytes big-endian.  Returns 64-byte RawBytes."""
+        m = Msm(self, points, scalars)
+        try:
+            return m.run()
+        finally:
+            m.close()
+
     def load_transfers(self, transfers):
         arr, keep = _abi.pack_transfers(transfers)
         n = len(keep) // 3
@@ -106,6 +115,44 @@ class Context:
         h = ctypes.c_void_p()
         _check(self._lib.ftz_batch_load_issues(self._h, n, arr, ctypes.byref(h)), self._lib)
         return Batch(self, h, n)
+
+
+class Msm:
+    """A device-resident G1 multi-scalar multiplication (BASELINE configs[2]):
+    run() returns sum_i k_i P_i as 64-byte gnark RawBytes."""
+
+    def __init__(self, ctx, points=None, scalars=b"", n=None, gen_offset=None):
+        self._ctx, self._lib, self._h = ctx, ctx._lib, None
+        scalars = bytes(scalars)
+        h = ctypes.c_void_p()
+        if gen_offset is not None:
+            self.n = len(scalars) // 32
+            _check(self._lib.ftz_msm_load_gen(ctx._h, self.n, int(gen_offset), scalars, ctypes.byref(h)), self._lib)
+        else:
+            points = bytes(points)
+            if len(points) % 64 or len(points) // 64 != len(scalars) // 32 or len(scalars) % 32:
+                raise ValueError("points must be n x 64 bytes and scalars n x 32 bytes")
+            self.n = len(points) // 64
+            _check(self._lib.ftz_msm_load(ctx._h, self.n, points, scalars, ctypes.byref(h)), self._lib)
+        self._h = h
+
+    def run(self):
+        out = (ctypes.c_uint8 * 64)()
+        _check(self._lib.ftz_msm_run(self._h, out), self._lib)
+        return bytes(out)
+
+    def info(self):
+        ms, c = ctypes.c_float(), ctypes.c_uint32()
+        _check(self._lib.ftz_msm_info(self._h, ctypes.byref(ms), ctypes.byref(c)), self._lib)
+        return {"last_ms": ms.value, "window_bits": c.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ftz_msm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
 
 
 class Batch:

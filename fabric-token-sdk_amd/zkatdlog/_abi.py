@@ -52,7 +52,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_threads", "ftz_ctx_info",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
-           "ftz_batch_destroy"]
+           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy"]
 
 _lib = None
 
@@ -85,6 +85,14 @@ def load():
     lib.ftz_batch_size.restype = sz
     lib.ftz_batch_destroy.argtypes = [vp]
     lib.ftz_batch_destroy.restype = None
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    lib.ftz_msm_g1.argtypes = [vp, sz, ctypes.c_char_p, ctypes.c_char_p, u8p]
+    lib.ftz_msm_load.argtypes = [vp, sz, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(vp)]
+    lib.ftz_msm_load_gen.argtypes = [vp, sz, u32, ctypes.c_char_p, ctypes.POINTER(vp)]
+    lib.ftz_msm_run.argtypes = [vp, u8p]
+    lib.ftz_msm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
+    lib.ftz_msm_destroy.argtypes = [vp]
+    lib.ftz_msm_destroy.restype = None
     _lib = lib
     return lib
 

@@ -103,6 +103,23 @@ int ftz_batch_stats(const ftz_batch* b, ftz_stats* out);
 size_t ftz_batch_size(const ftz_batch* b);
 void ftz_batch_destroy(ftz_batch* b);
 
+/* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE configs[2]):
+ * out = sum_i k_i P_i as 64-byte gnark RawBytes.  Points: n x 64-byte
+ * uncompressed RawBytes (must be canonical and on the curve); scalars: n x 32
+ * bytes big-endian, reduced mod r.  The reference path has no MSM; this is the
+ * operation mathlib exposes from gnark-crypto as G1Jac.MultiExp.  Pippenger
+ * with signed windows (c = log2(n) - 4 clamped to [8, 20]). */
+typedef struct ftz_msm ftz_msm;
+int ftz_msm_g1(ftz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[64]);
+/* staged form: upload once, run on HBM-resident inputs (bench) */
+int ftz_msm_load(ftz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, ftz_msm** out);
+/* test/bench inputs with known discrete logs: P_i = (i + offset) G generated on the device */
+int ftz_msm_load_gen(ftz_ctx* ctx, size_t n, uint32_t offset, const uint8_t* scalars, ftz_msm** out);
+int ftz_msm_run(ftz_msm* m, uint8_t out[64]);
+/* device time of the last ftz_msm_run in ms (HIP events) and the window size */
+int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits);
+void ftz_msm_destroy(ftz_msm* m);
+
 #ifdef __cplusplus
 }
 #endif

@@ -300,6 +300,13 @@ def g1_sum(points):
     return acc
 
 
+def g1_msm(points, scalars):
+    """sum_i k_i P_i: the group element gnark-crypto v0.6.0 G1Jac.MultiExp
+    returns (ecc/bn254/multiexp.go [EXT], the MSM mathlib wraps for the
+    BASELINE configs[2] benchmark); scalars taken mod r.  TEST-ONLY checker."""
+    return g1_sum(g1_mul(pt, k) for pt, k in zip(points, scalars))
+
+
 # ---------------------------------------------------------------- G2 (twist)
 B2 = f2_mul((3, 0), f2_inv(XI))
 G2_GEN = (

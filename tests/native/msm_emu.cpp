@@ -1,0 +1,63 @@
+// TEST-ONLY host run of the MSM pipeline (dev/msm.h) with the same stage order
+// as msm_rt.hip: digits -> counting sort -> bucket sums -> segment sums ->
+// window sums -> Horner.  Small window sizes exercise many windows and the
+// signed-digit carries; tests/test_msm.py compares with the Python oracle.
+#include <string.h>
+
+#include <vector>
+
+#include "../../fabric-token-sdk_amd/csrc/dev/msm.h"
+
+using namespace fts;
+
+extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
+                       uint32_t seg_len, uint8_t out[64]) {
+  MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len);
+  std::vector<G1Dev> pts(n);
+  std::vector<uint32_t> scal(8 * n);
+  uint32_t(*sc)[8] = reinterpret_cast<uint32_t(*)[8]>(scal.data());
+  for (size_t i = 0; i < n; i++) {
+    uint32_t x[8], y[8], k[8];
+    be32_to_limbs(x, points + 64 * i);
+    be32_to_limbs(y, points + 64 * i + 32);
+    g1a a;
+    a.x = fe_from_int<ModP>(x);
+    a.y = fe_from_int<ModP>(y);
+    a.inf = is_zero(a.x) && is_zero(a.y);
+    if (!g1_on_curve(a)) return -1;
+    g1_store(pts[i], a);
+    be32_to_limbs(k, scalars + 32 * i);
+    fe_to_int(sc[i], fe_from_int<ModR>(k));
+  }
+  size_t wb = (size_t)p.windows * p.buckets;
+  std::vector<uint32_t> key((size_t)p.windows * n), count(wb, 0), start(wb), perm((size_t)p.windows * n);
+  for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), count.data(), false);
+  uint32_t run = 0;
+  for (size_t b = 0; b < wb; b++) start[b] = run, run += count[b];
+  std::vector<uint32_t> cur(start);
+  for (uint32_t i = 0; i < n; i++)
+    for (uint32_t w = 0; w < p.windows; w++) {
+      uint32_t k = key[(size_t)w * n + i];
+      if (k != NONE) perm[cur[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)]++] = i | (k & 0x80000000u);
+    }
+  std::vector<uint32_t> soff(wb), owner((size_t)p.windows * p.max_slots, 0xFFFFFFFFu), wlo(p.windows), whi(p.windows);
+  run = 0;
+  for (size_t b = 0; b < wb; b++) soff[b] = run, run += msm_bucket_slots(p, count[b]);
+  if (run > (size_t)p.windows * p.max_slots) return -2;
+  for (uint32_t g = 0; g < wb; g++) msm_job_owner(p, g, count.data(), soff.data(), owner.data(), wlo.data(), whi.data());
+  if (whi[p.windows - 1] != run) return -3;
+  std::vector<G1JDev> slot_sum(run);
+  for (uint32_t j = 0; j < run; j++)
+    g1j_store(slot_sum[j], msm_job_slot(p, j, owner.data(), soff.data(), start.data(), count.data(), perm.data(),
+                                        pts.data()));
+  g1j acc = jac_inf<fp>();
+  for (int w = (int)p.windows - 1; w >= 0; w--) {
+    for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
+    g1j ws = jac_inf<fp>();
+    for (uint32_t s = 0; s < p.segs; s++)
+      ws = jac_add(ws, msm_job_segment(p, (uint32_t)w, s, wlo.data(), whi.data(), owner.data(), slot_sum.data()));
+    acc = jac_add(acc, ws);
+  }
+  g1_to_bytes(out, jac_to_aff(acc));
+  return 0;
+}

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared():
     src = open(os.path.join(ROOT, "include", "ftsamd.h")).read()
-    return sorted(set(re.findall(r"\b(ftz_[a-z_]+)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(ftz_[a-z0-9_]+)\s*\(", src)))
 
 
 def test_header_matches_binding_list():

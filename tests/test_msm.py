@@ -1,0 +1,119 @@
+"""The standalone G1 MSM (BASELINE configs[2]; dev/msm.h, k_msm.hip).
+
+CPU tier: the pipeline's device functions run on the host (TEST-ONLY
+tests/native/msm_emu.cpp) against the oracle's sum_i k_i P_i, at small window
+sizes so that many windows, carries, empty and shared buckets occur.
+GPU tier: ftz_msm_* through the C ABI, bit-exact against the oracle: explicit
+points at small n, and at 2^16 / 2^20 the known-log points P_i = (i + off) G,
+whose MSM is (sum_i k_i (i + off) mod r) G -- a size-independent check."""
+import ctypes
+import random
+
+import pytest
+
+from ftsoracle import bn254 as C
+
+
+def rnd_case(n, seed, special=True):
+    rng = random.Random(seed)
+    pts = [C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)) for _ in range(n)]
+    ks = [rng.randrange(1 << 256) for _ in range(n)]
+    if special and n >= 6:
+        pts[1] = pts[0]                 # repeated point: bucket doubling
+        ks[1] = ks[0]
+        pts[2] = C.g1_neg(pts[3])       # P + (-P) in one bucket
+        ks[2] = ks[3]
+        ks[4] = 0                       # zero scalar
+        ks[5] = C.R - 1                 # -1
+    return pts, ks
+
+
+def pack(pts, ks):
+    return b"".join(C.g1_bytes(p) for p in pts), b"".join(k.to_bytes(32, "big") for k in ks)
+
+
+def emu_msm(emu, pts, ks, c, cap, seg_len):
+    pb, kb = pack(pts, ks)
+    out = ctypes.create_string_buffer(64)
+    emu.emu_msm.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                            ctypes.c_uint32, ctypes.c_char_p]
+    assert emu.emu_msm(len(pts), pb, kb, c, cap, seg_len, out) == 0
+    return out.raw
+
+
+@pytest.mark.parametrize("n,c,cap,seg", [(1, 4, 1, 1), (7, 2, 1, 1), (33, 5, 2, 3), (40, 8, 0, 0), (64, 3, 3, 2),
+                                         (20, 1, 1, 1), (48, 6, 4, 5)])
+def test_emu_pipeline(emu, n, c, cap, seg):
+    pts, ks = rnd_case(n, 100 + n * 7 + c)
+    assert emu_msm(emu, pts, ks, c, cap, seg) == C.g1_bytes(C.g1_msm(pts, ks))
+
+
+def test_emu_skewed_scalars(emu):
+    # small scalars pile into few buckets: heavy buckets are split over slots
+    rng = random.Random(77)
+    pts, _ = rnd_case(60, 78, special=False)
+    ks = [rng.randrange(1, 6) for _ in pts]
+    assert emu_msm(emu, pts, ks, 4, 4, 3) == C.g1_bytes(C.g1_msm(pts, ks))
+
+
+def test_emu_cancelling_sum(emu):
+    pts, ks = rnd_case(8, 5, special=False)
+    pts2 = pts + [C.g1_neg(p) for p in pts]
+    assert emu_msm(emu, pts2, ks + ks, 4, 3, 2) == C.g1_bytes(None)
+
+
+def test_window_plan():
+    # msm_window_bits: log2(n) - 4 clamped to [8, 20] (dev/msm.h)
+    def bits(n):
+        lg = n.bit_length() - 1
+        return min(20, max(8, lg - 4 if lg > 4 else 1))
+    assert [bits(1 << k) for k in (10, 16, 20, 24, 28)] == [8, 12, 16, 20, 20]
+
+
+@pytest.fixture(scope="module")
+def ctx(golden):
+    import zkatdlog
+    c = zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5, 200, 1000])
+def test_gpu_msm_explicit(ctx, n):
+    pts, ks = rnd_case(n, 900 + n)
+    pb, kb = pack(pts, ks)
+    assert ctx.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
+
+
+@pytest.mark.gpu
+def test_gpu_msm_rejects_bad_point(ctx):
+    import zkatdlog
+    pts, ks = rnd_case(4, 3, special=False)
+    pb, kb = pack(pts, ks)
+    bad = bytearray(pb)
+    bad[63] ^= 1
+    with pytest.raises(zkatdlog.DeviceError, match="not a canonical"):
+        ctx.msm_g1(bytes(bad), kb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lg,bits", [(16, 256), (20, 256), (16, 3), (18, 64)])
+def test_gpu_msm_known_logs(ctx, lg, bits):
+    """bits < 256: skewed scalars (a few hot buckets, most windows empty)."""
+    import zkatdlog
+    n, off = 1 << lg, 12345
+    rng = random.Random(lg * 1000 + bits)
+    ks = [rng.randrange(1 << bits) for _ in range(n)]
+    kb = b"".join(k.to_bytes(32, "big") for k in ks)
+    m = zkatdlog.Msm(ctx, scalars=kb, gen_offset=off)
+    try:
+        got = m.run()
+        again = m.run()
+        info = m.info()
+    finally:
+        m.close()
+    want = C.g1_mul(C.G1_GEN, sum(k * (i + off) for i, k in enumerate(ks)) % C.R)
+    assert got == C.g1_bytes(want)
+    assert again == got
+    assert info["window_bits"] == lg - 4 and info["last_ms"] > 0
