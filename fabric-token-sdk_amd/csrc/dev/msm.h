@@ -32,7 +32,12 @@ struct MsmPlan {
   uint32_t seg_len;    // S: slots per segment
   uint32_t max_slots;  // per window: B + ceil(n / T) bounds sum_b m_b
   uint32_t segs;       // segments per window: ceil(max_slots / S)
+  uint32_t top_used;   // buckets the top window can reach (scalars < r < 2^254)
 };
+
+// LDS-aggregated counting / scattering for the top window when it reaches at
+// most this many buckets (its few buckets would otherwise serialise on atomics)
+static constexpr uint32_t MSM_TOP_LDS = 1024;
 
 FTS_HD uint32_t msm_window_bits(uint64_t n) {
   uint32_t lg = 0;
@@ -45,7 +50,7 @@ FTS_HD uint32_t msm_window_bits(uint64_t n) {
 
 // plan for n points with c-bit windows (0: msm_window_bits(n)), slot cap T
 // (0: twice the mean bucket load, at least 4) and S slots per segment (0: sized
-// for >= 16k segment lanes, in [4, 64])
+// for >= 64k segment lanes, in [4, 64])
 inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, uint32_t seg_len = 0) {
   MsmPlan p;
   p.n = (uint32_t)n;
@@ -61,10 +66,12 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   if (!seg_len) {
     uint64_t tot = (uint64_t)p.windows * p.max_slots;
     seg_len = 4;
-    while (seg_len < 64 && tot / (2 * seg_len) >= 16384) seg_len *= 2;
+    while (seg_len < 64 && tot / (2 * seg_len) >= 65536) seg_len *= 2;
   }
   p.seg_len = seg_len;
   p.segs = (p.max_slots + seg_len - 1) / seg_len;
+  int t = 254 - (int)(p.c * (p.windows - 1));  // bits left for the top window
+  p.top_used = t <= 0 ? 1 : (t >= 31 || (1u << t) > p.buckets ? p.buckets : 1u << t);
   return p;
 }
 
@@ -83,8 +90,10 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
 }
 
 // digits of point i: key[w * n + i] = bucket | sign << 31, or NONE for a zero digit
+// top_hist: if non-null, the top window's counts go there (an LDS histogram
+// the caller flushes) instead of to count
 FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key,
-                           uint32_t* count, bool atomic_count) {
+                           uint32_t* count, bool atomic_count, uint32_t* top_hist = nullptr) {
   uint32_t carry = 0;
   for (uint32_t w = 0; w < p.windows; w++) {
     int32_t d = msm_digit(scal[i], p.c, w, carry);
@@ -92,7 +101,7 @@ FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[
     if (d != 0) {
       uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
       kk = b | (d < 0 ? 0x80000000u : 0u);
-      uint32_t* ct = &count[(size_t)w * p.buckets + b];
+      uint32_t* ct = (top_hist && w == p.windows - 1) ? &top_hist[b] : &count[(size_t)w * p.buckets + b];
 #if defined(__HIP_DEVICE_COMPILE__)
       (void)atomic_count;
       atomicAdd(ct, 1u);
@@ -132,10 +141,19 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   if (hi > count[g]) hi = count[g];
   const uint32_t* e = perm + start[g];
   g1j acc = jac_inf<fp>();
+  if (lo >= hi) return acc;
+  uint32_t v = e[lo];
+  G1Dev nxt = pts[v & 0x7FFFFFFFu];
   for (uint32_t q = lo; q < hi; q++) {
-    uint32_t v = e[q];
-    g1a P = g1_load(pts[v & 0x7FFFFFFFu]);
-    if (v >> 31) P = aff_neg(P);
+    // the next point's load is issued before this point's addition
+    G1Dev cur = nxt;
+    uint32_t sign = v >> 31;
+    if (q + 1 < hi) {
+      v = e[q + 1];
+      nxt = pts[v & 0x7FFFFFFFu];
+    }
+    g1a P = g1_load(cur);
+    if (sign) P = aff_neg(P);
     acc = jac_add_aff(acc, P);
   }
   return acc;

@@ -40,8 +40,20 @@ __global__ void __launch_bounds__(256) k_msm_load_scal(uint32_t n, const uint8_t
 
 __global__ void __launch_bounds__(256) k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
                                                     uint32_t* count) {
-  LANE_PROLOGUE(p.n);
-  msm_job_digits(p, i, scal, key, count, true);
+  __shared__ uint32_t top[MSM_TOP_LDS];
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool lds = p.top_used <= MSM_TOP_LDS;  // uniform
+  if (lds) {
+    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x) top[b] = 0;
+    __syncthreads();
+  }
+  if (i < p.n) msm_job_digits(p, i, scal, key, count, true, lds ? top : nullptr);
+  if (lds) {
+    __syncthreads();
+    uint32_t* gtop = count + (size_t)(p.windows - 1) * p.buckets;
+    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x)
+      if (top[b]) atomicAdd(&gtop[b], top[b]);
+  }
 }
 
 // exclusive scan, 1024 elements per workgroup; block totals to `tot`
@@ -66,15 +78,33 @@ __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, co
   if (i < n) out[i] += add[blockIdx.x];
 }
 
+// one lane per (window, point): lanes of a wave hit random buckets of one window
+// (blocks reaching the top window reserve its few buckets' positions once per
+// block through an LDS histogram)
 __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor,
                                                      uint32_t* perm) {
-  LANE_PROLOGUE(p.n);
-  for (uint32_t w = 0; w < p.windows; w++) {
-    uint32_t k = key[(size_t)w * p.n + i];
-    if (k == NONE) continue;
-    uint32_t pos = atomicAdd(&cursor[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)], 1u);
-    perm[pos] = i | (k & 0x80000000u);
+  __shared__ uint32_t cnt[MSM_TOP_LDS];
+  uint64_t total = (uint64_t)p.windows * p.n, top0 = (uint64_t)(p.windows - 1) * p.n;
+  uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x, t = b0 + threadIdx.x;
+  bool lds = p.top_used <= MSM_TOP_LDS && b0 + blockDim.x > top0;  // uniform per block
+  uint32_t k = t < total ? key[t] : NONE;
+  uint32_t w = t < total ? (uint32_t)(t / p.n) : 0, i = (uint32_t)(t - (uint64_t)w * p.n);
+  bool mine = lds && t >= top0 && t < total && k != NONE;
+  uint32_t rank = 0;
+  if (lds) {
+    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    if (mine) rank = atomicAdd(&cnt[k & 0x7FFFFFFFu], 1u);
+    __syncthreads();
+    uint32_t* gcur = cursor + (size_t)(p.windows - 1) * p.buckets;
+    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x)
+      if (cnt[b]) cnt[b] = atomicAdd(&gcur[b], cnt[b]);
+    __syncthreads();
   }
+  if (t >= total || k == NONE) return;
+  uint32_t pos = mine ? cnt[k & 0x7FFFFFFFu] + rank
+                      : atomicAdd(&cursor[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)], 1u);
+  perm[pos] = i | (k & 0x80000000u);
 }
 
 __global__ void __launch_bounds__(256) k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m) {
@@ -88,19 +118,23 @@ __global__ void __launch_bounds__(256) k_msm_owner(MsmPlan p, const uint32_t* co
   msm_job_owner(p, i, count, soff, owner, wlo, whi);
 }
 
-// one lane per bucket slot; the grid covers the bound W * max_slots, lanes past
-// the last window's end exit
-__global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* owner,
+// one lane per bucket slot of windows [w0, w1); the grid covers the bound
+// (w1 - w0) * max_slots, lanes past the group's last slot exit
+__global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo,
+                                                    const uint32_t* whi, const uint32_t* owner,
                                                     const uint32_t* soff, const uint32_t* start,
                                                     const uint32_t* count, const uint32_t* perm, const G1Dev* pts,
                                                     G1JDev* slot_sum) {
-  LANE_PROLOGUE(whi[p.windows - 1]);
-  g1j_store(slot_sum[i], msm_job_slot(p, i, owner, soff, start, count, perm, pts));
+  uint32_t j = wlo[w0] + blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= whi[w1 - 1]) return;
+  g1j_store(slot_sum[j], msm_job_slot(p, j, owner, soff, start, count, perm, pts));
 }
 
-__global__ void __launch_bounds__(128) k_msm_segment(MsmPlan p, const uint32_t* wlo, const uint32_t* whi,
-                                                     const uint32_t* owner, const G1JDev* slot_sum, G1JDev* part) {
-  LANE_PROLOGUE(p.windows * p.segs);
+__global__ void __launch_bounds__(128) k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo,
+                                                     const uint32_t* whi, const uint32_t* owner,
+                                                     const G1JDev* slot_sum, G1JDev* part) {
+  uint32_t i = w0 * p.segs + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w1 * p.segs) return;
   uint32_t w = i / p.segs, s = i - w * p.segs;
   g1j_store(part[i], msm_job_segment(p, w, s, wlo, whi, owner, slot_sum));
 }
@@ -121,19 +155,27 @@ __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, 
   if (t == 0) out[(size_t)w * chunks + ch] = s[0];
 }
 
-// Horner over the window sums: sum_w 2^(c w) W_w; affine + RawBytes
-__global__ void k_msm_final(MsmPlan p, const G1JDev* wsum, G1Dev* res, uint8_t* bytes) {
+// Horner steps for windows w_hi-1 down to w_lo: acc = 2^c acc + W_w, one lane.
+// Runs on a side stream while the next (lower) window group accumulates, so
+// the c (W-1) serial doublings overlap the bucket work; the last call (w_lo = 0)
+// converts to affine and gnark RawBytes.
+__global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum, G1JDev* acc_buf,
+                             G1Dev* res, uint8_t* bytes) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  g1j acc = jac_inf<fp>();
-  for (int w = (int)p.windows - 1; w >= 0; w--) {
-    for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
+  g1j acc = w_hi == p.windows ? jac_inf<fp>() : g1j_load(*acc_buf);
+  for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
+    if (w != (int)p.windows - 1)
+      for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
     acc = jac_add_inl(acc, g1j_load(wsum[w]));
   }
-  g1a r = jac_to_aff(acc);
-  G1Dev d;
-  g1_store(d, r);
-  *res = d;
-  g1_to_bytes(bytes, r);
+  g1j_store(*acc_buf, acc);
+  if (w_lo == 0) {
+    g1a r = jac_to_aff(acc);
+    G1Dev d;
+    g1_store(d, r);
+    *res = d;
+    g1_to_bytes(bytes, r);
+  }
 }
 
 // test points with known logs: P_i = (i + off) G from the generator's fixed-base

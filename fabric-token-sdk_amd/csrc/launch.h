@@ -60,12 +60,13 @@ __global__ void k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor, 
 __global__ void k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m);
 __global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
                             uint32_t* whi);
-__global__ void k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* owner, const uint32_t* soff,
-                             const uint32_t* start, const uint32_t* count, const uint32_t* perm, const G1Dev* pts,
-                             G1JDev* slot_sum);
-__global__ void k_msm_segment(MsmPlan p, const uint32_t* wlo, const uint32_t* whi, const uint32_t* owner,
-                              const G1JDev* slot_sum, G1JDev* part);
+__global__ void k_msm_bucket(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo, const uint32_t* whi,
+                             const uint32_t* owner, const uint32_t* soff, const uint32_t* start,
+                             const uint32_t* count, const uint32_t* perm, const G1Dev* pts, G1JDev* slot_sum);
+__global__ void k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo, const uint32_t* whi,
+                              const uint32_t* owner, const G1JDev* slot_sum, G1JDev* part);
 __global__ void k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out);
-__global__ void k_msm_final(MsmPlan p, const G1JDev* wsum, G1Dev* res, uint8_t* bytes);
+__global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum, G1JDev* acc_buf,
+                             G1Dev* res, uint8_t* bytes);
 __global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const G1Dev* gtab, G1JDev* jtmp,
                                 uint32_t (*zs)[8], G1Dev* pts);

@@ -1,5 +1,6 @@
 // C ABI of the standalone G1 MSM (include/ftsamd.h, dev/msm.h).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -14,8 +15,12 @@ struct ftz_msm {
   DBuf<uint32_t> scal, key, count, start, cursor, perm, tot, nsl, soff, owner, wlo, whi;
   DBuf<G1JDev> slot_sum, part, tree;
   DBuf<G1Dev> res;
+  DBuf<G1JDev> hacc, wsum;
   DBuf<uint8_t> bytes, ok;
+  uint32_t group = 1;  // windows per accumulation group
   hipEvent_t ev[2];
+  hipEvent_t gev[32];  // group g's window sums ready (main stream -> side stream)
+  hipEvent_t hdone;    // Horner chain finished (side stream -> main stream)
   bool ev_init = false;
   float last_ms = 0;
 };
@@ -42,10 +47,22 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->part.alloc((size_t)p.windows * p.segs));
   HC(m->tree.alloc((size_t)p.windows * ((p.segs + 255) / 256) * 2));
   HC(m->res.alloc(1));
+  HC(m->hacc.alloc(1));
+  HC(m->wsum.alloc(p.windows));
   HC(m->bytes.alloc(64));
   HC(m->ok.alloc(n));
   for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
+  for (int k = 0; k < 32; k++) HC(hipEventCreateWithFlags(&m->gev[k], hipEventDisableTiming));
+  HC(hipEventCreateWithFlags(&m->hdone, hipEventDisableTiming));
   m->ev_init = true;
+  // windows per accumulation group (FTZ_MSM_GROUP; default all windows in one
+  // group: splitting multiplies the latency-bound segment / tree phases, which
+  // costs more than overlapping the Horner chain saves -- measured at 2^20/2^24)
+  const char* ge = getenv("FTZ_MSM_GROUP");
+  uint32_t g = ge ? (uint32_t)strtoul(ge, nullptr, 10) : 0;
+  if (g == 0 || g > p.windows) g = p.windows;
+  while ((p.windows + g - 1) / g > 32) g++;
+  m->group = g;
   return FTZ_SUCCESS;
 }
 
@@ -68,7 +85,11 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   HC(hipSetDevice(c->device));
   ftz_msm* m = new ftz_msm();
   m->ctx = c;
-  m->p = msm_make_plan(n);
+  // tuning overrides (window bits, slot cap, slots per segment); 0 = planner default
+  auto env = [](const char* k) { const char* v = getenv(k); return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u; };
+  uint32_t c_over = env("FTZ_MSM_C");
+  if (c_over > 24) c_over = 0;
+  m->p = msm_make_plan(n, c_over, env("FTZ_MSM_T"), env("FTZ_MSM_S"));
   int rc = msm_alloc(m, n);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);
@@ -178,24 +199,41 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
-  k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
-  k_msm_bucket<<<blocks((size_t)p.windows * p.max_slots, 128), 128, 0, s>>>(
-      p, m->whi.p, m->owner.p, m->soff.p, m->start.p, m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
-  k_msm_segment<<<blocks((size_t)p.windows * p.segs, 128), 128, 0, s>>>(p, m->wlo.p, m->whi.p, m->owner.p,
-                                                                       m->slot_sum.p, m->part.p);
-  // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
-  G1JDev* in = m->part.p;
-  uint32_t cnt = p.segs;
+  k_msm_scatter<<<blocks((size_t)p.windows * p.n, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
+  // window groups from the top: accumulate group g on the main stream while the
+  // side stream runs the Horner steps of group g-1
+  hipStream_t hs = c->stream3;
   G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.windows * ((p.segs + 255) / 256)};
-  int which = 0;
-  do {
-    uint32_t chunks = (cnt + 255) / 256;
-    k_msm_tree<<<p.windows * chunks, 256, 0, s>>>(in, cnt, bufs[which]);
-    in = bufs[which];
-    which ^= 1;
-    cnt = chunks;
-  } while (cnt > 1);
-  k_msm_final<<<1, 64, 0, s>>>(p, in, m->res.p, m->bytes.p);
+  G1JDev* wsum = nullptr;
+  uint32_t gi = 0;
+  for (uint32_t w1 = p.windows; w1 > 0; gi++) {
+    uint32_t w0 = w1 > m->group ? w1 - m->group : 0, nw = w1 - w0;
+    k_msm_bucket<<<blocks((size_t)nw * p.max_slots, 128), 128, 0, s>>>(
+        p, w0, w1, m->wlo.p, m->whi.p, m->owner.p, m->soff.p, m->start.p, m->count.p, m->perm.p, m->pts.p,
+        m->slot_sum.p);
+    k_msm_segment<<<blocks((size_t)nw * p.segs, 128), 128, 0, s>>>(p, w0, w1, m->wlo.p, m->whi.p, m->owner.p,
+                                                                  m->slot_sum.p, m->part.p);
+    // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
+    const G1JDev* in = m->part.p + (size_t)w0 * p.segs;
+    uint32_t cnt = p.segs;
+    int which = 0;
+    do {
+      uint32_t chunks = (cnt + 255) / 256;
+      // the last pass writes the dedicated window-sum array the side stream reads
+      G1JDev* out = chunks == 1 ? m->wsum.p + w0 : bufs[which] + (size_t)w0 * chunks;
+      k_msm_tree<<<nw * chunks, 256, 0, s>>>(in, cnt, out);
+      in = out;
+      wsum = m->wsum.p;
+      which ^= 1;
+      cnt = chunks;
+    } while (cnt > 1);
+    HC(hipEventRecord(m->gev[gi], s));
+    HC(hipStreamWaitEvent(hs, m->gev[gi], 0));
+    k_msm_horner<<<1, 64, 0, hs>>>(p, w1, w0, wsum, m->hacc.p, m->res.p, m->bytes.p);
+    w1 = w0;
+  }
+  HC(hipEventRecord(m->hdone, hs));
+  HC(hipStreamWaitEvent(s, m->hdone, 0));
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
   HC(hipMemcpyAsync(out, m->bytes.p, 64, hipMemcpyDeviceToHost, s));
@@ -215,7 +253,11 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
   if (!m) return;
   (void)hipSetDevice(m->ctx->device);
   if (m->ev_init)
+  {
     for (int k = 0; k < 2; k++) (void)hipEventDestroy(m->ev[k]);
+    for (int k = 0; k < 32; k++) (void)hipEventDestroy(m->gev[k]);
+    (void)hipEventDestroy(m->hdone);
+  }
   delete m;
 }
 

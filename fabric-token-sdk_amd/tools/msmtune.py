@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""MSM plan sweep: device latency of ftz_msm_run for window bits C, slot cap T
+and slots per segment S (FTZ_MSM_C / _T / _S planner overrides; 0 = default).
+    python msmtune.py 20 "0,0,0 16,16,0 16,32,0 15,0,0 17,0,0"
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
+import numpy as np  # noqa: E402
+
+import zkatdlog  # noqa: E402
+
+lg = int(sys.argv[1])
+combos = [tuple(int(v) for v in c.split(",")) for c in sys.argv[2].split()]
+pp = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]["pp"].encode()
+ctx = zkatdlog.Context(pp, device=0)
+scal = np.random.default_rng(lg).bytes(32 << lg)
+ref = None
+for c, t, s in combos:
+    os.environ["FTZ_MSM_C"], os.environ["FTZ_MSM_T"], os.environ["FTZ_MSM_S"] = str(c), str(t), str(s)
+    m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
+    out = m.run()
+    ms = []
+    for _ in range(4):
+        assert m.run() == out
+        ms.append(m.info()["last_ms"])
+    ref = ref or out
+    print("n=2^%d C=%2d T=%3d S=%3d  %8.3f ms  %s" % (lg, m.info()["window_bits"], t, s, min(ms),
+                                                     "ok" if out == ref else "MISMATCH"), flush=True)
+    m.close()
+ctx.close()
