@@ -119,6 +119,42 @@ def msm_latency(ctx, lg, reps=5, seed=7):
             "window_bits": info["window_bits"]}
 
 
+def prover_bench(ctx, batch, steps, warmup):
+    """BASELINE configs[4] (batch prover) at the configs[1] shape: `batch`
+    2-in/2-out transfer proofs per pass from HBM-resident witnesses (64 distinct
+    witnesses of tests/golden/bench_transfers.json tiled, a distinct 32-byte
+    seed per proof).  The proofs of the last pass are re-verified by the GPU
+    verifier (all must be accepted)."""
+    import hashlib
+
+    import zkatdlog
+    bs = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_transfers.json")))["transfers"]
+    ws = []
+    for i in range(batch):
+        t = bs[i % len(bs)]
+        ws.append({"inputs": bytes.fromhex(t["inputs"]), "outputs": bytes.fromhex(t["outputs"]),
+                   "in_values": t["in_values"], "in_bfs": [int(x) for x in t["in_bfs"]],
+                   "out_values": t["out_values"], "out_bfs": [int(x) for x in t["out_bfs"]],
+                   "type": t["type"], "seed": hashlib.sha256(b"bench-prover/%d" % i).digest()})
+    p = zkatdlog.Prover(ctx, ws, "transfer")
+    try:
+        for _ in range(warmup):
+            p.run()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            p.run()
+        dt = time.perf_counter() - t0
+        proofs, codes = p.proofs()
+        stats = p.stats()
+    finally:
+        p.close()
+    verdicts = ctx.verify_transfers([(w["inputs"], w["outputs"], pr) for w, pr in zip(ws, proofs)])
+    return {"proofs_per_s": round(batch * steps / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3),
+            "batch": batch, "all_accepted_by_gpu_verifier": bool(all(c == 0 for c in codes)
+                                                                 and all(v == 0 for v in verdicts)),
+            "stage_ms": {k: round(v[0], 3) for k, v in stats.items()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,6 +164,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
+    ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,6 +231,7 @@ def main():
                                 "x 136 MAD; HBM traffic ~2 KB/tx is not a bound"}
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
+        prover = None if args.no_prover else prover_bench(ctx, args.batch, args.steps, args.warmup)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(pp_json, items, expect, args.cpu_seconds)
@@ -210,7 +248,7 @@ def main():
             "kernel_ms": {k: round(v[0], 3) for k, v in stats.items()},
             "plan_upload_s": round(t_plan, 3),
             "roofline": roof, "cpu_baseline": cpu,
-            "msm_2^20_latency_ms": msm20, "msm": msm,
+            "msm_2^20_latency_ms": msm20, "msm": msm, "prover": prover,
         }
         print(json.dumps(line), flush=True)
     batch.close()

@@ -54,9 +54,11 @@ struct ZrJob {
 };
 static constexpr uint32_t ZR_MAX_LEN = 256;
 
-enum ScalOp : uint32_t { SOP_MUL = 0, SOP_MULK = 1, SOP_SUM = 2 };
+enum ScalOp : uint32_t { SOP_MUL = 0, SOP_MULK = 1, SOP_SUM = 2, SOP_MADD = 3, SOP_MULK64 = 4 };
 struct ScalJob {
-  uint32_t op, a, b, out;  // MUL: a*b; MULK: a*(uint32)b; SUM: sum of list[a .. a+b)
+  // MUL: a*b; MULK: a*(uint32)b; SUM: sum of list[a .. a+b); MADD: a + b*c
+  // (Schnorr response r + c*w); MULK64: a*(b | c << 32)
+  uint32_t op, a, b, out, c;
 };
 
 struct VTerm {
@@ -74,6 +76,7 @@ struct G1Job {
   uint32_t vneg;            // 1: subtract the variable part
   uint32_t out;             // g1out index
   uint32_t bytes;           // arena offset for RawBytes (NONE: skip)
+  uint32_t b64;             // arena offset for the 88 base64 chars of RawBytes (NONE: skip)
 };
 
 struct G2Job {
@@ -98,6 +101,26 @@ struct HashJob {
   uint32_t seg_start, seg_count;
   uint32_t expect;    // scalar index of the claimed challenge (NONE: no compare)
   uint32_t out_scal;  // write HashToZr(data) to this scalar (NONE: skip)
+};
+
+// prover: rand(tag) = SHA-256(seed||tag||0) || SHA-256(seed||tag||1) mod r
+// (the oracle's deterministic stand-in for crypto/rand, ftsoracle/zkat.py Rand)
+struct RandJob {
+  uint32_t seed;      // arena offset of the 32-byte per-proof seed
+  uint32_t tag, len;  // arena range of the tag string
+  uint32_t out;       // scalar index
+};
+// prover output: one fixed-length hole of a JSON template (base64 of an element)
+enum EmitKind : uint32_t { EM_ZR = 0, EM_G1 = 1 };
+struct EmitJob {
+  uint32_t dst;   // arena offset of the 44 (Zr) / 88 (G1) base64 chars
+  uint32_t kind;
+  uint32_t src;   // EM_ZR: scalar index; EM_G1: arena offset of 64 RawBytes
+};
+// prover output: base64 of an inner JSON document into the outer proof
+struct B64Job {
+  uint32_t src, len;  // arena range
+  uint32_t dst;       // offset in the proof output buffer
 };
 
 enum CheckKind : uint8_t { CK_STATIC = 0, CK_PTS = 1, CK_HASH = 2 };
@@ -187,6 +210,22 @@ FTS_HD void b64_encode_64(uint8_t* out, const uint8_t* in) {
   out[o++] = a[(v >> 12) & 63];
   out[o++] = '=';
   out[o++] = '=';
+}
+
+// standard base64 (with '=' padding) of the 3-byte group g of in[0..len)
+FTS_HD void b64_group(uint8_t* out, const uint8_t* in, uint32_t len, uint32_t g) {
+  const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  uint32_t k = 3 * g, rem = len - k;
+  uint32_t v = (uint32_t)in[k] << 16;
+  if (rem > 1) v |= (uint32_t)in[k + 1] << 8;
+  if (rem > 2) v |= in[k + 2];
+  out[0] = a[v >> 18];
+  out[1] = a[(v >> 12) & 63];
+  out[2] = rem > 1 ? a[(v >> 6) & 63] : '=';
+  out[3] = rem > 2 ? a[v & 63] : '=';
+}
+FTS_HD void b64_encode(uint8_t* out, const uint8_t* in, uint32_t len) {
+  for (uint32_t g = 0; 3 * g < len; g++) b64_group(out + 4 * g, in, len, g);
 }
 
 // ------------------------------------------------------------------ jobs
@@ -358,6 +397,11 @@ FTS_HD void job_scalar(const ScalJob& j, uint32_t (*scal)[8], const uint32_t* li
   if (j.op == SOP_SUM) {
     r = fe_zero<ModR>();
     for (uint32_t k = 0; k < j.b; k++) r = r + fe_from_int<ModR>(scal[list[j.a + k]]);
+  } else if (j.op == SOP_MADD) {
+    r = fe_from_int<ModR>(scal[j.a]) + fe_from_int<ModR>(scal[j.b]) * fe_from_int<ModR>(scal[j.c]);
+  } else if (j.op == SOP_MULK64) {
+    uint32_t k[8] = {j.b, j.c, 0, 0, 0, 0, 0, 0};
+    r = fe_from_int<ModR>(scal[j.a]) * fe_from_int<ModR>(k);
   } else {
     fr x = fe_from_int<ModR>(scal[j.a]);
     fr y;
@@ -493,6 +537,15 @@ FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
   return acc;
 }
 
+FTS_HD void g1_emit_bytes(const G1Job& j, const g1a& r, uint8_t* arena) {
+  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+  if (j.b64 != NONE) {
+    uint8_t tmp[64];
+    g1_to_bytes(tmp, r);
+    b64_encode_64(arena + j.b64, tmp);
+  }
+}
+
 FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const uint32_t (*scal)[8],
                    const G1Dev* tab, G1Dev* g1out, uint8_t* arena) {
   g1j acc = jac_inf<fp>();
@@ -523,7 +576,7 @@ FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const 
   G1Dev d;
   g1_store(d, r);
   g1out[j.out] = d;
-  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+  g1_emit_bytes(j, r, arena);
 }
 
 // ---- G1 jobs split into uniform parts (device path): item i of [0, 4n) is
@@ -592,7 +645,7 @@ FTS_HD void job_g1_combine(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev
   G1Dev d;
   g1_store(d, r);
   g1out[j.out] = d;
-  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+  g1_emit_bytes(j, r, arena);
 }
 
 FTS_HD void job_g2(const G2Job& j, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out) {
@@ -632,6 +685,40 @@ FTS_HD uint8_t job_hash(const HashJob& j, const Seg* segs, const uint8_t* arena,
   uint32_t o = 0;
   for (int k = 0; k < 8; k++) o |= h[k] ^ scal[j.expect][k];
   return (o == 0 && canon[j.expect]) ? 1 : 0;
+}
+
+// prover randomness (RandJob)
+FTS_HD void job_rand(const RandJob& j, const uint8_t* arena, uint32_t (*scal)[8]) {
+  uint8_t h[2][32];
+  for (int q = 0; q < 2; q++) {
+    Sha256 s;
+    s.init();
+    s.update(arena + j.seed, 32);
+    s.update(arena + j.tag, j.len);
+    uint8_t b = (uint8_t)q;
+    s.update(&b, 1);
+    s.final(h[q]);
+  }
+  uint32_t t0[8], t1[8];
+  be32_to_limbs(t0, h[0]);
+  be32_to_limbs(t1, h[1]);
+  // (h0 * 2^256 + h1) mod r; mont(h0) * R2 is the Montgomery form of h0 * 2^256
+  fr v = fe_from_int<ModR>(t0) * fe_const<ModR>(R_R2) + fe_from_int<ModR>(t1);
+  uint32_t out[8];
+  fe_to_int(out, v);
+  for (int k = 0; k < 8; k++) scal[j.out][k] = out[k];
+}
+
+// prover output holes (EmitJob): base64 of a 32-byte big-endian scalar or of
+// 64 RawBytes already written into the arena
+FTS_HD void job_emit(const EmitJob& j, const uint32_t (*scal)[8], uint8_t* arena) {
+  if (j.kind == EM_ZR) {
+    uint8_t b[32];
+    limbs_to_be32(b, scal[j.src]);
+    b64_encode(arena + j.dst, b, 32);
+  } else {
+    b64_encode_64(arena + j.dst, arena + j.src);
+  }
 }
 
 FTS_HD int32_t eval_part(const Check* ck, uint32_t start, uint32_t count, const uint8_t* pt_ok,

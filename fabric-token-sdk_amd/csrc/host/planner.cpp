@@ -23,6 +23,13 @@
 namespace ftsh {
 
 void Plan::clear() {
+  rnd.clear();
+  sc1.clear();
+  sc_post.clear();
+  emit.clear();
+  b64.clear();
+  out.clear();
+  out_off.clear();
   wire.clear();
   arena.clear();
   dec.clear();
@@ -228,6 +235,7 @@ class Builder {
     j.vneg = 1;
     j.out = pl.n_g1out++;
     j.bytes = bytes;
+    j.b64 = NONE;
     (feeds_pairing ? pl.g1p : pl.g1).push_back(j);
     return j.out;
   }
@@ -780,8 +788,10 @@ void Builder::issue(const IssueIn& t) {
   end_tx();
 }
 
+}  // namespace
+
 // Append piece `b` (local indices) to plan `a`, relocating every index.
-void merge(Plan& a, const Plan& b) {
+void plan_merge(Plan& a, const Plan& b) {
   uint32_t o_wire = (uint32_t)a.wire.size(), o_arena = (uint32_t)a.arena.size();
   uint32_t o_pts = a.n_pts, o_scal = a.n_scal, o_g1 = a.n_g1out, o_g2 = a.n_g2out;
   uint32_t o_list = (uint32_t)a.sclist.size(), o_vt = (uint32_t)a.vt.size(), o_seg = (uint32_t)a.seg.size();
@@ -801,16 +811,20 @@ void merge(Plan& a, const Plan& b) {
     j.out += o_scal;
     a.zr.push_back(j);
   }
-  for (ScalJob j : b.sc) {
+  auto rel_sc = [&](ScalJob j) {
     if (j.op == SOP_SUM) {
       j.a += o_list;
     } else {
       j.a += o_scal;
-      if (j.op == SOP_MUL) j.b += o_scal;
+      if (j.op == SOP_MUL || j.op == SOP_MADD) j.b += o_scal;
+      if (j.op == SOP_MADD) j.c += o_scal;
     }
     j.out += o_scal;
-    a.sc.push_back(j);
-  }
+    return j;
+  };
+  for (const ScalJob& j : b.sc) a.sc.push_back(rel_sc(j));
+  for (const ScalJob& j : b.sc1) a.sc1.push_back(rel_sc(j));
+  for (const ScalJob& j : b.sc_post) a.sc_post.push_back(rel_sc(j));
   for (uint32_t v : b.sclist) a.sclist.push_back(v + o_scal);
   for (VTerm v : b.vt) {
     v.pt += o_pts;
@@ -823,6 +837,7 @@ void merge(Plan& a, const Plan& b) {
       j.vscal = rel(j.vscal, o_scal);
       j.out += o_g1;
       j.bytes = rel(j.bytes, o_arena);
+      j.b64 = rel(j.b64, o_arena);
       (side ? a.g1p : a.g1).push_back(j);
     }
   }
@@ -833,7 +848,7 @@ void merge(Plan& a, const Plan& b) {
   }
   for (PairJob j : b.pr) {
     j.p1 += o_g1;
-    j.p2 += o_pts;
+    j.p2 += a.p2_g1out ? o_g1 : o_pts;
     j.q2 += o_g2;
     j.bytes += o_arena;
     a.pr.push_back(j);
@@ -867,11 +882,33 @@ void merge(Plan& a, const Plan& b) {
     t.rg_start += o_ck;
     a.tx.push_back(t);
   }
+  // prover pieces
+  for (RandJob j : b.rnd) {
+    j.seed += o_arena;
+    j.tag += o_arena;
+    j.out += o_scal;
+    a.rnd.push_back(j);
+  }
+  for (EmitJob j : b.emit) {
+    j.dst += o_arena;
+    j.src += j.kind == EM_ZR ? o_scal : o_arena;
+    a.emit.push_back(j);
+  }
+  uint32_t o_out = (uint32_t)a.out.size();
+  for (B64Job j : b.b64) {
+    j.src += o_arena;
+    j.dst += o_out;
+    a.b64.push_back(j);
+  }
+  a.out.insert(a.out.end(), b.out.begin(), b.out.end());
+  for (uint32_t v : b.out_off) a.out_off.push_back(v + o_out);
   a.n_pts += b.n_pts;
   a.n_scal += b.n_scal;
   a.n_g1out += b.n_g1out;
   a.n_g2out += b.n_g2out;
 }
+
+namespace {
 
 template <class In, class Fn>
 void plan_batch(const PPInfo& pp, size_t n, const In* in, Plan& out, int threads, Fn fn) {
@@ -889,7 +926,7 @@ void plan_batch(const PPInfo& pp, size_t n, const In* in, Plan& out, int threads
     });
   }
   for (auto& t : th) t.join();
-  for (auto& p : pieces) merge(out, p);
+  for (auto& p : pieces) plan_merge(out, p);
 }
 
 }  // namespace

@@ -53,6 +53,15 @@ struct Plan {
   std::vector<HashJob> hpre, hmain;
   std::vector<Check> ck;
   std::vector<TxChecks> tx;
+  // prover plans (planner_prove.cpp)
+  std::vector<RandJob> rnd;
+  std::vector<ScalJob> sc1;      // scalar jobs that read outputs of `sc` (run after it)
+  std::vector<ScalJob> sc_post;  // responses, after the transcript hashes
+  std::vector<EmitJob> emit;
+  std::vector<B64Job> b64;
+  std::vector<uint8_t> out;       // outer proof JSON templates, concatenated
+  std::vector<uint32_t> out_off;  // per proof: start in `out` (plus a final end)
+  bool p2_g1out = false;          // PairJob.p2 indexes g1out (prover) instead of pts
   uint32_t n_pts = 0, n_scal = 0, n_g1out = 0, n_g2out = 0;
   void clear();
 };
@@ -77,5 +86,39 @@ struct IssueIn {
 // plan are absolute: the const region occupies [0, C_SIZE).
 void plan_transfers(const PPInfo& pp, size_t n, const TransferIn* tx, Plan& out, int threads);
 void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int threads);
+
+// Append piece b (indices local to b) to a, relocating every index.
+void plan_merge(Plan& a, const Plan& b);
+
+// ------------------------------------------------------------------ prover
+// Witness of one transfer / issue (token.TokenDataWitness: Type, Value,
+// BlindingFactor; values and blinding factors as 32-byte big-endian Zr).
+struct TransferWit {
+  const uint8_t* inputs;   // n_in x 64-byte RawBytes
+  uint32_t n_in;
+  const uint8_t* outputs;  // n_out x 64-byte RawBytes
+  uint32_t n_out;
+  const uint8_t* in_values;
+  const uint8_t* in_bfs;
+  const uint8_t* out_values;
+  const uint8_t* out_bfs;
+  const char* type;
+  size_t type_len;
+  const uint8_t* seed;     // 32 bytes
+};
+struct IssueWit {
+  const uint8_t* outputs;
+  uint32_t n_out;
+  const uint8_t* values;
+  const uint8_t* bfs;
+  const char* type;
+  size_t type_len;
+  uint8_t anonymous;
+  const uint8_t* seed;
+};
+// Build prover plans (planner_prove.cpp).  Returns "" or the first witness
+// error ("proof i: ...", e.g. a value outside [0, base^exponent)).
+std::string plan_prove_transfers(const PPInfo& pp, size_t n, const TransferWit* w, Plan& out, int threads);
+std::string plan_prove_issues(const PPInfo& pp, size_t n, const IssueWit* w, Plan& out, int threads);
 
 }  // namespace ftsh

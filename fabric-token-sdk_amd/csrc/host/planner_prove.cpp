@@ -1,0 +1,636 @@
+// Host planner of the batch PROVER: lays out, per transfer / issue, the GPU
+// jobs that compute a zkatdlog proof and the JSON templates the device fills.
+// Reference (paths under token/core/zkatdlog/crypto/):
+//   transfer.Prover.Prove                 transfer/transfer.go:89-121
+//   transfer WellFormednessProver         transfer/wellformedness.go:131-154, 243-378
+//   rangeproof.Prover.Prove               range/proof.go:141-209, preProcess :288-337,
+//                                         computeCommitment :340-368
+//   MembershipProver.Prove                sigproof/membership.go:112-158,
+//                                         obfuscateSignature :196-222, computeCommitment :225-257
+//   issue.Prover.Prove / WF prover        issue/issue.go:151-184; issue/wellformedness.go:74-184
+//   token commitments                     token/token.go:64-98
+// Randomness: the reference draws every blinding value from crypto/rand.  The
+// batch prover derives them from a per-proof 32-byte seed and a tag naming the
+// value, rand(tag) = SHA-256(seed||tag||0) || SHA-256(seed||tag||1) mod r, the
+// same derivation as the oracle's prover (ftsoracle/zkat.py Rand), so proofs
+// are reproducible and checkable byte for byte.  The Go shim passes 32 bytes
+// of crypto/rand per proof as the seed.
+//
+// No arithmetic happens here: the planner writes tag strings, witness bytes and
+// JSON templates into the arena and emits jobs; every scalar, point, GT element,
+// hash and base64 character of the proof is produced on the GPU.
+#include <string.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "planner.h"
+
+namespace ftsh {
+namespace {
+
+static const char ZR_PRE[] = "{\"curve\":1,\"element\":\"";  // mathlib curveElement JSON, BN254
+static const char EL_END[] = "\"}";
+static constexpr uint32_t SIG_JSON_LEN = 27 + 88 + 29 + 88 + 3;
+static const char SIG_JSON_R[] = "{\"R\":{\"curve\":1,\"element\":\"";
+static const char SIG_JSON_S[] = "\"},\"S\":{\"curve\":1,\"element\":\"";
+static const char SIG_JSON_E[] = "\"}}";
+
+// Go encoding/json string encoding (HTML-safe escaping of <, >, &, U+2028/9).
+std::string go_json_str(const char* s, size_t n) {
+  std::string o = "\"";
+  static const char* hex = "0123456789abcdef";
+  for (size_t i = 0; i < n; i++) {
+    unsigned char c = (unsigned char)s[i];
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      case '<': o += "\\u003c"; break;
+      case '>': o += "\\u003e"; break;
+      case '&': o += "\\u0026"; break;
+      default:
+        if (c < 0x20) {
+          o += "\\u00";
+          o += hex[c >> 4];
+          o += hex[c & 15];
+        } else if (c == 0xE2 && i + 2 < n && (unsigned char)s[i + 1] == 0x80 &&
+                   ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+          o += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+          i += 2;
+        } else {
+          o += (char)c;
+        }
+    }
+  }
+  return o + "\"";
+}
+
+struct PB {
+  Plan& pl;
+  const PPInfo& pp;
+  uint32_t seed_off = 0;
+  std::string tagp;  // tag prefix
+  std::string err;
+  PB(Plan& p, const PPInfo& q) : pl(p), pp(q) {}
+
+  uint32_t arena_put(const void* p, size_t n) {
+    uint32_t off = (uint32_t)pl.arena.size();
+    pl.arena.insert(pl.arena.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+    return off;
+  }
+  uint32_t arena_alloc(uint32_t n) {
+    uint32_t off = (uint32_t)pl.arena.size();
+    pl.arena.resize(pl.arena.size() + n, 0);
+    return off;
+  }
+  uint32_t seg(uint32_t off, uint32_t len) {
+    pl.seg.push_back({off, len});
+    return (uint32_t)pl.seg.size() - 1;
+  }
+  uint32_t rnd(const std::string& tag) {
+    std::string t = tagp + tag;
+    RandJob j;
+    j.seed = seed_off;
+    j.tag = arena_put(t.data(), t.size());
+    j.len = (uint32_t)t.size();
+    j.out = pl.n_scal++;
+    pl.rnd.push_back(j);
+    return j.out;
+  }
+  // 32-byte big-endian scalar from the wire (mod r)
+  uint32_t zr32(const uint8_t* b) {
+    ZrJob j;
+    j.raw = (uint32_t)pl.wire.size();
+    pl.wire.insert(pl.wire.end(), b, b + 32);
+    j.len = 32;
+    j.out = pl.n_scal++;
+    pl.zr.push_back(j);
+    return j.out;
+  }
+  uint32_t zr_u64(uint64_t v) {
+    uint8_t b[32] = {0};
+    for (int k = 0; k < 8; k++) b[31 - k] = (uint8_t)(v >> (8 * k));
+    return zr32(b);
+  }
+  // HashToZr of an arena range (before the group work)
+  uint32_t hash_pre(uint32_t off, uint32_t len) {
+    HashJob h;
+    h.seg_start = (uint32_t)pl.seg.size();
+    seg(off, len);
+    h.seg_count = 1;
+    h.expect = NONE;
+    h.out_scal = pl.n_scal++;
+    pl.hpre.push_back(h);
+    return h.out_scal;
+  }
+  uint32_t challenge(std::initializer_list<std::pair<uint32_t, uint32_t>> segs) {
+    HashJob h;
+    h.seg_start = (uint32_t)pl.seg.size();
+    for (auto& s : segs) seg(s.first, s.second);
+    h.seg_count = (uint32_t)segs.size();
+    h.expect = NONE;
+    h.out_scal = pl.n_scal++;
+    pl.hmain.push_back(h);
+    return h.out_scal;
+  }
+  uint32_t sc(uint32_t op, uint32_t a, uint32_t b, uint32_t c = 0) {
+    uint32_t o = pl.n_scal++;
+    pl.sc.push_back({op, a, b, o, c});
+    return o;
+  }
+  // level 1: the summands are outputs of level-0 scalar jobs (k_scalar runs
+  // one lane per job, so dependent jobs go to a second launch)
+  uint32_t sum(const std::vector<uint32_t>& v, bool level1 = false) {
+    uint32_t o = pl.n_scal++;
+    (level1 ? pl.sc1 : pl.sc).push_back({SOP_SUM, (uint32_t)pl.sclist.size(), (uint32_t)v.size(), o, 0});
+    pl.sclist.insert(pl.sclist.end(), v.begin(), v.end());
+    return o;
+  }
+  // response r + c*w (after the challenge hash)
+  uint32_t resp(uint32_t r, uint32_t c, uint32_t w) {
+    uint32_t o = pl.n_scal++;
+    pl.sc_post.push_back({SOP_MADD, r, c, o, w});
+    return o;
+  }
+  uint32_t point(const uint8_t* raw, uint32_t len, uint32_t bytes) {
+    DecodeJob j;
+    j.raw = (uint32_t)pl.wire.size();
+    pl.wire.insert(pl.wire.end(), raw, raw + len);
+    j.len = len;
+    j.out = pl.n_pts++;
+    j.bytes = bytes;
+    j.b64 = NONE;
+    pl.dec.push_back(j);
+    return j.out;
+  }
+  uint32_t g1job(std::initializer_list<std::pair<uint8_t, uint32_t>> fixed, uint32_t var_pt, uint32_t vscal,
+                 uint32_t bytes, uint32_t b64, bool feeds_pairing) {
+    G1Job j;
+    memset(&j, 0, sizeof(j));
+    for (auto& f : fixed) {
+      j.fbase[j.nfix] = f.first;
+      j.fscal[j.nfix] = f.second;
+      j.nfix++;
+    }
+    j.vstart = (uint32_t)pl.vt.size();
+    j.vcount = 0;
+    j.vscal = NONE;
+    if (var_pt != NONE) {
+      VTerm v;
+      v.pt = var_pt;
+      v.w_lo = 1;
+      v.w_hi = 0;
+      v.pad = 0;
+      pl.vt.push_back(v);
+      j.vcount = 1;
+      j.vscal = vscal;
+    }
+    j.vneg = 0;
+    j.out = pl.n_g1out++;
+    j.bytes = bytes;
+    j.b64 = b64;
+    (feeds_pairing ? pl.g1p : pl.g1).push_back(j);
+    return j.out;
+  }
+
+  // ---- JSON template writer: literal text plus fixed-length base64 holes
+  std::string doc;
+  struct Hole {
+    uint32_t pos, kind, src;
+  };
+  std::vector<Hole> holes;
+  void lit(const char* s) { doc += s; }
+  void zr(uint32_t scal) {
+    doc += ZR_PRE;
+    holes.push_back({(uint32_t)doc.size(), EM_ZR, scal});
+    doc.append(44, '=');
+    doc += EL_END;
+  }
+  void g1(uint32_t bytes_off) {
+    doc += ZR_PRE;
+    holes.push_back({(uint32_t)doc.size(), EM_G1, bytes_off});
+    doc.append(88, '=');
+    doc += EL_END;
+  }
+  void zr_list(const std::vector<uint32_t>& v) {
+    lit("[");
+    for (size_t i = 0; i < v.size(); i++) {
+      if (i) lit(",");
+      zr(v[i]);
+    }
+    lit("]");
+  }
+  // move the document into the arena; returns (offset, length)
+  std::pair<uint32_t, uint32_t> flush_doc() {
+    uint32_t off = arena_put(doc.data(), doc.size());
+    for (auto& h : holes) pl.emit.push_back({off + h.pos, h.kind, h.src});
+    std::pair<uint32_t, uint32_t> r(off, (uint32_t)doc.size());
+    doc.clear();
+    holes.clear();
+    return r;
+  }
+
+  // outer proof {"WellFormedness":b64,"RangeCorrectness":b64|null}
+  void outer(std::pair<uint32_t, uint32_t> wf, bool has_rc, std::pair<uint32_t, uint32_t> rc) {
+    pl.out_off.push_back((uint32_t)pl.out.size());
+    auto put = [&](const char* s) { pl.out.insert(pl.out.end(), s, s + strlen(s)); };
+    auto b64 = [&](std::pair<uint32_t, uint32_t> d) {
+      put("\"");
+      pl.b64.push_back({d.first, d.second, (uint32_t)pl.out.size()});
+      pl.out.resize(pl.out.size() + 4 * ((d.second + 2) / 3), '=');
+      put("\"");
+    };
+    put("{\"WellFormedness\":");
+    b64(wf);
+    put(",\"RangeCorrectness\":");
+    if (has_rc)
+      b64(rc);
+    else
+      put("null");
+    put("}");
+  }
+
+  // rangeproof.Prover.Prove over tokens (output commitments at tok_bytes);
+  // v[k], bf[k] witness scalars, vals[k] the integer values, h_type HashToZr(type)
+  std::pair<uint32_t, uint32_t> range(uint32_t tok_bytes, uint32_t n, const std::vector<uint32_t>& v,
+                                      const std::vector<uint32_t>& bf, const std::vector<uint64_t>& vals,
+                                      uint32_t h_type, const std::string& tag);
+  void transfer(const TransferWit& w, size_t idx);
+  void issue(const IssueWit& w, size_t idx);
+  void begin(const uint8_t* seed) { seed_off = arena_put(seed, 32); }
+  void checks(uint32_t first_pt) {
+    TxChecks t;
+    t.wf_start = (uint32_t)pl.ck.size();
+    t.wf_count = 0;
+    if (pl.n_pts > first_pt) {
+      Check c;
+      c.kind = CK_PTS;
+      c.code = E_PARSE;
+      c.pad = 0;
+      c.a = first_pt;
+      c.b = pl.n_pts - first_pt;
+      pl.ck.push_back(c);
+      t.wf_count = 1;
+    }
+    t.rg_start = (uint32_t)pl.ck.size();
+    t.rg_count = 0;
+    t.mode = 0;
+    pl.tx.push_back(t);
+  }
+};
+
+static bool value_u64(const uint8_t* b, uint64_t& v) {
+  for (int k = 0; k < 24; k++)
+    if (b[k]) return false;
+  v = 0;
+  for (int k = 24; k < 32; k++) v = (v << 8) | b[k];
+  return true;
+}
+
+std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const std::vector<uint32_t>& v,
+                                        const std::vector<uint32_t>& bf, const std::vector<uint64_t>& vals,
+                                        uint32_t h_type, const std::string& tag) {
+  const uint32_t e = (uint32_t)pp.exponent, base = pp.base;
+  uint32_t coms = arena_alloc(64 * n * e);
+  uint32_t rg = arena_alloc(128 * n);
+  struct Dig {
+    uint32_t com, rp, obfs, chal, val, cbf, sbf, hash;
+  };
+  std::vector<std::vector<Dig>> dg(n, std::vector<Dig>(e));
+  std::vector<uint32_t> cbf(n);
+  for (uint32_t k = 0; k < n; k++) {
+    uint64_t x = vals[k];
+    std::vector<uint32_t> parts;
+    for (uint32_t i = 0; i < e; i++) {
+      uint32_t d = (uint32_t)(x % base);
+      x /= base;
+      std::string mt = tag + "/mp/" + std::to_string(k) + "/" + std::to_string(i);
+      uint32_t dbf = rnd(tag + "/digit/" + std::to_string(k) + "/" + std::to_string(i) + "/bf");
+      uint32_t sd = zr_u64(d);
+      // Commitments[k][i] = d*Ped0 + dbf*Ped1   (range/proof.go:340-368)
+      uint32_t com_off = coms + 64 * (k * e + i);
+      g1job({{G1B_PED0, sd}, {G1B_PED1, dbf}}, NONE, NONE, com_off, NONE, false);
+      // membership proof of d on the PS signature of d (sigproof/membership.go:112-158)
+      uint32_t blinding = rnd(mt + "/sigbf"), rr = rnd(mt + "/randomize");
+      uint32_t Rd = point(pp.sig_r[d].data(), (uint32_t)pp.sig_r[d].size(), NONE);
+      uint32_t Sd = point(pp.sig_s[d].data(), (uint32_t)pp.sig_s[d].size(), NONE);
+      // slot: [g1c 64 | GT 384 | sig JSON 235 | R' 64 | S'' 64]
+      uint32_t slot = arena_alloc(64 + 384 + SIG_JSON_LEN + 128);
+      uint8_t* js = &pl.arena[slot + 448];
+      memcpy(js, SIG_JSON_R, 27);
+      memcpy(js + 27 + 88, SIG_JSON_S, 29);
+      memcpy(js + 27 + 88 + 29 + 88, SIG_JSON_E, 3);
+      uint32_t rp_bytes = slot + 448 + SIG_JSON_LEN, obfs_bytes = rp_bytes + 64;
+      // R' = rr*R, S'' = rr*S + blinding*P  (obfuscateSignature, :196-222)
+      uint32_t Rp = g1job({}, Rd, rr, rp_bytes, slot + 448 + 27, true);
+      g1job({{G1B_PEDGEN, blinding}}, Sd, rr, obfs_bytes, slot + 448 + 27 + 88 + 29, false);
+      // h = HashToZr(d.Bytes())
+      uint8_t db[32] = {0};
+      db[28] = (uint8_t)(d >> 24);
+      db[29] = (uint8_t)(d >> 16);
+      db[30] = (uint8_t)(d >> 8);
+      db[31] = (uint8_t)d;
+      uint32_t h = hash_pre(arena_put(db, 32), 32);
+      uint32_t rv = rnd(mt + "/r_value"), rh = rnd(mt + "/r_hash"), rsbf = rnd(mt + "/r_sigbf");
+      // GT = FExp(e(R', rv*PK1 + rh*PK2) * e(rsbf*P, Q))   (computeCommitment, :225-257)
+      uint32_t p1 = g1job({{G1B_PEDGEN, rsbf}}, NONE, NONE, NONE, NONE, true);
+      G2Job g2;
+      memset(&g2, 0, sizeof(g2));
+      g2.nfix = 2;
+      g2.fbase[0] = G2B_PK1;
+      g2.fscal[0] = rv;
+      g2.fbase[1] = G2B_PK2;
+      g2.fscal[1] = rh;
+      g2.out = pl.n_g2out++;
+      pl.g2.push_back(g2);
+      pl.pr.push_back({p1, Rp, g2.out, slot + 64});
+      uint32_t rcb = rnd(mt + "/r_combf");
+      g1job({{G1B_PED0, rv}, {G1B_PED1, rcb}}, NONE, NONE, slot, NONE, false);
+      // challenge (computeChallenge, membership.go:260-277)
+      uint32_t c = challenge({{CONST_FLAG | C_PED0, 128},
+                              {com_off, 64},
+                              {slot, 64},
+                              {CONST_FLAG | C_PEDGEN, 64},
+                              {CONST_FLAG | C_PK_Q, 512},
+                              {slot + 64, 384 + SIG_JSON_LEN}});
+      Dig& D = dg[k][i];
+      D.com = com_off;
+      D.rp = rp_bytes;
+      D.obfs = obfs_bytes;
+      D.chal = c;
+      D.val = resp(rv, c, sd);
+      D.cbf = resp(rcb, c, dbf);
+      D.sbf = resp(rsbf, c, blinding);
+      D.hash = resp(rh, c, h);
+      // commitment blinding factor of the token: sum_i dbf_i base^i
+      uint64_t w = pp.pow[i];
+      parts.push_back(sc(SOP_MULK64, dbf, (uint32_t)w, (uint32_t)(w >> 32)));
+    }
+    cbf[k] = sum(parts, true);
+  }
+  // equality proofs (range/proof.go:141-209)
+  uint32_t rtype = rnd(tag + "/r_type");
+  std::vector<uint32_t> rv(n), rcbf(n), rtbf(n);
+  for (uint32_t k = 0; k < n; k++) {
+    rv[k] = rnd(tag + "/r_value/" + std::to_string(k));
+    rcbf[k] = rnd(tag + "/r_combf/" + std::to_string(k));
+    rtbf[k] = rnd(tag + "/r_tokbf/" + std::to_string(k));
+  }
+  for (uint32_t k = 0; k < n; k++)
+    g1job({{G1B_PED0, rtype}, {G1B_PED1, rv[k]}, {G1B_PED2, rtbf[k]}}, NONE, NONE, rg + 64 * k, NONE, false);
+  for (uint32_t k = 0; k < n; k++)
+    g1job({{G1B_PED0, rv[k]}, {G1B_PED1, rcbf[k]}}, NONE, NONE, rg + 64 * (n + k), NONE, false);
+  uint32_t c = challenge({{CONST_FLAG | C_PEDGEN, 64},
+                          {tok_bytes, 64 * n},
+                          {rg, 128 * n},
+                          {CONST_FLAG | C_PED0, 192},
+                          {CONST_FLAG | C_Q_PK, 512},
+                          {coms, 64 * n * e}});
+  std::vector<uint32_t> ev(n), etb(n), ecb(n);
+  for (uint32_t k = 0; k < n; k++) {
+    ev[k] = resp(rv[k], c, v[k]);
+    etb[k] = resp(rtbf[k], c, bf[k]);
+    ecb[k] = resp(rcbf[k], c, cbf[k]);
+  }
+  uint32_t et = resp(rtype, c, h_type);
+  // RangeProof JSON (range/proof.go:25-57)
+  lit("{\"Challenge\":");
+  zr(c);
+  lit(",\"EqualityProofs\":{\"Type\":");
+  zr(et);
+  lit(",\"Value\":");
+  zr_list(ev);
+  lit(",\"TokenBlindingFactor\":");
+  zr_list(etb);
+  lit(",\"CommitmentBlindingFactor\":");
+  zr_list(ecb);
+  lit("},\"MembershipProofs\":[");
+  for (uint32_t k = 0; k < n; k++) {
+    if (k) lit(",");
+    lit("{\"Commitments\":[");
+    for (uint32_t i = 0; i < e; i++) {
+      if (i) lit(",");
+      g1(dg[k][i].com);
+    }
+    lit("],\"SignatureProofs\":[");
+    for (uint32_t i = 0; i < e; i++) {
+      const Dig& D = dg[k][i];
+      if (i) lit(",");
+      lit("{\"Challenge\":");
+      zr(D.chal);
+      lit(",\"Signature\":{\"R\":");
+      g1(D.rp);
+      lit(",\"S\":");
+      g1(D.obfs);
+      lit("},\"Value\":");
+      zr(D.val);
+      lit(",\"ComBlindingFactor\":");
+      zr(D.cbf);
+      lit(",\"SigBlindingFactor\":");
+      zr(D.sbf);
+      lit(",\"Hash\":");
+      zr(D.hash);
+      lit(",\"Commitment\":");
+      g1(D.com);
+      lit("}");
+    }
+    lit("]}");
+  }
+  lit("]}");
+  return flush_doc();
+}
+
+void PB::transfer(const TransferWit& w, size_t idx) {
+  const uint32_t ni = w.n_in, no = w.n_out;
+  uint64_t bound = 1;
+  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;  // parse_pp keeps base^e < 2^64
+  std::vector<uint64_t> ov(no);
+  bool need_range = !(ni == 1 && no == 1);
+  for (uint32_t k = 0; k < no; k++)
+    if (!value_u64(w.out_values + 32 * k, ov[k]) || (need_range && ov[k] >= bound)) {
+      if (err.empty())
+        err = "proof " + std::to_string(idx) +
+              ": can't compute range proof: value of token outside authorized range";
+      ov[k] = 0;
+    }
+  begin(w.seed);
+  uint32_t first_pt = pl.n_pts;
+  // tokens: inputs then outputs, canonical RawBytes (hashed by both transcripts)
+  uint32_t tok = arena_alloc(64 * (ni + no));
+  for (uint32_t i = 0; i < ni; i++) point(w.inputs + 64 * i, 64, tok + 64 * i);
+  for (uint32_t k = 0; k < no; k++) point(w.outputs + 64 * k, 64, tok + 64 * (ni + k));
+  std::vector<uint32_t> iv(ni), ibf(ni), ovs(no), obf(no);
+  for (uint32_t i = 0; i < ni; i++) {
+    iv[i] = zr32(w.in_values + 32 * i);
+    ibf[i] = zr32(w.in_bfs + 32 * i);
+  }
+  for (uint32_t k = 0; k < no; k++) {
+    ovs[k] = zr32(w.out_values + 32 * k);
+    obf[k] = zr32(w.out_bfs + 32 * k);
+  }
+  uint32_t h_type = hash_pre(arena_put(w.type, w.type_len), (uint32_t)w.type_len);
+  // range proof first (transfer.go:100-107), then well-formedness
+  std::pair<uint32_t, uint32_t> rc(0, 0);
+  if (need_range) {
+    tagp = "";
+    rc = range(tok + 64 * ni, no, ovs, obf, ov, h_type, "tx/range");
+  }
+  // WellFormednessProver (transfer/wellformedness.go:243-378)
+  const std::string t = "tx/wf";
+  uint32_t rt = rnd(t + "/r_type");
+  std::vector<uint32_t> riv(ni), ribf(ni), rov(no), robf(no);
+  for (uint32_t i = 0; i < ni; i++) {
+    riv[i] = rnd(t + "/r_inv/" + std::to_string(i));
+    ribf[i] = rnd(t + "/r_inbf/" + std::to_string(i));
+  }
+  uint32_t rs = rnd(t + "/r_sum");
+  for (uint32_t k = 0; k < no; k++) {
+    rov[k] = rnd(t + "/r_outv/" + std::to_string(k));
+    robf[k] = rnd(t + "/r_outbf/" + std::to_string(k));
+  }
+  uint32_t nwf = ni + 1 + no + 1;
+  uint32_t wf = arena_alloc(64 * nwf);
+  // in_i = rv_i Ped1 + rt Ped0 + rbf_i Ped2; InputSum = (sum rbf) Ped2 + rs Ped1 + n_in rt Ped0
+  for (uint32_t i = 0; i < ni; i++)
+    g1job({{G1B_PED0, rt}, {G1B_PED1, riv[i]}, {G1B_PED2, ribf[i]}}, NONE, NONE, wf + 64 * i, NONE, false);
+  g1job({{G1B_PED0, sc(SOP_MULK, rt, ni)}, {G1B_PED1, rs}, {G1B_PED2, sum(ribf)}}, NONE, NONE, wf + 64 * ni, NONE,
+        false);
+  for (uint32_t k = 0; k < no; k++)
+    g1job({{G1B_PED0, rt}, {G1B_PED1, rov[k]}, {G1B_PED2, robf[k]}}, NONE, NONE, wf + 64 * (ni + 1 + k), NONE,
+          false);
+  g1job({{G1B_PED0, sc(SOP_MULK, rt, no)}, {G1B_PED1, rs}, {G1B_PED2, sum(robf)}}, NONE, NONE,
+        wf + 64 * (nwf - 1), NONE, false);
+  uint32_t c = challenge({{wf, 64 * nwf}, {tok, 64 * (ni + no)}});
+  std::vector<uint32_t> r_ibf(ni), r_obf(no), r_iv(ni), r_ov(no);
+  for (uint32_t i = 0; i < ni; i++) {
+    r_ibf[i] = resp(ribf[i], c, ibf[i]);
+    r_iv[i] = resp(riv[i], c, iv[i]);
+  }
+  for (uint32_t k = 0; k < no; k++) {
+    r_obf[k] = resp(robf[k], c, obf[k]);
+    r_ov[k] = resp(rov[k], c, ovs[k]);
+  }
+  uint32_t r_t = resp(rt, c, h_type), r_s = resp(rs, c, sum(iv));
+  lit("{\"InputBlindingFactors\":");
+  zr_list(r_ibf);
+  lit(",\"OutputBlindingFactors\":");
+  zr_list(r_obf);
+  lit(",\"InputValues\":");
+  zr_list(r_iv);
+  lit(",\"OutputValues\":");
+  zr_list(r_ov);
+  lit(",\"Type\":");
+  zr(r_t);
+  lit(",\"Sum\":");
+  zr(r_s);
+  lit(",\"Challenge\":");
+  zr(c);
+  lit("}");
+  std::pair<uint32_t, uint32_t> wfd = flush_doc();
+  outer(wfd, need_range, rc);
+  checks(first_pt);
+}
+
+void PB::issue(const IssueWit& w, size_t idx) {
+  const uint32_t n = w.n_out;
+  uint64_t bound = 1;
+  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
+  std::vector<uint64_t> vv(n);
+  for (uint32_t k = 0; k < n; k++)
+    if (!value_u64(w.values + 32 * k, vv[k]) || vv[k] >= bound) {
+      if (err.empty())
+        err = "proof " + std::to_string(idx) +
+              ": can't compute range proof: value of token outside authorized range";
+      vv[k] = 0;
+    }
+  begin(w.seed);
+  uint32_t first_pt = pl.n_pts;
+  uint32_t tok = arena_alloc(64 * n);
+  for (uint32_t k = 0; k < n; k++) point(w.outputs + 64 * k, 64, tok + 64 * k);
+  std::vector<uint32_t> v(n), bf(n);
+  for (uint32_t k = 0; k < n; k++) {
+    v[k] = zr32(w.values + 32 * k);
+    bf[k] = zr32(w.bfs + 32 * k);
+  }
+  uint32_t h_type = hash_pre(arena_put(w.type, w.type_len), (uint32_t)w.type_len);
+  // issue WellFormednessProver (issue/wellformedness.go:74-184)
+  const std::string t = "issue/wf";
+  uint32_t rt = w.anonymous ? rnd(t + "/r_type") : NONE;
+  std::vector<uint32_t> rv(n), rbf(n);
+  uint32_t coms = arena_alloc(64 * n);
+  for (uint32_t k = 0; k < n; k++) {
+    rv[k] = rnd(t + "/r_value/" + std::to_string(k));
+    rbf[k] = rnd(t + "/r_bf/" + std::to_string(k));
+    if (w.anonymous)
+      g1job({{G1B_PED1, rv[k]}, {G1B_PED2, rbf[k]}, {G1B_PED0, rt}}, NONE, NONE, coms + 64 * k, NONE, false);
+    else
+      g1job({{G1B_PED1, rv[k]}, {G1B_PED2, rbf[k]}}, NONE, NONE, coms + 64 * k, NONE, false);
+  }
+  uint32_t c = challenge({{coms, 64 * n}, {tok, 64 * n}});
+  std::vector<uint32_t> r_v(n), r_b(n);
+  for (uint32_t k = 0; k < n; k++) {
+    r_v[k] = resp(rv[k], c, v[k]);
+    r_b[k] = resp(rbf[k], c, bf[k]);
+  }
+  lit("{\"Type\":");
+  if (w.anonymous)
+    zr(resp(rt, c, h_type));
+  else
+    lit("null");
+  lit(",\"Values\":");
+  zr_list(r_v);
+  lit(",\"BlindingFactors\":");
+  zr_list(r_b);
+  lit(",\"TypeInTheClear\":");
+  doc += w.anonymous ? std::string("\"\"") : go_json_str(w.type, w.type_len);
+  lit(",\"Challenge\":");
+  zr(c);
+  lit("}");
+  std::pair<uint32_t, uint32_t> wfd = flush_doc();
+  std::pair<uint32_t, uint32_t> rc = range(tok, n, v, bf, vv, h_type, "issue/range");
+  outer(wfd, true, rc);
+  checks(first_pt);
+}
+
+template <class W, class Fn>
+std::string plan_prove(const PPInfo& pp, size_t n, const W* w, Plan& out, int threads, Fn fn) {
+  out.clear();
+  out.arena.resize(C_SIZE, 0);
+  out.p2_g1out = true;
+  if (threads < 1) threads = 1;
+  size_t chunks = std::min<size_t>((size_t)threads, std::max<size_t>(1, n / 64));
+  std::vector<Plan> pieces(chunks);
+  std::vector<std::string> errs(chunks);
+  std::vector<std::thread> th;
+  for (size_t c = 0; c < chunks; c++) {
+    size_t lo = n * c / chunks, hi = n * (c + 1) / chunks;
+    th.emplace_back([&, c, lo, hi]() {
+      PB b(pieces[c], pp);
+      for (size_t i = lo; i < hi; i++) fn(b, w[i], i);
+      errs[c] = b.err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (!e.empty()) return e;
+  for (auto& p : pieces) plan_merge(out, p);
+  return "";
+}
+
+}  // namespace
+
+std::string plan_prove_transfers(const PPInfo& pp, size_t n, const TransferWit* w, Plan& out, int threads) {
+  return plan_prove(pp, n, w, out, threads, [](PB& b, const TransferWit& x, size_t i) { b.transfer(x, i); });
+}
+
+std::string plan_prove_issues(const PPInfo& pp, size_t n, const IssueWit* w, Plan& out, int threads) {
+  return plan_prove(pp, n, w, out, threads, [](PB& b, const IssueWit& x, size_t i) { b.issue(x, i); });
+}
+
+}  // namespace ftsh

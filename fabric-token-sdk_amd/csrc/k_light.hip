@@ -45,6 +45,27 @@ __global__ void __launch_bounds__(256) k_verdict(const TxChecks* tx, uint32_t n,
   if (c == E_OK) atomicOr(&bitmap[i >> 5], 1u << (i & 31));
 }
 
+// ---- prover
+__global__ void __launch_bounds__(128) k_rand(const RandJob* jobs, uint32_t n, const uint8_t* arena,
+                                              uint32_t (*scal)[8]) {
+  JOB_KERNEL_PROLOGUE(n);
+  job_rand(jobs[i], arena, scal);
+}
+
+__global__ void __launch_bounds__(256) k_emit(const EmitJob* jobs, uint32_t n, const uint32_t (*scal)[8],
+                                              uint8_t* arena) {
+  JOB_KERNEL_PROLOGUE(n);
+  job_emit(jobs[i], scal, arena);
+}
+
+// one workgroup per inner document: threads stride over its 3-byte groups
+__global__ void __launch_bounds__(256) k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint8_t* out) {
+  if (blockIdx.x >= n) return;
+  B64Job j = jobs[blockIdx.x];
+  uint32_t groups = (j.len + 2) / 3;
+  for (uint32_t g = threadIdx.x; g < groups; g += blockDim.x) b64_group(out + j.dst + 4 * g, arena + j.src, j.len, g);
+}
+
 // context construction
 
 __global__ void k_pp_decode(const uint8_t* raw, const uint32_t* g1off, uint32_t n1, const uint32_t* g2off,

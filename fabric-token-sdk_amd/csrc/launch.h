@@ -50,6 +50,11 @@ __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 
+// prover (k_light.hip)
+__global__ void k_rand(const RandJob* jobs, uint32_t n, const uint8_t* arena, uint32_t (*scal)[8]);
+__global__ void k_emit(const EmitJob* jobs, uint32_t n, const uint32_t (*scal)[8], uint8_t* arena);
+__global__ void k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint8_t* out);
+
 // standalone MSM (k_msm.hip)
 __global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok);
 __global__ void k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]);

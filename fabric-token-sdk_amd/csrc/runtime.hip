@@ -58,6 +58,12 @@ struct ftz_batch {
   DBuf<G1JDev> part1, part1p;  // G1 job parts (4 per job) of the side / pairing G1 jobs
   DBuf<int32_t> codes;
   DBuf<uint32_t> bitmap;
+  // prover
+  DBuf<RandJob> rnd;
+  DBuf<ScalJob> sc1, sc_post;
+  DBuf<EmitJob> emit;
+  DBuf<B64Job> b64;
+  DBuf<uint8_t> out;
   hipEvent_t ev[16];
   bool ev_init = false;
   ftz_stats stats;
@@ -265,6 +271,12 @@ static int batch_upload(ftz_batch* b) {
   if (p.g2.size() != p.pr.size()) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   for (size_t i = 0; i < p.pr.size(); i++)
     if (p.pr[i].q2 != p.g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
+  HC(b->rnd.upload(p.rnd, s));
+  HC(b->sc1.upload(p.sc1, s));
+  HC(b->sc_post.upload(p.sc_post, s));
+  HC(b->emit.upload(p.emit, s));
+  HC(b->b64.upload(p.b64, s));
+  HC(b->out.upload(p.out, s));
   HC(b->hash_ok.alloc(std::max<size_t>(p.hmain.size(), 1)));
   HC(b->hash_ok_pre.alloc(std::max<size_t>(p.hpre.size(), 1)));
   HC(b->codes.alloc(std::max<size_t>(b->n, 1)));
@@ -465,4 +477,208 @@ extern "C" int ftz_verify_issues(ftz_ctx* c, size_t n, const ftz_issue* is, int3
   if (rc == FTZ_SUCCESS) rc = ftz_batch_codes(b, codes);
   ftz_batch_destroy(b);
   return rc;
+}
+
+// ------------------------------------------------------------------ prover
+// Plans from host/planner_prove.cpp; the pipeline of ftz_batch_run with the
+// prover's extra stages: randomness before the group work, responses, JSON
+// hole filling and base64 of the inner documents after the transcript hashes.
+struct ftz_prover : ftz_batch {};
+
+template <class W, class In, class Plan_fn>
+static int prover_load(ftz_ctx* c, size_t n, const W* w, ftz_prover** out, Plan_fn plan) {
+  if (!c || !out || (n && !w)) return set_err(FTZ_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  ftz_prover* b = new ftz_prover();
+  b->ctx = c;
+  b->n = n;
+  std::string e = plan(b->plan);
+  if (!e.empty()) {
+    delete b;
+    return set_err(FTZ_E_INVALID, e);
+  }
+  int rc = batch_upload(b);
+  if (rc != FTZ_SUCCESS) {
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return FTZ_SUCCESS;
+}
+
+static bool seeds_ok(const uint8_t* seed) { return seed != nullptr; }
+
+extern "C" int ftz_prover_load_transfers(ftz_ctx* c, size_t n, const ftz_transfer_witness* w, ftz_prover** out) {
+  for (size_t i = 0; i < n && w; i++)
+    if ((w[i].n_in && (!w[i].inputs || !w[i].in_values || !w[i].in_bfs)) ||
+        (w[i].n_out && (!w[i].outputs || !w[i].out_values || !w[i].out_bfs)) || !seeds_ok(w[i].seed) ||
+        (w[i].type_len && !w[i].type))
+      return set_err(FTZ_E_INVALID, "null buffer in witness " + std::to_string(i));
+  return prover_load<ftz_transfer_witness, TransferWit>(c, n, w, out, [&](Plan& p) {
+    std::vector<TransferWit> t(n);
+    for (size_t i = 0; i < n; i++)
+      t[i] = {w[i].inputs, w[i].n_in, w[i].outputs, w[i].n_out, w[i].in_values, w[i].in_bfs,
+              w[i].out_values, w[i].out_bfs, w[i].type, w[i].type_len, w[i].seed};
+    return plan_prove_transfers(c->pp, n, t.data(), p, c->threads);
+  });
+}
+
+extern "C" int ftz_prover_load_issues(ftz_ctx* c, size_t n, const ftz_issue_witness* w, ftz_prover** out) {
+  for (size_t i = 0; i < n && w; i++)
+    if ((w[i].n_out && (!w[i].outputs || !w[i].values || !w[i].bfs)) || !seeds_ok(w[i].seed) ||
+        (w[i].type_len && !w[i].type))
+      return set_err(FTZ_E_INVALID, "null buffer in witness " + std::to_string(i));
+  return prover_load<ftz_issue_witness, IssueWit>(c, n, w, out, [&](Plan& p) {
+    std::vector<IssueWit> t(n);
+    for (size_t i = 0; i < n; i++)
+      t[i] = {w[i].outputs, w[i].n_out, w[i].values, w[i].bfs, w[i].type, w[i].type_len, w[i].anonymous, w[i].seed};
+    return plan_prove_issues(c->pp, n, t.data(), p, c->threads);
+  });
+}
+
+extern "C" int ftz_prover_run(ftz_prover* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null prover");
+  ftz_ctx* c = b->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  Plan& p = b->plan;
+  hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
+  static const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';
+  if (serial) s2 = s3 = s;
+  uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
+  uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
+  uint32_t n_rnd = (uint32_t)p.rnd.size(), n_sp = (uint32_t)p.sc_post.size(), n_em = (uint32_t)p.emit.size();
+  uint32_t n_b64 = (uint32_t)p.b64.size();
+  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
+  uint32_t n_pr = (uint32_t)p.pr.size();
+  uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
+  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, (uint64_t)n_rnd + n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1,
+                                 (uint64_t)n_hm + n_sp, (uint64_t)n_em + n_b64, n_tx};
+  hipEvent_t* e = b->ev;
+  HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
+  HC(hipEventRecord(e[0], s));
+  if (n_dec) k_decode<<<blocks_for(n_dec, 256), 256, 0, s>>>(b->dec.p, n_dec, b->wire.p, b->pts.p, b->pt_ok.p, b->arena.p);
+  HC(hipEventRecord(e[1], s));
+  if (n_zr) k_zr<<<blocks_for(n_zr, 256), 256, 0, s>>>(b->zr.p, n_zr, b->wire.p, scal, b->canon.p);
+  HC(hipEventRecord(e[2], s));
+  if (n_rnd) k_rand<<<blocks_for(n_rnd, 128), 128, 0, s>>>(b->rnd.p, n_rnd, b->arena.p, scal);
+  if (n_hp)
+    k_hash<<<blocks_for(n_hp, 128), 128, 0, s>>>(b->hpre.p, n_hp, b->seg.p, b->arena.p, scal, b->canon.p,
+                                                 b->hash_ok_pre.p);
+  HC(hipEventRecord(e[3], s));
+  if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
+  uint32_t n_sc1 = (uint32_t)p.sc1.size();
+  if (n_sc1) k_scalar<<<blocks_for(n_sc1, 256), 256, 0, s>>>(b->sc1.p, n_sc1, scal, b->sclist.p);
+  HC(hipEventRecord(e[4], s));
+  // stream2: G1 jobs no pairing depends on
+  HC(hipStreamWaitEvent(s2, e[4], 0));
+  HC(hipEventRecord(e[11], s2));
+  if (n_g1) {
+    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
+                                                         b->part1.p);
+    k_g1_combine<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+  }
+  HC(hipEventRecord(e[12], s2));
+  // main: R' = rr R and rsbf P (the pairing inputs)
+  if (n_g1p) {
+    k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
+                                                         b->part1p.p);
+    k_g1_combine<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
+  }
+  HC(hipEventRecord(e[5], s));
+  // stream3: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)
+  HC(hipStreamWaitEvent(s3, e[5], 0));
+  HC(hipEventRecord(e[14], s3));
+  if (n_g2)
+    k_g2lines<<<blocks_for(n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p,
+                                                                 b->g2out.p, b->g1out.p, b->lines2.p);
+  HC(hipEventRecord(e[15], s3));
+  HC(hipStreamWaitEvent(s, e[15], 0));
+  HC(hipEventRecord(e[6], s));
+  if (n_pr)
+    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->lines2.p, b->g1out.p,
+                                                               b->fbuf.p);
+  HC(hipEventRecord(e[7], s));
+  if (n_pr) k_fexp<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
+  HC(hipEventRecord(e[8], s));
+  HC(hipStreamWaitEvent(s, e[12], 0));
+  HC(hipEventRecord(e[9], s));
+  if (n_hm)
+    k_hash<<<blocks_for(n_hm, 128), 128, 0, s>>>(b->hmain.p, n_hm, b->seg.p, b->arena.p, scal, b->canon.p,
+                                                 b->hash_ok.p);
+  if (n_sp) k_scalar<<<blocks_for(n_sp, 256), 256, 0, s>>>(b->sc_post.p, n_sp, scal, b->sclist.p);
+  HC(hipEventRecord(e[10], s));
+  if (n_em) k_emit<<<blocks_for(n_em, 256), 256, 0, s>>>(b->emit.p, n_em, scal, b->arena.p);
+  if (n_b64) k_b64<<<n_b64, 256, 0, s>>>(b->b64.p, n_b64, b->arena.p, b->out.p);
+  HC(hipEventRecord(e[13], s));
+  if (n_tx)
+    k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
+                                                    b->bitmap.p);
+  HC(hipGetLastError());
+  HC(hipStreamSynchronize(s));
+  // stats order: decode zr rand+hash_pre scalar g1p g2+lines miller fexp g1(side) hash+responses emit+b64 total
+  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 14, 6, 7, 11, 9, 10, 0};
+  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
+  for (int k = 0; k < FTZ_NKERNELS; k++) {
+    float ms = 0;
+    HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
+    b->stats.ms[k] = ms;
+    b->stats.jobs[k] = jobs[k];
+  }
+  return FTZ_SUCCESS;
+}
+
+extern "C" size_t ftz_prover_bytes(const ftz_prover* b) { return b ? b->plan.out.size() : 0; }
+
+extern "C" int ftz_prover_proofs(ftz_prover* b, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes) {
+  if (!b) return set_err(FTZ_E_INVALID, "null prover");
+  const Plan& p = b->plan;
+  if (cap < p.out.size() || (p.out.size() && !buf)) return set_err(FTZ_E_INVALID, "proof buffer too small");
+  HC(hipSetDevice(b->ctx->device));
+  hipStream_t s = b->ctx->stream;
+  if (p.out.size()) HC(hipMemcpyAsync(buf, b->out.p, p.out.size(), hipMemcpyDeviceToHost, s));
+  if (codes && b->n) HC(hipMemcpyAsync(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HC(hipStreamSynchronize(s));
+  if (offsets) {
+    for (size_t i = 0; i < b->n; i++) offsets[i] = p.out_off[i];
+    offsets[b->n] = p.out.size();
+  }
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_prover_stats(const ftz_prover* b, ftz_stats* out) {
+  if (!b || !out) return set_err(FTZ_E_INVALID, "null argument");
+  *out = b->stats;
+  return FTZ_SUCCESS;
+}
+
+extern "C" void ftz_prover_destroy(ftz_prover* b) {
+  if (!b) return;
+  (void)hipSetDevice(b->ctx->device);
+  if (b->ev_init)
+    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev[k]);
+  delete b;
+}
+
+template <class W, class Load>
+static int prove_once(ftz_ctx* c, size_t n, const W* w, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes,
+                      Load load) {
+  ftz_prover* p = nullptr;
+  int rc = load(c, n, w, &p);
+  if (rc != FTZ_SUCCESS) return rc;
+  rc = ftz_prover_run(p);
+  if (rc == FTZ_SUCCESS) rc = ftz_prover_proofs(p, buf, cap, offsets, codes);
+  ftz_prover_destroy(p);
+  return rc;
+}
+
+extern "C" int ftz_prove_transfers(ftz_ctx* c, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,
+                                   size_t* offsets, int32_t* codes) {
+  return prove_once(c, n, w, buf, cap, offsets, codes, ftz_prover_load_transfers);
+}
+
+extern "C" int ftz_prove_issues(ftz_ctx* c, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap,
+                                size_t* offsets, int32_t* codes) {
+  return prove_once(c, n, w, buf, cap, offsets, codes, ftz_prover_load_issues);
 }

@@ -22,7 +22,7 @@ from . import _abi
 from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_PANIC, FTZ_ERR_PARSE, FTZ_ERR_RANGE,  # noqa: F401
                    FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
 
-__all__ = ["Context", "Batch", "Msm", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
+__all__ = ["Context", "Batch", "Msm", "Prover", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
            "FTZ_OK", "MESSAGES"]
 
 
@@ -93,6 +93,24 @@ class Context:
         _check(self._lib.ftz_verify_issues(self._h, n, arr, codes), self._lib)
         return list(codes)[:n]
 
+    def prove_transfers(self, witnesses):
+        """Proof bytes for each witness (see Prover); raises ZKError-free
+        DeviceError on bad arguments (e.g. a value outside the range)."""
+        p = Prover(self, list(witnesses), "transfer")
+        try:
+            p.run()
+            return p.proofs()
+        finally:
+            p.close()
+
+    def prove_issues(self, witnesses):
+        p = Prover(self, list(witnesses), "issue")
+        try:
+            p.run()
+            return p.proofs()
+        finally:
+            p.close()
+
     def msm_g1(self, points, scalars):
         """sum_i k_i P_i (gnark G1Jac.MultiExp semantics): points n x 64-byte
         RawBytes, scalars n x 32 bytes big-endian.  Returns 64-byte RawBytes."""
@@ -149,6 +167,48 @@ class Msm:
     def close(self):
         if getattr(self, "_h", None):
             self._lib.ftz_msm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+class Prover:
+    """Device-resident batch prover (transfer.NewProver(...).Prove(),
+    transfer/transfer.go:89-121; issue.NewProver(...).Prove(), issue/issue.go:162-184).
+    witnesses: dicts as in _abi.pack_transfer_witnesses / pack_issue_witnesses."""
+
+    def __init__(self, ctx, witnesses, kind="transfer"):
+        self._ctx, self._lib, self._h = ctx, ctx._lib, None
+        pack = _abi.pack_transfer_witnesses if kind == "transfer" else _abi.pack_issue_witnesses
+        load = self._lib.ftz_prover_load_transfers if kind == "transfer" else self._lib.ftz_prover_load_issues
+        arr, keep = pack(witnesses)
+        self.n = len(list(witnesses)) if not isinstance(witnesses, list) else len(witnesses)
+        h = ctypes.c_void_p()
+        _check(load(ctx._h, self.n, arr, ctypes.byref(h)), self._lib)
+        self._h = h
+
+    def run(self):
+        _check(self._lib.ftz_prover_run(self._h), self._lib)
+
+    def proofs(self):
+        """(list of proof bytes, list of codes)"""
+        size = self._lib.ftz_prover_bytes(self._h)
+        buf = (ctypes.c_uint8 * max(1, size))()
+        offs = (ctypes.c_size_t * (self.n + 1))()
+        codes = (ctypes.c_int32 * max(1, self.n))()
+        _check(self._lib.ftz_prover_proofs(self._h, buf, size, offs, codes), self._lib)
+        raw = bytes(buf)[:size]
+        return [raw[offs[i]:offs[i + 1]] for i in range(self.n)], list(codes)[:self.n]
+
+    def stats(self):
+        s = _abi.Stats()
+        _check(self._lib.ftz_prover_stats(self._h, ctypes.byref(s)), self._lib)
+        return {name: (s.ms[k], s.jobs[k]) for k, name in enumerate(_abi.PROVER_STAGE_NAMES)}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.ftz_prover_destroy(self._h)
             self._h = None
 
     def __del__(self):

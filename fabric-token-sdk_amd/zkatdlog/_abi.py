@@ -18,6 +18,9 @@ FTZ_E_NOMEM = -4
 
 FTZ_NKERNELS = 12
 KERNEL_NAMES = ["decode", "zr", "hash_pre", "scalar", "g1p", "g2", "miller", "fexp", "g1", "hash", "verdict", "total"]
+# ftz_prover_stats uses the same slots with the prover's stages
+PROVER_STAGE_NAMES = ["decode", "zr", "rand+hash_pre", "scalar", "g1p", "g2", "miller", "fexp", "g1", "hash+responses",
+                      "emit+b64", "total"]
 
 # error strings of the reference for each class (tests match substrings)
 MESSAGES = {
@@ -42,6 +45,62 @@ class Issue(ctypes.Structure):
                 ("anonymous", ctypes.c_uint8)]
 
 
+class TransferWitness(ctypes.Structure):
+    _fields_ = [("inputs", ctypes.c_void_p), ("n_in", ctypes.c_uint32),
+                ("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
+                ("in_values", ctypes.c_void_p), ("in_bfs", ctypes.c_void_p),
+                ("out_values", ctypes.c_void_p), ("out_bfs", ctypes.c_void_p),
+                ("type", ctypes.c_void_p), ("type_len", ctypes.c_size_t), ("seed", ctypes.c_void_p)]
+
+
+class IssueWitness(ctypes.Structure):
+    _fields_ = [("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
+                ("values", ctypes.c_void_p), ("bfs", ctypes.c_void_p),
+                ("type", ctypes.c_void_p), ("type_len", ctypes.c_size_t),
+                ("anonymous", ctypes.c_uint8), ("seed", ctypes.c_void_p)]
+
+
+def _buf(b, keep):
+    if not b:
+        return None
+    c = ctypes.create_string_buffer(bytes(b), len(b))
+    keep.append(c)
+    return ctypes.addressof(c)
+
+
+def _zr32(vals):
+    return b"".join(int(v).to_bytes(32, "big") for v in vals)
+
+
+def pack_transfer_witnesses(ws):
+    """ws: iterable of dicts with inputs/outputs (concatenated 64-byte RawBytes),
+    in_values/in_bfs/out_values/out_bfs (ints), type (str) and seed (32 bytes).
+    Returns (ctypes array, keep-alive list)."""
+    ws = list(ws)
+    keep = []
+    arr = (TransferWitness * max(1, len(ws)))()
+    for i, w in enumerate(ws):
+        t = w["type"].encode() if isinstance(w["type"], str) else bytes(w["type"])
+        arr[i] = TransferWitness(_buf(w["inputs"], keep), len(w["inputs"]) // 64,
+                                 _buf(w["outputs"], keep), len(w["outputs"]) // 64,
+                                 _buf(_zr32(w["in_values"]), keep), _buf(_zr32(w["in_bfs"]), keep),
+                                 _buf(_zr32(w["out_values"]), keep), _buf(_zr32(w["out_bfs"]), keep),
+                                 _buf(t, keep), len(t), _buf(w["seed"], keep))
+    return arr, keep
+
+
+def pack_issue_witnesses(ws):
+    ws = list(ws)
+    keep = []
+    arr = (IssueWitness * max(1, len(ws)))()
+    for i, w in enumerate(ws):
+        t = w["type"].encode() if isinstance(w["type"], str) else bytes(w["type"])
+        arr[i] = IssueWitness(_buf(w["outputs"], keep), len(w["outputs"]) // 64,
+                              _buf(_zr32(w["values"]), keep), _buf(_zr32(w["bfs"]), keep),
+                              _buf(t, keep), len(t), 1 if w.get("anonymous") else 0, _buf(w["seed"], keep))
+    return arr, keep
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("ms", ctypes.c_float * FTZ_NKERNELS), ("jobs", ctypes.c_uint64 * FTZ_NKERNELS)]
 
@@ -52,7 +111,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_threads", "ftz_ctx_info",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
-           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy"]
+           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
+           "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
+           "ftz_prover_run", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
 _lib = None
 
@@ -93,6 +154,19 @@ def load():
     lib.ftz_msm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     lib.ftz_msm_destroy.argtypes = [vp]
     lib.ftz_msm_destroy.restype = None
+    szp = ctypes.POINTER(ctypes.c_size_t)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    lib.ftz_prove_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), u8p, sz, szp, i32p]
+    lib.ftz_prove_issues.argtypes = [vp, sz, ctypes.POINTER(IssueWitness), u8p, sz, szp, i32p]
+    lib.ftz_prover_load_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), ctypes.POINTER(vp)]
+    lib.ftz_prover_load_issues.argtypes = [vp, sz, ctypes.POINTER(IssueWitness), ctypes.POINTER(vp)]
+    lib.ftz_prover_run.argtypes = [vp]
+    lib.ftz_prover_bytes.argtypes = [vp]
+    lib.ftz_prover_bytes.restype = sz
+    lib.ftz_prover_proofs.argtypes = [vp, u8p, sz, szp, i32p]
+    lib.ftz_prover_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    lib.ftz_prover_destroy.argtypes = [vp]
+    lib.ftz_prover_destroy.restype = None
     _lib = lib
     return lib
 

@@ -120,6 +120,58 @@ int ftz_msm_run(ftz_msm* m, uint8_t out[64]);
 int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits);
 void ftz_msm_destroy(ftz_msm* m);
 
+/* ---- batch prover (BASELINE configs[4]).
+ * Replaces transfer.NewProver(inW, outW, in, out, pp).Prove()
+ * (token/core/zkatdlog/crypto/transfer/transfer.go:42,89-121) and
+ * issue.NewProver(...).Prove() (crypto/issue/issue.go:151,162-184): the proof
+ * JSON bytes, byte-identical to the reference's encoding.  Witnesses follow
+ * token.TokenDataWitness (crypto/token/token.go): Value and BlindingFactor as
+ * 32-byte big-endian Zr.  Randomness: the reference draws from crypto/rand;
+ * here every random scalar is SHA-256(seed||tag||0)||SHA-256(seed||tag||1) mod r
+ * from a caller-supplied 32-byte seed per proof (the Go shim passes 32 bytes of
+ * crypto/rand), so proofs are reproducible for testing.  A value outside
+ * [0, base^exponent) fails the load with FTZ_E_INVALID ("can't compute range
+ * proof: value of token outside authorized range", range/proof.go:300-302). */
+typedef struct {
+  const uint8_t* inputs;     /* n_in x 64-byte RawBytes (ledger input commitments) */
+  uint32_t n_in;
+  const uint8_t* outputs;    /* n_out x 64-byte RawBytes (output commitments)      */
+  uint32_t n_out;
+  const uint8_t* in_values;  /* n_in x 32-byte BE Zr                               */
+  const uint8_t* in_bfs;     /* n_in x 32-byte BE Zr                               */
+  const uint8_t* out_values; /* n_out x 32-byte BE Zr                              */
+  const uint8_t* out_bfs;    /* n_out x 32-byte BE Zr                              */
+  const char* type;          /* token type (TokenDataWitness.Type)                 */
+  size_t type_len;
+  const uint8_t* seed;       /* 32 bytes                                           */
+} ftz_transfer_witness;
+typedef struct {
+  const uint8_t* outputs;    /* n_out x 64-byte RawBytes (issued commitments)      */
+  uint32_t n_out;
+  const uint8_t* values;     /* n_out x 32-byte BE Zr                              */
+  const uint8_t* bfs;        /* n_out x 32-byte BE Zr                              */
+  const char* type;
+  size_t type_len;
+  uint8_t anonymous;
+  const uint8_t* seed;       /* 32 bytes                                           */
+} ftz_issue_witness;
+typedef struct ftz_prover ftz_prover;
+/* one call: proofs concatenated into buf (cap bytes; ftz_prover_bytes tells the
+ * size), offsets[n+1] delimit proof i; codes[i] = FTZ_ERR_PARSE if a commitment
+ * of proof i does not decode, else FTZ_OK */
+int ftz_prove_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,
+                        size_t* offsets, int32_t* codes);
+int ftz_prove_issues(ftz_ctx* ctx, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap,
+                     size_t* offsets, int32_t* codes);
+/* staged form: plan + upload once, run on HBM-resident witnesses (bench) */
+int ftz_prover_load_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer_witness* w, ftz_prover** out);
+int ftz_prover_load_issues(ftz_ctx* ctx, size_t n, const ftz_issue_witness* w, ftz_prover** out);
+int ftz_prover_run(ftz_prover* p);
+size_t ftz_prover_bytes(const ftz_prover* p);
+int ftz_prover_proofs(ftz_prover* p, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes);
+int ftz_prover_stats(const ftz_prover* p, ftz_stats* out);
+void ftz_prover_destroy(ftz_prover* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-T=fabric-token-sdk_amd/tools/msmtune.py
-timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof -o run -- python $T 20 "0,0,0" > gpurun_out/prof.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_prover.py -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/prover_tests.log 2>&1 && \
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/bench.log 2>&1
 echo EXIT $?

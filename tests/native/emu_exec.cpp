@@ -191,6 +191,89 @@ int emu_opcount_transfers(void* ctx, size_t n, const ftz_transfer* tx, unsigned 
 }
 #endif
 
+// prover plan (host/planner_prove.cpp) in the order of ftz_prover_run
+static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t cap, size_t* offsets,
+                           int32_t* codes) {
+  memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
+  std::vector<uint8_t> wire = p.wire;
+  wire.resize(wire.size() + 64, 0);
+  std::vector<G1Dev> pts(std::max<uint32_t>(p.n_pts, 1));
+  std::vector<uint8_t> pt_ok(std::max<uint32_t>(p.n_pts, 1), 1);
+  std::vector<uint32_t> scalv(8 * (size_t)std::max<uint32_t>(p.n_scal, 1));
+  uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(scalv.data());
+  std::vector<uint8_t> canon(std::max<uint32_t>(p.n_scal, 1));
+  std::vector<G1Dev> g1out(std::max<uint32_t>(p.n_g1out, 1));
+  std::vector<G2Dev> g2out(std::max<uint32_t>(p.n_g2out, 1));
+  std::vector<F12Dev> fbuf(std::max<size_t>(p.pr.size(), 1));
+  std::vector<uint8_t> hok(std::max<size_t>(p.hmain.size(), 1));
+  par_for((uint32_t)p.dec.size(), [&](uint32_t i) { pt_ok[p.dec[i].out] = job_decode(p.dec[i], wire.data(), pts.data(), p.arena.data()); });
+  par_for((uint32_t)p.zr.size(), [&](uint32_t i) { job_zr(p.zr[i], wire.data(), scal, canon.data()); });
+  par_for((uint32_t)p.rnd.size(), [&](uint32_t i) { job_rand(p.rnd[i], p.arena.data(), scal); });
+  par_for((uint32_t)p.hpre.size(), [&](uint32_t i) { job_hash(p.hpre[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  // one parallel pass per level, as the device runs them
+  par_for((uint32_t)p.sc.size(), [&](uint32_t i) { job_scalar(p.sc[i], scal, p.sclist.data()); });
+  par_for((uint32_t)p.sc1.size(), [&](uint32_t i) { job_scalar(p.sc1[i], scal, p.sclist.data()); });
+  par_for((uint32_t)p.g1p.size(), [&](uint32_t i) {
+    job_g1(p.g1p[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data());
+  });
+  {
+    uint32_t n1 = (uint32_t)p.g1.size();
+    std::vector<G1JDev> part(4 * (size_t)std::max<uint32_t>(n1, 1));
+    par_for(4 * n1, [&](uint32_t i) {
+      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data());
+    });
+    par_for(n1, [&](uint32_t i) { job_g1_combine(p.g1[i], i, n1, part.data(), g1out.data(), p.arena.data()); });
+  }
+  par_for((uint32_t)p.g2.size(), [&](uint32_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
+  // pair 2 of a prover pairing job is R' = rr R (a G1 job output)
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
+    job_miller(p.pr[i], c->qlines.data(), g1out.data(), g1out.data(), g2out.data(), fbuf.data(), i);
+  });
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data()); });
+  par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
+  par_for((uint32_t)p.sc_post.size(), [&](uint32_t i) { job_scalar(p.sc_post[i], scal, p.sclist.data()); });
+  par_for((uint32_t)p.emit.size(), [&](uint32_t i) { job_emit(p.emit[i], scal, p.arena.data()); });
+  std::vector<uint8_t> out = p.out;
+  for (const B64Job& j : p.b64) b64_encode(out.data() + j.dst, p.arena.data() + j.src, j.len);
+  for (size_t i = 0; i < n; i++) codes[i] = job_verdict(p.tx[i], p.ck.data(), pt_ok.data(), hok.data());
+  if (out.size() > cap) return -(long)out.size();
+  memcpy(buf, out.data(), out.size());
+  for (size_t i = 0; i < n; i++) offsets[i] = p.out_off[i];
+  offsets[n] = out.size();
+  return (long)out.size();
+}
+
+long emu_prove_transfers(void* ctx, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,
+                         size_t* offsets, int32_t* codes, char* err, size_t errlen) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<TransferWit> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {w[i].inputs, w[i].n_in, w[i].outputs, w[i].n_out, w[i].in_values, w[i].in_bfs,
+            w[i].out_values, w[i].out_bfs, w[i].type, w[i].type_len, w[i].seed};
+  Plan p;
+  std::string e = plan_prove_transfers(c->pp, n, t.data(), p, 4);
+  if (!e.empty()) {
+    snprintf(err, errlen, "%s", e.c_str());
+    return -1;
+  }
+  return run_prove_plan(c, p, n, buf, cap, offsets, codes);
+}
+
+long emu_prove_issues(void* ctx, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap, size_t* offsets,
+                      int32_t* codes, char* err, size_t errlen) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<IssueWit> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {w[i].outputs, w[i].n_out, w[i].values, w[i].bfs, w[i].type, w[i].type_len, w[i].anonymous, w[i].seed};
+  Plan p;
+  std::string e = plan_prove_issues(c->pp, n, t.data(), p, 4);
+  if (!e.empty()) {
+    snprintf(err, errlen, "%s", e.c_str());
+    return -1;
+  }
+  return run_prove_plan(c, p, n, buf, cap, offsets, codes);
+}
+
 int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* codes) {
   EmuCtx* c = (EmuCtx*)ctx;
   std::vector<TransferIn> t(n);

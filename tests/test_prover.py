@@ -1,0 +1,178 @@
+"""Batch prover (include/ftsamd.h ftz_prove_*).
+
+The prover's randomness is rand(tag) = SHA-256(seed||tag||0)||SHA-256(seed||tag||1)
+mod r per proof (the oracle's ``Rand``), so its proofs must equal the oracle's
+``transfer_prove`` / ``issue_prove`` (tags "tx" / "issue") byte for byte.
+
+CPU tier: the planner + device job code compiled for the host (TEST-ONLY
+tests/native) against the oracle.  GPU tier: the same through the C ABI on the
+MI355X, plus GPU-verify of a batch of GPU-made proofs."""
+import ctypes
+import hashlib
+import random
+
+import pytest
+
+from ftsoracle import bn254 as C
+from ftsoracle import zkat as Z
+from zkatdlog import _abi as A
+
+
+@pytest.fixture(scope="module")
+def pp_a(golden):
+    js = golden["pp_a"]["pp"].encode()
+    return js, Z.PublicParams.from_json(js)
+
+
+def witness(pp, seed_i, n_in, n_out, ttype="ABC", bound=None):
+    rng = random.Random(seed_i)
+    top = bound or pp.base ** pp.exponent
+    ins_v = [rng.randrange(top) for _ in range(n_in)]
+    outs_v = list(ins_v) if n_in == n_out else [rng.randrange(top) for _ in range(n_out)]
+    in_bf = [rng.randrange(C.R) for _ in range(n_in)]
+    out_bf = [rng.randrange(C.R) for _ in range(n_out)]
+    ins = [Z.token_commitment(pp, ttype, v, b) for v, b in zip(ins_v, in_bf)]
+    outs = [Z.token_commitment(pp, ttype, v, b) for v, b in zip(outs_v, out_bf)]
+    seed = hashlib.sha256(b"prover-seed-%d" % seed_i).digest()
+    return {"inputs": b"".join(C.g1_bytes(p) for p in ins), "outputs": b"".join(C.g1_bytes(p) for p in outs),
+            "in_values": ins_v, "in_bfs": in_bf, "out_values": outs_v, "out_bfs": out_bf, "type": ttype,
+            "seed": seed, "_ins": ins, "_outs": outs}
+
+
+def oracle_transfer(pp, w):
+    return Z.transfer_prove(pp, Z.Rand(w["seed"]), w["_ins"], w["_outs"],
+                            list(zip(w["in_values"], w["in_bfs"])), list(zip(w["out_values"], w["out_bfs"])),
+                            w["type"], tag="tx")
+
+
+def issue_witness(pp, seed_i, n, ttype="ABC", anonymous=False):
+    w = witness(pp, seed_i, 0, n, ttype)
+    return {"outputs": w["outputs"], "values": w["out_values"], "bfs": w["out_bfs"], "type": ttype,
+            "anonymous": anonymous, "seed": w["seed"], "_outs": w["_outs"]}
+
+
+def oracle_issue(pp, w):
+    return Z.issue_prove(pp, Z.Rand(w["seed"]), w["_outs"], list(zip(w["values"], w["bfs"])), w["type"],
+                         anonymous=w["anonymous"], tag="issue")
+
+
+def emu_prove(emu, pp_json, ws, issue=False):
+    ctx = emu.emu_ctx_create(pp_json, len(pp_json), ctypes.create_string_buffer(256), 256)
+    assert ctx
+    try:
+        arr, keep = (A.pack_issue_witnesses if issue else A.pack_transfer_witnesses)(ws)
+        fn = emu.emu_prove_issues if issue else emu.emu_prove_transfers
+        fn.restype = ctypes.c_long
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t,
+                       ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int32), ctypes.c_char_p,
+                       ctypes.c_size_t]
+        cap = 1 << 22
+        buf = ctypes.create_string_buffer(cap)
+        offs = (ctypes.c_size_t * (len(ws) + 1))()
+        codes = (ctypes.c_int32 * max(1, len(ws)))()
+        err = ctypes.create_string_buffer(512)
+        r = fn(ctx, len(ws), arr, buf, cap, offs, codes, err, 512)
+        if r < 0:
+            raise ValueError(err.value.decode())
+        return [buf.raw[offs[i]:offs[i + 1]] for i in range(len(ws))], list(codes)[:len(ws)]
+    finally:
+        emu.emu_ctx_destroy(ctx)
+
+
+@pytest.mark.parametrize("n_in,n_out", [(2, 2), (1, 1), (1, 2)])
+def test_emu_transfer_proofs_match_oracle(emu, pp_a, n_in, n_out):
+    js, pp = pp_a
+    ws = [witness(pp, 10 * n_in + n_out, n_in, n_out)]
+    if n_in != n_out:  # keep the sum balanced: outputs split the input value
+        v = ws[0]["in_values"][0]
+        ws[0]["out_values"] = [v // 3, v - v // 3]
+        ws[0]["_outs"] = [Z.token_commitment(pp, "ABC", a, b) for a, b in zip(ws[0]["out_values"], ws[0]["out_bfs"])]
+        ws[0]["outputs"] = b"".join(C.g1_bytes(p) for p in ws[0]["_outs"])
+    got, codes = emu_prove(emu, js, ws)
+    assert codes == [0]
+    want = oracle_transfer(pp, ws[0])
+    assert got[0] == want
+    # and the oracle verifier accepts it
+    assert Z.transfer_verify(pp, ws[0]["_ins"], ws[0]["_outs"], got[0])[1] == Z.OK
+
+
+@pytest.mark.parametrize("anonymous", [False, True])
+def test_emu_issue_proofs_match_oracle(emu, pp_a, anonymous):
+    js, pp = pp_a
+    w = issue_witness(pp, 77 + anonymous, 2, ttype="tok<&>\"x\"", anonymous=anonymous)
+    got, codes = emu_prove(emu, js, [w], issue=True)
+    assert codes == [0]
+    assert got[0] == oracle_issue(pp, w)
+
+
+def test_emu_value_out_of_range(emu, pp_a):
+    js, pp = pp_a
+    w = witness(pp, 5, 2, 2)
+    w["out_values"] = [pp.base ** pp.exponent, 0]
+    with pytest.raises(ValueError, match="outside authorized range"):
+        emu_prove(emu, js, [w])
+
+
+def test_emu_bad_commitment_code(emu, pp_a):
+    js, pp = pp_a
+    w = witness(pp, 6, 1, 1)
+    bad = bytearray(w["inputs"])
+    bad[63] ^= 1
+    w["inputs"] = bytes(bad)
+    _, codes = emu_prove(emu, js, [w])
+    assert codes == [A.FTZ_ERR_PARSE]
+
+
+# ---------------------------------------------------------------- GPU tier
+@pytest.fixture(scope="module")
+def gctx(golden):
+    import zkatdlog
+    c = zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_transfer_proofs_match_oracle(gctx, pp_a):
+    _, pp = pp_a
+    ws = [witness(pp, 300 + i, 2, 2) for i in range(3)] + [witness(pp, 310, 1, 1)]
+    proofs, codes = gctx.prove_transfers(ws)
+    assert codes == [0] * len(ws)
+    for w, p in zip(ws, proofs):
+        assert p == oracle_transfer(pp, w)
+
+
+@pytest.mark.gpu
+def test_gpu_issue_proofs_match_oracle(gctx, pp_a):
+    _, pp = pp_a
+    ws = [issue_witness(pp, 400, 2), issue_witness(pp, 401, 1, ttype="USD", anonymous=True)]
+    proofs, codes = gctx.prove_issues(ws)
+    assert codes == [0, 0]
+    for w, p in zip(ws, proofs):
+        assert p == oracle_issue(pp, w)
+
+
+@pytest.mark.gpu
+def test_gpu_prove_then_verify_batch(gctx, pp_a):
+    """A batch of GPU-made proofs is accepted by the GPU verifier; a proof
+    checked against swapped outputs is rejected."""
+    _, pp = pp_a
+    base = [witness(pp, 500 + i, 2, 2) for i in range(8)]
+    ws = [base[i % 8] | {"seed": hashlib.sha256(b"b%d" % i).digest()} for i in range(256)]
+    proofs, codes = gctx.prove_transfers(ws)
+    assert codes == [0] * len(ws)
+    assert len(set(proofs)) == len(proofs)  # fresh randomness per proof
+    tx = [(w["inputs"], w["outputs"], p) for w, p in zip(ws, proofs)]
+    tx.append((ws[0]["inputs"], ws[1]["outputs"], proofs[0]))
+    got = gctx.verify_transfers(tx)
+    assert list(got[:-1]) == [0] * len(ws) and got[-1] != 0
+
+
+@pytest.mark.gpu
+def test_gpu_prover_rejects_out_of_range(gctx, pp_a):
+    import zkatdlog
+    _, pp = pp_a
+    w = witness(pp, 7, 2, 2)
+    w["out_values"] = [pp.base ** pp.exponent + 1, 0]
+    with pytest.raises(zkatdlog.DeviceError, match="outside authorized range"):
+        gctx.prove_transfers([w])
