@@ -155,6 +155,48 @@ def prover_bench(ctx, batch, steps, warmup):
             "stage_ms": {k: round(v[0], 3) for k, v in stats.items()}}
 
 
+def roofline(batch, device, tx_per_s):
+    """Integer-VALU roofline of the dominant kernel.  The timed steps overlap
+    three streams, so per-kernel wall times there include shared SIMDs; the
+    roofline pass re-runs 3 steps with every kernel on one stream (FTZ_SERIAL=1,
+    same kernels, same inputs) and takes each kernel's HIP-event time there.
+    achieved = counted Montgomery products per job (profiles/opcounts.json, the
+    oracle-checked job code run with an op counter) x jobs x 136 MAD / time."""
+    os.environ["FTZ_SERIAL"] = "1"
+    try:
+        acc = None
+        for _ in range(3):
+            batch.run()
+            st = batch.stats()
+            acc = st if acc is None else {k: (acc[k][0] + st[k][0], st[k][1]) for k in st}
+    finally:
+        del os.environ["FTZ_SERIAL"]
+    kern = {k: (v[0] / 3, v[1]) for k, v in acc.items() if k != "total"}
+    peak = madpeak(device)
+    opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["pp_a"]
+    # k_g1_part + k_g1_combine run the job_g1 work of "g1" (side) / "g1p" (pairing inputs)
+    names = {"g1": "k_g1_part+k_g1_combine (side stream)", "g1p": "k_g1_part+k_g1_combine (pairing inputs)",
+             "g2": "k_g2lines", "miller": "k_miller", "fexp": "k_fexp", "hash": "k_hash", "decode": "k_decode"}
+    dom = max((k for k in kern if k in names), key=lambda k: kern[k][0])
+    m_job = opc["m_per_job"]["g1" if dom == "g1p" else dom]
+    achieved = m_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_fetch.json")
+    if os.path.exists(pmc):
+        t = json.load(open(pmc)).get("per_launch_bytes", {})
+        traffic = t.get(dom)
+    step_mad = opc["m_per_tx"] * tx_per_s * MAD_PER_M
+    return {"bound": "valu", "kernel": names[dom], "achieved": round(achieved / 1e12, 4),
+            "peak": round(peak / 1e12, 4), "unit": "TMAD/s", "frac": round(achieved / peak, 4),
+            "traffic": traffic, "kernel_ms_serial": round(kern[dom][0], 3), "jobs": kern[dom][1],
+            "m_per_job": round(m_job, 1),
+            "pipeline": {"achieved": round(step_mad / 1e12, 4), "frac": round(step_mad / peak, 4),
+                         "note": "whole step: counted products per transfer x 136 x transfers/s"},
+            "note": "integer VALU roofline (v_mad_u64_u32, peak = measured madpeak); per-kernel time from a "
+                    "serial pass (FTZ_SERIAL=1) of the same batch; traffic = HBM bytes per launch from "
+                    "rocprofv3 FETCH_SIZE (profiles/pmc_fetch.json, x1024 B, x2 gfx950 correction)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,21 +256,7 @@ def main():
     if rank == 0:
         total = args.batch * world * args.steps
         value = total / elapsed
-        kern = {k: v for k, v in stats.items() if k not in ("total",)}
-        dom = max(kern, key=lambda k: kern[k][0])
-        opc_path = os.path.join(ROOT, "profiles", "opcounts.json")
-        roof = None
-        peak = madpeak(local)
-        if os.path.exists(opc_path):
-            opc = json.load(open(opc_path))["pp_a"]
-            m_per_job = opc["m_per_job"].get("g1" if dom == "g1p" else dom)
-            if m_per_job and kern[dom][0] > 0:
-                achieved = m_per_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
-                roof = {"bound": "valu", "kernel": "k_" + dom, "achieved": round(achieved / 1e12, 4),
-                        "peak": round(peak / 1e12, 4), "unit": "TMAD/s", "frac": round(achieved / peak, 4),
-                        "traffic": None,
-                        "note": "integer VALU roofline (v_mad_u64_u32); work = counted Montgomery products "
-                                "x 136 MAD; HBM traffic ~2 KB/tx is not a bound"}
+        roof = roofline(batch, local, value)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
         prover = None if args.no_prover else prover_bench(ctx, args.batch, args.steps, args.warmup)

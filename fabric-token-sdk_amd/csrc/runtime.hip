@@ -64,7 +64,7 @@ struct ftz_batch {
   DBuf<EmitJob> emit;
   DBuf<B64Job> b64;
   DBuf<uint8_t> out;
-  hipEvent_t ev[16];
+  hipEvent_t ev[20];
   bool ev_init = false;
   ftz_stats stats;
 };
@@ -284,7 +284,7 @@ static int batch_upload(ftz_batch* b) {
   HC(hipMemsetAsync(b->pt_ok.p, 1, std::max<uint32_t>(p.n_pts, 1), s));
   HC(hipStreamSynchronize(s));
   if (!b->ev_init) {
-    for (int k = 0; k < 16; k++) HC(hipEventCreate(&b->ev[k]));
+    for (int k = 0; k < 20; k++) HC(hipEventCreate(&b->ev[k]));
     b->ev_init = true;
   }
   return FTZ_SUCCESS;
@@ -351,7 +351,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
   // FTZ_SERIAL=1: run every kernel on one stream (per-kernel timings without
   // overlap, for profiling)
-  static const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';
+  const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
   if (serial) s2 = s3 = s;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
@@ -389,6 +389,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   }
   HC(hipEventRecord(e[12], s2));
   // main stream: pairing chain
+  HC(hipEventRecord(e[16], s));
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1p.p);
@@ -416,7 +417,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   HC(hipGetLastError());
   HC(hipStreamSynchronize(s));
   // stats order: decode zr hash_pre scalar g1p g2+lines miller fexp g1(side) hash verdict total
-  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 14, 6, 7, 11, 9, 10, 0};
+  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
   const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
   for (int k = 0; k < FTZ_NKERNELS; k++) {
     float ms = 0;
@@ -455,7 +456,7 @@ extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
   if (b->ev_init)
-    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev[k]);
+    for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
   delete b;
 }
 
@@ -544,7 +545,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
   hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
-  static const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';
+  const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
   if (serial) s2 = s3 = s;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
@@ -581,6 +582,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   }
   HC(hipEventRecord(e[12], s2));
   // main: R' = rr R and rsbf P (the pairing inputs)
+  HC(hipEventRecord(e[16], s));
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1p.p);
@@ -618,7 +620,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   HC(hipGetLastError());
   HC(hipStreamSynchronize(s));
   // stats order: decode zr rand+hash_pre scalar g1p g2+lines miller fexp g1(side) hash+responses emit+b64 total
-  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 4, 14, 6, 7, 11, 9, 10, 0};
+  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
   const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
   for (int k = 0; k < FTZ_NKERNELS; k++) {
     float ms = 0;
@@ -657,7 +659,7 @@ extern "C" void ftz_prover_destroy(ftz_prover* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
   if (b->ev_init)
-    for (int k = 0; k < 16; k++) (void)hipEventDestroy(b->ev[k]);
+    for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
   delete b;
 }
 
