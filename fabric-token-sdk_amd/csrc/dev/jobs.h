@@ -510,7 +510,21 @@ FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
   P2.x = p.x * fe_const<ModP>(GLV_BETA);
   P2.y = n2 ? fe_neg(p.y) : p.y;
   P2.inf = false;
-  g1a S = jac_to_aff(jac_add_aff(jac_from_aff(P1), P2));  // P1 != +-P2 for points of order r
+  // S = P1 + P2 stays Jacobian (X:Y:Z); P1 != +-P2 for points of order r, so
+  // Z != 0.  Instead of an inversion, run the loop on the isomorphic curve
+  // y^2 = x^3 + b Z^6 through (x, y) -> (Z^2 x, Z^3 y): there S is the affine
+  // point (X, Y), and the a = 0 doubling / mixed-addition formulas do not
+  // involve b.  A result (X':Y':Z') there is (X':Y':Z' Z) on E.
+  g1j Sj = jac_add_aff(jac_from_aff(P1), P2);
+  fp z2 = sqr(Sj.z), z3 = z2 * Sj.z;
+  P1.x = P1.x * z2;
+  P1.y = P1.y * z3;
+  P2.x = P2.x * z2;
+  P2.y = P2.y * z3;
+  g1a S;
+  S.x = Sj.x;
+  S.y = Sj.y;
+  S.inf = false;
   // the scalars are consumed from the top bit by shifting them left (a
   // dynamically indexed limb array would live in scratch memory)
   uint32_t u0 = k1[0], u1 = k1[1], u2 = k1[2], u3 = k1[3];
@@ -534,6 +548,7 @@ FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
     g1j nacc = jac_add_aff(acc, T);
     if (b1 | b2) acc = nacc;
   }
+  acc.z = acc.z * Sj.z;  // back to E (the point at infinity keeps z = 0)
   return acc;
 }
 
