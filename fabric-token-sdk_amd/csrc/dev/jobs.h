@@ -651,16 +651,30 @@ FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* 
   g1j_store(part[i], acc);
 }
 
-FTS_HD void job_g1_combine(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev* part, G1Dev* g1out,
-                           uint8_t* arena) {
+FTS_HD g1j job_g1_sum_parts(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev* part) {
   g1j acc = g1j_load(part[3 * (size_t)n + jb]);
   for (uint32_t f = 0; f < 3; f++)
     if (f < j.nfix) acc = jac_add(acc, g1j_load(part[(size_t)f * n + jb]));
-  g1a r = jac_to_aff(acc);
+  return acc;
+}
+
+// affine result from the Jacobian sum and 1/z (any value when z = 0)
+FTS_HD void job_g1_finish(const G1Job& j, const g1j& acc, const fp& zi, G1Dev* g1out, uint8_t* arena) {
+  g1a r;
+  r.inf = is_zero(acc.z);
+  fp zi2 = sqr(zi);
+  r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
+  r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
   G1Dev d;
   g1_store(d, r);
   g1out[j.out] = d;
   g1_emit_bytes(j, r, arena);
+}
+
+FTS_HD void job_g1_combine(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev* part, G1Dev* g1out,
+                           uint8_t* arena) {
+  g1j acc = job_g1_sum_parts(j, jb, n, part);
+  job_g1_finish(j, acc, is_zero(acc.z) ? fe_one<ModP>() : fp_inv(acc.z), g1out, arena);
 }
 
 FTS_HD void job_g2(const G2Job& j, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out) {

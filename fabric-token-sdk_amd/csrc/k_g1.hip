@@ -26,10 +26,72 @@ __global__ void __launch_bounds__(128) k_g1_part(const G1Job* jobs, uint32_t n, 
   job_g1_part(jobs, n, i, vt, pts, scal, tab, part);
 }
 
-__global__ void __launch_bounds__(128) k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part,
-                                                    G1Dev* g1out, uint8_t* arena) {
-  JOB_KERNEL_PROLOGUE(n);
-  job_g1_combine(jobs[i], i, n, part, g1out, arena);
+// Block-wide Montgomery batch inversion: thread t holds x_t (zero -> treated
+// as 1); returns 1/x_t.  Prefix and suffix products by Hillis-Steele scans in
+// LDS (2 log2(NT) products per thread), one field inversion per block done by
+// wave 0 alone (a wave issues an inversion at the same cost for 1 lane as for
+// 64, so inverting per lane costs every wave a full inversion).
+template <int NT>
+__device__ fp block_batch_inv(fp x, uint32_t (*pre)[NT], uint32_t (*suf)[NT], uint32_t* tot) {
+  const int t = threadIdx.x;
+  if (is_zero(x)) x = fe_one<ModP>();
+  fp p = x, q = x;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    pre[k][t] = p.v[k];
+    suf[k][t] = q.v[k];
+  }
+  __syncthreads();
+#pragma nounroll
+  for (int off = 1; off < NT; off <<= 1) {
+    fp a = fe_one<ModP>(), b = fe_one<ModP>();
+    if (t >= off)
+#pragma unroll
+      for (int k = 0; k < 8; k++) a.v[k] = pre[k][t - off];
+    if (t + off < NT)
+#pragma unroll
+      for (int k = 0; k < 8; k++) b.v[k] = suf[k][t + off];
+    __syncthreads();
+    p = p * a;
+    q = q * b;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      pre[k][t] = p.v[k];
+      suf[k][t] = q.v[k];
+    }
+    __syncthreads();
+  }
+  if (t < 64) {  // wave 0 only
+    fp all;
+#pragma unroll
+    for (int k = 0; k < 8; k++) all.v[k] = pre[k][NT - 1];
+    fp ia = fp_inv(all);
+    if (t == 0)
+#pragma unroll
+      for (int k = 0; k < 8; k++) tot[k] = ia.v[k];
+  }
+  __syncthreads();
+  fp r, a = fe_one<ModP>(), b = fe_one<ModP>();
+#pragma unroll
+  for (int k = 0; k < 8; k++) r.v[k] = tot[k];
+  if (t > 0)
+#pragma unroll
+    for (int k = 0; k < 8; k++) a.v[k] = pre[k][t - 1];
+  if (t + 1 < NT)
+#pragma unroll
+    for (int k = 0; k < 8; k++) b.v[k] = suf[k][t + 1];
+  return r * a * b;
+}
+
+static constexpr int COMBINE_NT = 256;
+__global__ void __launch_bounds__(COMBINE_NT) k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part,
+                                                           G1Dev* g1out, uint8_t* arena) {
+  __shared__ uint32_t pre[8][COMBINE_NT], suf[8][COMBINE_NT], tot[8];
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = i < n;  // every thread of the block takes part in the scans
+  g1j acc = valid ? job_g1_sum_parts(jobs[i], i, n, part) : jac_inf<fp>();
+  fp zi = block_batch_inv<COMBINE_NT>(acc.z, pre, suf, tot);
+  if (valid) job_g1_finish(jobs[i], acc, zi, g1out, arena);
 }
 
 __global__ void __launch_bounds__(64) k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab) {

@@ -385,7 +385,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   if (n_g1) {
     k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1.p);
-    k_g1_combine<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[12], s2));
   // main stream: pairing chain
@@ -393,7 +393,7 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1p.p);
-    k_g1_combine<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
+    k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[5], s));
   HC(hipStreamWaitEvent(s, e[15], 0));
@@ -578,7 +578,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   if (n_g1) {
     k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1.p);
-    k_g1_combine<<<blocks_for(n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[12], s2));
   // main: R' = rr R and rsbf P (the pairing inputs)
@@ -586,7 +586,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
                                                          b->part1p.p);
-    k_g1_combine<<<blocks_for(n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
+    k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[5], s));
   // stream3: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)
