@@ -326,6 +326,51 @@ FTS_HDN Fe<M> fe_pow(const Fe<M>& a, const uint32_t* e) {
 }
 
 FTS_HD fp fp_inv(const fp& a) { return fe_pow<ModP>(a, P_MINUS_2); }
+
+// Variable-time inverse by the binary extended Euclidean algorithm: ~2 log2 p
+// halvings and ~log2 p subtractions of 8-limb integers, about 5x fewer
+// instructions than the Fermat chain.  For latency-bound single-lane code on
+// public values only (MSM Horner); the data-dependent loop diverges in a wave.
+FTS_HD fp fp_inv_var(const fp& am) {
+  if (fe_is_zero(am)) return am;
+  uint32_t u[8], v[8], x1[8], x2[8], pm[8], t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u[i] = am.v[i];  // the Montgomery representative a R as a plain integer
+    v[i] = P_MOD[i];
+    pm[i] = P_MOD[i];
+    x1[i] = i == 0 ? 1u : 0u;
+    x2[i] = 0;
+  }
+  auto is_one = [](const uint32_t* a) {
+    uint32_t o = a[0] ^ 1u;
+    for (int i = 1; i < 8; i++) o |= a[i];
+    return o == 0;
+  };
+  // a / 2 and x / 2 mod p (x + p < 2^255 when x is odd)
+  auto halve = [&](uint32_t* a, uint32_t* x) {
+    for (int i = 0; i < 7; i++) a[i] = (a[i] >> 1) | (a[i + 1] << 31);
+    a[7] >>= 1;
+    if (x[0] & 1) add8(x, x, pm);
+    for (int i = 0; i < 7; i++) x[i] = (x[i] >> 1) | (x[i + 1] << 31);
+    x[7] >>= 1;
+  };
+  while (!is_one(u) && !is_one(v)) {
+    while (!(u[0] & 1)) halve(u, x1);
+    while (!(v[0] & 1)) halve(v, x2);
+    if (sub8(t, u, v) == 0) {  // u >= v
+      for (int i = 0; i < 8; i++) u[i] = t[i];
+      if (sub8(x1, x1, x2)) add8(x1, x1, pm);
+    } else {
+      sub8(v, v, u);
+      if (sub8(x2, x2, x1)) add8(x2, x2, pm);
+    }
+  }
+  // x = (a R)^-1 as a plain integer; the Montgomery form of a^-1 is x R^2
+  fp x = fe_const<ModP>(is_one(u) ? x1 : x2);
+  fp r2 = fe_const<ModP>(P_R2);
+  return (x * r2) * r2;
+}
 FTS_HD fr fr_inv(const fr& a) { return fe_pow<ModR>(a, R_MINUS_2); }
 
 // square root for p = 3 mod 4; returns false if a is not a square

@@ -25,8 +25,10 @@ namespace fts {
 
 struct MsmPlan {
   uint32_t n;          // points
+  uint32_t glv;        // 1: scalars split k = k1 + k2 lambda (|k_i| < 2^128) over P_i and phi(P_i)
+  uint32_t nv;         // virtual points: 2n with GLV (index n + i is phi(P_i) = (beta x_i, y_i)), else n
   uint32_t c;          // window bits
-  uint32_t windows;    // W = ceil(255 / c)
+  uint32_t windows;    // W = ceil(bits / c), bits = 129 (GLV halves) or 255
   uint32_t buckets;    // B = 2^(c-1) per window
   uint32_t slot_cap;   // T: points per bucket slot
   uint32_t seg_len;    // S: slots per segment
@@ -39,30 +41,39 @@ struct MsmPlan {
 // most this many buckets (its few buckets would otherwise serialise on atomics)
 static constexpr uint32_t MSM_TOP_LDS = 1024;
 
+// window bits for n (virtual) points: floor(log2 n / 2) + 7 clamped to [8, 20]
+// (measured on MI355X with GLV: 2^17 -> 15, 2^21 -> 17, 2^25 -> 19; the
+// latency-bound reduction favours fewer windows than the usual log2 n - 4)
 FTS_HD uint32_t msm_window_bits(uint64_t n) {
   uint32_t lg = 0;
   while ((1ull << (lg + 1)) <= n) lg++;
-  uint32_t c = lg > 4 ? lg - 4 : 1;
+  uint32_t c = lg / 2 + 7;
   if (c < 8) c = 8;
   if (c > 20) c = 20;
   return c;
 }
 
-// plan for n points with c-bit windows (0: msm_window_bits(n)), slot cap T
-// (0: twice the mean bucket load, at least 4) and S slots per segment (0: sized
-// for >= 64k segment lanes, in [4, 64])
-inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, uint32_t seg_len = 0) {
+// plan for n points with c-bit windows (0: msm_window_bits of the virtual point
+// count), slot cap T (0: twice the mean bucket load, at least 4) and S slots per
+// segment (0: sized for >= 64k segment lanes, in [4, 64]).  GLV halves the
+// scalar length, so the Horner chain of c (W-1) doublings and the bucket
+// reduction shrink by half for the same number of bucket additions.
+inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, uint32_t seg_len = 0,
+                             bool glv = true) {
   MsmPlan p;
   p.n = (uint32_t)n;
-  p.c = c ? c : msm_window_bits(n);
-  p.windows = (255 + p.c - 1) / p.c;
+  p.glv = glv ? 1 : 0;
+  p.nv = glv ? 2 * p.n : p.n;
+  p.c = c ? c : msm_window_bits(p.nv);
+  uint32_t bits = glv ? 129 : 255;  // magnitude bits + 1 for the signed-digit carry
+  p.windows = (bits + p.c - 1) / p.c;
   p.buckets = 1u << (p.c - 1);
   if (!slot_cap) {
-    uint64_t mean = (n + p.buckets - 1) / p.buckets;
+    uint64_t mean = (p.nv + p.buckets - 1) / p.buckets;
     slot_cap = (uint32_t)(2 * mean < 4 ? 4 : 2 * mean);
   }
   p.slot_cap = slot_cap;
-  p.max_slots = p.buckets + (uint32_t)((n + slot_cap - 1) / slot_cap);
+  p.max_slots = p.buckets + (uint32_t)((p.nv + slot_cap - 1) / slot_cap);
   if (!seg_len) {
     uint64_t tot = (uint64_t)p.windows * p.max_slots;
     seg_len = 4;
@@ -70,7 +81,7 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   }
   p.seg_len = seg_len;
   p.segs = (p.max_slots + seg_len - 1) / seg_len;
-  int t = 254 - (int)(p.c * (p.windows - 1));  // bits left for the top window
+  int t = (int)(bits - 1) - (int)(p.c * (p.windows - 1));  // bits left for the top window
   p.top_used = t <= 0 ? 1 : (t >= 31 || (1u << t) > p.buckets ? p.buckets : 1u << t);
   return p;
 }
@@ -90,30 +101,54 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
 }
 
 // digits of point i: key[w * n + i] = bucket | sign << 31, or NONE for a zero digit
-// top_hist: if non-null, the top window's counts go there (an LDS histogram
-// the caller flushes) instead of to count
+// key of one (window, virtual point): bucket | sign << 31, or NONE for a zero digit
+FTS_HD void msm_put_digit(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
+                          uint32_t* count, bool atomic_count, uint32_t* top_hist) {
+  uint32_t kk = NONE;
+  if (d != 0) {
+    uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+    kk = b | (((d < 0) != neg) ? 0x80000000u : 0u);
+    uint32_t* ct = (top_hist && w == p.windows - 1) ? &top_hist[b] : &count[(size_t)w * p.buckets + b];
+#if defined(__HIP_DEVICE_COMPILE__)
+    (void)atomic_count;
+    atomicAdd(ct, 1u);
+#else
+    if (atomic_count)
+      __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
+    else
+      (*ct)++;
+#endif
+  }
+  key[(size_t)w * p.nv + vi] = kk;
+}
+
+// digits of point i (both GLV halves); top_hist: if non-null, the top window's
+// counts go there (an LDS histogram the caller flushes) instead of to count
 FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key,
                            uint32_t* count, bool atomic_count, uint32_t* top_hist = nullptr) {
-  uint32_t carry = 0;
-  for (uint32_t w = 0; w < p.windows; w++) {
-    int32_t d = msm_digit(scal[i], p.c, w, carry);
-    uint32_t kk = NONE;
-    if (d != 0) {
-      uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-      kk = b | (d < 0 ? 0x80000000u : 0u);
-      uint32_t* ct = (top_hist && w == p.windows - 1) ? &top_hist[b] : &count[(size_t)w * p.buckets + b];
-#if defined(__HIP_DEVICE_COMPILE__)
-      (void)atomic_count;
-      atomicAdd(ct, 1u);
-#else
-      if (atomic_count)
-        __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
-      else
-        (*ct)++;
-#endif
+  if (p.glv) {
+    uint32_t k1[4], k2[4];
+    bool n1, n2;
+    glv_split(scal[i], k1, n1, k2, n2);
+    uint32_t a[8] = {k1[0], k1[1], k1[2], k1[3], 0, 0, 0, 0}, b[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
+    uint32_t ca = 0, cb = 0;
+    for (uint32_t w = 0; w < p.windows; w++) {
+      msm_put_digit(p, w, i, msm_digit(a, p.c, w, ca), n1, key, count, atomic_count, top_hist);
+      msm_put_digit(p, w, p.n + i, msm_digit(b, p.c, w, cb), n2, key, count, atomic_count, top_hist);
     }
-    key[(size_t)w * p.n + i] = kk;
+  } else {
+    uint32_t carry = 0;
+    for (uint32_t w = 0; w < p.windows; w++)
+      msm_put_digit(p, w, i, msm_digit(scal[i], p.c, w, carry), false, key, count, atomic_count, top_hist);
   }
+}
+
+// virtual point v: P_v, or phi(P_(v-n)) = (beta x, y) for v >= n (GLV)
+FTS_HD g1a msm_point(const MsmPlan& p, uint32_t v, const G1Dev* pts) {
+  if (v < p.n) return g1_load(pts[v]);
+  g1a P = g1_load(pts[v - p.n]);
+  P.x = P.x * fe_const<ModP>(GLV_BETA);
+  return P;
 }
 
 // bucket g = w B + b: its slot count and, once the counts are scanned into
@@ -143,16 +178,19 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   g1j acc = jac_inf<fp>();
   if (lo >= hi) return acc;
   uint32_t v = e[lo];
-  G1Dev nxt = pts[v & 0x7FFFFFFFu];
+  const fp beta = fe_const<ModP>(GLV_BETA);
+  auto at = [&](uint32_t vi) { return pts[vi < p.n ? vi : vi - p.n]; };
+  G1Dev nxt = at(v & 0x7FFFFFFFu);
   for (uint32_t q = lo; q < hi; q++) {
     // the next point's load is issued before this point's addition
     G1Dev cur = nxt;
-    uint32_t sign = v >> 31;
+    uint32_t sign = v >> 31, vi = v & 0x7FFFFFFFu;
     if (q + 1 < hi) {
       v = e[q + 1];
-      nxt = pts[v & 0x7FFFFFFFu];
+      nxt = at(v & 0x7FFFFFFFu);
     }
     g1a P = g1_load(cur);
+    if (vi >= p.n) P.x = P.x * beta;  // phi(P) for the second GLV half
     if (sign) P = aff_neg(P);
     acc = jac_add_aff(acc, P);
   }

@@ -84,11 +84,11 @@ __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, co
 __global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor,
                                                      uint32_t* perm) {
   __shared__ uint32_t cnt[MSM_TOP_LDS];
-  uint64_t total = (uint64_t)p.windows * p.n, top0 = (uint64_t)(p.windows - 1) * p.n;
+  uint64_t total = (uint64_t)p.windows * p.nv, top0 = (uint64_t)(p.windows - 1) * p.nv;
   uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x, t = b0 + threadIdx.x;
   bool lds = p.top_used <= MSM_TOP_LDS && b0 + blockDim.x > top0;  // uniform per block
   uint32_t k = t < total ? key[t] : NONE;
-  uint32_t w = t < total ? (uint32_t)(t / p.n) : 0, i = (uint32_t)(t - (uint64_t)w * p.n);
+  uint32_t w = t < total ? (uint32_t)(t / p.nv) : 0, i = (uint32_t)(t - (uint64_t)w * p.nv);
   bool mine = lds && t >= top0 && t < total && k != NONE;
   uint32_t rank = 0;
   if (lds) {
@@ -155,22 +155,131 @@ __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, 
   if (t == 0) out[(size_t)w * chunks + ch] = s[0];
 }
 
-// Horner steps for windows w_hi-1 down to w_lo: acc = 2^c acc + W_w, one lane.
-// Runs on a side stream while the next (lower) window group accumulates, so
-// the c (W-1) serial doublings overlap the bucket work; the last call (w_lo = 0)
-// converts to affine and gnark RawBytes.
-__global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum, G1JDev* acc_buf,
-                             G1Dev* res, uint8_t* bytes) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+// ---- 4-lane cooperative point arithmetic for the serial Horner chain.  A
+// wave issues a one-lane Montgomery product at the cost of a 64-lane one, so
+// the chain's latency is the number of dependent products: every lane holds
+// the same point, lane k < 4 computes the k-th independent product of each
+// dependency level, and the products are exchanged through LDS.
+struct Coop {
+  int k;
+  uint32_t (*sh)[8];
+  // one level: lane k computes a_k * b_k (k < cnt); returns all cnt products
+  __device__ void level(int cnt, const fp* a, const fp* b, fp* out) const {
+    fp x = a[0], y = b[0];
+#pragma unroll
+    for (int i = 1; i < 4; i++)
+      if (i < cnt && k == i) {
+        x = a[i];
+        y = b[i];
+      }
+    fp r = x * y;
+    if (k < cnt)
+#pragma unroll
+      for (int q = 0; q < 8; q++) sh[k][q] = r.v[q];
+    __syncthreads();
+    for (int i = 0; i < cnt; i++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) out[i].v[q] = sh[i][q];
+    __syncthreads();
+  }
+};
+
+// dbl-2009-l (same values as jac_dbl): 3 product levels instead of 7 products
+__device__ g1j coop_dbl(const Coop& c, const g1j& p) {
+  fp o[4];
+  {
+    fp a[4] = {p.x, p.y, p.y, p.y}, b[4] = {p.x, p.y, p.z, p.z};
+    c.level(3, a, b, o);
+  }
+  fp A = o[0], B = o[1], YZ = o[2];
+  fp E = A + A + A, s = p.x + B;
+  {
+    fp a[4] = {B, s, E, E}, b[4] = {B, s, E, E};
+    c.level(3, a, b, o);
+  }
+  fp C = o[0], D = o[1] - A - C;
+  D = D + D;
+  fp X3 = o[2] - D - D;
+  {
+    fp dx = D - X3;
+    fp a[4] = {E, E, E, E}, b[4] = {dx, dx, dx, dx};
+    c.level(1, a, b, o);
+  }
+  fp C8 = C + C;
+  C8 = C8 + C8;
+  C8 = C8 + C8;
+  return {X3, o[0] - C8, YZ + YZ};
+}
+
+// add-2007-bl (same values as jac_add_inl): 6 product levels instead of 16 products
+__device__ g1j coop_add(const Coop& c, const g1j& p, const g1j& q) {
+  if (is_zero(p.z)) return q;
+  if (is_zero(q.z)) return p;
+  fp o[4];
+  {
+    fp a[4] = {p.z, q.z, p.z, p.z}, b[4] = {p.z, q.z, q.z, q.z};
+    c.level(3, a, b, o);
+  }
+  fp Z1Z1 = o[0], Z2Z2 = o[1], Z1Z2 = o[2];
+  {
+    fp a[4] = {p.x, q.x, p.y, q.y}, b[4] = {Z2Z2, Z1Z1, q.z, p.z};
+    c.level(4, a, b, o);
+  }
+  fp U1 = o[0], U2 = o[1];
+  {
+    fp a[4] = {o[2], o[3], o[2], o[2]}, b[4] = {Z2Z2, Z1Z1, Z2Z2, Z2Z2};
+    c.level(2, a, b, o);
+  }
+  fp S1 = o[0];
+  fp H = U2 - U1, rr = o[1] - S1;
+  if (is_zero(H)) {
+    if (is_zero(rr)) return coop_dbl(c, p);
+    return jac_inf<fp>();
+  }
+  fp H2 = H + H;
+  rr = rr + rr;
+  {
+    fp a[4] = {H2, rr, Z1Z2, Z1Z2}, b[4] = {H2, rr, H, H};
+    c.level(3, a, b, o);
+  }
+  fp I = o[0], R2 = o[1], Zh = o[2];
+  {
+    fp a[4] = {H, U1, H, H}, b[4] = {I, I, I, I};
+    c.level(2, a, b, o);
+  }
+  fp J = o[0], V = o[1];
+  fp X3 = R2 - J - V - V;
+  {
+    fp vx = V - X3;
+    fp a[4] = {rr, S1, rr, rr}, b[4] = {vx, J, vx, vx};
+    c.level(2, a, b, o);
+  }
+  return {X3, o[0] - o[1] - o[1], Zh + Zh};
+}
+
+// Horner steps for windows w_hi-1 down to w_lo: acc = 2^c acc + W_w, on one
+// wave with the 4-lane cooperative point ops; the last call (w_lo = 0)
+// converts to affine (binary-EEA inverse) and gnark RawBytes.  (With
+// FTZ_MSM_GROUP it runs on a side stream while lower window groups accumulate.)
+__global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
+                                                   G1JDev* acc_buf, G1Dev* res, uint8_t* bytes) {
+  __shared__ uint32_t sh[4][8];
+  if (blockIdx.x != 0) return;
+  Coop c{(int)threadIdx.x, sh};
   g1j acc = w_hi == p.windows ? jac_inf<fp>() : g1j_load(*acc_buf);
   for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
     if (w != (int)p.windows - 1)
-      for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
-    acc = jac_add_inl(acc, g1j_load(wsum[w]));
+      for (uint32_t q = 0; q < p.c; q++) acc = coop_dbl(c, acc);
+    acc = coop_add(c, acc, g1j_load(wsum[w]));
   }
+  if (threadIdx.x != 0) return;
   g1j_store(*acc_buf, acc);
   if (w_lo == 0) {
-    g1a r = jac_to_aff(acc);
+    g1a r;
+    r.inf = is_zero(acc.z);
+    fp zi = fp_inv_var(acc.z), zi2 = sqr(zi);
+    r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
+    r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
     G1Dev d;
     g1_store(d, r);
     *res = d;

@@ -29,7 +29,7 @@ static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
 static int msm_alloc(ftz_msm* m, size_t n) {
   const MsmPlan& p = m->p;
-  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * n, ws = (size_t)p.windows * p.max_slots;
+  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * p.nv, ws = (size_t)p.windows * p.max_slots;
   HC(m->pts.alloc(n));
   HC(m->scal.alloc(8 * n));
   HC(m->key.alloc(wn));
@@ -89,7 +89,8 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   auto env = [](const char* k) { const char* v = getenv(k); return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u; };
   uint32_t c_over = env("FTZ_MSM_C");
   if (c_over > 24) c_over = 0;
-  m->p = msm_make_plan(n, c_over, env("FTZ_MSM_T"), env("FTZ_MSM_S"));
+  const char* glv = getenv("FTZ_MSM_GLV");
+  m->p = msm_make_plan(n, c_over, env("FTZ_MSM_T"), env("FTZ_MSM_S"), !(glv && glv[0] == '0'));
   int rc = msm_alloc(m, n);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);
@@ -199,7 +200,7 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
-  k_msm_scatter<<<blocks((size_t)p.windows * p.n, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
+  k_msm_scatter<<<blocks((size_t)p.windows * p.nv, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
   // window groups from the top: accumulate group g on the main stream while the
   // side stream runs the Horner steps of group g-1
   hipStream_t hs = c->stream3;

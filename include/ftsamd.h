@@ -108,7 +108,8 @@ void ftz_batch_destroy(ftz_batch* b);
  * uncompressed RawBytes (must be canonical and on the curve); scalars: n x 32
  * bytes big-endian, reduced mod r.  The reference path has no MSM; this is the
  * operation mathlib exposes from gnark-crypto as G1Jac.MultiExp.  Pippenger
- * with signed windows (c = log2(n) - 4 clamped to [8, 20]). */
+ * with signed windows over GLV half-scalars (k = k1 + k2 lambda, |k_i| < 2^128,
+ * points P_i and phi(P_i)), c = floor(log2(2n) / 2) + 7 clamped to [8, 20]. */
 typedef struct ftz_msm ftz_msm;
 int ftz_msm_g1(ftz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[64]);
 /* staged form: upload once, run on HBM-resident inputs (bench) */

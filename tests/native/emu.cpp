@@ -46,6 +46,10 @@ int emu_fp_inv(const uint8_t* a, uint8_t* out) {
   st_fp(out, fp_inv(ld_fp(a)));
   return 0;
 }
+int emu_fp_inv_var(const uint8_t* a, uint8_t* out) {
+  st_fp(out, fp_inv_var(ld_fp(a)));
+  return 0;
+}
 int emu_fr_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) {
   uint32_t t[8];
   be32_to_limbs(t, a);

@@ -11,8 +11,8 @@
 using namespace fts;
 
 extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
-                       uint32_t seg_len, uint8_t out[64]) {
-  MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len);
+                       uint32_t seg_len, uint32_t glv, uint8_t out[64]) {
+  MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len, glv != 0);
   std::vector<G1Dev> pts(n);
   std::vector<uint32_t> scal(8 * n);
   uint32_t(*sc)[8] = reinterpret_cast<uint32_t(*)[8]>(scal.data());
@@ -30,14 +30,14 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
     fe_to_int(sc[i], fe_from_int<ModR>(k));
   }
   size_t wb = (size_t)p.windows * p.buckets;
-  std::vector<uint32_t> key((size_t)p.windows * n), count(wb, 0), start(wb), perm((size_t)p.windows * n);
+  std::vector<uint32_t> key((size_t)p.windows * p.nv), count(wb, 0), start(wb), perm((size_t)p.windows * p.nv);
   for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), count.data(), false);
   uint32_t run = 0;
   for (size_t b = 0; b < wb; b++) start[b] = run, run += count[b];
   std::vector<uint32_t> cur(start);
-  for (uint32_t i = 0; i < n; i++)
+  for (uint32_t i = 0; i < p.nv; i++)
     for (uint32_t w = 0; w < p.windows; w++) {
-      uint32_t k = key[(size_t)w * n + i];
+      uint32_t k = key[(size_t)w * p.nv + i];
       if (k != NONE) perm[cur[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)]++] = i | (k & 0x80000000u);
     }
   std::vector<uint32_t> soff(wb), owner((size_t)p.windows * p.max_slots, 0xFFFFFFFFu), wlo(p.windows), whi(p.windows);

@@ -31,6 +31,18 @@ def test_field_ops(emu):
         assert int.from_bytes(o.raw, "big") == a * b % C.R
 
 
+def test_fp_inv_var(emu):
+    """binary-EEA inverse (dev/fp.h fp_inv_var) against Fermat, incl. edge values"""
+    rng = random.Random(17)
+    vals = [1, 2, C.P - 1, C.P - 2, (C.P + 1) // 2, 1 << 200] + [rng.randrange(1, C.P) for _ in range(300)]
+    o = buf(32)
+    for x in vals:
+        emu.emu_fp_inv_var(x.to_bytes(32, "big"), o)
+        assert int.from_bytes(o.raw, "big") == pow(x, C.P - 2, C.P)
+    emu.emu_fp_inv_var(bytes(32), o)
+    assert o.raw == bytes(32)
+
+
 def test_group_ops(emu):
     rng = random.Random(8)
     for _ in range(8):

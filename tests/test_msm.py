@@ -32,20 +32,21 @@ def pack(pts, ks):
     return b"".join(C.g1_bytes(p) for p in pts), b"".join(k.to_bytes(32, "big") for k in ks)
 
 
-def emu_msm(emu, pts, ks, c, cap, seg_len):
+def emu_msm(emu, pts, ks, c, cap, seg_len, glv=1):
     pb, kb = pack(pts, ks)
     out = ctypes.create_string_buffer(64)
     emu.emu_msm.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
-                            ctypes.c_uint32, ctypes.c_char_p]
-    assert emu.emu_msm(len(pts), pb, kb, c, cap, seg_len, out) == 0
+                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+    assert emu.emu_msm(len(pts), pb, kb, c, cap, seg_len, glv, out) == 0
     return out.raw
 
 
 @pytest.mark.parametrize("n,c,cap,seg", [(1, 4, 1, 1), (7, 2, 1, 1), (33, 5, 2, 3), (40, 8, 0, 0), (64, 3, 3, 2),
                                          (20, 1, 1, 1), (48, 6, 4, 5)])
-def test_emu_pipeline(emu, n, c, cap, seg):
+@pytest.mark.parametrize("glv", [1, 0])
+def test_emu_pipeline(emu, n, c, cap, seg, glv):
     pts, ks = rnd_case(n, 100 + n * 7 + c)
-    assert emu_msm(emu, pts, ks, c, cap, seg) == C.g1_bytes(C.g1_msm(pts, ks))
+    assert emu_msm(emu, pts, ks, c, cap, seg, glv) == C.g1_bytes(C.g1_msm(pts, ks))
 
 
 def test_emu_skewed_scalars(emu):
@@ -63,11 +64,11 @@ def test_emu_cancelling_sum(emu):
 
 
 def test_window_plan():
-    # msm_window_bits: log2(n) - 4 clamped to [8, 20] (dev/msm.h)
+    # msm_window_bits: floor(log2(virtual points) / 2) + 7 clamped to [8, 20] (dev/msm.h); GLV doubles the points
     def bits(n):
         lg = n.bit_length() - 1
-        return min(20, max(8, lg - 4 if lg > 4 else 1))
-    assert [bits(1 << k) for k in (10, 16, 20, 24, 28)] == [8, 12, 16, 20, 20]
+        return min(20, max(8, lg // 2 + 7))
+    assert [bits(2 << k) for k in (10, 16, 20, 24, 28)] == [12, 15, 17, 19, 21 if False else 20]
 
 
 @pytest.fixture(scope="module")
@@ -82,6 +83,14 @@ def ctx(golden):
 @pytest.mark.parametrize("n", [1, 5, 200, 1000])
 def test_gpu_msm_explicit(ctx, n):
     pts, ks = rnd_case(n, 900 + n)
+    pb, kb = pack(pts, ks)
+    assert ctx.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
+
+
+@pytest.mark.gpu
+def test_gpu_msm_without_glv(ctx, monkeypatch):
+    monkeypatch.setenv("FTZ_MSM_GLV", "0")
+    pts, ks = rnd_case(300, 901)
     pb, kb = pack(pts, ks)
     assert ctx.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
 
@@ -116,4 +125,4 @@ def test_gpu_msm_known_logs(ctx, lg, bits):
     want = C.g1_mul(C.G1_GEN, sum(k * (i + off) for i, k in enumerate(ks)) % C.R)
     assert got == C.g1_bytes(want)
     assert again == got
-    assert info["window_bits"] == lg - 4 and info["last_ms"] > 0
+    assert info["window_bits"] == (lg + 1) // 2 + 7 and info["last_ms"] > 0
