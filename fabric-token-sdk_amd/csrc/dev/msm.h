@@ -72,6 +72,7 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
     uint64_t mean = (p.nv + p.buckets - 1) / p.buckets;
     slot_cap = (uint32_t)(2 * mean < 4 ? 4 : 2 * mean);
   }
+  if (slot_cap > 1023) slot_cap = 1023;  // length bins of the slot ordering (k_msm.hip)
   p.slot_cap = slot_cap;
   p.max_slots = p.buckets + (uint32_t)((p.nv + slot_cap - 1) / slot_cap);
   if (!seg_len) {
@@ -143,12 +144,14 @@ FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[
   }
 }
 
-// virtual point v: P_v, or phi(P_(v-n)) = (beta x, y) for v >= n (GLV)
-FTS_HD g1a msm_point(const MsmPlan& p, uint32_t v, const G1Dev* pts) {
-  if (v < p.n) return g1_load(pts[v]);
-  g1a P = g1_load(pts[v - p.n]);
-  P.x = P.x * fe_const<ModP>(GLV_BETA);
-  return P;
+// virtual point v of the resident array: P_v for v < n, phi(P_(v-n)) =
+// (beta x, y) for n <= v < 2n (GLV; filled once at load, msm_job_phi)
+FTS_HD void msm_job_phi(const MsmPlan& p, uint32_t i, G1Dev* pts) {
+  g1a P = g1_load(pts[i]);
+  if (!P.inf) P.x = P.x * fe_const<ModP>(GLV_BETA);
+  G1Dev d;
+  g1_store(d, P);
+  pts[p.n + i] = d;
 }
 
 // bucket g = w B + b: its slot count and, once the counts are scanned into
@@ -167,6 +170,14 @@ FTS_HD void msm_job_owner(const MsmPlan& p, uint32_t g, const uint32_t* count, c
   if (b == p.buckets - 1) whi[w] = o + m;
 }
 
+// number of points in slot j (1..T, 0 for the slot of an empty bucket)
+FTS_HD uint32_t msm_slot_len(const MsmPlan& p, uint32_t j, const uint32_t* owner, const uint32_t* soff,
+                             const uint32_t* count) {
+  uint32_t g = owner[j], s = j - soff[g], lo = s * p.slot_cap, hi = lo + p.slot_cap;
+  if (hi > count[g]) hi = count[g];
+  return hi > lo ? hi - lo : 0;
+}
+
 // Jacobian sum of slot j: points [s T, s T + T) of its bucket's sorted list
 // (negated where bit 31 of the entry is set)
 FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, const uint32_t* soff,
@@ -178,19 +189,16 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   g1j acc = jac_inf<fp>();
   if (lo >= hi) return acc;
   uint32_t v = e[lo];
-  const fp beta = fe_const<ModP>(GLV_BETA);
-  auto at = [&](uint32_t vi) { return pts[vi < p.n ? vi : vi - p.n]; };
-  G1Dev nxt = at(v & 0x7FFFFFFFu);
+  G1Dev nxt = pts[v & 0x7FFFFFFFu];
   for (uint32_t q = lo; q < hi; q++) {
     // the next point's load is issued before this point's addition
     G1Dev cur = nxt;
-    uint32_t sign = v >> 31, vi = v & 0x7FFFFFFFu;
+    uint32_t sign = v >> 31;
     if (q + 1 < hi) {
       v = e[q + 1];
-      nxt = at(v & 0x7FFFFFFFu);
+      nxt = pts[v & 0x7FFFFFFFu];
     }
     g1a P = g1_load(cur);
-    if (vi >= p.n) P.x = P.x * beta;  // phi(P) for the second GLV half
     if (sign) P = aff_neg(P);
     acc = jac_add_aff(acc, P);
   }

@@ -118,15 +118,72 @@ __global__ void __launch_bounds__(256) k_msm_owner(MsmPlan p, const uint32_t* co
   msm_job_owner(p, i, count, soff, owner, wlo, whi);
 }
 
-// one lane per bucket slot of windows [w0, w1); the grid covers the bound
-// (w1 - w0) * max_slots, lanes past the group's last slot exit
-__global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo,
-                                                    const uint32_t* whi, const uint32_t* owner,
-                                                    const uint32_t* soff, const uint32_t* start,
-                                                    const uint32_t* count, const uint32_t* perm, const G1Dev* pts,
-                                                    G1JDev* slot_sum) {
-  uint32_t j = wlo[w0] + blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= whi[w1 - 1]) return;
+__global__ void __launch_bounds__(256) k_msm_phi(MsmPlan p, G1Dev* pts) {
+  LANE_PROLOGUE(p.n);
+  msm_job_phi(p, i, pts);
+}
+
+// ---- bucket slots ordered by length, so that the lanes of a wave add about
+// the same number of points (bucket loads are Poisson-distributed).  Counting
+// sort over the T + 1 lengths with per-block LDS histograms: one global atomic
+// per (block, length) instead of one per slot on a handful of counters.
+static constexpr uint32_t MSM_LEN_BINS = 1024;  // > slot_cap (checked by the planner)
+
+__global__ void __launch_bounds__(256) k_msm_len_hist(MsmPlan p, const uint32_t* whi, const uint32_t* owner,
+                                                      const uint32_t* soff, const uint32_t* count, uint32_t* hist) {
+  __shared__ uint32_t h[MSM_LEN_BINS];
+  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.windows - 1];
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  if (j < L) atomicAdd(&h[p.slot_cap - msm_slot_len(p, j, owner, soff, count)], 1u);  // longest first
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// exclusive scan of the (<= 1024) length bins, one block
+__global__ void __launch_bounds__(1024) k_msm_len_scan(MsmPlan p, uint32_t* hist) {
+  __shared__ uint32_t s[MSM_LEN_BINS];
+  uint32_t t = threadIdx.x, nb = p.slot_cap + 1;
+  uint32_t v = t < nb ? hist[t] : 0;
+  s[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < MSM_LEN_BINS; o <<= 1) {
+    uint32_t a = t >= o ? s[t - o] : 0;
+    __syncthreads();
+    s[t] += a;
+    __syncthreads();
+  }
+  if (t < nb) hist[t] = s[t] - v;
+}
+
+__global__ void __launch_bounds__(256) k_msm_len_scatter(MsmPlan p, const uint32_t* whi, const uint32_t* owner,
+                                                         const uint32_t* soff, const uint32_t* count,
+                                                         uint32_t* cursor, uint32_t* order) {
+  __shared__ uint32_t h[MSM_LEN_BINS];
+  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.windows - 1];
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  uint32_t bin = 0, rank = 0;
+  if (j < L) {
+    bin = p.slot_cap - msm_slot_len(p, j, owner, soff, count);
+    rank = atomicAdd(&h[bin], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);
+  __syncthreads();
+  if (j < L) order[h[bin] + rank] = j;
+}
+
+// one lane per bucket slot, slots taken in length order (all windows)
+__global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* order,
+                                                    const uint32_t* owner, const uint32_t* soff,
+                                                    const uint32_t* start, const uint32_t* count,
+                                                    const uint32_t* perm, const G1Dev* pts, G1JDev* slot_sum) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= whi[p.windows - 1]) return;
+  uint32_t j = order[i];
   g1j_store(slot_sum[j], msm_job_slot(p, j, owner, soff, start, count, perm, pts));
 }
 
@@ -259,8 +316,7 @@ __device__ g1j coop_add(const Coop& c, const g1j& p, const g1j& q) {
 
 // Horner steps for windows w_hi-1 down to w_lo: acc = 2^c acc + W_w, on one
 // wave with the 4-lane cooperative point ops; the last call (w_lo = 0)
-// converts to affine (binary-EEA inverse) and gnark RawBytes.  (With
-// FTZ_MSM_GROUP it runs on a side stream while lower window groups accumulate.)
+// converts to affine (binary-EEA inverse) and gnark RawBytes.
 __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
                                                    G1JDev* acc_buf, G1Dev* res, uint8_t* bytes) {
   __shared__ uint32_t sh[4][8];

@@ -65,9 +65,15 @@ __global__ void k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor, 
 __global__ void k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m);
 __global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
                             uint32_t* whi);
-__global__ void k_msm_bucket(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo, const uint32_t* whi,
-                             const uint32_t* owner, const uint32_t* soff, const uint32_t* start,
-                             const uint32_t* count, const uint32_t* perm, const G1Dev* pts, G1JDev* slot_sum);
+__global__ void k_msm_phi(MsmPlan p, G1Dev* pts);
+__global__ void k_msm_len_hist(MsmPlan p, const uint32_t* whi, const uint32_t* owner, const uint32_t* soff,
+                               const uint32_t* count, uint32_t* hist);
+__global__ void k_msm_len_scan(MsmPlan p, uint32_t* hist);
+__global__ void k_msm_len_scatter(MsmPlan p, const uint32_t* whi, const uint32_t* owner, const uint32_t* soff,
+                                  const uint32_t* count, uint32_t* cursor, uint32_t* order);
+__global__ void k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* order, const uint32_t* owner,
+                             const uint32_t* soff, const uint32_t* start, const uint32_t* count,
+                             const uint32_t* perm, const G1Dev* pts, G1JDev* slot_sum);
 __global__ void k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo, const uint32_t* whi,
                               const uint32_t* owner, const G1JDev* slot_sum, G1JDev* part);
 __global__ void k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out);

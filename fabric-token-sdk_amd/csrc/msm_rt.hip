@@ -12,15 +12,12 @@ struct ftz_msm {
   ftz_ctx* ctx = nullptr;
   MsmPlan p{};
   DBuf<G1Dev> pts;
-  DBuf<uint32_t> scal, key, count, start, cursor, perm, tot, nsl, soff, owner, wlo, whi;
+  DBuf<uint32_t> scal, key, count, start, cursor, perm, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
   DBuf<G1JDev> slot_sum, part, tree;
   DBuf<G1Dev> res;
   DBuf<G1JDev> hacc, wsum;
   DBuf<uint8_t> bytes, ok;
-  uint32_t group = 1;  // windows per accumulation group
   hipEvent_t ev[2];
-  hipEvent_t gev[32];  // group g's window sums ready (main stream -> side stream)
-  hipEvent_t hdone;    // Horner chain finished (side stream -> main stream)
   bool ev_init = false;
   float last_ms = 0;
 };
@@ -30,7 +27,7 @@ static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
 static int msm_alloc(ftz_msm* m, size_t n) {
   const MsmPlan& p = m->p;
   size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * p.nv, ws = (size_t)p.windows * p.max_slots;
-  HC(m->pts.alloc(n));
+  HC(m->pts.alloc(p.nv));  // P_i, then phi(P_i) for GLV
   HC(m->scal.alloc(8 * n));
   HC(m->key.alloc(wn));
   HC(m->perm.alloc(wn));
@@ -44,6 +41,9 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->wlo.alloc(p.windows));
   HC(m->whi.alloc(p.windows));
   HC(m->slot_sum.alloc(ws));
+  HC(m->order.alloc(ws));
+  HC(m->lenhist.alloc(1024));
+  HC(m->lencur.alloc(1024));
   HC(m->part.alloc((size_t)p.windows * p.segs));
   HC(m->tree.alloc((size_t)p.windows * ((p.segs + 255) / 256) * 2));
   HC(m->res.alloc(1));
@@ -52,17 +52,8 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->bytes.alloc(64));
   HC(m->ok.alloc(n));
   for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
-  for (int k = 0; k < 32; k++) HC(hipEventCreateWithFlags(&m->gev[k], hipEventDisableTiming));
-  HC(hipEventCreateWithFlags(&m->hdone, hipEventDisableTiming));
   m->ev_init = true;
-  // windows per accumulation group (FTZ_MSM_GROUP; default all windows in one
-  // group: splitting multiplies the latency-bound segment / tree phases, which
-  // costs more than overlapping the Horner chain saves -- measured at 2^20/2^24)
-  const char* ge = getenv("FTZ_MSM_GROUP");
-  uint32_t g = ge ? (uint32_t)strtoul(ge, nullptr, 10) : 0;
-  if (g == 0 || g > p.windows) g = p.windows;
-  while ((p.windows + g - 1) / g > 32) g++;
-  m->group = g;
+
   return FTZ_SUCCESS;
 }
 
@@ -103,6 +94,8 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
 static int upload_scalars(ftz_msm* m, const uint8_t* scalars) {
   hipStream_t s = m->ctx->stream;
   size_t n = m->p.n;
+  // resident points: phi(P_i) = (beta x_i, y_i) next to P_i for the GLV halves
+  if (m->p.glv) k_msm_phi<<<blocks(n, 256), 256, 0, s>>>(m->p, m->pts.p);
   DBuf<uint8_t> raw;
   HC(raw.alloc(32 * n));
   HC(hipMemcpyAsync(raw.p, scalars, 32 * n, hipMemcpyHostToDevice, s));
@@ -201,40 +194,31 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
   k_msm_scatter<<<blocks((size_t)p.windows * p.nv, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
-  // window groups from the top: accumulate group g on the main stream while the
-  // side stream runs the Horner steps of group g-1
-  hipStream_t hs = c->stream3;
+  // bucket slots in length order, then one lane per slot
+  size_t sl = (size_t)p.windows * p.max_slots;
+  HC(hipMemsetAsync(m->lenhist.p, 0, 1024 * sizeof(uint32_t), s));
+  k_msm_len_hist<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p, m->lenhist.p);
+  k_msm_len_scan<<<1, 1024, 0, s>>>(p, m->lenhist.p);
+  k_msm_len_scatter<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p,
+                                                     m->lenhist.p, m->order.p);
+  k_msm_bucket<<<blocks(sl, 128), 128, 0, s>>>(p, m->whi.p, m->order.p, m->owner.p, m->soff.p, m->start.p,
+                                               m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
+  k_msm_segment<<<blocks((size_t)p.windows * p.segs, 128), 128, 0, s>>>(p, 0, p.windows, m->wlo.p, m->whi.p,
+                                                                       m->owner.p, m->slot_sum.p, m->part.p);
+  // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
   G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.windows * ((p.segs + 255) / 256)};
-  G1JDev* wsum = nullptr;
-  uint32_t gi = 0;
-  for (uint32_t w1 = p.windows; w1 > 0; gi++) {
-    uint32_t w0 = w1 > m->group ? w1 - m->group : 0, nw = w1 - w0;
-    k_msm_bucket<<<blocks((size_t)nw * p.max_slots, 128), 128, 0, s>>>(
-        p, w0, w1, m->wlo.p, m->whi.p, m->owner.p, m->soff.p, m->start.p, m->count.p, m->perm.p, m->pts.p,
-        m->slot_sum.p);
-    k_msm_segment<<<blocks((size_t)nw * p.segs, 128), 128, 0, s>>>(p, w0, w1, m->wlo.p, m->whi.p, m->owner.p,
-                                                                  m->slot_sum.p, m->part.p);
-    // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
-    const G1JDev* in = m->part.p + (size_t)w0 * p.segs;
-    uint32_t cnt = p.segs;
-    int which = 0;
-    do {
-      uint32_t chunks = (cnt + 255) / 256;
-      // the last pass writes the dedicated window-sum array the side stream reads
-      G1JDev* out = chunks == 1 ? m->wsum.p + w0 : bufs[which] + (size_t)w0 * chunks;
-      k_msm_tree<<<nw * chunks, 256, 0, s>>>(in, cnt, out);
-      in = out;
-      wsum = m->wsum.p;
-      which ^= 1;
-      cnt = chunks;
-    } while (cnt > 1);
-    HC(hipEventRecord(m->gev[gi], s));
-    HC(hipStreamWaitEvent(hs, m->gev[gi], 0));
-    k_msm_horner<<<1, 64, 0, hs>>>(p, w1, w0, wsum, m->hacc.p, m->res.p, m->bytes.p);
-    w1 = w0;
-  }
-  HC(hipEventRecord(m->hdone, hs));
-  HC(hipStreamWaitEvent(s, m->hdone, 0));
+  const G1JDev* in = m->part.p;
+  uint32_t cnt = p.segs;
+  int which = 0;
+  do {
+    uint32_t chunks = (cnt + 255) / 256;
+    G1JDev* out = chunks == 1 ? m->wsum.p : bufs[which];
+    k_msm_tree<<<p.windows * chunks, 256, 0, s>>>(in, cnt, out);
+    in = out;
+    which ^= 1;
+    cnt = chunks;
+  } while (cnt > 1);
+  k_msm_horner<<<1, 64, 0, s>>>(p, p.windows, 0, m->wsum.p, m->hacc.p, m->res.p, m->bytes.p);
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
   HC(hipMemcpyAsync(out, m->bytes.p, 64, hipMemcpyDeviceToHost, s));
@@ -256,8 +240,6 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
   if (m->ev_init)
   {
     for (int k = 0; k < 2; k++) (void)hipEventDestroy(m->ev[k]);
-    for (int k = 0; k < 32; k++) (void)hipEventDestroy(m->gev[k]);
-    (void)hipEventDestroy(m->hdone);
   }
   delete m;
 }

@@ -13,7 +13,7 @@ using namespace fts;
 extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
                        uint32_t seg_len, uint32_t glv, uint8_t out[64]) {
   MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len, glv != 0);
-  std::vector<G1Dev> pts(n);
+  std::vector<G1Dev> pts(p.nv);
   std::vector<uint32_t> scal(8 * n);
   uint32_t(*sc)[8] = reinterpret_cast<uint32_t(*)[8]>(scal.data());
   for (size_t i = 0; i < n; i++) {
@@ -29,6 +29,8 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
     be32_to_limbs(k, scalars + 32 * i);
     fe_to_int(sc[i], fe_from_int<ModR>(k));
   }
+  if (p.glv)
+    for (uint32_t i = 0; i < n; i++) msm_job_phi(p, i, pts.data());
   size_t wb = (size_t)p.windows * p.buckets;
   std::vector<uint32_t> key((size_t)p.windows * p.nv), count(wb, 0), start(wb), perm((size_t)p.windows * p.nv);
   for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), count.data(), false);
