@@ -102,30 +102,34 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
 }
 
 // digits of point i: key[w * n + i] = bucket | sign << 31, or NONE for a zero digit
-// key of one (window, virtual point): bucket | sign << 31, or NONE for a zero digit
+// key of one (window, virtual point): bucket | sign << 31, or NONE for a zero
+// digit; rank = the entry's position within its bucket (the count before it),
+// so the sorted position is start[bucket] + rank with no second atomic.  With
+// top_hist the top window counts in an LDS histogram (rank local to the block;
+// the caller adds the block's base).
 FTS_HD void msm_put_digit(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
-                          uint32_t* count, bool atomic_count, uint32_t* top_hist) {
-  uint32_t kk = NONE;
+                          uint32_t* rank, uint32_t* count, bool atomic_count, uint32_t* top_hist) {
+  uint32_t kk = NONE, rk = 0;
   if (d != 0) {
     uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
     kk = b | (((d < 0) != neg) ? 0x80000000u : 0u);
     uint32_t* ct = (top_hist && w == p.windows - 1) ? &top_hist[b] : &count[(size_t)w * p.buckets + b];
 #if defined(__HIP_DEVICE_COMPILE__)
     (void)atomic_count;
-    atomicAdd(ct, 1u);
+    rk = atomicAdd(ct, 1u);
 #else
     if (atomic_count)
-      __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
+      rk = __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
     else
-      (*ct)++;
+      rk = (*ct)++;
 #endif
   }
   key[(size_t)w * p.nv + vi] = kk;
+  rank[(size_t)w * p.nv + vi] = rk;
 }
 
-// digits of point i (both GLV halves); top_hist: if non-null, the top window's
-// counts go there (an LDS histogram the caller flushes) instead of to count
-FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key,
+// digits of point i (both GLV halves)
+FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key, uint32_t* rank,
                            uint32_t* count, bool atomic_count, uint32_t* top_hist = nullptr) {
   if (p.glv) {
     uint32_t k1[4], k2[4];
@@ -134,14 +138,23 @@ FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[
     uint32_t a[8] = {k1[0], k1[1], k1[2], k1[3], 0, 0, 0, 0}, b[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
     uint32_t ca = 0, cb = 0;
     for (uint32_t w = 0; w < p.windows; w++) {
-      msm_put_digit(p, w, i, msm_digit(a, p.c, w, ca), n1, key, count, atomic_count, top_hist);
-      msm_put_digit(p, w, p.n + i, msm_digit(b, p.c, w, cb), n2, key, count, atomic_count, top_hist);
+      msm_put_digit(p, w, i, msm_digit(a, p.c, w, ca), n1, key, rank, count, atomic_count, top_hist);
+      msm_put_digit(p, w, p.n + i, msm_digit(b, p.c, w, cb), n2, key, rank, count, atomic_count, top_hist);
     }
   } else {
     uint32_t carry = 0;
     for (uint32_t w = 0; w < p.windows; w++)
-      msm_put_digit(p, w, i, msm_digit(scal[i], p.c, w, carry), false, key, count, atomic_count, top_hist);
+      msm_put_digit(p, w, i, msm_digit(scal[i], p.c, w, carry), false, key, rank, count, atomic_count, top_hist);
   }
+}
+
+// sorted position of one (window, virtual point) entry
+FTS_HD void msm_job_scatter(const MsmPlan& p, uint64_t t, const uint32_t* key, const uint32_t* rank,
+                            const uint32_t* start, uint32_t* perm) {
+  uint32_t k = key[t];
+  if (k == NONE) return;
+  uint32_t w = (uint32_t)(t / p.nv), vi = (uint32_t)(t - (uint64_t)w * p.nv);
+  perm[start[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)] + rank[t]] = vi | (k & 0x80000000u);
 }
 
 // virtual point v of the resident array: P_v for v < n, phi(P_(v-n)) =

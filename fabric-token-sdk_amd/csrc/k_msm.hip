@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) k_msm_load_scal(uint32_t n, const uint8_t
 }
 
 __global__ void __launch_bounds__(256) k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
-                                                    uint32_t* count) {
+                                                    uint32_t* rank, uint32_t* count) {
   __shared__ uint32_t top[MSM_TOP_LDS];
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool lds = p.top_used <= MSM_TOP_LDS;  // uniform
@@ -47,12 +47,23 @@ __global__ void __launch_bounds__(256) k_msm_digits(MsmPlan p, const uint32_t (*
     for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x) top[b] = 0;
     __syncthreads();
   }
-  if (i < p.n) msm_job_digits(p, i, scal, key, count, true, lds ? top : nullptr);
+  if (i < p.n) msm_job_digits(p, i, scal, key, rank, count, true, lds ? top : nullptr);
   if (lds) {
+    // the block's top-window counts: one returning atomic per bucket gives the
+    // block's base; the entries' ranks were local to the block
     __syncthreads();
     uint32_t* gtop = count + (size_t)(p.windows - 1) * p.buckets;
     for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x)
-      if (top[b]) atomicAdd(&gtop[b], top[b]);
+      if (top[b]) top[b] = atomicAdd(&gtop[b], top[b]);
+    __syncthreads();
+    if (i < p.n) {
+      size_t base = (size_t)(p.windows - 1) * p.nv;
+      for (uint32_t h = 0; h < (p.glv ? 2u : 1u); h++) {
+        size_t t = base + i + h * p.n;
+        uint32_t k = key[t];
+        if (k != NONE) rank[t] += top[k & 0x7FFFFFFFu];
+      }
+    }
   }
 }
 
@@ -79,32 +90,12 @@ __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, co
 }
 
 // one lane per (window, point): lanes of a wave hit random buckets of one window
-// (blocks reaching the top window reserve its few buckets' positions once per
-// block through an LDS histogram)
-__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, uint32_t* cursor,
-                                                     uint32_t* perm) {
-  __shared__ uint32_t cnt[MSM_TOP_LDS];
-  uint64_t total = (uint64_t)p.windows * p.nv, top0 = (uint64_t)(p.windows - 1) * p.nv;
-  uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x, t = b0 + threadIdx.x;
-  bool lds = p.top_used <= MSM_TOP_LDS && b0 + blockDim.x > top0;  // uniform per block
-  uint32_t k = t < total ? key[t] : NONE;
-  uint32_t w = t < total ? (uint32_t)(t / p.nv) : 0, i = (uint32_t)(t - (uint64_t)w * p.nv);
-  bool mine = lds && t >= top0 && t < total && k != NONE;
-  uint32_t rank = 0;
-  if (lds) {
-    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x) cnt[b] = 0;
-    __syncthreads();
-    if (mine) rank = atomicAdd(&cnt[k & 0x7FFFFFFFu], 1u);
-    __syncthreads();
-    uint32_t* gcur = cursor + (size_t)(p.windows - 1) * p.buckets;
-    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x)
-      if (cnt[b]) cnt[b] = atomicAdd(&gcur[b], cnt[b]);
-    __syncthreads();
-  }
-  if (t >= total || k == NONE) return;
-  uint32_t pos = mine ? cnt[k & 0x7FFFFFFFu] + rank
-                      : atomicAdd(&cursor[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)], 1u);
-  perm[pos] = i | (k & 0x80000000u);
+// one lane per (window, virtual point): position = start + rank (no atomics)
+__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, const uint32_t* rank,
+                                                     const uint32_t* start, uint32_t* perm) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (uint64_t)p.windows * p.nv) return;
+  msm_job_scatter(p, t, key, rank, start, perm);
 }
 
 __global__ void __launch_bounds__(256) k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m) {

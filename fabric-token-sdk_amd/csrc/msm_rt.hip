@@ -12,7 +12,7 @@ struct ftz_msm {
   ftz_ctx* ctx = nullptr;
   MsmPlan p{};
   DBuf<G1Dev> pts;
-  DBuf<uint32_t> scal, key, count, start, cursor, perm, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
+  DBuf<uint32_t> scal, key, rank, count, start, perm, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
   DBuf<G1JDev> slot_sum, part, tree;
   DBuf<G1Dev> res;
   DBuf<G1JDev> hacc, wsum;
@@ -33,7 +33,7 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->perm.alloc(wn));
   HC(m->count.alloc(wb));
   HC(m->start.alloc(wb));
-  HC(m->cursor.alloc(wb));
+  HC(m->rank.alloc(wn));
   HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
   HC(m->nsl.alloc(wb));
   HC(m->soff.alloc(wb));
@@ -185,15 +185,15 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   HC(hipEventRecord(m->ev[0], s));
   HC(hipMemsetAsync(m->count.p, 0, wb * sizeof(uint32_t), s));
   const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
-  k_msm_digits<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->count.p);
+  k_msm_digits<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->rank.p, m->count.p);
   int rc = scan(m->count.p, m->start.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
-  HC(hipMemcpyAsync(m->cursor.p, m->start.p, wb * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   k_msm_nslots<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->nsl.p);
   rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
-  k_msm_scatter<<<blocks((size_t)p.windows * p.nv, 256), 256, 0, s>>>(p, m->key.p, m->cursor.p, m->perm.p);
+  k_msm_scatter<<<blocks((size_t)p.windows * p.nv, 256), 256, 0, s>>>(p, m->key.p, m->rank.p, m->start.p,
+                                                                       m->perm.p);
   // bucket slots in length order, then one lane per slot
   size_t sl = (size_t)p.windows * p.max_slots;
   HC(hipMemsetAsync(m->lenhist.p, 0, 1024 * sizeof(uint32_t), s));

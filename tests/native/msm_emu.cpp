@@ -32,16 +32,13 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   if (p.glv)
     for (uint32_t i = 0; i < n; i++) msm_job_phi(p, i, pts.data());
   size_t wb = (size_t)p.windows * p.buckets;
-  std::vector<uint32_t> key((size_t)p.windows * p.nv), count(wb, 0), start(wb), perm((size_t)p.windows * p.nv);
-  for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), count.data(), false);
+  std::vector<uint32_t> key((size_t)p.windows * p.nv), rank((size_t)p.windows * p.nv), count(wb, 0), start(wb),
+      perm((size_t)p.windows * p.nv);
+  for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), rank.data(), count.data(), false);
   uint32_t run = 0;
   for (size_t b = 0; b < wb; b++) start[b] = run, run += count[b];
-  std::vector<uint32_t> cur(start);
-  for (uint32_t i = 0; i < p.nv; i++)
-    for (uint32_t w = 0; w < p.windows; w++) {
-      uint32_t k = key[(size_t)w * p.nv + i];
-      if (k != NONE) perm[cur[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)]++] = i | (k & 0x80000000u);
-    }
+  for (uint64_t t = 0; t < (uint64_t)p.windows * p.nv; t++)
+    msm_job_scatter(p, t, key.data(), rank.data(), start.data(), perm.data());
   std::vector<uint32_t> soff(wb), owner((size_t)p.windows * p.max_slots, 0xFFFFFFFFu), wlo(p.windows), whi(p.windows);
   run = 0;
   for (size_t b = 0; b < wb; b++) soff[b] = run, run += msm_bucket_slots(p, count[b]);
