@@ -129,8 +129,50 @@ FTS_HD uint32_t add8(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
   return c;
 }
 
+#ifndef FTS_ASM_CHAINS
+#define FTS_ASM_CHAINS 1  // device: modular add/sub and final subtractions as asm carry chains
+#endif
+#include "fp_asm.h"
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+template <class M>
+__device__ __forceinline__ void addmod_asm(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]);
+template <>
+__device__ __forceinline__ void addmod_asm<ModP>(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  addmod_p_asm(r, a, b);
+}
+template <>
+__device__ __forceinline__ void addmod_asm<ModR>(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  addmod_r_asm(r, a, b);
+}
+template <class M>
+__device__ __forceinline__ void submod_asm(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]);
+template <>
+__device__ __forceinline__ void submod_asm<ModP>(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  submod_p_asm(r, a, b);
+}
+template <>
+__device__ __forceinline__ void submod_asm<ModR>(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {
+  submod_r_asm(r, a, b);
+}
+template <class M>
+__device__ __forceinline__ void condsub_asm(uint32_t x[8]);
+template <>
+__device__ __forceinline__ void condsub_asm<ModP>(uint32_t x[8]) {
+  condsub_p_asm(x);
+}
+template <>
+__device__ __forceinline__ void condsub_asm<ModR>(uint32_t x[8]) {
+  condsub_r_asm(x);
+}
+#endif
+
 template <class M>
 FTS_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+  Fe<M> o;
+  addmod_asm<M>(o.v, a.v, b.v);
+  return o;
+#endif
   Fe<M> r, t;
   add8(r.v, a.v, b.v);  // < 2m < 2^256: no carry out
   uint32_t mm[8];
@@ -142,6 +184,11 @@ FTS_HD Fe<M> operator+(const Fe<M>& a, const Fe<M>& b) {
 
 template <class M>
 FTS_HD Fe<M> operator-(const Fe<M>& a, const Fe<M>& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+  Fe<M> o;
+  submod_asm<M>(o.v, a.v, b.v);
+  return o;
+#endif
   Fe<M> r, t;
   uint32_t br = sub8(r.v, a.v, b.v);
   uint32_t mm[8];
@@ -168,11 +215,17 @@ template <class M>
 __device__ __forceinline__ Fe<M> mont_mul_fips(const Fe<M>& a, const Fe<M>& b) {
   Fe<M> x, y;
   mont_mul_fips_limbs<M>(x.v, a.v, b.v);
+#if FTS_ASM_CHAINS
+  condsub_asm<M>(x.v);
+  (void)y;
+  return x;
+#else
   uint32_t pm[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) pm[j] = M::m[j];
   uint32_t br = sub8(y.v, x.v, pm);
   return br ? x : y;
+#endif
 }
 #endif
 

@@ -79,6 +79,10 @@ FTS_HD fp redc_wide(const uint32_t t[16]) {
     hi = 0;
   }
 #endif
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+  condsub2_p_asm(r.v);
+  return r;
+#else
   uint32_t t2[8], pm[8], p2[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -88,15 +92,24 @@ FTS_HD fp redc_wide(const uint32_t t[16]) {
   if (!sub8(t2, r.v, p2)) r = fe_const<ModP>(t2);
   if (!sub8(t2, r.v, pm)) r = fe_const<ModP>(t2);
   return r;
+#endif
 }
 
 FTS_HD void add16(uint32_t r[16], const uint32_t a[16]) {
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+  add16_asm(r, a);
+  return;
+#endif
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) r[i] = addc32(r[i], a[i], c, &c);
 }
 
 FTS_HD void sub16(uint32_t r[16], const uint32_t a[16]) {
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ASM_CHAINS
+  sub16_asm(r, a);
+  return;
+#endif
   uint32_t b = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) r[i] = subb32(r[i], a[i], b, &b);
