@@ -9,7 +9,7 @@ using namespace fts;
 // Final exponentiations, sextet layout (see k_miller).
 __global__ void __launch_bounds__(64, 2) k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf,
                                              uint8_t* arena) {
-  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_FEXP];
+  SX_SLOTS_DECL(SX_SLOTS_FEXP)
   SX_KERNEL_PROLOGUE(n);
   sx_job_fexp(x, jobs[jc], fbuf, jc, arena, valid);
 }

@@ -21,7 +21,7 @@ __global__ void __launch_bounds__(128) k_g2(const G2Job* jobs, uint32_t n, const
 __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n,
                                                    const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out,
                                                    const G1Dev* pts, EvLineDev* lines) {
-  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_MILLER_F];
+  SX_SLOTS_DECL(SX_SLOTS_MILLER_F)
   SX_KERNEL_PROLOGUE(n);
   sx_job_g2lines(x, g2[jc], pr[jc], scal, tab, g2out, pts, lines, jc, n, valid);
 }

@@ -10,7 +10,7 @@ using namespace fts;
 // shadow the last sextet read-only), one wave per workgroup.
 __global__ void __launch_bounds__(64, 2) k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines,
                                                   const EvLineDev* lines2, const G1Dev* g1out, F12Dev* fbuf) {
-  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_MILLER_F];
+  SX_SLOTS_DECL(SX_SLOTS_MILLER_F)
   SX_KERNEL_PROLOGUE(n);
   sx_job_miller(x, jobs[jc], qlines, lines2, g1out, fbuf, jc, n, valid);
 }

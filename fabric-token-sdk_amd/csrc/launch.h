@@ -13,6 +13,14 @@ static constexpr uint32_t SX_JOBS_PER_WAVE = 10;
 struct SyncWave {
   __device__ __forceinline__ void operator()() const { __syncthreads(); }
 };
+// LDS of the sextets of one workgroup: region i holds sextet i's NS slots plus
+// 16 bytes of padding, so the regions of the sextets that share a ds_read_b128
+// lane group start on different 16-byte bank slots (64 B slots and 1152 / 1920 B
+// regions would put them on the same banks: 3-way conflicts measured by
+// SQ_LDS_BANK_CONFLICT; the padded layout is conflict-free for broadcast reads).
+#define SX_SLOTS_DECL(NS)                                                          \
+  static constexpr uint32_t sx_stride_ = (NS) * (sizeof(F2Slot) / 16) + 1;          \
+  __shared__ uint4 sx_raw_[SX_JOBS_PER_WAVE * sx_stride_];
 // Lane -> (sextet, role); lanes 60..63 are ghosts that shadow sextet 9 without
 // writing its slots.  Every lane runs the whole program (barriers inside).
 #define SX_KERNEL_PROLOGUE(n)                                           \
@@ -23,7 +31,7 @@ struct SyncWave {
   uint32_t job_ = blockIdx.x * SX_JOBS_PER_WAVE + sx_;                  \
   bool valid = !ghost_ && job_ < (n);                                   \
   uint32_t jc = job_ < (n) ? job_ : (n) - 1;                            \
-  Sx<SyncWave> x{k_, (SlotT*)(slots[sx_]), !ghost_, {}};
+  Sx<SyncWave> x{k_, (SlotT*)(sx_raw_ + sx_ * sx_stride_), !ghost_, {}};
 
 __global__ void k_decode(const DecodeJob* jobs, uint32_t n, const uint8_t* wire, G1Dev* pts, uint8_t* pt_ok,
                          uint8_t* arena);

@@ -10,7 +10,7 @@ using namespace fts;
 
 template <int OP>
 __global__ void __launch_bounds__(64, 2) k_sxbench(const fp2* seed, fp2* out, int iters) {
-  __shared__ F2Slot slots[SX_JOBS_PER_WAVE][SX_SLOTS_FEXP];
+  SX_SLOTS_DECL(SX_SLOTS_FEXP)
   uint32_t n = gridDim.x * SX_JOBS_PER_WAVE;
   SX_KERNEL_PROLOGUE(n);
   fp2 a = seed[(jc * 6 + k_) & 1023], b = seed[(jc * 6 + k_ + 7) & 1023];
