@@ -190,6 +190,7 @@ def roofline(batch, device, tx_per_s):
             "peak": round(peak / 1e12, 4), "unit": "TMAD/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "kernel_ms_serial": round(kern[dom][0], 3), "jobs": kern[dom][1],
             "m_per_job": round(m_job, 1),
+            "serial_ms": {k: round(v[0], 3) for k, v in kern.items()},
             "pipeline": {"achieved": round(step_mad / 1e12, 4), "frac": round(step_mad / peak, 4),
                          "note": "whole step: counted products per transfer x 136 x transfers/s"},
             "note": "integer VALU roofline (v_mad_u64_u32, peak = measured madpeak); per-kernel time from a "

@@ -15,7 +15,7 @@ FTS_HD bool is_zero(const fp& a) { return fe_is_zero(a); }
 FTS_HD bool is_zero(const fp2& a) { return f2_is_zero(a); }
 FTS_HD bool eqf(const fp& a, const fp& b) { return fe_eq(a, b); }
 FTS_HD bool eqf(const fp2& a, const fp2& b) { return f2_eq(a, b); }
-FTS_HD fp inv(const fp& a) { return fp_inv(a); }
+FTS_HD fp inv(const fp& a) { return fp_inv_var(a); }  // variable time: public values only
 FTS_HD fp2 inv(const fp2& a) { return f2_inv(a); }
 template <class F> FTS_HD F zero_of();
 template <> FTS_HD fp zero_of<fp>() { return fe_zero<ModP>(); }

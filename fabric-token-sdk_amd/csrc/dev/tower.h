@@ -55,7 +55,7 @@ FTS_HD fp2 f2_mul_xi(const fp2& a) {
 
 FTS_HDN fp2 f2_inv(const fp2& a) {
   fp n = fe_sqr(a.c0) + fe_sqr(a.c1);
-  fp ni = fp_inv(n);
+  fp ni = fp_inv_var(n);  // variable time: every value inverted on this path is public
   return {a.c0 * ni, fe_neg(a.c1 * ni)};
 }
 

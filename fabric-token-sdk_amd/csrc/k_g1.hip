@@ -65,7 +65,7 @@ __device__ fp block_batch_inv(fp x, uint32_t (*pre)[NT], uint32_t (*suf)[NT], ui
     fp all;
 #pragma unroll
     for (int k = 0; k < 8; k++) all.v[k] = pre[k][NT - 1];
-    fp ia = fp_inv(all);
+    fp ia = fp_inv_var(all);  // public values; one wave, one value: no divergence
     if (t == 0)
 #pragma unroll
       for (int k = 0; k < 8; k++) tot[k] = ia.v[k];
