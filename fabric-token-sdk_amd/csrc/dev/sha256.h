@@ -35,10 +35,14 @@ struct Sha256 {
     for (int i = 0; i < 16; i++) w[i] = 0;
   }
 
-  FTS_HD void compress() {
+  // one 64-byte block given as 16 big-endian words (fully unrolled: the
+  // message schedule stays in registers)
+  FTS_HD void compress_words(const uint32_t* in) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
     uint32_t W[16];
-    for (int i = 0; i < 16; i++) W[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < 16; i++) W[i] = in[i];
+#pragma unroll
     for (int i = 0; i < 64; i++) {
       uint32_t wi;
       if (i < 16) {
@@ -59,6 +63,10 @@ struct Sha256 {
       hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+
+  FTS_HD void compress() {
+    compress_words(w);
     for (int i = 0; i < 16; i++) w[i] = 0;
     fill = 0;
   }
@@ -71,8 +79,31 @@ struct Sha256 {
   }
 
   FTS_HD void update(const uint8_t* p, uint32_t n) {
-    // fast path: whole aligned words when the block is word-aligned
     uint32_t i = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // whole blocks straight from memory with 16-byte loads while the block is
+    // empty and the source 16-byte aligned (the planners align every arena
+    // allocation to 16 bytes; transcript segments are 64-byte multiples except
+    // the last)
+    if (fill == 0 && (((uintptr_t)p) & 15) == 0) {
+      while (n - i >= 64) {
+        const uint4* q = reinterpret_cast<const uint4*>(p + i);
+        uint32_t W[16];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          uint4 v = q[k];
+          W[4 * k] = __builtin_bswap32(v.x);
+          W[4 * k + 1] = __builtin_bswap32(v.y);
+          W[4 * k + 2] = __builtin_bswap32(v.z);
+          W[4 * k + 3] = __builtin_bswap32(v.w);
+        }
+        compress_words(W);
+        total += 64;
+        i += 64;
+      }
+    }
+#endif
+    // whole words when the block position is word-aligned
     while (i < n && (fill & 3)) byte(p[i++]);
     while (i + 4 <= n) {
       w[fill >> 2] = ((uint32_t)p[i] << 24) | ((uint32_t)p[i + 1] << 16) | ((uint32_t)p[i + 2] << 8) | p[i + 3];

@@ -188,9 +188,10 @@ class Builder {
   }
   void fail(uint8_t code) { check(CK_STATIC, code); }
 
+  // 16-byte aligned (the device SHA-256 streams aligned whole blocks)
   uint32_t arena_alloc(uint32_t n) {
-    uint32_t off = (uint32_t)pl.arena.size();
-    pl.arena.resize(pl.arena.size() + n, 0);
+    uint32_t off = (uint32_t)((pl.arena.size() + 15) & ~(size_t)15);
+    pl.arena.resize(off + n, 0);
     return off;
   }
   uint32_t scalar(const Ref& r) {
@@ -792,6 +793,7 @@ void Builder::issue(const IssueIn& t) {
 
 // Append piece `b` (local indices) to plan `a`, relocating every index.
 void plan_merge(Plan& a, const Plan& b) {
+  a.arena.resize((a.arena.size() + 15) & ~(size_t)15, 0);  // keep the piece's 16-byte alignment
   uint32_t o_wire = (uint32_t)a.wire.size(), o_arena = (uint32_t)a.arena.size();
   uint32_t o_pts = a.n_pts, o_scal = a.n_scal, o_g1 = a.n_g1out, o_g2 = a.n_g2out;
   uint32_t o_list = (uint32_t)a.sclist.size(), o_vt = (uint32_t)a.vt.size(), o_seg = (uint32_t)a.seg.size();

@@ -79,14 +79,15 @@ struct PB {
   std::string err;
   PB(Plan& p, const PPInfo& q) : pl(p), pp(q) {}
 
-  uint32_t arena_put(const void* p, size_t n) {
-    uint32_t off = (uint32_t)pl.arena.size();
-    pl.arena.insert(pl.arena.end(), (const uint8_t*)p, (const uint8_t*)p + n);
+  // 16-byte aligned allocations (the device SHA-256 streams aligned whole blocks)
+  uint32_t arena_alloc(uint32_t n) {
+    uint32_t off = (uint32_t)((pl.arena.size() + 15) & ~(size_t)15);
+    pl.arena.resize(off + n, 0);
     return off;
   }
-  uint32_t arena_alloc(uint32_t n) {
-    uint32_t off = (uint32_t)pl.arena.size();
-    pl.arena.resize(pl.arena.size() + n, 0);
+  uint32_t arena_put(const void* p, size_t n) {
+    uint32_t off = arena_alloc((uint32_t)n);
+    if (n) memcpy(pl.arena.data() + off, p, n);
     return off;
   }
   uint32_t seg(uint32_t off, uint32_t len) {
