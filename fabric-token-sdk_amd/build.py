@@ -22,7 +22,9 @@ MADPEAK = os.path.join(HERE, "zkatdlog", "_lib", "libftsmadpeak.so")
 FPCHECK = os.path.join(HERE, "zkatdlog", "_lib", "libftsfpcheck.so")
 ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH]
+# 16-bit signed windows for the G1 fixed-base tables (dev/jobs.h FTS_G1TAB_C)
+DEFS = ["-DFTS_G1TAB_C=16"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH] + DEFS
 
 SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip"))) + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "msm_rt.hip")]
            + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))))
@@ -43,7 +45,7 @@ def compile_one(src, force, hdr_time):
         return obj, None
     cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "-c", src, "-o", obj]
+        cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas"] + DEFS + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, "%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr)

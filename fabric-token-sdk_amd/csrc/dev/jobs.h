@@ -37,8 +37,20 @@ struct F12Dev {
 
 enum G1Base : uint8_t { G1B_PED0 = 0, G1B_PED1, G1B_PED2, G1B_PEDGEN, G1B_GEN, G1B_COUNT };
 enum G2Base : uint8_t { G2B_PK0 = 0, G2B_PK1, G2B_PK2, G2B_Q, G2B_COUNT };
-static constexpr int TAB_WINDOWS = 32;  // 8-bit windows over 256-bit scalars
+// G2 fixed-base tables: unsigned 8-bit windows over 256-bit scalars
+static constexpr int TAB_WINDOWS = 32;
 static constexpr int TAB_DIGITS = 256;
+// G1 fixed-base tables: signed FTS_G1TAB_C-bit windows, digits d in
+// [-2^(C-1), 2^(C-1)], entries for |d| = 1 .. 2^(C-1) (d < 0: negate y).  The
+// product library is built with C = 16 (16 mixed additions per fixed term;
+// 5 bases x 16 x 32768 x 64 B = 168 MB, read by 64-byte gathers); the test-only
+// host build keeps C = 8 (tables it can build per entry on the CPU).
+#ifndef FTS_G1TAB_C
+#define FTS_G1TAB_C 8
+#endif
+static constexpr int G1TAB_C = FTS_G1TAB_C;
+static constexpr int G1TAB_WINDOWS = (256 + G1TAB_C - 1) / G1TAB_C;
+static constexpr int G1TAB_DIGITS = 1 << (G1TAB_C - 1);
 
 struct DecodeJob {
   uint32_t raw;       // offset of the element bytes in the wire pool
@@ -326,11 +338,19 @@ FTS_HD uint8_t decode_g2(const uint8_t* b, uint32_t len, G2Dev& out, uint8_t* by
   return ok ? 1 : 0;
 }
 
-// table entry: digit * 2^(8 window) * B
+// G1 table entry idx = (base, window, |d| - 1): |d| * 2^(C window) * B (one
+// scalar multiplication per entry: the host build and small C)
 FTS_HD void job_tab_g1(uint32_t idx, const G1Dev* bases, G1Dev* tab) {
-  uint32_t d = idx % TAB_DIGITS, w = (idx / TAB_DIGITS) % TAB_WINDOWS, b = idx / (TAB_DIGITS * TAB_WINDOWS);
+  uint32_t d = idx % G1TAB_DIGITS + 1, w = (idx / G1TAB_DIGITS) % G1TAB_WINDOWS,
+           b = idx / (G1TAB_DIGITS * G1TAB_WINDOWS);
   uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  k[w >> 2] = d << ((w & 3) * 8);
+  // d << (C w) as 8 limbs (d < 2^C <= 2^16, C w < 256)
+  uint32_t bit = (uint32_t)G1TAB_C * w, limb = bit >> 5, sh = bit & 31;
+  uint64_t v = (uint64_t)d << sh;
+  for (int q = 0; q < 8; q++) {
+    if ((uint32_t)q == limb) k[q] = (uint32_t)v;
+    if ((uint32_t)q == limb + 1) k[q] = (uint32_t)(v >> 32);
+  }
   g1a r = jac_to_aff(aff_mul(g1_load(bases[b]), k));
   G1Dev o;
   g1_store(o, r);
@@ -424,11 +444,27 @@ FTS_HD const Dev& tab_at(const Dev* tab, int base, int window, int digit) {
   return tab[((size_t)base * TAB_WINDOWS + window) * TAB_DIGITS + digit];
 }
 
+// sum_w d_w 2^(C w) B over the signed C-bit digits of s (s < r < 2^254, so the
+// top window absorbs the last carry)
 FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]) {
+  uint32_t carry = 0;
+  const G1Dev* tb = tab + (size_t)base * G1TAB_WINDOWS * G1TAB_DIGITS;
 #pragma nounroll
-  for (int w = 0; w < TAB_WINDOWS; w++) {
-    uint32_t d = (s[w >> 2] >> ((w & 3) * 8)) & 0xFF;
-    if (d) acc = jac_add_aff(acc, g1_load(tab_at(tab, base, w, (int)d)));
+  for (int w = 0; w < G1TAB_WINDOWS; w++) {
+    uint32_t bit = (uint32_t)G1TAB_C * w, limb = bit >> 5, sh = bit & 31;
+    uint64_t lo = limb < 8 ? s[limb] : 0, hi = limb + 1 < 8 ? s[limb + 1] : 0;
+    uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1ull << G1TAB_C) - 1)) + carry;
+    int32_t d = (int32_t)raw;
+    carry = 0;
+    if (raw > (1u << (G1TAB_C - 1))) {
+      d = (int32_t)raw - (int32_t)(1u << G1TAB_C);
+      carry = 1;
+    }
+    if (d) {
+      g1a T = g1_load(tb[(size_t)w * G1TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+      if (d < 0) T.y = fe_neg(T.y);
+      acc = jac_add_aff(acc, T);
+    }
   }
   return acc;
 }

@@ -94,6 +94,54 @@ __global__ void __launch_bounds__(COMBINE_NT) k_g1_combine(const G1Job* jobs, ui
   if (valid) job_g1_finish(jobs[i], acc, zi, g1out, arena);
 }
 
+// ---- wide-window G1 tables (C = 16): per (base, window) the point
+// B_w = 2^(C w) B, then every lane fills a chunk of consecutive digits by
+// repeated mixed additions of B_w, made affine together (Montgomery batch
+// inversion; jtmp / zs hold chunk * lanes Jacobian points / prefix products).
+__global__ void __launch_bounds__(64) k_tab_g1_bw(const G1Dev* bases, G1Dev* bw) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint32_t)(G1B_COUNT * G1TAB_WINDOWS)) return;
+  uint32_t b = i / G1TAB_WINDOWS, w = i - b * G1TAB_WINDOWS;
+  g1j acc = jac_from_aff(g1_load(bases[b]));
+  for (uint32_t q = 0; q < (uint32_t)G1TAB_C * w; q++) acc = jac_dbl(acc);
+  G1Dev d;
+  g1_store(d, jac_to_aff(acc));
+  bw[i] = d;
+}
+
+__global__ void __launch_bounds__(128) k_tab_g1_fill(const G1Dev* bw, uint32_t chunk, G1JDev* jtmp,
+                                                     uint32_t (*zs)[8], G1Dev* tab) {
+  uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x, per = G1TAB_DIGITS / chunk;
+  if (lane >= (uint32_t)(G1B_COUNT * G1TAB_WINDOWS) * per) return;
+  uint32_t t = lane / per, c = lane - t * per;
+  size_t base = (size_t)t * G1TAB_DIGITS + (size_t)c * chunk;  // entry of |d| = c chunk + 1
+  g1a B = g1_load(bw[t]);
+  g1j acc = aff_mul_u64(B, (uint64_t)c * chunk + 1);
+  fp prod = fe_one<ModP>();
+  for (uint32_t e = 0; e < chunk; e++) {
+    if (e) acc = jac_add_aff(acc, B);
+    g1j_store(jtmp[base + e], acc);
+    prod = prod * acc.z;
+#pragma unroll
+    for (int q = 0; q < 8; q++) zs[base + e][q] = prod.v[q];
+  }
+  fp inv = fp_inv_var(prod);
+  for (int e = (int)chunk - 1; e >= 0; e--) {
+    g1j pj = g1j_load(jtmp[base + e]);
+    fp prev = e ? fe_const<ModP>(zs[base + e - 1]) : fe_one<ModP>();
+    fp zi = inv * prev;
+    inv = inv * pj.z;
+    fp zi2 = sqr(zi);
+    g1a a;
+    a.x = pj.x * zi2;
+    a.y = pj.y * zi2 * zi;
+    a.inf = false;
+    G1Dev d;
+    g1_store(d, a);
+    tab[base + e] = d;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab) {
   JOB_KERNEL_PROLOGUE(n);
   job_tab_g1(i, bases, tab);

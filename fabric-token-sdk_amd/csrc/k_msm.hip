@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(128) k_msm_genpoints(uint32_t n, uint32_t off,
   uint32_t cnt = n - i0 < chunk ? n - i0 : chunk;
   uint32_t k[8] = {i0 + off, 0, 0, 0, 0, 0, 0, 0};
   g1j acc = g1_fixed_acc(jac_inf<fp>(), gtab, G1B_GEN, k);
-  g1a G = g1_load(gtab[((size_t)G1B_GEN * TAB_WINDOWS + 0) * TAB_DIGITS + 1]);
+  g1a G = g1_load(gtab[(size_t)G1B_GEN * G1TAB_WINDOWS * G1TAB_DIGITS]);  // |d| = 1 of window 0
   fp prod = fe_one<ModP>();
   for (uint32_t e = 0; e < cnt; e++) {
     if (e) acc = jac_add_aff(acc, G);

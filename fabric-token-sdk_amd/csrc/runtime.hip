@@ -180,13 +180,28 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
       fail(FTZ_E_NOMEM, "alloc");
       break;
     }
-    uint32_t n1 = G1B_COUNT * TAB_WINDOWS * TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
+    uint32_t n1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
     if (c->g1tab.alloc(n1) != hipSuccess || c->g2tab.alloc(n2) != hipSuccess ||
         c->qlines.alloc(MILLER_LINES) != hipSuccess) {
       fail(FTZ_E_NOMEM, "table allocation failed");
       break;
     }
-    k_tab_g1<<<blocks_for(n1, 64), 64, 0, c->stream>>>(d_b1.p, n1, c->g1tab.p);
+    DBuf<G1Dev> d_bw;
+    DBuf<G1JDev> d_jt;
+    DBuf<uint32_t> d_zs;
+    if (G1TAB_C <= 8) {
+      k_tab_g1<<<blocks_for(n1, 64), 64, 0, c->stream>>>(d_b1.p, n1, c->g1tab.p);
+    } else {
+      const uint32_t chunk = 128, lanes = G1B_COUNT * G1TAB_WINDOWS * (G1TAB_DIGITS / chunk);
+      if (d_bw.alloc(G1B_COUNT * G1TAB_WINDOWS) != hipSuccess || d_jt.alloc(n1) != hipSuccess ||
+          d_zs.alloc(8 * (size_t)n1) != hipSuccess) {
+        fail(FTZ_E_NOMEM, "table scratch allocation failed");
+        break;
+      }
+      k_tab_g1_bw<<<blocks_for(G1B_COUNT * G1TAB_WINDOWS, 64), 64, 0, c->stream>>>(d_b1.p, d_bw.p);
+      k_tab_g1_fill<<<blocks_for(lanes, 128), 128, 0, c->stream>>>(
+          d_bw.p, chunk, d_jt.p, reinterpret_cast<uint32_t (*)[8]>(d_zs.p), c->g1tab.p);
+    }
     k_tab_g2<<<blocks_for(n2, 64), 64, 0, c->stream>>>(d_g2.p, n2, c->g2tab.p);  // PK0, PK1, PK2, Q
     DBuf<int> d_n;
     if (d_n.alloc(1) != hipSuccess) {
