@@ -23,7 +23,7 @@ FPCHECK = os.path.join(HERE, "zkatdlog", "_lib", "libftsfpcheck.so")
 ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # 16-bit signed windows for the G1 fixed-base tables (dev/jobs.h FTS_G1TAB_C)
-DEFS = ["-DFTS_G1TAB_C=16"]
+DEFS = ["-DFTS_G1TAB_C=16", "-DFTS_G2TAB_C=13"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH] + DEFS
 
 SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip"))) + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "msm_rt.hip")]

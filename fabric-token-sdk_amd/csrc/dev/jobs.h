@@ -37,9 +37,15 @@ struct F12Dev {
 
 enum G1Base : uint8_t { G1B_PED0 = 0, G1B_PED1, G1B_PED2, G1B_PEDGEN, G1B_GEN, G1B_COUNT };
 enum G2Base : uint8_t { G2B_PK0 = 0, G2B_PK1, G2B_PK2, G2B_Q, G2B_COUNT };
-// G2 fixed-base tables: unsigned 8-bit windows over 256-bit scalars
-static constexpr int TAB_WINDOWS = 32;
-static constexpr int TAB_DIGITS = 256;
+// G2 fixed-base tables: signed FTS_G2TAB_C-bit windows, same layout as G1
+// below (product library: C = 13, 20 windows, 4 x 20 x 4096 x 128 B = 42 MB;
+// test-only host build: C = 8)
+#ifndef FTS_G2TAB_C
+#define FTS_G2TAB_C 8
+#endif
+static constexpr int G2TAB_C = FTS_G2TAB_C;
+static constexpr int G2TAB_WINDOWS = (256 + G2TAB_C - 1) / G2TAB_C;
+static constexpr int G2TAB_DIGITS = 1 << (G2TAB_C - 1);
 // G1 fixed-base tables: signed FTS_G1TAB_C-bit windows, digits d in
 // [-2^(C-1), 2^(C-1)], entries for |d| = 1 .. 2^(C-1) (d < 0: negate y).  The
 // product library is built with C = 16 (16 mixed additions per fixed term;
@@ -356,10 +362,17 @@ FTS_HD void job_tab_g1(uint32_t idx, const G1Dev* bases, G1Dev* tab) {
   g1_store(o, r);
   tab[idx] = o;
 }
+// G2 table entry idx = (base, window, |d| - 1): |d| * 2^(C window) * B
 FTS_HD void job_tab_g2(uint32_t idx, const G2Dev* bases, G2Dev* tab) {
-  uint32_t d = idx % TAB_DIGITS, w = (idx / TAB_DIGITS) % TAB_WINDOWS, b = idx / (TAB_DIGITS * TAB_WINDOWS);
+  uint32_t d = idx % G2TAB_DIGITS + 1, w = (idx / G2TAB_DIGITS) % G2TAB_WINDOWS,
+           b = idx / (G2TAB_DIGITS * G2TAB_WINDOWS);
   uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  k[w >> 2] = d << ((w & 3) * 8);
+  uint32_t bit = (uint32_t)G2TAB_C * w, limb = bit >> 5, sh = bit & 31;
+  uint64_t v = (uint64_t)d << sh;
+  for (int q = 0; q < 8; q++) {
+    if ((uint32_t)q == limb) k[q] = (uint32_t)v;
+    if ((uint32_t)q == limb + 1) k[q] = (uint32_t)(v >> 32);
+  }
   g2a r = jac_to_aff(aff_mul(g2_load(bases[b]), k));
   G2Dev o;
   g2_store(o, r);
@@ -438,10 +451,47 @@ FTS_HD void job_scalar(const ScalJob& j, uint32_t (*scal)[8], const uint32_t* li
   for (int k = 0; k < 8; k++) scal[j.out][k] = out[k];
 }
 
-// fixed-base table entry T[base][window][digit] = digit * 2^(8 window) * B
-template <class Dev>
-FTS_HD const Dev& tab_at(const Dev* tab, int base, int window, int digit) {
-  return tab[((size_t)base * TAB_WINDOWS + window) * TAB_DIGITS + digit];
+// signed C-bit digit of window w of s (s < 2^254): the raw chunk plus the
+// carry of the windows below, recomputed from window 0 (for code that visits
+// windows out of order)
+FTS_HD int32_t sdigit_at(const uint32_t s[8], int C, int w) {
+  uint32_t carry = 0;
+  int32_t d = 0;
+  for (int v = 0; v <= w; v++) {
+    uint32_t bit = (uint32_t)C * v, limb = bit >> 5, sh = bit & 31;
+    uint64_t lo = limb < 8 ? s[limb] : 0, hi = limb + 1 < 8 ? s[limb + 1] : 0;
+    uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1ull << C) - 1)) + carry;
+    d = (int32_t)raw;
+    carry = 0;
+    if (raw > (1u << (C - 1))) {
+      d = (int32_t)raw - (int32_t)(1u << C);
+      carry = 1;
+    }
+  }
+  return d;
+}
+
+FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]) {
+  uint32_t carry = 0;
+  const G2Dev* tb = tab + (size_t)base * G2TAB_WINDOWS * G2TAB_DIGITS;
+#pragma nounroll
+  for (int w = 0; w < G2TAB_WINDOWS; w++) {
+    uint32_t bit = (uint32_t)G2TAB_C * w, limb = bit >> 5, sh = bit & 31;
+    uint64_t lo = limb < 8 ? s[limb] : 0, hi = limb + 1 < 8 ? s[limb + 1] : 0;
+    uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1ull << G2TAB_C) - 1)) + carry;
+    int32_t d = (int32_t)raw;
+    carry = 0;
+    if (raw > (1u << (G2TAB_C - 1))) {
+      d = (int32_t)raw - (int32_t)(1u << G2TAB_C);
+      carry = 1;
+    }
+    if (d) {
+      g2a T = g2_load(tb[(size_t)w * G2TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+      if (d < 0) T.y = f2_neg(T.y);
+      acc = jac_add_aff(acc, T);
+    }
+  }
+  return acc;
 }
 
 // sum_w d_w 2^(C w) B over the signed C-bit digits of s (s < r < 2^254, so the
@@ -465,15 +515,6 @@ FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]
       if (d < 0) T.y = fe_neg(T.y);
       acc = jac_add_aff(acc, T);
     }
-  }
-  return acc;
-}
-
-FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]) {
-#pragma nounroll
-  for (int w = 0; w < TAB_WINDOWS; w++) {
-    uint32_t d = (s[w >> 2] >> ((w & 3) * 8)) & 0xFF;
-    if (d) acc = jac_add_aff(acc, g2_load(tab_at(tab, base, w, (int)d)));
   }
   return acc;
 }
@@ -881,11 +922,15 @@ FTS_HD void sx_job_g2lines(const X& x, const G2Job& g, const PairJob& j, const u
   // ---- phase A
   g2j acc = jac_inf<fp2>();
 #pragma nounroll
-  for (int p = k; p < 3 * TAB_WINDOWS; p += 6) {
-    int f = p / TAB_WINDOWS, w = p % TAB_WINDOWS;
+  for (int p = k; p < 3 * G2TAB_WINDOWS; p += 6) {
+    int f = p / G2TAB_WINDOWS, w = p % G2TAB_WINDOWS;
     if (f < g.nfix) {
-      uint32_t d = (scal[g.fscal[f]][w >> 2] >> ((w & 3) * 8)) & 0xFF;
-      if (d) acc = jac_add_aff(acc, g2_load(tab_at(tab, g.fbase[f], w, (int)d)));
+      int32_t d = sdigit_at(scal[g.fscal[f]], G2TAB_C, w);
+      if (d) {
+        g2a T = g2_load(tab[((size_t)g.fbase[f] * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+        if (d < 0) T.y = f2_neg(T.y);
+        acc = jac_add_aff(acc, T);
+      }
     }
   }
   x.put(3 * k + 0, acc.x);

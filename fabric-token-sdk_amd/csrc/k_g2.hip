@@ -26,6 +26,72 @@ __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJo
   sx_job_g2lines(x, g2[jc], pr[jc], scal, tab, g2out, pts, lines, jc, n, valid);
 }
 
+// ---- wide-window G2 tables (C > 8), as k_tab_g1_bw / k_tab_g1_fill
+__global__ void __launch_bounds__(64) k_tab_g2_bw(const G2Dev* bases, G2Dev* bw) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint32_t)(G2B_COUNT * G2TAB_WINDOWS)) return;
+  uint32_t b = i / G2TAB_WINDOWS, w = i - b * G2TAB_WINDOWS;
+  g2j acc = jac_from_aff(g2_load(bases[b]));
+  for (uint32_t q = 0; q < (uint32_t)G2TAB_C * w; q++) acc = jac_dbl(acc);
+  G2Dev d;
+  g2_store(d, jac_to_aff(acc));
+  bw[i] = d;
+}
+
+struct G2JDev {
+  uint32_t w[48];
+};
+
+__global__ void __launch_bounds__(128) k_tab_g2_fill(const G2Dev* bw, uint32_t chunk, uint32_t (*jt)[48],
+                                                     uint32_t (*zs)[16], G2Dev* tab) {
+  uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x, per = G2TAB_DIGITS / chunk;
+  if (lane >= (uint32_t)(G2B_COUNT * G2TAB_WINDOWS) * per) return;
+  uint32_t t = lane / per, c = lane - t * per;
+  size_t base = (size_t)t * G2TAB_DIGITS + (size_t)c * chunk;
+  g2a B = g2_load(bw[t]);
+  g2j acc = aff_mul_u64(B, (uint64_t)c * chunk + 1);
+  fp2 prod = f2_one();
+  auto st = [](uint32_t* o, const fp2& a) {
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      o[q] = a.c0.v[q];
+      o[8 + q] = a.c1.v[q];
+    }
+  };
+  auto ld = [](const uint32_t* o) {
+    fp2 a;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      a.c0.v[q] = o[q];
+      a.c1.v[q] = o[8 + q];
+    }
+    return a;
+  };
+  for (uint32_t e = 0; e < chunk; e++) {
+    if (e) acc = jac_add_aff(acc, B);
+    st(jt[base + e], acc.x);
+    st(jt[base + e] + 16, acc.y);
+    st(jt[base + e] + 32, acc.z);
+    prod = prod * acc.z;
+    st(zs[base + e], prod);
+  }
+  fp2 inv = f2_inv(prod);
+  for (int e = (int)chunk - 1; e >= 0; e--) {
+    fp2 X = ld(jt[base + e]), Y = ld(jt[base + e] + 16), Z = ld(jt[base + e] + 32);
+    fp2 prev = e ? ld(zs[base + e - 1]) : f2_one();
+    fp2 zi = inv * prev;
+    inv = inv * Z;
+    fp2 zi2 = zi * zi;
+    g2a a;
+    a.x = X * zi2;
+    a.y = Y * zi2 * zi;
+    a.inf = false;
+    G2Dev d;
+    g2_store(d, a);
+    tab[base + e] = d;
+  }
+}
+
 __global__ void __launch_bounds__(64) k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab) {
   JOB_KERNEL_PROLOGUE(n);
   job_tab_g2(i, bases, tab);

@@ -55,6 +55,8 @@ __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], c
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
+__global__ void k_tab_g2_bw(const G2Dev* bases, G2Dev* bw);
+__global__ void k_tab_g2_fill(const G2Dev* bw, uint32_t chunk, uint32_t (*jt)[48], uint32_t (*zs)[16], G2Dev* tab);
 __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines, const EvLineDev* lines2,
                          const G1Dev* g1out, F12Dev* fbuf);
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);

@@ -180,7 +180,7 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
       fail(FTZ_E_NOMEM, "alloc");
       break;
     }
-    uint32_t n1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
+    uint32_t n1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, n2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
     if (c->g1tab.alloc(n1) != hipSuccess || c->g2tab.alloc(n2) != hipSuccess ||
         c->qlines.alloc(MILLER_LINES) != hipSuccess) {
       fail(FTZ_E_NOMEM, "table allocation failed");
@@ -202,7 +202,22 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
       k_tab_g1_fill<<<blocks_for(lanes, 128), 128, 0, c->stream>>>(
           d_bw.p, chunk, d_jt.p, reinterpret_cast<uint32_t (*)[8]>(d_zs.p), c->g1tab.p);
     }
-    k_tab_g2<<<blocks_for(n2, 64), 64, 0, c->stream>>>(d_g2.p, n2, c->g2tab.p);  // PK0, PK1, PK2, Q
+    DBuf<G2Dev> d_bw2;
+    DBuf<uint32_t> d_jt2, d_zs2;
+    if (G2TAB_C <= 8) {
+      k_tab_g2<<<blocks_for(n2, 64), 64, 0, c->stream>>>(d_g2.p, n2, c->g2tab.p);  // PK0, PK1, PK2, Q
+    } else {
+      const uint32_t chunk = 64, lanes = G2B_COUNT * G2TAB_WINDOWS * (G2TAB_DIGITS / chunk);
+      if (d_bw2.alloc(G2B_COUNT * G2TAB_WINDOWS) != hipSuccess || d_jt2.alloc(48 * (size_t)n2) != hipSuccess ||
+          d_zs2.alloc(16 * (size_t)n2) != hipSuccess) {
+        fail(FTZ_E_NOMEM, "table scratch allocation failed");
+        break;
+      }
+      k_tab_g2_bw<<<blocks_for(G2B_COUNT * G2TAB_WINDOWS, 64), 64, 0, c->stream>>>(d_g2.p, d_bw2.p);
+      k_tab_g2_fill<<<blocks_for(lanes, 128), 128, 0, c->stream>>>(
+          d_bw2.p, chunk, reinterpret_cast<uint32_t (*)[48]>(d_jt2.p), reinterpret_cast<uint32_t (*)[16]>(d_zs2.p),
+          c->g2tab.p);
+    }
     DBuf<int> d_n;
     if (d_n.alloc(1) != hipSuccess) {
       fail(FTZ_E_NOMEM, "alloc");

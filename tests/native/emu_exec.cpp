@@ -94,7 +94,7 @@ void* emu_ctx_create(const uint8_t* pp, size_t len, char* err, size_t errlen) {
   hb[G1B_PED2] = g1[3];
   hb[G1B_PEDGEN] = g1[0];
   hb[G1B_GEN] = g1[4];
-  uint32_t n1 = G1B_COUNT * TAB_WINDOWS * TAB_DIGITS, n2 = G2B_COUNT * TAB_WINDOWS * TAB_DIGITS;
+  uint32_t n1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, n2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
   c->g1tab.resize(n1);
   c->g2tab.resize(n2);
   par_for(n1, [&](uint32_t i) { job_tab_g1(i, hb.data(), c->g1tab.data()); });

@@ -176,11 +176,12 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   for (int i = 0; i < 3; i++) g2_store(b[i], ld_g2(bases + 128 * i));
   std::vector<uint32_t> sc(8 * 3);
   for (int i = 0; i < 3; i++) be32_to_limbs(&sc[8 * i], scalars + 32 * i);
-  std::vector<G2Dev> tab((size_t)G2B_COUNT * TAB_WINDOWS * TAB_DIGITS);
+  std::vector<G2Dev> tab((size_t)G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS);
   for (int f = 0; f < 3; f++)
-    for (int w = 0; w < TAB_WINDOWS; w++) {
-      uint32_t d = (sc[8 * f + (w >> 2)] >> ((w & 3) * 8)) & 0xFF;
-      if (d) job_tab_g2((uint32_t)((f * TAB_WINDOWS + w) * TAB_DIGITS + d), b.data(), tab.data());
+    for (int w = 0; w < G2TAB_WINDOWS; w++) {
+      int32_t d = sdigit_at(&sc[8 * f], G2TAB_C, w);
+      if (d)
+        job_tab_g2((uint32_t)((f * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (d < 0 ? -d : d) - 1), b.data(), tab.data());
     }
   G2Job g;
   memset(&g, 0, sizeof(g));
