@@ -449,8 +449,8 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
 
 void PB::transfer(const TransferWit& w, size_t idx) {
   const uint32_t ni = w.n_in, no = w.n_out;
-  uint64_t bound = 1;
-  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;  // parse_pp keeps base^e < 2^64
+  unsigned __int128 bound = 1;  // base^e (2^64 for b = 16, e = 16)
+  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
   std::vector<uint64_t> ov(no);
   bool need_range = !(ni == 1 && no == 1);
   for (uint32_t k = 0; k < no; k++)
@@ -540,7 +540,7 @@ void PB::transfer(const TransferWit& w, size_t idx) {
 
 void PB::issue(const IssueWit& w, size_t idx) {
   const uint32_t n = w.n_out;
-  uint64_t bound = 1;
+  unsigned __int128 bound = 1;
   for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
   std::vector<uint64_t> vv(n);
   for (uint32_t k = 0; k < n; k++)

@@ -79,13 +79,13 @@ def emu_prove(emu, pp_json, ws, issue=False):
         emu.emu_ctx_destroy(ctx)
 
 
-@pytest.mark.parametrize("n_in,n_out", [(2, 2), (1, 1), (1, 2)])
+@pytest.mark.parametrize("n_in,n_out", [(2, 2), (1, 1), (1, 2), (3, 1)])
 def test_emu_transfer_proofs_match_oracle(emu, pp_a, n_in, n_out):
     js, pp = pp_a
     ws = [witness(pp, 10 * n_in + n_out, n_in, n_out)]
-    if n_in != n_out:  # keep the sum balanced: outputs split the input value
-        v = ws[0]["in_values"][0]
-        ws[0]["out_values"] = [v // 3, v - v // 3]
+    if n_in != n_out:  # keep the sum balanced: outputs split the inputs' value
+        v = sum(ws[0]["in_values"]) % (pp.base ** pp.exponent)
+        ws[0]["out_values"] = [v // 3, v - v // 3][:n_out] if n_out == 2 else [v]
         ws[0]["_outs"] = [Z.token_commitment(pp, "ABC", a, b) for a, b in zip(ws[0]["out_values"], ws[0]["out_bfs"])]
         ws[0]["outputs"] = b"".join(C.g1_bytes(p) for p in ws[0]["_outs"])
     got, codes = emu_prove(emu, js, ws)
@@ -176,3 +176,21 @@ def test_gpu_prover_rejects_out_of_range(gctx, pp_a):
     w["out_values"] = [pp.base ** pp.exponent + 1, 0]
     with pytest.raises(zkatdlog.DeviceError, match="outside authorized range"):
         gctx.prove_transfers([w])
+
+
+@pytest.mark.gpu
+def test_gpu_prove_verify_pp_b(golden):
+    """PP-B (b=16, e=16: 16 membership proofs per output): GPU proofs accepted
+    by the GPU verifier, and tampering with one output rejects."""
+    import zkatdlog
+    if "pp_b" not in golden:
+        pytest.skip("no PP-B fixtures")
+    js = golden["pp_b"]["pp"].encode()
+    pp = Z.PublicParams.from_json(js)
+    ws = [witness(pp, 600 + i, 2, 2, bound=1 << 40) for i in range(4)]
+    with zkatdlog.Context(js, device=0) as c:
+        proofs, codes = c.prove_transfers(ws)
+        assert codes == [0] * 4
+        tx = [(w["inputs"], w["outputs"], p) for w, p in zip(ws, proofs)]
+        tx.append((ws[0]["inputs"], ws[1]["outputs"], proofs[0]))
+        assert list(c.verify_transfers(tx)) == [0, 0, 0, 0, A.FTZ_ERR_WF]
