@@ -223,6 +223,21 @@ FTS_HD void g1_to_bytes(uint8_t* out, const g1a& a) {
   limbs_to_be32(out + 32, t);
 }
 
+// gnark RawBytes into global memory (vector stores when 16-byte aligned)
+FTS_HD void g1_to_bytes_g(uint8_t* out, const g1a& a) {
+  uint32_t t[8];
+  if (a.inf) {
+    for (int i = 0; i < 8; i++) t[i] = 0;
+    limbs_to_be32_g(out, t);
+    limbs_to_be32_g(out + 32, t);
+    return;
+  }
+  fe_to_int(t, a.x);
+  limbs_to_be32_g(out, t);
+  fe_to_int(t, a.y);
+  limbs_to_be32_g(out + 32, t);
+}
+
 FTS_HD void g2_to_bytes(uint8_t* out, const g2a& a) {
   if (a.inf) {
     for (int i = 0; i < 128; i++) out[i] = 0;

@@ -345,6 +345,49 @@ FTS_HD void be32_to_limbs(uint32_t out[8], const uint8_t* b) {
   }
 }
 
+// be32_to_limbs / limbs_to_be32 for GLOBAL memory: 16-byte vector accesses
+// when the address is 16-byte aligned (the planners align wire and arena
+// entries), byte accesses otherwise.  (Not for private arrays: taking a vector
+// view of a local array would put it in scratch memory.)
+FTS_HD void be32_to_limbs_g(uint32_t out[8], const uint8_t* b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if ((((uintptr_t)b) & 15) == 0) {
+    uint4 v0 = reinterpret_cast<const uint4*>(b)[0], v1 = reinterpret_cast<const uint4*>(b)[1];
+    out[7] = __builtin_bswap32(v0.x);
+    out[6] = __builtin_bswap32(v0.y);
+    out[5] = __builtin_bswap32(v0.z);
+    out[4] = __builtin_bswap32(v0.w);
+    out[3] = __builtin_bswap32(v1.x);
+    out[2] = __builtin_bswap32(v1.y);
+    out[1] = __builtin_bswap32(v1.z);
+    out[0] = __builtin_bswap32(v1.w);
+    return;
+  }
+#endif
+  be32_to_limbs(out, b);
+}
+
+FTS_HD void limbs_to_be32(uint8_t* b, const uint32_t in[8]);
+FTS_HD void limbs_to_be32_g(uint8_t* b, const uint32_t in[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if ((((uintptr_t)b) & 15) == 0) {
+    uint4 v0, v1;
+    v0.x = __builtin_bswap32(in[7]);
+    v0.y = __builtin_bswap32(in[6]);
+    v0.z = __builtin_bswap32(in[5]);
+    v0.w = __builtin_bswap32(in[4]);
+    v1.x = __builtin_bswap32(in[3]);
+    v1.y = __builtin_bswap32(in[2]);
+    v1.z = __builtin_bswap32(in[1]);
+    v1.w = __builtin_bswap32(in[0]);
+    reinterpret_cast<uint4*>(b)[0] = v0;
+    reinterpret_cast<uint4*>(b)[1] = v1;
+    return;
+  }
+#endif
+  limbs_to_be32(b, in);
+}
+
 FTS_HD void limbs_to_be32(uint8_t* b, const uint32_t in[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) {

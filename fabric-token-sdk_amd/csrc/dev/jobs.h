@@ -267,9 +267,9 @@ FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, u
       a.inf = true;
     } else {
       uint32_t t[8];
-      be32_to_limbs(t, b);
+      be32_to_limbs_g(t, b);
       a.x = fe_from_int<ModP>(t);
-      be32_to_limbs(t, b + 32);
+      be32_to_limbs_g(t, b + 32);
       a.y = fe_from_int<ModP>(t);
       if (is_zero(a.x) && is_zero(a.y)) {
         a.inf = true;
@@ -312,7 +312,7 @@ FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, u
   G1Dev d;
   g1_store(d, a);
   pts[j.out] = d;
-  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, a);
+  if (j.bytes != NONE) g1_to_bytes_g(arena + j.bytes, a);
   if (j.b64 != NONE) {
     uint8_t tmp[64];
     g1_to_bytes(tmp, a);
@@ -630,7 +630,7 @@ FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
 }
 
 FTS_HD void g1_emit_bytes(const G1Job& j, const g1a& r, uint8_t* arena) {
-  if (j.bytes != NONE) g1_to_bytes(arena + j.bytes, r);
+  if (j.bytes != NONE) g1_to_bytes_g(arena + j.bytes, r);
   if (j.b64 != NONE) {
     uint8_t tmp[64];
     g1_to_bytes(tmp, r);

@@ -92,6 +92,7 @@ struct Doc {
       err = true;
       return r;
     }
+    pl->wire.resize((pl->wire.size() + 15) & ~(size_t)15, 0);  // 16-byte aligned element (vector loads)
     r.off = (int64_t)pl->wire.size();
     r.len = (uint32_t)e.raw.size();
     pl->wire.insert(pl->wire.end(), e.raw.begin(), e.raw.end());
@@ -281,6 +282,7 @@ uint32_t Builder::tokens(const uint8_t* p, uint32_t n, uint32_t& bytes_off) {
   bytes_off = arena_alloc(64 * n);
   uint32_t first = pl.n_pts;
   for (uint32_t k = 0; k < n; k++) {
+    pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
     uint32_t raw = (uint32_t)pl.wire.size();
     pl.wire.insert(pl.wire.end(), p + 64 * k, p + 64 * k + 64);
     point(raw, 64, bytes_off + 64 * k, NONE);
@@ -793,7 +795,8 @@ void Builder::issue(const IssueIn& t) {
 
 // Append piece `b` (local indices) to plan `a`, relocating every index.
 void plan_merge(Plan& a, const Plan& b) {
-  a.arena.resize((a.arena.size() + 15) & ~(size_t)15, 0);  // keep the piece's 16-byte alignment
+  a.arena.resize((a.arena.size() + 15) & ~(size_t)15, 0);  // keep the pieces' 16-byte alignment
+  a.wire.resize((a.wire.size() + 15) & ~(size_t)15, 0);
   uint32_t o_wire = (uint32_t)a.wire.size(), o_arena = (uint32_t)a.arena.size();
   uint32_t o_pts = a.n_pts, o_scal = a.n_scal, o_g1 = a.n_g1out, o_g2 = a.n_g2out;
   uint32_t o_list = (uint32_t)a.sclist.size(), o_vt = (uint32_t)a.vt.size(), o_seg = (uint32_t)a.seg.size();

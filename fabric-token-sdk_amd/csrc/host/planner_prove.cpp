@@ -107,6 +107,7 @@ struct PB {
   // 32-byte big-endian scalar from the wire (mod r)
   uint32_t zr32(const uint8_t* b) {
     ZrJob j;
+    pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
     j.raw = (uint32_t)pl.wire.size();
     pl.wire.insert(pl.wire.end(), b, b + 32);
     j.len = 32;
@@ -161,6 +162,7 @@ struct PB {
   }
   uint32_t point(const uint8_t* raw, uint32_t len, uint32_t bytes) {
     DecodeJob j;
+    pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
     j.raw = (uint32_t)pl.wire.size();
     pl.wire.insert(pl.wire.end(), raw, raw + len);
     j.len = len;
