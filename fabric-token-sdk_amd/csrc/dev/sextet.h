@@ -285,13 +285,19 @@ FTS_HD fp2 sx_inv(X x, fp2 f) {
 // a^x (x = BN parameter, NAF), a in the cyclotomic subgroup (f12_expt)
 template <class X>
 FTS_HD fp2 sx_expt(X x, fp2 a) {
+  // a (and xi a) published once for all NAF multiplications; a digit -1
+  // multiplies by conj(a) = a^-1 through r conj(a) = conj(conj(r) a)
+  sx_pub(x, SX_B, a);
   fp2 r = a;
-  fp2 ai = sx_conj(x.k, a);
 #pragma nounroll
   for (int i = 61; i >= 0; i--) {
     r = sx_cyc_sqr(x, r);
     bool pos = (BN_X_NAF_POS >> i) & 1, neg = (BN_X_NAF_NEG >> i) & 1;
-    if (pos || neg) r = sx_mulv(x, r, f2_sel(pos, a, ai));
+    if (pos || neg) {
+      fp2 t = neg ? sx_conj(x.k, r) : r;
+      t = sx_mul(x, t);
+      r = neg ? sx_conj(x.k, t) : t;
+    }
   }
   return r;
 }
