@@ -209,12 +209,20 @@ FTS_HD Fe<M> fe_dbl(const Fe<M>& a) {
 }
 
 #include "fp_fips.h"
+#ifndef FTS_ONEASM
+#define FTS_ONEASM 1  // device: whole limb products as one asm statement (gen_oneasm.py)
+#endif
+#include "fp_oneasm.h"
 
 #if defined(__HIP_DEVICE_COMPILE__)
 template <class M>
 __device__ __forceinline__ Fe<M> mont_mul_fips(const Fe<M>& a, const Fe<M>& b) {
   Fe<M> x, y;
+#if FTS_ONEASM
+  mont_mul_oneasm<M>(x.v, a.v, b.v);
+#else
   mont_mul_fips_limbs<M>(x.v, a.v, b.v);
+#endif
 #if FTS_ASM_CHAINS
   condsub_asm<M>(x.v);
   (void)y;

@@ -22,7 +22,9 @@ namespace fts {
 
 // r[16] = a[8] * b[8]
 FTS_HD void mul_wide(uint32_t r[16], const uint32_t a[8], const uint32_t b[8]) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ONEASM
+  mul_wide_oneasm(r, a, b);
+#elif defined(__HIP_DEVICE_COMPILE__)
   mul_wide_asm(r, a, b);
 #else
   uint64_t acc = 0;
@@ -48,7 +50,9 @@ FTS_HD void mul_wide(uint32_t r[16], const uint32_t a[8], const uint32_t b[8]) {
 FTS_HD fp redc_wide(const uint32_t t[16]) {
   FTS_COUNT_MAD(72);
   fp r;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && FTS_ONEASM
+  redc_wide_oneasm<ModP>(r.v, t);
+#elif defined(__HIP_DEVICE_COMPILE__)
   redc_wide_asm(r.v, t);
 #else
   uint64_t acc = 0;

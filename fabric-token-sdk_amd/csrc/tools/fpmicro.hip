@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../dev/fp.h"
+#include "../dev/fp_wide.h"
 
 using namespace fts;
 
@@ -20,6 +20,10 @@ __global__ void __launch_bounds__(256) k_fpmicro(fp* io, int iters) {
     for (int c = 0; c < CH; c++) {
       if (IMPL == 0) {
         x[c] = mont_mul_cios(x[c], y);
+      } else if (IMPL == 2) {
+        uint32_t t[16];
+        mul_wide(t, x[c].v, y.v);
+        x[c] = redc_wide(t);
       } else {
 #if defined(__HIP_DEVICE_COMPILE__)
         x[c] = mont_mul_fips(x[c], y);
@@ -60,7 +64,7 @@ extern "C" double ftz_fpmicro(int device, int impl, int chains, int total_waves,
   (void)hipMemset(io, 1, n * sizeof(fp));
   float ms = -1;
 #define R(I, C) if (impl == I && chains == C) ms = run<I, C>(io, blocks, threads, iters);
-  R(0, 1) R(0, 2) R(0, 4) R(1, 1) R(1, 2) R(1, 4)
+  R(0, 1) R(0, 2) R(0, 4) R(1, 1) R(1, 2) R(1, 4) R(2, 1) R(2, 2) R(2, 4)
 #undef R
   (void)hipFree(io);
   return (double)threads * blocks * chains * (double)iters / (ms * 1e-3);
