@@ -62,6 +62,7 @@ enum : int {
   SX_A = 0,    // a_0..a_5   (published operand)
   SX_AX = 6,   // xi * a_0..a_5
   SX_P = 12,   // per-lane products
+  SX_A2 = 12,  // 2 a_0..2 a_5 (sx_sqr only; aliases SX_P)
   SX_B = 18,   // b_0..b_5   (second operand of full products; final exponentiation)
   SX_BX = 24,  // xi * b_0..b_5
   SX_SLOTS_FEXP = 30,
@@ -160,29 +161,39 @@ FTS_HD fp2 sx_mulv(const X& x, const fp2& a, const fp2& b) {
   return sx_mul(x, a);
 }
 
-// c = a^2: lane k sums a_i a_j over i + j = k (mod 6), i <= j, doubled for i < j.
+// c = a^2.  Term macros shared with the cyclotomic table below.
 #define SQ_(i, j, wrap, dbl) SX_T(SX_A + (i), ((wrap) ? SX_AX : SX_A) + (j), (dbl) ? TM_DBL : 0)
 #define SQZ SX_T(0, 0, TM_ZERO)
-static constexpr TermRow SX_SQR_TAB[4] = {
-    term_row(SQ_(0, 0, 0, 0), SQ_(0, 1, 0, 1), SQ_(1, 1, 0, 0), SQ_(0, 3, 0, 1), SQ_(2, 2, 0, 0), SQ_(0, 5, 0, 1)),
-    term_row(SQ_(3, 3, 1, 0), SQ_(2, 5, 1, 1), SQ_(4, 4, 1, 0), SQ_(1, 2, 0, 1), SQ_(5, 5, 1, 0), SQ_(1, 4, 0, 1)),
-    term_row(SQ_(1, 5, 1, 1), SQ_(3, 4, 1, 1), SQ_(0, 2, 0, 1), SQ_(4, 5, 1, 1), SQ_(0, 4, 0, 1), SQ_(2, 3, 0, 1)),
-    term_row(SQ_(2, 4, 1, 1), SQZ, SQ_(3, 5, 1, 1), SQZ, SQ_(1, 3, 0, 1), SQZ),
-};
 
-// (The symmetric 4-term form above is kept as a table for reference; the
-// 6-term schoolbook loop runs faster on the device: no per-term selects.)
+// Symmetric form with the doubled coefficients published (SX_A2): lane k
+// sums a_i a_j over i + j = k (mod 6), i <= j, taking 2 a_i from SX_A2 for
+// i < j and xi a_j from SX_AX for wrapped terms: 4 products on even lanes, 3
+// (+ one zeroed) on odd lanes, no per-term selects but the last.
+#define S4_(i, j) SX_T(i, j, 0)
+static constexpr TermRow SX_SQR4_TAB[4] = {
+    term_row(S4_(SX_A + 0, SX_A + 0), S4_(SX_A2 + 0, SX_A + 1), S4_(SX_A + 1, SX_A + 1), S4_(SX_A2 + 0, SX_A + 3),
+             S4_(SX_A + 2, SX_A + 2), S4_(SX_A2 + 0, SX_A + 5)),
+    term_row(S4_(SX_A + 3, SX_AX + 3), S4_(SX_A2 + 2, SX_AX + 5), S4_(SX_A2 + 0, SX_A + 2), S4_(SX_A2 + 1, SX_A + 2),
+             S4_(SX_A2 + 0, SX_A + 4), S4_(SX_A2 + 1, SX_A + 4)),
+    term_row(S4_(SX_A2 + 1, SX_AX + 5), S4_(SX_A2 + 3, SX_AX + 4), S4_(SX_A + 4, SX_AX + 4), S4_(SX_A2 + 4, SX_AX + 5),
+             S4_(SX_A2 + 1, SX_A + 3), S4_(SX_A2 + 2, SX_A + 3)),
+    term_row(S4_(SX_A2 + 2, SX_AX + 4), SX_T(0, 0, TM_ZERO), S4_(SX_A2 + 3, SX_AX + 5), SX_T(0, 0, TM_ZERO),
+             S4_(SX_A + 5, SX_AX + 5), SX_T(0, 0, TM_ZERO)),
+};
+#undef S4_
 template <class X>
 FTS_HD fp2 sx_sqr(X x, fp2 a) {
   sx_pub(x, SX_A, a);
+  x.put(SX_A2 + x.k, f2_dbl(a));
   x.sync();
   Wide2 w;
   w2_init(w);
 #pragma nounroll
-  for (int i = 0; i < 6; i++) {
-    int j = x.k - i;
-    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
-    w2_mac(w, x.get(SX_A + i), x.get(sb));
+  for (int t = 0; t < 4; t++) {
+    uint32_t e = term_at(SX_SQR4_TAB[t], x.k);
+    fp2 u = x.get(e & 63);
+    fp2 v = x.get((e >> 6) & 63);
+    w2_mac(w, f2_sel((e & TM_ZERO) != 0, f2_zero(), u), v);
   }
   x.sync();
   return w2_reduce(w);

@@ -9,6 +9,28 @@ back, the same form as the FIPS multiplier's v_mad -> v_addc carries.  Modulus
 limbs are VOP2 literal operands (v_subrev / v_subbrev / v_addc with a literal
 src0), so the statements need no SGPRs."""
 import os
+import re
+
+# Carry flag of the chains: "vcc" (VOP2 _e32 encodings) or "sgpr" (an SGPR pair
+# output operand, VOP3 _e64 encodings).
+CARRY = os.environ.get("FTS_FPASM_CARRY", "vcc")  # sgpr measured neutral (393k vs 399k)
+
+
+def sgpr_carry(body, names=("cy",), first_in=16):
+    """Rewrite a vcc chain to use %[cy] (and %[cy2] after a marker).  The carry
+    pairs are extra output operands, so input operands >= first_in move up."""
+    body = [re.sub(r"%(\d+)", lambda g: "%%%d" % (int(g.group(1)) + (int(g.group(1)) >= first_in)), l) for l in body]
+    out, cur = [], names[0]
+    for line in body:
+        if line == "@SWITCH@":
+            cur = names[1]
+            continue
+        if line.startswith("s_mov_b64 %[bw], vcc"):
+            continue
+        line = line.replace("_e32", "_e64")
+        line = re.sub(r"\bvcc\b", "%%[%s]" % cur, line)
+        out.append(line)
+    return out
 
 P = 21888242871839275222246405745257275088696311157297823662689037894645226208583
 R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -39,7 +61,7 @@ def fn_submod(name, m):
     body += ["v_subb_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (8 + i, 17 + i, 25 + i) for i in range(1, 8)]
     # keep the borrow mask: t = d + m does not touch it if computed with the
     # carry in an SGPR pair; here: save vcc, add, restore by re-deriving
-    body += ["s_mov_b64 %[bw], vcc"]
+    body += ["s_mov_b64 %[bw], vcc", "@SWITCH@"]
     body += ["v_add_co_u32_e32 %0, vcc, %8, %33"]
     body += ["v_addc_co_u32_e32 %%%d, vcc, %%%d, %%%d, vcc" % (i, 8 + i, 33 + i) for i in range(1, 8)]
     body += ["v_cndmask_b32_e64 %%%d, %%%d, %%%d, %%[bw]" % (i, 8 + i, i) for i in range(8)]
@@ -48,19 +70,31 @@ def fn_submod(name, m):
 
 def emit(name, body, x, y, extra_sgpr=False, mod=None):
     outs = ", ".join(['"=&v"(r[%d])' % i for i in range(8)] + ['"=&v"(t[%d])' % i for i in range(8)])
-    if extra_sgpr:
-        outs += ', [bw] "=&s"(bw)'
+    decl = []
+    if CARRY == "sgpr":
+        # submod: cy takes bw's place (operand 16) and cy2 is operand 17
+        body = [l.replace("%[bw]", "%[cy]") for l in sgpr_carry(body, ("cy", "cy2"), 17 if extra_sgpr else 16)]
+        outs += ', [cy] "=&s"(cy)'
+        decl.append("  uint64_t cy;")
+        if extra_sgpr:
+            outs += ', [cy2] "=&s"(cy2)'
+            decl.append("  uint64_t cy2;")
+        clob = ""
+    else:
+        body = [l for l in body if l != "@SWITCH@"]
+        if extra_sgpr:
+            outs += ', [bw] "=&s"(bw)'
+            decl.append("  uint64_t bw;")
+        clob = '\n               : "vcc"'
     ins = ", ".join(['"v"(%s[%d])' % (x, i) for i in range(8)] + ['"v"(%s[%d])' % (y, i) for i in range(8)] +
                     ['"v"(0x%08xu)' % v for v in limbs(mod)])
     s = []
     s.append("__device__ __forceinline__ void %s(uint32_t r[8], const uint32_t a[8], const uint32_t b[8]) {" % name)
     s.append("  uint32_t t[8];")
-    if extra_sgpr:
-        s.append("  uint64_t bw;")
+    s += decl
     s.append("  asm(\"%s\"" % "\\n\\t".join(body))
     s.append("               : %s" % outs)
-    s.append("               : %s" % ins)
-    s.append("               : \"vcc\");")
+    s.append("               : %s%s);" % (ins, clob))
     s.append("}")
     return "\n".join(s)
 
@@ -74,11 +108,16 @@ def fn_condsub(name, m, twice=False):
         body += ["v_cndmask_b32_e32 %%%d, %%%d, %%%d, vcc" % (i, 8 + i, i) for i in range(8)]
         out.append((body, limbs(mm)))
     s = ["__device__ __forceinline__ void %s(uint32_t x[8]) {" % name, "  uint32_t t[8];"]
+    if CARRY == "sgpr":
+        s.append("  uint64_t cy;")
     for body, L in out:
+        sg = CARRY == "sgpr"
+        if sg:
+            body = sgpr_carry(body)
         s.append('  asm("%s"' % "\\n\\t".join(body))
-        s.append("      : %s" % ", ".join(['"+v"(x[%d])' % i for i in range(8)] + ['"=&v"(t[%d])' % i for i in range(8)]))
-        s.append("      : %s" % ", ".join('"v"(0x%08xu)' % v for v in L))
-        s.append('      : "vcc");')
+        s.append("      : %s" % ", ".join(['"+v"(x[%d])' % i for i in range(8)] + ['"=&v"(t[%d])' % i for i in range(8)]
+                                         + (['[cy] "=&s"(cy)'] if sg else [])))
+        s.append("      : %s%s);" % (", ".join('"v"(0x%08xu)' % v for v in L), "" if sg else ': "vcc"'))
     s.append("}")
     return "\n".join(s)
 
@@ -89,10 +128,13 @@ def fn_acc16(name, op):
     body = ["%s %%0, vcc, %%0, %%16" % first]
     body += ["%s %%%d, vcc, %%%d, %%%d, vcc" % (rest, i, i, 16 + i) for i in range(1, 16)]
     s = ["__device__ __forceinline__ void %s(uint32_t r[16], const uint32_t a[16]) {" % name]
+    sg = CARRY == "sgpr"
+    if sg:
+        body = sgpr_carry(body)
+        s.append("  uint64_t cy;")
     s.append("  asm(\"%s\"" % "\\n\\t".join(body))
-    s.append("               : %s" % ", ".join('"+v"(r[%d])' % i for i in range(16)))
-    s.append("               : %s" % ", ".join('"v"(a[%d])' % i for i in range(16)))
-    s.append("               : \"vcc\");")
+    s.append("               : %s" % ", ".join(['"+v"(r[%d])' % i for i in range(16)] + (['[cy] "=&s"(cy)'] if sg else [])))
+    s.append("               : %s%s);" % (", ".join('"v"(a[%d])' % i for i in range(16)), "" if sg else ' : "vcc"'))
     s.append("}")
     return "\n".join(s)
 
