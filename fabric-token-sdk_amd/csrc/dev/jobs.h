@@ -629,6 +629,117 @@ FTS_HD g1j g1_mul_glv(const g1a& p, const uint32_t k[8]) {
   return acc;
 }
 
+// Radix-16 Booth digit i of a 128-bit scalar: bits 4i-1 .. 4i+3 (bit -1 and
+// bits >= 128 read as 0) give d = b(4i-1) + b(4i) + 2 b(4i+1) + 4 b(4i+2) - 8 b(4i+3)
+// in [-8, 8]; k = sum_{i=0..32} d_i 16^i.  Limb selects instead of a
+// dynamically indexed array (which would live in scratch memory).
+FTS_HD int booth16(const uint32_t k[4], int i) {
+  int pos = 4 * i - 1;
+  uint32_t v;
+  if (pos < 0) {
+    v = (k[0] << 1) & 31u;
+  } else {
+    int l = pos >> 5, o = pos & 31;
+    uint32_t lo = l == 0 ? k[0] : (l == 1 ? k[1] : (l == 2 ? k[2] : (l == 3 ? k[3] : 0u)));
+    uint32_t hi = l == 0 ? k[1] : (l == 1 ? k[2] : (l == 2 ? k[3] : 0u));
+    v = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> o) & 31u;
+  }
+  return (int)(v & 1u) + (int)((v >> 1) & 7u) - 8 * (int)(v >> 4);
+}
+
+// k P with 4-bit signed windows over the two GLV halves: 33 windows of four
+// doublings and two mixed additions with (|d| P1) and phi(|d| P1) from an
+// 8-entry table -- 128 doublings + 66 additions instead of 128 + 128
+// (g1_mul_glv).  The table 1..8 P1 is built in Jacobian coordinates and brought
+// to ONE common Z = Zc without an inversion: entry e becomes the affine point
+// (X_e s_e^2, Y_e s_e^3), s_e = Zc / Z_e, of the isomorphic curve
+// y^2 = x^3 + b Zc^6 (the a = 0 doubling and mixed-addition formulas do not
+// involve b), and the result (X:Y:Z) there is (X:Y:Z Zc) on E.
+FTS_HD void g1dev_put(G1Dev& d, const fp& a, const fp& b) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    d.x[q] = a.v[q];
+    d.y[q] = b.v[q];
+  }
+}
+FTS_HD void g1dev_get(const G1Dev& d, fp& a, fp& b) {
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    a.v[q] = d.x[q];
+    b.v[q] = d.y[q];
+  }
+}
+// tb: 16 G1Dev entries at stride st (device: a per-batch buffer laid out
+// [entry][job] so that a wave's accesses coalesce; host: a local array).
+// Entries 0..7 hold the table, 8..15 the (Z, prefix) pairs while it is built.
+FTS_HD g1j g1_mul_glv16(const g1a& p, const uint32_t k[8], G1Dev* tb, size_t st) {
+  g1j acc = jac_inf<fp>();
+  if (p.inf) return acc;
+  uint32_t k1[4], k2[4];
+  bool n1, n2;
+  glv_split(k, k1, n1, k2, n2);
+  g1a P1 = n1 ? aff_neg(p) : p;
+  g1j T = jac_from_aff(P1);
+  fp pre = fe_one<ModP>();
+#pragma nounroll
+  for (int e = 0; e < 8; e++) {
+    if (e == 1) T = jac_dbl(T);
+    if (e >= 2) T = jac_add_aff(T, P1);
+    g1dev_put(tb[e * st], T.x, T.y);
+    g1dev_put(tb[(8 + e) * st], T.z, pre);
+    pre = pre * T.z;
+  }
+  const fp Zc = pre;
+  fp suf = fe_one<ModP>();
+#pragma nounroll
+  for (int e = 7; e >= 0; e--) {
+    fp X, Y, Z, pe;
+    g1dev_get(tb[e * st], X, Y);
+    g1dev_get(tb[(8 + e) * st], Z, pe);
+    fp se = pe * suf;
+    fp s2 = sqr(se);
+    suf = suf * Z;
+    g1dev_put(tb[e * st], X * s2, Y * (s2 * se));
+  }
+  const bool flip = n1 != n2;  // phi(e P1) = +-phi(e p): sign of the second half
+  const fp beta = fe_const<ModP>(GLV_BETA);
+#pragma nounroll
+  for (int i = 32; i >= 0; i--) {
+    int d1 = booth16(k1, i), d2 = booth16(k2, i);
+    int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
+    fp x1, y1, x2, y2;
+    g1dev_get(tb[(size_t)(m1 ? m1 - 1 : 0) * st], x1, y1);
+    g1dev_get(tb[(size_t)(m2 ? m2 - 1 : 0) * st], x2, y2);
+    if (i != 32) {
+      acc = jac_dbl(acc);
+      acc = jac_dbl(acc);
+      acc = jac_dbl(acc);
+      acc = jac_dbl(acc);
+    }
+    g1a A;
+    A.x = x1;
+    A.y = (d1 < 0) ? fe_neg(y1) : y1;
+    A.inf = false;
+    g1j nacc = jac_add_aff(acc, A);
+    if (m1) acc = nacc;
+    A.x = x2 * beta;
+    A.y = ((d2 < 0) != flip) ? fe_neg(y2) : y2;
+    nacc = jac_add_aff(acc, A);
+    if (m2) acc = nacc;
+  }
+  acc.z = acc.z * Zc;  // back to E (the point at infinity keeps z = 0)
+  return acc;
+}
+
+#ifndef FTS_G1_VAR_W
+#define FTS_G1_VAR_W 16  // 16: g1_mul_glv16 (signed 4-bit windows), 2: g1_mul_glv (joint binary)
+#endif
+#if FTS_G1_VAR_W == 16
+#define G1_MUL_VAR(P, K, TB, ST) g1_mul_glv16(P, K, TB, ST)
+#else
+#define G1_MUL_VAR(P, K, TB, ST) g1_mul_glv(P, K)
+#endif
+
 FTS_HD void g1_emit_bytes(const G1Job& j, const g1a& r, uint8_t* arena) {
   if (j.bytes != NONE) g1_to_bytes_g(arena + j.bytes, r);
   if (j.b64 != NONE) {
@@ -661,7 +772,8 @@ FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const 
       Va = jac_to_aff(V);
     }
     if (j.vneg) Va = aff_neg(Va);
-    acc = g1_mul_glv(Va, scal[j.vscal]);
+    G1Dev loc[16];
+    acc = G1_MUL_VAR(Va, scal[j.vscal], loc, 1);
   }
   for (int f = 0; f < j.nfix; f++) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
   g1a r = jac_to_aff(acc);
@@ -696,8 +808,10 @@ FTS_HD g1j g1j_load(const G1JDev& d) {
   return p;
 }
 
+// vtab: per-batch scratch of 16 n G1Dev entries for the variable parts'
+// window tables (device); the host emulation passes nullptr (local table).
 FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* vterms, const G1Dev* pts,
-                        const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part) {
+                        const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part, G1Dev* vtab) {
   uint32_t f = i / n, jb = i - f * n;
   const G1Job& j = jobs[jb];
   g1j acc = jac_inf<fp>();
@@ -723,7 +837,12 @@ FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* 
       Va = jac_to_aff(V);
     }
     if (j.vneg) Va = aff_neg(Va);
-    acc = g1_mul_glv(Va, scal[j.vscal]);
+#if defined(__HIP_DEVICE_COMPILE__)
+    acc = G1_MUL_VAR(Va, scal[j.vscal], vtab + jb, n);
+#else
+    G1Dev loc[16];
+    acc = G1_MUL_VAR(Va, scal[j.vscal], vtab ? vtab + jb : loc, vtab ? n : 1);
+#endif
   }
   g1j_store(part[i], acc);
 }

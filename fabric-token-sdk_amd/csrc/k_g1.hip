@@ -20,10 +20,11 @@ __global__ void __launch_bounds__(128) k_g1(const G1Job* jobs, uint32_t n, const
 // Uniform parts of the G1 jobs (fixed-base slots and GLV variable parts), one
 // lane per part: lanes [f n, (f+1) n) all run the same code path.
 __global__ void __launch_bounds__(128) k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
-                                                 const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part) {
+                                                 const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part,
+                                                 G1Dev* vtab) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 4 * n) return;
-  job_g1_part(jobs, n, i, vt, pts, scal, tab, part);
+  job_g1_part(jobs, n, i, vt, pts, scal, tab, part, vtab);
 }
 
 // Block-wide Montgomery batch inversion: thread t holds x_t (zero -> treated

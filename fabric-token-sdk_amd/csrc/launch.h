@@ -46,7 +46,7 @@ __global__ void k_pp_decode(const uint8_t* raw, const uint32_t* g1off, uint32_t 
 __global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts, const uint32_t (*scal)[8],
                      const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
 __global__ void k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
-                          const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part);
+                          const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part, G1Dev* vtab);
 __global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena);
 __global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
 __global__ void k_tab_g1_bw(const G1Dev* bases, G1Dev* bw);

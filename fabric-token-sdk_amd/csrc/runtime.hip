@@ -56,6 +56,7 @@ struct ftz_batch {
   DBuf<F12Dev> fbuf;
   DBuf<EvLineDev> lines2;  // pair-2 Miller lines, [line][pair job]
   DBuf<G1JDev> part1, part1p;  // G1 job parts (4 per job) of the side / pairing G1 jobs
+  DBuf<G1Dev> vtab1, vtab1p;   // window tables of their variable parts (16 entries per job)
   DBuf<int32_t> codes;
   DBuf<uint32_t> bitmap;
   // prover
@@ -298,6 +299,8 @@ static int batch_upload(ftz_batch* b) {
   HC(b->lines2.alloc(std::max<size_t>(p.pr.size(), 1) * MILLER_LINES));
   HC(b->part1.alloc(4 * std::max<size_t>(p.g1.size(), 1)));
   HC(b->part1p.alloc(4 * std::max<size_t>(p.g1p.size(), 1)));
+  HC(b->vtab1.alloc(16 * std::max<size_t>(p.g1.size(), 1)));
+  HC(b->vtab1p.alloc(16 * std::max<size_t>(p.g1p.size(), 1)));
   if (p.g2.size() != p.pr.size()) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   for (size_t i = 0; i < p.pr.size(); i++)
     if (p.pr[i].q2 != p.g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
@@ -409,23 +412,27 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
     k_g2lines<<<blocks_for(n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p, b->g2out.p, b->pts.p,
                                                    b->lines2.p);
   HC(hipEventRecord(e[15], s3));
-  // stream2: pairing-independent G1 jobs
-  HC(hipStreamWaitEvent(s2, e[4], 0));
-  HC(hipEventRecord(e[11], s2));
-  if (n_g1) {
-    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1.p);
-    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
-  }
-  HC(hipEventRecord(e[12], s2));
   // main stream: pairing chain
   HC(hipEventRecord(e[16], s));
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1p.p);
+                                                         b->part1p.p, b->vtab1p.p);
     k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[5], s));
+  // stream2: pairing-independent G1 jobs, started after the jobs the pairing
+  // chain waits for (FTZ_G1_AFTER: 0 with them, 1 after the pairing G1 jobs,
+  // 2 after the G2 jobs and lines)
+  const char* ga = getenv("FTZ_G1_AFTER");
+  const int g1_after = ga ? atoi(ga) : 0;
+  HC(hipStreamWaitEvent(s2, g1_after == 1 ? e[5] : (g1_after == 2 ? e[15] : e[4]), 0));
+  HC(hipEventRecord(e[11], s2));
+  if (n_g1) {
+    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
+                                                         b->part1.p, b->vtab1.p);
+    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+  }
+  HC(hipEventRecord(e[12], s2));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (n_pr)
@@ -607,7 +614,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   HC(hipEventRecord(e[11], s2));
   if (n_g1) {
     k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1.p);
+                                                         b->part1.p, b->vtab1.p);
     k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[12], s2));
@@ -615,7 +622,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   HC(hipEventRecord(e[16], s));
   if (n_g1p) {
     k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1p.p);
+                                                         b->part1p.p, b->vtab1p.p);
     k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
   }
   HC(hipEventRecord(e[5], s));

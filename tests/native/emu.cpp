@@ -5,6 +5,7 @@
 #include <string.h>
 #include "../../fabric-token-sdk_amd/csrc/dev/pairing.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sha256.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 
 using namespace fts;
 
@@ -64,6 +65,16 @@ int emu_g1_mul(const uint8_t* p64, const uint8_t* k32, uint8_t* out64) {
   uint32_t k[8];
   be32_to_limbs(k, k32);
   g1a r = jac_to_aff(aff_mul(ld_g1(p64), k));
+  g1_to_bytes(out64, r);
+  return g1_on_curve(r) ? 0 : 1;
+}
+// GLV variable-base multiplications of the G1 jobs (k < r): 0 joint binary, 1 signed 4-bit windows
+int emu_g1_mul_glv(const uint8_t* p64, const uint8_t* k32, int which, uint8_t* out64) {
+  uint32_t k[8];
+  be32_to_limbs(k, k32);
+  g1a p = ld_g1(p64);
+  G1Dev tb[16];
+  g1a r = jac_to_aff(which ? g1_mul_glv16(p, k, tb, 1) : g1_mul_glv(p, k));
   g1_to_bytes(out64, r);
   return g1_on_curve(r) ? 0 : 1;
 }

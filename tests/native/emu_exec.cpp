@@ -128,8 +128,9 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   {
     uint32_t n1 = (uint32_t)p.g1.size();
     std::vector<G1JDev> part(4 * (size_t)std::max<uint32_t>(n1, 1));
+    std::vector<G1Dev> vtab(16 * (size_t)std::max<uint32_t>(n1, 1));  // the device's strided table layout
     par_for(4 * n1, [&](uint32_t i) {
-      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data());
+      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data(), vtab.data());
     });
     par_for(n1, [&](uint32_t i) { job_g1_combine(p.g1[i], i, n1, part.data(), g1out.data(), p.arena.data()); });
   }
@@ -220,7 +221,7 @@ static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t ca
     uint32_t n1 = (uint32_t)p.g1.size();
     std::vector<G1JDev> part(4 * (size_t)std::max<uint32_t>(n1, 1));
     par_for(4 * n1, [&](uint32_t i) {
-      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data());
+      job_g1_part(p.g1.data(), n1, i, p.vt.data(), pts.data(), scal, c->g1tab.data(), part.data(), nullptr);
     });
     par_for(n1, [&](uint32_t i) { job_g1_combine(p.g1[i], i, n1, part.data(), g1out.data(), p.arena.data()); });
   }

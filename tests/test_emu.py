@@ -116,3 +116,20 @@ def test_pipeline_golden_pp_b(emu, golden):
     cases = golden["pp_b"]["cases"]
     got = _run(emu, golden["pp_b"]["pp"].encode(), cases)
     assert got == {c["name"]: c["expect"] for c in cases}
+
+
+def test_g1_mul_glv_variants(emu):
+    """Both GLV variable-base multiplications of the G1 jobs (dev/jobs.h:
+    g1_mul_glv, g1_mul_glv16) against the oracle, edge scalars included."""
+    rng = random.Random(11)
+    lam = next(w for w in (pow(g, (C.R - 1) // 3, C.R) for g in range(2, 50)) if w != 1)  # a cube root of unity
+    ks = [0, 1, 2, 3, 15, 16, 17, C.R - 1, C.R - 2, lam, C.R - lam, (1 << 127) - 1, 1 << 127, (1 << 128) + 5,
+          8 * sum(16 ** i for i in range(32))]
+    ks += [rng.randrange(C.R) for _ in range(24)]
+    for n, k in enumerate(ks):
+        P = C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)) if n % 3 else C.G1_GEN
+        want = C.g1_bytes(C.g1_mul(P, k % C.R))
+        for which in (0, 1):
+            o = buf(64)
+            assert emu.emu_g1_mul_glv(C.g1_bytes(P), (k % C.R).to_bytes(32, "big"), which, o) == 0
+            assert o.raw == want, (k, which)
