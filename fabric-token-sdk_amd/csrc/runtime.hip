@@ -68,7 +68,24 @@ struct ftz_batch {
   hipEvent_t ev[20];
   bool ev_init = false;
   ftz_stats stats;
+  // the batch's own streams (pairing chain, side G1 jobs, G2 jobs + lines), so
+  // that several batches can be in flight at once (ftz_batch_submit)
+  hipStream_t st[3] = {nullptr, nullptr, nullptr};
+  bool pending = false;
+  uint64_t jobs_last[FTZ_NKERNELS] = {};
 };
+
+// Same priorities as the context streams: the pairing chain high, the side G1
+// jobs low.
+static int batch_streams(ftz_batch* b) {
+  if (b->st[0]) return FTZ_SUCCESS;
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  HC(hipStreamCreateWithPriority(&b->st[0], hipStreamNonBlocking, prio_hi));
+  HC(hipStreamCreateWithPriority(&b->st[1], hipStreamNonBlocking, prio_lo));
+  HC(hipStreamCreateWithPriority(&b->st[2], hipStreamNonBlocking, prio_hi));
+  return FTZ_SUCCESS;
+}
 
 static int blocks_for(uint32_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
@@ -269,7 +286,9 @@ extern "C" int ftz_ctx_info(const ftz_ctx* c, uint32_t* base, uint32_t* exponent
 static int batch_upload(ftz_batch* b) {
   ftz_ctx* c = b->ctx;
   Plan& p = b->plan;
-  hipStream_t s = c->stream;
+  int rc = batch_streams(b);
+  if (rc != FTZ_SUCCESS) return rc;
+  hipStream_t s = b->st[0];
   memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
   std::vector<uint8_t> wire = p.wire;
   wire.resize(wire.size() + 64, 0);  // decode jobs may look at 64 bytes past a short element
@@ -375,23 +394,27 @@ extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, 
 //   stream2: the G1 jobs no pairing depends on (well-formedness, range
 //            equality, membership Schnorr commitments)
 // The transcript hashes wait for all three.
-extern "C" int ftz_batch_run(ftz_batch* b) {
+extern "C" int ftz_batch_submit(ftz_batch* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null batch");
   ftz_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
-  hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
+  hipStream_t s = b->st[0], s2 = b->st[1], s3 = b->st[2];
   // FTZ_SERIAL=1: run every kernel on one stream (per-kernel timings without
   // overlap, for profiling)
   const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
-  if (serial) s2 = s3 = s;
+  // FTZ_BATCH_STREAMS=1: the whole batch on its pairing-chain stream (several
+  // batches in flight then overlap each other instead)
+  const bool one = getenv("FTZ_BATCH_STREAMS") && getenv("FTZ_BATCH_STREAMS")[0] == '1';
+  if (serial || one) s2 = s3 = s;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
   uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
   uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
   uint32_t n_pr = (uint32_t)p.pr.size();
   uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
-  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1, n_hm, n_tx, n_tx};
+  const uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1, n_hm, n_tx, n_tx};
+  for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
   HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
   HC(hipEventRecord(e[0], s));
@@ -452,7 +475,18 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
                                                     b->bitmap.p);
   HC(hipEventRecord(e[13], s));
   HC(hipGetLastError());
-  HC(hipStreamSynchronize(s));
+  b->pending = true;
+  return FTZ_SUCCESS;
+}
+
+// Wait for the batch's last submission and collect its per-kernel timings.
+extern "C" int ftz_batch_wait(ftz_batch* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+  if (!b->pending) return FTZ_SUCCESS;
+  HC(hipSetDevice(b->ctx->device));
+  HC(hipStreamSynchronize(b->st[0]));
+  b->pending = false;
+  hipEvent_t* e = b->ev;
   // stats order: decode zr hash_pre scalar g1p g2+lines miller fexp g1(side) hash verdict total
   const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
   const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
@@ -460,13 +494,22 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
     float ms = 0;
     HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
     b->stats.ms[k] = ms;
-    b->stats.jobs[k] = jobs[k];
+    b->stats.jobs[k] = b->jobs_last[k];
   }
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_batch_run(ftz_batch* b) {
+  int rc = ftz_batch_submit(b);
+  return rc == FTZ_SUCCESS ? ftz_batch_wait(b) : rc;
+}
+
 extern "C" int ftz_batch_codes(ftz_batch* b, int32_t* codes) {
   if (!b || (b->n && !codes)) return set_err(FTZ_E_INVALID, "null argument");
+  if (b->pending) {
+    int rc = ftz_batch_wait(b);
+    if (rc != FTZ_SUCCESS) return rc;
+  }
   HC(hipSetDevice(b->ctx->device));
   if (b->n) HC(hipMemcpy(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return FTZ_SUCCESS;
@@ -474,6 +517,10 @@ extern "C" int ftz_batch_codes(ftz_batch* b, int32_t* codes) {
 
 extern "C" int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits) {
   if (!b || (b->n && !bits)) return set_err(FTZ_E_INVALID, "null argument");
+  if (b->pending) {
+    int rc = ftz_batch_wait(b);
+    if (rc != FTZ_SUCCESS) return rc;
+  }
   HC(hipSetDevice(b->ctx->device));
   std::vector<uint32_t> w((b->n + 31) / 32);
   if (!w.empty()) HC(hipMemcpy(w.data(), b->bitmap.p, w.size() * 4, hipMemcpyDeviceToHost));
@@ -492,8 +539,12 @@ extern "C" size_t ftz_batch_size(const ftz_batch* b) { return b ? b->n : 0; }
 extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
+  for (int k = 0; k < 3; k++)
+    if (b->st[k]) (void)hipStreamSynchronize(b->st[k]);
   if (b->ev_init)
     for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
+  for (int k = 0; k < 3; k++)
+    if (b->st[k]) (void)hipStreamDestroy(b->st[k]);
   delete b;
 }
 
@@ -581,7 +632,7 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   Plan& p = b->plan;
-  hipStream_t s = c->stream, s2 = c->stream2, s3 = c->stream3;
+  hipStream_t s = b->st[0], s2 = b->st[1], s3 = b->st[2];
   const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
   if (serial) s2 = s3 = s;
   uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);

@@ -224,6 +224,14 @@ class Batch:
     def run(self):
         _check(self._lib.ftz_batch_run(self._h), self._lib)
 
+    def submit(self):
+        """Enqueue the pipeline on the batch's own streams and return (ftz_batch_submit)."""
+        _check(self._lib.ftz_batch_submit(self._h), self._lib)
+
+    def wait(self):
+        """Block until the last submission finished (ftz_batch_wait)."""
+        _check(self._lib.ftz_batch_wait(self._h), self._lib)
+
     def codes(self):
         c = (ctypes.c_int32 * max(1, self.n))()
         _check(self._lib.ftz_batch_codes(self._h, c), self._lib)

@@ -110,7 +110,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_threads", "ftz_ctx_info",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
-           "ftz_batch_run", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
+           "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
@@ -139,6 +139,8 @@ def load():
     lib.ftz_batch_load_transfers.argtypes = [vp, sz, ctypes.POINTER(Transfer), ctypes.POINTER(vp)]
     lib.ftz_batch_load_issues.argtypes = [vp, sz, ctypes.POINTER(Issue), ctypes.POINTER(vp)]
     lib.ftz_batch_run.argtypes = [vp]
+    lib.ftz_batch_submit.argtypes = [vp]
+    lib.ftz_batch_wait.argtypes = [vp]
     lib.ftz_batch_codes.argtypes = [vp, ctypes.POINTER(i32)]
     lib.ftz_batch_bitmap.argtypes = [vp, ctypes.POINTER(ctypes.c_uint8)]
     lib.ftz_batch_stats.argtypes = [vp, ctypes.POINTER(Stats)]

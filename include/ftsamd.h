@@ -95,7 +95,14 @@ int ftz_verify_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, int32_t* code
  * inputs any number of times (used by bench.py to time the device path). */
 int ftz_batch_load_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, ftz_batch** out);
 int ftz_batch_load_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, ftz_batch** out);
-int ftz_batch_run(ftz_batch* b);
+int ftz_batch_run(ftz_batch* b); /* = ftz_batch_submit + ftz_batch_wait */
+/* Asynchronous form: enqueue the pipeline on the batch's own HIP streams and
+ * return; several batches may be in flight at once (a validator pipelining
+ * blocks).  ftz_batch_wait blocks until the batch's last submission is done
+ * and records its ftz_stats; codes/bitmap wait implicitly.  A batch must not
+ * be resubmitted before its previous submission was waited for. */
+int ftz_batch_submit(ftz_batch* b);
+int ftz_batch_wait(ftz_batch* b);
 int ftz_batch_codes(ftz_batch* b, int32_t* codes);
 /* verdict bitmap: bit i set <=> proof i accepted; (n+7)/8 bytes */
 int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits);

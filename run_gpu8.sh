@@ -1,7 +1,10 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for a in 0 1 2; do
-  FTZ_G1_AFTER=$a timeout -k 10 200 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --msm '' --no-prover > gpurun_out/bench_after$a.log 2>&1 || exit 1
+B="timeout -k 10 200 python bench.py --steps 40 --warmup 3 --no-cpu-baseline --msm= --no-prover"
+for q in 8 12 16; do
+  for i in 3 4 5; do
+    GPU_MAX_HW_QUEUES=$q $B --inflight $i > gpurun_out/bench_q${q}_$i.log 2>&1 || exit 1
+  done
 done
 echo EXIT $?

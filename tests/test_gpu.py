@@ -90,6 +90,16 @@ def test_batch_4096_verdict_positions(zk, ctx_a, golden):
     assert b.codes() == expect
     st = b.stats()
     assert st["total"][0] > 0 and st["miller"][1] > 0
+    # two batches in flight on their own streams (ftz_batch_submit / wait):
+    # same verdicts as the synchronous runs, each batch resubmitted once
+    b2 = ctx_a.load_transfers(items[::-1])
+    for _ in range(2):
+        b.submit()
+        b2.submit()
+        b.wait()
+        b2.wait()
+    assert b.codes() == expect and b2.codes() == expect[::-1]
+    b2.close()
     b.close()
 
 
