@@ -124,7 +124,7 @@ def msm_latency(ctx, lg, reps=5, seed=7):
             "window_bits": info["window_bits"]}
 
 
-def prover_bench(ctx, batch, steps, warmup):
+def prover_bench(ctx, batch, steps, warmup, inflight=1):
     """BASELINE configs[4] (batch prover) at the configs[1] shape: `batch`
     2-in/2-out transfer proofs per pass from HBM-resident witnesses (64 distinct
     witnesses of tests/golden/bench_transfers.json tiled, a distinct 32-byte
@@ -141,22 +141,31 @@ def prover_bench(ctx, batch, steps, warmup):
                    "in_values": t["in_values"], "in_bfs": [int(x) for x in t["in_bfs"]],
                    "out_values": t["out_values"], "out_bfs": [int(x) for x in t["out_bfs"]],
                    "type": t["type"], "seed": hashlib.sha256(b"bench-prover/%d" % i).digest()})
-    p = zkatdlog.Prover(ctx, ws, "transfer")
+    provers = [zkatdlog.Prover(ctx, ws, "transfer") for _ in range(max(1, inflight))]
+    p = provers[0]
     try:
         for _ in range(warmup):
-            p.run()
+            for q in provers:
+                q.run()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            p.run()
+        for k in range(steps):  # `inflight` provers on their own streams, as the verifier batches
+            q = provers[k % len(provers)]
+            if k >= len(provers):
+                q.wait()
+            q.submit()
+        for q in provers:
+            q.wait()
         dt = time.perf_counter() - t0
         proofs, codes = p.proofs()
         stats = p.stats()
+        same = all(q.proofs()[0] == proofs for q in provers[1:])  # deterministic seeds: identical bytes
     finally:
-        p.close()
+        for q in provers:
+            q.close()
     verdicts = ctx.verify_transfers([(w["inputs"], w["outputs"], pr) for w, pr in zip(ws, proofs)])
     return {"proofs_per_s": round(batch * steps / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3),
-            "batch": batch, "all_accepted_by_gpu_verifier": bool(all(c == 0 for c in codes)
-                                                                 and all(v == 0 for v in verdicts)),
+            "batch": batch, "in_flight": len(provers),
+            "all_accepted_by_gpu_verifier": bool(same and all(c == 0 for c in codes) and all(v == 0 for v in verdicts)),
             "stage_ms": {k: round(v[0], 3) for k, v in stats.items()}}
 
 
@@ -206,8 +215,8 @@ def roofline(batch, device, tx_per_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="transfers per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -282,7 +291,7 @@ def main():
         roof = roofline(batch, local, value)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
-        prover = None if args.no_prover else prover_bench(ctx, args.batch, args.steps, args.warmup)
+        prover = None if args.no_prover else prover_bench(ctx, args.batch, args.steps, args.warmup, args.inflight)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(pp_json, items, expect, args.cpu_seconds)

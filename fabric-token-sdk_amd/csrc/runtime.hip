@@ -626,7 +626,7 @@ extern "C" int ftz_prover_load_issues(ftz_ctx* c, size_t n, const ftz_issue_witn
   });
 }
 
-extern "C" int ftz_prover_run(ftz_prover* b) {
+extern "C" int ftz_prover_submit(ftz_prover* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null prover");
   ftz_ctx* c = b->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -706,7 +706,18 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
     k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
                                                     b->bitmap.p);
   HC(hipGetLastError());
-  HC(hipStreamSynchronize(s));
+  for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
+  b->pending = true;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_prover_wait(ftz_prover* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null prover");
+  if (!b->pending) return FTZ_SUCCESS;
+  HC(hipSetDevice(b->ctx->device));
+  HC(hipStreamSynchronize(b->st[0]));
+  b->pending = false;
+  hipEvent_t* e = b->ev;
   // stats order: decode zr rand+hash_pre scalar g1p g2+lines miller fexp g1(side) hash+responses emit+b64 total
   const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
   const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
@@ -714,9 +725,14 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
     float ms = 0;
     HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
     b->stats.ms[k] = ms;
-    b->stats.jobs[k] = jobs[k];
+    b->stats.jobs[k] = b->jobs_last[k];
   }
   return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_prover_run(ftz_prover* b) {
+  int rc = ftz_prover_submit(b);
+  return rc == FTZ_SUCCESS ? ftz_prover_wait(b) : rc;
 }
 
 extern "C" size_t ftz_prover_bytes(const ftz_prover* b) { return b ? b->plan.out.size() : 0; }
@@ -725,8 +741,12 @@ extern "C" int ftz_prover_proofs(ftz_prover* b, uint8_t* buf, size_t cap, size_t
   if (!b) return set_err(FTZ_E_INVALID, "null prover");
   const Plan& p = b->plan;
   if (cap < p.out.size() || (p.out.size() && !buf)) return set_err(FTZ_E_INVALID, "proof buffer too small");
+  if (b->pending) {
+    int rc = ftz_prover_wait(b);
+    if (rc != FTZ_SUCCESS) return rc;
+  }
   HC(hipSetDevice(b->ctx->device));
-  hipStream_t s = b->ctx->stream;
+  hipStream_t s = b->st[0];
   if (p.out.size()) HC(hipMemcpyAsync(buf, b->out.p, p.out.size(), hipMemcpyDeviceToHost, s));
   if (codes && b->n) HC(hipMemcpyAsync(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HC(hipStreamSynchronize(s));

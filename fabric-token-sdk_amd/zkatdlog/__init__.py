@@ -191,6 +191,12 @@ class Prover:
     def run(self):
         _check(self._lib.ftz_prover_run(self._h), self._lib)
 
+    def submit(self):
+        _check(self._lib.ftz_prover_submit(self._h), self._lib)
+
+    def wait(self):
+        _check(self._lib.ftz_prover_wait(self._h), self._lib)
+
     def proofs(self):
         """(list of proof bytes, list of codes)"""
         size = self._lib.ftz_prover_bytes(self._h)

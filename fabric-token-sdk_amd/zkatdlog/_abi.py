@@ -113,7 +113,7 @@ SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_t
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
-           "ftz_prover_run", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
+           "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
 _lib = None
 
@@ -163,6 +163,8 @@ def load():
     lib.ftz_prover_load_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), ctypes.POINTER(vp)]
     lib.ftz_prover_load_issues.argtypes = [vp, sz, ctypes.POINTER(IssueWitness), ctypes.POINTER(vp)]
     lib.ftz_prover_run.argtypes = [vp]
+    lib.ftz_prover_submit.argtypes = [vp]
+    lib.ftz_prover_wait.argtypes = [vp]
     lib.ftz_prover_bytes.argtypes = [vp]
     lib.ftz_prover_bytes.restype = sz
     lib.ftz_prover_proofs.argtypes = [vp, u8p, sz, szp, i32p]

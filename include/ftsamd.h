@@ -174,7 +174,10 @@ int ftz_prove_issues(ftz_ctx* ctx, size_t n, const ftz_issue_witness* w, uint8_t
 /* staged form: plan + upload once, run on HBM-resident witnesses (bench) */
 int ftz_prover_load_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer_witness* w, ftz_prover** out);
 int ftz_prover_load_issues(ftz_ctx* ctx, size_t n, const ftz_issue_witness* w, ftz_prover** out);
-int ftz_prover_run(ftz_prover* p);
+int ftz_prover_run(ftz_prover* p); /* = ftz_prover_submit + ftz_prover_wait */
+/* asynchronous form on the prover's own streams (as ftz_batch_submit / ftz_batch_wait) */
+int ftz_prover_submit(ftz_prover* p);
+int ftz_prover_wait(ftz_prover* p);
 size_t ftz_prover_bytes(const ftz_prover* p);
 int ftz_prover_proofs(ftz_prover* p, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes);
 int ftz_prover_stats(const ftz_prover* p, ftz_stats* out);
