@@ -17,7 +17,8 @@ import os as _os
 
 # Hardware queues per process: 4 batches in flight x 3 streams need more than
 # HIP's default of 4 (set before the HIP runtime initialises; <= 32).
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+if int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import argparse
 import base64
 import json

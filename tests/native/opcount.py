@@ -19,7 +19,7 @@ NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "ha
 def main():
     lib = "/tmp/libftsemu_count.so"
     srcs = ["tests/native/emu.cpp", "tests/native/emu_exec.cpp", "fabric-token-sdk_amd/csrc/host/planner.cpp",
-            "fabric-token-sdk_amd/csrc/host/gojson.cpp"]
+            "fabric-token-sdk_amd/csrc/host/gojson.cpp", "fabric-token-sdk_amd/csrc/host/planner_prove.cpp"]
     subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-pthread",
                     "-DFTS_COUNT_OPS"] + [os.path.join(ROOT, s) for s in srcs] + ["-o", lib], check=True)
     L = ctypes.CDLL(lib)
