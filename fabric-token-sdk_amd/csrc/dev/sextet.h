@@ -293,34 +293,40 @@ FTS_HD fp2 sx_inv(X x, fp2 f) {
   return sx_mulv(x, fc, inv6);
 }
 
-// Width-3 NAF of the BN parameter x: digits in {+-1, +-3}, 18 non-zero over
-// bits 62..0 (the binary NAF used by f12_expt has 24), top digit +1 at bit 62.
-static constexpr uint64_t BN_X_W3_P1 = 0x4800120040011001ull;
-static constexpr uint64_t BN_X_W3_N1 = 0x0000000000000010ull;
-static constexpr uint64_t BN_X_W3_P3 = 0x0000804004000000ull;
-static constexpr uint64_t BN_X_W3_N3 = 0x0108000400880200ull;
+// Width-4 NAF of the BN parameter x: digits in {+-1, +-3, +-5, +-7}, 14 non-zero
+// over bits 62..0 (the binary NAF used by f12_expt has 24), top digit +1 at bit
+// 62.  Masks: any non-zero digit, negative digits, magnitude 3 / 5 / 7.
+static constexpr uint64_t BN_X_W4_NZ = 0x4108844442110211ull;
+static constexpr uint64_t BN_X_W4_NEG = 0x0008004400010010ull;
+static constexpr uint64_t BN_X_W4_M3 = 0x0008800400000000ull;
+static constexpr uint64_t BN_X_W4_M5 = 0x0100044002000200ull;
+static constexpr uint64_t BN_X_W4_M7 = 0x0000000000110000ull;
 
 // a^x (x = BN parameter), a in the cyclotomic subgroup: the same element as
-// f12_expt (any addition chain for x gives it), by the width-3 NAF with a^3
-// precomputed -- 17 + 1 multiplications and one extra squaring instead of 23.
-// The operand (a or a^3) is re-published in SX_B / SX_BX only when the digit's
-// magnitude changes; a digit -d multiplies by conj(a^d) = a^-d through
-// r conj(a^d) = conj(conj(r) a^d).
+// f12_expt (any addition chain for x gives it), by the width-4 NAF with a^3,
+// a^5, a^7 precomputed -- 13 + 3 multiplications and one extra squaring
+// instead of 23 multiplications.  The digit's odd power (a^7 kept in LDS to
+// stay within the register budget) is published in
+// SX_B / SX_BX when its magnitude changes; a digit -d multiplies by
+// conj(a^d) = a^-d through r conj(a^d) = conj(conj(r) a^d).
 template <class X>
 FTS_HD fp2 sx_expt(X x, fp2 a) {
-  fp2 a3 = sx_mulv(x, sx_cyc_sqr(x, a), a);  // publishes a
-  bool cur3 = false;
+  fp2 a2 = sx_cyc_sqr(x, a);
+  fp2 a3 = sx_mulv(x, a2, a);
+  fp2 a5 = sx_mulv(x, a3, a2);  // publishes a^2 for a^7 too
+  x.put(SX_P + x.k, sx_mul(x, a5));  // a^7 parked in the lane's own SX_P slot (free during expt)
+  int cur = 0;  // magnitude published in SX_B (0: a^2)
   fp2 r = a;
 #pragma nounroll
   for (int i = 61; i >= 0; i--) {
     r = sx_cyc_sqr(x, r);
-    bool d1 = ((BN_X_W3_P1 | BN_X_W3_N1) >> i) & 1, d3 = ((BN_X_W3_P3 | BN_X_W3_N3) >> i) & 1;
-    bool neg = ((BN_X_W3_N1 | BN_X_W3_N3) >> i) & 1;
-    if (d1 || d3) {
-      if (d3 != cur3) {
-        sx_pub(x, SX_B, d3 ? a3 : a);
-        cur3 = d3;
+    if ((BN_X_W4_NZ >> i) & 1) {
+      int m = ((BN_X_W4_M3 >> i) & 1) ? 3 : (((BN_X_W4_M5 >> i) & 1) ? 5 : (((BN_X_W4_M7 >> i) & 1) ? 7 : 1));
+      if (m != cur) {
+        sx_pub(x, SX_B, m == 7 ? x.get(SX_P + x.k) : (m == 1 ? a : (m == 3 ? a3 : a5)));
+        cur = m;
       }
+      bool neg = (BN_X_W4_NEG >> i) & 1;
       fp2 t = neg ? sx_conj(x.k, r) : r;
       t = sx_mul(x, t);
       r = neg ? sx_conj(x.k, t) : t;
