@@ -276,6 +276,65 @@ FTS_HD Fe<M> mont_mul_cios(const Fe<M>& a, const Fe<M>& b) {
   return br ? r : u;
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(FTS_HOST64)
+// Host-only (CPU baseline build, oracle/cpu): the same Montgomery product
+// with 4 x 64-bit limbs and 128-bit products.  R = 2^256 in both limb
+// layouts and the 8 x u32 little-endian limbs ARE the 4 x u64 limbs in
+// memory, so results are bit-identical to the 32-bit CIOS.
+constexpr uint64_t fts_neg_inv64(uint64_t m0) {
+  uint64_t y = 1;
+  for (int i = 0; i < 7; i++) y *= 2 - m0 * y;  // Newton: y = m0^-1 mod 2^64
+  return (uint64_t)0 - y;
+}
+template <class M>
+inline Fe<M> mont_mul_host64(const Fe<M>& a, const Fe<M>& b) {
+  typedef unsigned __int128 u128;
+  constexpr uint64_t m0 = (uint64_t)M::m[0] | ((uint64_t)M::m[1] << 32), m1 = (uint64_t)M::m[2] | ((uint64_t)M::m[3] << 32),
+                     m2 = (uint64_t)M::m[4] | ((uint64_t)M::m[5] << 32), m3 = (uint64_t)M::m[6] | ((uint64_t)M::m[7] << 32);
+  constexpr uint64_t inv = fts_neg_inv64(m0);
+  const uint64_t m[4] = {m0, m1, m2, m3};
+  uint64_t x[4], y[4];
+  for (int i = 0; i < 4; i++) {
+    x[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+    y[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
+  }
+  uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; i++) {
+    u128 c = 0;
+    for (int j = 0; j < 4; j++) {
+      c = (u128)x[j] * y[i] + t[j] + (uint64_t)(c >> 64);
+      t[j] = (uint64_t)c;
+    }
+    u128 s = (u128)t[4] + (uint64_t)(c >> 64);
+    t[4] = (uint64_t)s;
+    t[5] = (uint64_t)(s >> 64);
+    uint64_t q = t[0] * inv;
+    c = (u128)q * m[0] + t[0];
+    for (int j = 1; j < 4; j++) {
+      c = (u128)q * m[j] + t[j] + (uint64_t)(c >> 64);
+      t[j - 1] = (uint64_t)c;
+    }
+    s = (u128)t[4] + (uint64_t)(c >> 64);
+    t[3] = (uint64_t)s;
+    t[4] = t[5] + (uint64_t)(s >> 64);
+  }
+  // t < 2m: one conditional subtraction
+  uint64_t u[4], br = 0;
+  for (int j = 0; j < 4; j++) {
+    u128 d = (u128)t[j] - m[j] - br;
+    u[j] = (uint64_t)d;
+    br = (uint64_t)(d >> 64) & 1;
+  }
+  const uint64_t* r = br ? t : u;
+  Fe<M> o;
+  for (int i = 0; i < 4; i++) {
+    o.v[2 * i] = (uint32_t)r[i];
+    o.v[2 * i + 1] = (uint32_t)(r[i] >> 32);
+  }
+  return o;
+}
+#endif
+
 #ifndef FTS_MUL_IMPL
 #define FTS_MUL_IMPL 1  // 0: CIOS in C, 1: FIPS with inline v_mad_u64_u32 (device)
 #endif
@@ -285,6 +344,8 @@ FTS_HD Fe<M> operator*(const Fe<M>& a, const Fe<M>& b) {
   FTS_COUNT_MUL();
 #if defined(__HIP_DEVICE_COMPILE__) && FTS_MUL_IMPL == 1
   return mont_mul_fips(a, b);
+#elif !defined(__HIP_DEVICE_COMPILE__) && defined(FTS_HOST64)
+  return mont_mul_host64(a, b);
 #else
   return mont_mul_cios(a, b);
 #endif

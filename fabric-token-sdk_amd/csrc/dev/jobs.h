@@ -887,8 +887,8 @@ FTS_HD void job_miller(const PairJob& j, const LineCoef* qlines, const G1Dev* g1
   f12_store(fout[idx], f);
 }
 
-FTS_HD void job_fexp(const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena) {
-  fp12 g = final_exp(f12_load(fin[idx]));
+FTS_HD void job_fexp(const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena, int variant = 0) {
+  fp12 g = final_exp(f12_load(fin[idx]), variant);
   f12_to_bytes(arena + j.bytes, g);
 }
 
@@ -1176,7 +1176,8 @@ FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, 
   }
 }
 
-template <class X>
+// EXACT: 0 = Fuentes chain (sx_final_exp), 1 = exact (sx_final_exp_exact)
+template <int EXACT, class X>
 FTS_HD void sx_job_fexp(const X& x, const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena, bool valid) {
   const uint32_t* w = &fin[idx].w[16 * sx_f12_index(x.k)];
   fp2 f;
@@ -1185,7 +1186,7 @@ FTS_HD void sx_job_fexp(const X& x, const PairJob& j, const F12Dev* fin, uint32_
     f.c0.v[i] = w[i];
     f.c1.v[i] = w[8 + i];
   }
-  fp2 g = sx_final_exp(x, f);
+  fp2 g = EXACT ? sx_final_exp_exact(x, f) : sx_final_exp(x, f);
   if (valid) sx_gt_bytes(arena + j.bytes, x.k, g);
 }
 

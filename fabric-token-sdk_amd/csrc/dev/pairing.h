@@ -228,8 +228,8 @@ FTS_HDN fp12 f12_expt(const fp12& a) {
 // final exponentiation: easy part (p^6-1)(p^2+1), hard part
 //   FUENTES: 2x(6x^2+3x+1)(p^4-p^2+1)/r  via f^(l0 + l1 p + l2 p^2 + l3 p^3),
 //   l0 = 1+6x+12x^2+12x^3, l1 = 4x+6x^2+12x^3, l2 = 6x+6x^2+12x^3,
-//   l3 = -1+4x+6x^2+12x^3   (Fuentes-Castaneda et al.; [EXT] gnark variant).
-FTS_HDN fp12 final_exp(const fp12& f) {
+//   l3 = -1+4x+6x^2+12x^3   (Fuentes-Castaneda et al.; later gnark releases).
+FTS_HDN fp12 final_exp_fuentes(const fp12& f) {
   fp12 t = f12_conj(f) * f12_inv(f);
   t = f12_frob2(t) * t;
   fp12 a = f12_expt(t);                 // t^x
@@ -244,6 +244,38 @@ FTS_HDN fp12 final_exp(const fp12& f) {
   res = res * f12_frob(B);
   res = res * f12_frob3(B * f12_conj(t));  // l3
   return res;
+}
+
+// EXACT: hard part (p^4-p^2+1)/r by the Scott et al. vectorial addition chain
+// (ePrint 2008/490) that gnark-crypto v0.6.0's bn254 FinalExponentiation runs
+// (the version IBM/mathlib 0a7378db6912 pins, go.mod:7,53): with m the easy-part
+// output and m_k = m^(x^k),
+//   y0 = m^p m^p^2 m^p^3, y1 = 1/m, y2 = (m_2)^p^2, y3 = 1/(m_1)^p,
+//   y4 = 1/(m_1 (m_2)^p), y5 = 1/m_2, y6 = 1/(m_3 (m_3)^p),
+//   result = y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36.
+FTS_HDN fp12 final_exp_exact(const fp12& f) {
+  fp12 m = f12_conj(f) * f12_inv(f);
+  m = f12_frob2(m) * m;
+  fp12 mx = f12_expt(m), mx2 = f12_expt(mx), mx3 = f12_expt(mx2);
+  fp12 y0 = f12_frob(m) * f12_frob2(m) * f12_frob3(m);
+  fp12 y1 = f12_conj(m);
+  fp12 y2 = f12_frob2(mx2);
+  fp12 y3 = f12_conj(f12_frob(mx));
+  fp12 y4 = f12_conj(mx * f12_frob(mx2));
+  fp12 y5 = f12_conj(mx2);
+  fp12 y6 = f12_conj(mx3 * f12_frob(mx3));
+  fp12 t0 = f12_cyclo_sqr(y6) * y4 * y5;
+  fp12 t1 = y3 * y5 * t0;
+  t0 = t0 * y2;
+  t1 = f12_cyclo_sqr(f12_cyclo_sqr(t1) * t0);
+  t0 = t1 * y1;
+  t1 = t1 * y0;
+  return f12_cyclo_sqr(t0) * t1;
+}
+
+// variant: 0 = exact (FTZ_FEXP_EXACT), 1 = Fuentes (FTZ_FEXP_FUENTES)
+FTS_HD fp12 final_exp(const fp12& f, int variant = 0) {
+  return variant == 1 ? final_exp_fuentes(f) : final_exp_exact(f);
 }
 
 }  // namespace fts

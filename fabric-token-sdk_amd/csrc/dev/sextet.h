@@ -366,6 +366,43 @@ FTS_HD fp2 sx_final_exp(const X& x, const fp2& f) {
   return res;
 }
 
+// Exact final exponentiation (f^((p^12-1)/r), Scott et al. chain as
+// final_exp_exact in pairing.h).  The three x-powers run as one loop; the
+// y_i are formed as soon as their inputs exist so at most six Fp12 values
+// (one Fp2 per lane each) are live.
+template <class X>
+FTS_HD fp2 sx_final_exp_exact(const X& x, const fp2& f) {
+  const int k = x.k;
+  fp2 m = sx_mulv(x, sx_conj(k, f), sx_inv(x, f));
+  m = sx_mulv(x, sx_frob2(k, m), m);
+  fp2 in = m, mx, mx2, mx3;
+#pragma nounroll
+  for (int e = 0; e < 3; e++) {
+    fp2 r = sx_expt(x, in);
+    if (e == 0) {
+      mx = r;
+    } else if (e == 1) {
+      mx2 = r;
+    } else {
+      mx3 = r;
+    }
+    in = r;
+  }
+  fp2 y3 = sx_conj(k, sx_frob1(k, mx));
+  fp2 y4 = sx_conj(k, sx_mulv(x, mx, sx_frob1(k, mx2)));
+  fp2 y5 = sx_conj(k, mx2);
+  fp2 y2 = sx_frob2(k, mx2);
+  fp2 y6 = sx_conj(k, sx_mulv(x, mx3, sx_frob1(k, mx3)));
+  fp2 t0 = sx_mulv(x, sx_mulv(x, sx_cyc_sqr(x, y6), y4), y5);
+  fp2 t1 = sx_mulv(x, sx_mulv(x, y3, y5), t0);
+  t0 = sx_mulv(x, t0, y2);
+  t1 = sx_cyc_sqr(x, sx_mulv(x, sx_cyc_sqr(x, t1), t0));
+  fp2 y0 = sx_mulv(x, sx_mulv(x, sx_frob1(k, m), sx_frob2(k, m)), sx_frob3(k, m));
+  t0 = sx_mulv(x, t1, sx_conj(k, m));
+  t1 = sx_mulv(x, t1, y0);
+  return sx_mulv(x, sx_cyc_sqr(x, t0), t1);
+}
+
 // gnark E12.Bytes position (in 64-byte Fp2 units) of coefficient k:
 // C1.B2 (f5), C1.B1 (f3), C1.B0 (f1), C0.B2 (f4), C0.B1 (f2), C0.B0 (f0)
 FTS_HD int sx_gt_pos(int k) { return (int)((0x031425u >> (4 * k)) & 0xF); }

@@ -1,0 +1,276 @@
+// Job engine behind ftz_verify_transfers / ftz_verify_issues: one per context.
+//
+// The reference verifies one action per call and fans out goroutines inside
+// it (validator_transfer.go:84-98, range/proof.go:247-257); concurrency comes
+// from the peer running many validations at once (tcc.go:223-237) and the
+// client-side double-checks (token/request.go:295-298).  A GPU pass only pays
+// off on thousands of proofs, so every call becomes a *request* in one queue
+// per context and a dispatcher thread cuts the queue into device batches:
+//
+//   * a big call (a block, a 1M-transfer job) is split into batches of at most
+//     opt.batch proofs -- which also keeps every 32-bit job index of a batch in
+//     range -- and fills the pipeline by itself;
+//   * small concurrent calls (the Go shim verifies ONE TransferAction per call)
+//     are coalesced: while the GPU has >= 2 batches in flight a partial batch
+//     waits up to opt.window_us for more callers, otherwise it goes at once;
+//   * transfers and issues share batches (the planner emits the same jobs).
+//
+// Batches cycle through opt.slots reusable slots (pinned staging blob, device
+// buffers, streams, events): the dispatcher plans batch k+1 on the host pool
+// while batches k, k-1, ... run on the device; a completion thread waits for
+// the oldest batch in flight, scatters its verdict codes back to the requests
+// and recycles the slot.  A request returns when all its proofs are done.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ftsamd.h"
+#include "rt_internal.h"
+
+using Clock = std::chrono::steady_clock;
+
+struct Request {
+  const ftz_transfer* tx = nullptr;  // exactly one of tx / is
+  const ftz_issue* is = nullptr;
+  size_t n = 0;
+  int32_t* codes = nullptr;
+  size_t next = 0;         // next proof to hand to a batch (dispatcher, under mu)
+  size_t outstanding = 0;  // proofs not yet completed (under mu)
+  int rc = FTZ_SUCCESS;
+  std::string err;
+  bool done = false;
+  Clock::time_point t0;
+};
+
+// proof bytes per batch stay well below the 2^31 arena / wire limits
+static constexpr size_t BATCH_PROOF_BYTES = (size_t)256 << 20;
+
+struct Engine {
+  ftz_ctx* ctx = nullptr;
+  std::mutex mu;
+  std::condition_variable cv_q, cv_done, cv_free, cv_comp;
+  std::deque<Request*> q;
+  std::vector<ftz_batch*> slots;
+  std::deque<ftz_batch*> free_slots, inflight;
+  bool stop = false;
+  bool disp_done = false;  // the dispatcher has exited (nothing more will be put in flight)
+  std::thread disp, comp;
+
+  void dispatcher();
+  void completer();
+  void fail_parts(ftz_batch* b, int rc, const std::string& err);
+};
+
+static PlanItem item_of(const Request* r, size_t i) {
+  PlanItem it;
+  memset(&it, 0, sizeof(it));
+  if (r->tx) {
+    const ftz_transfer& t = r->tx[i];
+    it.kind = 0;
+    it.t = {t.inputs, t.n_in, t.outputs, t.n_out, t.proof, t.proof_len};
+  } else {
+    const ftz_issue& s = r->is[i];
+    it.kind = 1;
+    it.i = {s.outputs, s.n_out, s.proof, s.proof_len, s.anonymous};
+  }
+  return it;
+}
+
+static size_t item_bytes(const Request* r, size_t i) {
+  return r->tx ? r->tx[i].proof_len + 64 * ((size_t)r->tx[i].n_in + r->tx[i].n_out)
+               : r->is[i].proof_len + 64 * (size_t)r->is[i].n_out;
+}
+
+// Deliver a failed batch's error to its requests (mu held).
+void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err) {
+  for (auto& p : b->parts) {
+    if (p.req->rc == FTZ_SUCCESS) {
+      p.req->rc = rc;
+      p.req->err = err;
+    }
+    p.req->outstanding -= p.count;
+    if (p.req->outstanding == 0 && p.req->next == p.req->n) p.req->done = true;
+  }
+  b->parts.clear();
+  cv_done.notify_all();
+}
+
+void Engine::dispatcher() {
+  (void)hipSetDevice(ctx->device);
+  const size_t B = ctx->opt.batch;
+  const auto window = std::chrono::microseconds(ctx->opt.window_us);
+  std::unique_lock<std::mutex> lk(mu);
+  while (true) {
+    cv_q.wait(lk, [&]() { return stop || !q.empty(); });
+    if (q.empty()) {
+      if (stop) {
+        disp_done = true;
+        cv_comp.notify_all();
+        return;
+      }
+      continue;
+    }
+    size_t pending = 0;
+    for (Request* r : q) pending += r->n - r->next;
+    if (pending < B && inflight.size() >= 2 && !stop) {
+      // the device is busy: let a partial batch wait (a bounded time) for company
+      Clock::time_point deadline = q.front()->t0 + window;
+      if (Clock::now() < deadline) {
+        cv_q.wait_until(lk, deadline);
+        continue;  // re-evaluate: more requests, a completion, or the deadline
+      }
+    }
+    cv_free.wait(lk, [&]() { return !free_slots.empty(); });
+    ftz_batch* b = free_slots.front();
+    free_slots.pop_front();
+    b->parts.clear();
+    b->items.clear();
+    size_t bytes = 0;
+    while (!q.empty() && b->items.size() < B) {
+      Request* r = q.front();
+      size_t start = r->next;
+      while (r->next < r->n && b->items.size() < B && (bytes < BATCH_PROOF_BYTES || b->items.empty())) {
+        bytes += item_bytes(r, r->next);
+        b->items.push_back(item_of(r, r->next));
+        r->next++;
+      }
+      if (r->next > start) b->parts.push_back({r, start, r->next - start});
+      if (r->next == r->n) q.pop_front();
+      if (bytes >= BATCH_PROOF_BYTES) break;
+    }
+    lk.unlock();
+    int rc = slot_plan_items(b, b->items.size(), b->items.data());
+    if (rc == FTZ_SUCCESS) rc = slot_submit(b, true, true);
+    std::string err = rc == FTZ_SUCCESS ? std::string() : g_err;
+    lk.lock();
+    if (rc != FTZ_SUCCESS) {
+      if (b->pending) {  // enqueued part of the work before failing: let it drain first
+        lk.unlock();
+        (void)slot_wait(b);
+        lk.lock();
+      }
+      fail_parts(b, rc, err);
+      free_slots.push_back(b);
+      cv_free.notify_one();
+      continue;
+    }
+    inflight.push_back(b);
+    cv_comp.notify_one();
+  }
+}
+
+void Engine::completer() {
+  (void)hipSetDevice(ctx->device);
+  std::unique_lock<std::mutex> lk(mu);
+  while (true) {
+    cv_comp.wait(lk, [&]() { return disp_done || !inflight.empty(); });
+    if (inflight.empty()) return;  // disp_done: nothing more will arrive
+    ftz_batch* b = inflight.front();
+    lk.unlock();
+    int rc = slot_wait(b);
+    std::string err = rc == FTZ_SUCCESS ? std::string() : g_err;
+    if (rc == FTZ_SUCCESS) {
+      const int32_t* codes = slot_codes(b);
+      size_t off = 0;
+      for (auto& p : b->parts) {  // each request's range is written by this thread only
+        memcpy(p.req->codes + p.start, codes + off, p.count * sizeof(int32_t));
+        off += p.count;
+      }
+    }
+    lk.lock();
+    inflight.pop_front();
+    if (rc != FTZ_SUCCESS) {
+      fail_parts(b, rc, err);
+    } else {
+      for (auto& p : b->parts) {
+        p.req->outstanding -= p.count;
+        if (p.req->outstanding == 0 && p.req->next == p.req->n) p.req->done = true;
+      }
+      b->parts.clear();
+      cv_done.notify_all();
+    }
+    free_slots.push_back(b);
+    cv_free.notify_one();
+    cv_q.notify_one();  // a partial batch may go now that the device has room
+  }
+}
+
+static Engine* get_engine(ftz_ctx* c, int& rc) {
+  std::lock_guard<std::mutex> lk(c->eng_mu);
+  rc = FTZ_SUCCESS;
+  if (c->eng) return c->eng;
+  Engine* e = new Engine();
+  e->ctx = c;
+  for (uint32_t k = 0; k < c->opt.slots; k++) {
+    ftz_batch* b = new ftz_batch();
+    b->ctx = c;
+    rc = slot_init(b);
+    e->slots.push_back(b);
+    e->free_slots.push_back(b);
+    if (rc != FTZ_SUCCESS) break;
+  }
+  if (rc != FTZ_SUCCESS) {
+    for (ftz_batch* b : e->slots) {
+      slot_free(b);
+      delete b;
+    }
+    delete e;
+    return nullptr;
+  }
+  e->disp = std::thread([e]() { e->dispatcher(); });
+  e->comp = std::thread([e]() { e->completer(); });
+  c->eng = e;
+  return e;
+}
+
+int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue* is, int32_t* codes) {
+  int rc;
+  Engine* e = get_engine(c, rc);
+  if (!e) return rc;
+  Request r;
+  r.tx = tx;
+  r.is = is;
+  r.n = n;
+  r.codes = codes;
+  r.outstanding = n;
+  r.t0 = Clock::now();
+  std::unique_lock<std::mutex> lk(e->mu);
+  if (e->stop) return set_err(FTZ_E_INVALID, "context is being destroyed");
+  e->q.push_back(&r);
+  e->cv_q.notify_one();
+  e->cv_done.wait(lk, [&]() { return r.done; });
+  if (r.rc != FTZ_SUCCESS) return set_err(r.rc, r.err);
+  return FTZ_SUCCESS;
+}
+
+void engine_destroy(ftz_ctx* c) {
+  Engine* e;
+  {
+    std::lock_guard<std::mutex> lk(c->eng_mu);
+    e = c->eng;
+    c->eng = nullptr;
+  }
+  if (!e) return;
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->stop = true;
+  }
+  e->cv_q.notify_all();
+  e->cv_comp.notify_all();
+  e->cv_free.notify_all();
+  e->disp.join();
+  e->comp.join();
+  for (ftz_batch* b : e->slots) {
+    slot_free(b);
+    delete b;
+  }
+  delete e;
+}

@@ -1,118 +1,189 @@
 #include "gojson.h"
 
-#include <string.h>
-
 namespace ftsh {
 
 namespace {
+
+constexpr uint32_t MAX_DEPTH = 10000;  // encoding/json scanner.go maxNestingDepth
+
+inline bool is_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+
+void put_utf8(std::string& o, uint32_t cp) {
+  char b[4];
+  if (cp < 0x80) {
+    o.push_back((char)cp);
+    return;
+  }
+  if (cp < 0x800) {
+    b[0] = (char)(0xC0 | (cp >> 6));
+    b[1] = (char)(0x80 | (cp & 0x3F));
+    o.append(b, 2);
+  } else if (cp < 0x10000) {
+    b[0] = (char)(0xE0 | (cp >> 12));
+    b[1] = (char)(0x80 | ((cp >> 6) & 0x3F));
+    b[2] = (char)(0x80 | (cp & 0x3F));
+    o.append(b, 3);
+  } else {
+    b[0] = (char)(0xF0 | (cp >> 18));
+    b[1] = (char)(0x80 | ((cp >> 12) & 0x3F));
+    b[2] = (char)(0x80 | ((cp >> 6) & 0x3F));
+    b[3] = (char)(0x80 | (cp & 0x3F));
+    o.append(b, 4);
+  }
+}
+
+// unicode/utf8.DecodeRune: returns the rune and its size; invalid -> (U+FFFD, 1)
+uint32_t decode_rune(const uint8_t* s, size_t n, size_t& size) {
+  size = 1;
+  uint8_t b0 = s[0];
+  if (b0 < 0x80) return b0;
+  auto cont = [&](size_t k, uint8_t lo, uint8_t hi) { return k < n && s[k] >= lo && s[k] <= hi; };
+  if (b0 >= 0xC2 && b0 <= 0xDF) {
+    if (!cont(1, 0x80, 0xBF)) return 0xFFFD;
+    size = 2;
+    return ((uint32_t)(b0 & 0x1F) << 6) | (s[1] & 0x3F);
+  }
+  if (b0 >= 0xE0 && b0 <= 0xEF) {
+    uint8_t lo = b0 == 0xE0 ? 0xA0 : 0x80, hi = b0 == 0xED ? 0x9F : 0xBF;
+    if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF)) return 0xFFFD;
+    size = 3;
+    return ((uint32_t)(b0 & 0x0F) << 12) | ((uint32_t)(s[1] & 0x3F) << 6) | (s[2] & 0x3F);
+  }
+  if (b0 >= 0xF0 && b0 <= 0xF4) {
+    uint8_t lo = b0 == 0xF0 ? 0x90 : 0x80, hi = b0 == 0xF4 ? 0x8F : 0xBF;
+    if (!cont(1, lo, hi) || !cont(2, 0x80, 0xBF) || !cont(3, 0x80, 0xBF)) return 0xFFFD;
+    size = 4;
+    return ((uint32_t)(b0 & 0x07) << 18) | ((uint32_t)(s[1] & 0x3F) << 12) | ((uint32_t)(s[2] & 0x3F) << 6) |
+           (s[3] & 0x3F);
+  }
+  return 0xFFFD;
+}
+
+int hexv(uint8_t c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+// 4 hex digits at s[i..i+4) -> v; false if not hex (encoding/json getu4)
+bool hex4(const uint8_t* s, size_t n, size_t i, uint32_t& v) {
+  if (i + 4 > n) return false;
+  v = 0;
+  for (int k = 0; k < 4; k++) {
+    int h = hexv(s[i + k]);
+    if (h < 0) return false;
+    v = (v << 4) | (uint32_t)h;
+  }
+  return true;
+}
 
 struct Parser {
   const uint8_t* s;
   size_t n, i;
   JDoc* d;
-  int depth;
 
   void ws() {
-    while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\r' || s[i] == '\n')) i++;
+    while (i < n && is_ws(s[i])) i++;
   }
 
-  static void put_utf8(std::string& o, uint32_t cp) {
-    if (cp < 0x80) {
-      o.push_back((char)cp);
-    } else if (cp < 0x800) {
-      o.push_back((char)(0xC0 | (cp >> 6)));
-      o.push_back((char)(0x80 | (cp & 0x3F)));
-    } else if (cp < 0x10000) {
-      o.push_back((char)(0xE0 | (cp >> 12)));
-      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-      o.push_back((char)(0x80 | (cp & 0x3F)));
-    } else {
-      o.push_back((char)(0xF0 | (cp >> 18)));
-      o.push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
-      o.push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
-      o.push_back((char)(0x80 | (cp & 0x3F)));
+  // index of the first byte at or after j that is '"', '\\', < 0x20 or >= 0x80
+  size_t scan_plain(size_t j) const {
+    const uint64_t ones = 0x0101010101010101ull, high = 0x8080808080808080ull;
+    while (j + 8 <= n) {
+      uint64_t v;
+      memcpy(&v, s + j, 8);
+      uint64_t q = v ^ (ones * '"'), b = v ^ (ones * '\\');
+      uint64_t t = ((q - ones) & ~q) | ((b - ones) & ~b) | (v - ones * 0x20) | v;
+      if (t & high) {  // a candidate in this word (borrows may flag false positives)
+        for (size_t e = j + 8; j < e; j++) {
+          uint8_t c = s[j];
+          if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) return j;
+        }
+        continue;
+      }
+      j += 8;
     }
-  }
-
-  static int hexv(uint8_t c) {
-    if (c >= '0' && c <= '9') return c - '0';
-    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
-    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
-    return -1;
-  }
-
-  bool hex4(uint32_t& v) {
-    if (i + 4 > n) return false;
-    v = 0;
-    for (int k = 0; k < 4; k++) {
-      int h = hexv(s[i + k]);
-      if (h < 0) return false;
-      v = (v << 4) | (uint32_t)h;
+    while (j < n) {
+      uint8_t c = s[j];
+      if (c == '"' || c == '\\' || c < 0x20 || c >= 0x80) break;
+      j++;
     }
-    i += 4;
-    return true;
+    return j;
   }
 
-  // parses a string starting at s[i] == '"', appends to pool; returns node index
+  // string at s[i] == '"' -> J_STR node, unquoted as encoding/json unquoteBytes.
+  // Plain strings (no escapes, ASCII) stay in the source text (bval = 1).
   bool string(uint32_t& node) {
     i++;
-    uint32_t start = (uint32_t)d->pool.size();
+    size_t j0 = scan_plain(i);
+    if (j0 < n && s[j0] == '"') {
+      node = (uint32_t)d->nodes.size();
+      d->nodes.push_back({J_STR, 1, (uint32_t)i, (uint32_t)(j0 - i)});
+      i = j0 + 1;
+      return true;
+    }
     std::string& o = d->pool;
+    uint32_t start = (uint32_t)o.size();
     while (true) {
+      // bulk-copy the run of plain printable ASCII
+      size_t j = scan_plain(i);
+      if (j > i) o.append((const char*)s + i, j - i);
+      i = j;
       if (i >= n) return false;
       uint8_t c = s[i];
       if (c == '"') {
         i++;
         break;
       }
-      if (c == '\\') {
-        i++;
-        if (i >= n) return false;
-        uint8_t e = s[i++];
-        switch (e) {
-          case '"': o.push_back('"'); break;
-          case '\\': o.push_back('\\'); break;
-          case '/': o.push_back('/'); break;
-          case 'b': o.push_back('\b'); break;
-          case 'f': o.push_back('\f'); break;
-          case 'n': o.push_back('\n'); break;
-          case 'r': o.push_back('\r'); break;
-          case 't': o.push_back('\t'); break;
-          case 'u': {
-            uint32_t cp;
-            if (!hex4(cp)) return false;
-            if (cp >= 0xD800 && cp < 0xDC00) {
-              uint32_t lo = 0;
-              size_t save = i;
-              if (i + 1 < n && s[i] == '\\' && s[i + 1] == 'u') {
-                i += 2;
-                if (hex4(lo) && lo >= 0xDC00 && lo < 0xE000) {
-                  cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-                } else {
-                  i = save;
-                  cp = 0xFFFD;
-                }
-              } else {
-                cp = 0xFFFD;
-              }
-            } else if (cp >= 0xD800 && cp < 0xE000) {
-              cp = 0xFFFD;
-            }
-            put_utf8(o, cp);
-            break;
-          }
-          default:
-            return false;
-        }
+      if (c < 0x20) return false;
+      if (c >= 0x80) {  // coerce to well-formed UTF-8
+        size_t sz;
+        uint32_t r = decode_rune(s + i, n - i, sz);
+        if (r == 0xFFFD && sz == 1)
+          put_utf8(o, 0xFFFD);
+        else
+          o.append((const char*)s + i, sz);
+        i += sz;
         continue;
       }
-      if (c < 0x20) return false;
-      o.push_back((char)c);
+      // escape
       i++;
+      if (i >= n) return false;
+      uint8_t e = s[i++];
+      switch (e) {
+        case '"': o.push_back('"'); break;
+        case '\\': o.push_back('\\'); break;
+        case '/': o.push_back('/'); break;
+        case 'b': o.push_back('\b'); break;
+        case 'f': o.push_back('\f'); break;
+        case 'n': o.push_back('\n'); break;
+        case 'r': o.push_back('\r'); break;
+        case 't': o.push_back('\t'); break;
+        case 'u': {
+          uint32_t cp;
+          if (!hex4(s, n, i, cp)) return false;
+          i += 4;
+          if (cp >= 0xD800 && cp < 0xE000) {
+            uint32_t lo = 0;
+            if (cp < 0xDC00 && i + 1 < n && s[i] == '\\' && s[i + 1] == 'u' && hex4(s, n, i + 2, lo) &&
+                lo >= 0xDC00 && lo < 0xE000) {
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+              i += 6;
+            } else {
+              cp = 0xFFFD;
+            }
+          }
+          put_utf8(o, cp);
+          break;
+        }
+        default:
+          return false;
+      }
     }
     node = (uint32_t)d->nodes.size();
-    d->nodes.push_back({J_STR, 0, start, (uint32_t)(d->pool.size() - start)});
-    d->pool.push_back('\0');
+    d->nodes.push_back({J_STR, 0, start, (uint32_t)(o.size() - start)});
+    o.push_back('\0');
     return true;
   }
 
@@ -146,120 +217,103 @@ struct Parser {
     return true;
   }
 
-  bool value(uint32_t& node) {
-    if (++depth > 10000) return false;
-    ws();
-    if (i >= n) return false;
+  // scalar value at s[i] (not a container)
+  bool scalar(uint32_t& node) {
     uint8_t c = s[i];
-    bool ok;
-    if (c == '{') {
-      ok = object(node);
-    } else if (c == '[') {
-      ok = array(node);
-    } else if (c == '"') {
-      ok = string(node);
-    } else if (c == 'n' && i + 4 <= n && memcmp(s + i, "null", 4) == 0) {
+    if (c == '"') return string(node);
+    if (c == 'n' && i + 4 <= n && memcmp(s + i, "null", 4) == 0) {
       i += 4;
       node = (uint32_t)d->nodes.size();
       d->nodes.push_back({J_NULL, 0, 0, 0});
-      ok = true;
-    } else if (c == 't' && i + 4 <= n && memcmp(s + i, "true", 4) == 0) {
+      return true;
+    }
+    if (c == 't' && i + 4 <= n && memcmp(s + i, "true", 4) == 0) {
       i += 4;
       node = (uint32_t)d->nodes.size();
       d->nodes.push_back({J_BOOL, 1, 0, 0});
-      ok = true;
-    } else if (c == 'f' && i + 5 <= n && memcmp(s + i, "false", 5) == 0) {
+      return true;
+    }
+    if (c == 'f' && i + 5 <= n && memcmp(s + i, "false", 5) == 0) {
       i += 5;
       node = (uint32_t)d->nodes.size();
       d->nodes.push_back({J_BOOL, 0, 0, 0});
-      ok = true;
-    } else {
-      ok = number(node);
+      return true;
     }
-    depth--;
-    return ok;
+    return number(node);
   }
 
-  bool object(uint32_t& node) {
-    i++;
-    std::vector<uint32_t> tmp;
+  // frames: (tmp start << 1) | is_object
+  bool run(uint32_t& root) {
+    std::vector<uint64_t>& fr = d->frames;
+    std::vector<uint32_t>& tmp = d->tmp;
+    fr.clear();
+    tmp.clear();
+    uint32_t v = 0;
+    // parse a value; containers push a frame and continue with their first member
+  value:
     ws();
-    if (i < n && s[i] == '}') {
+    if (i >= n) return false;
+    if (s[i] == '{' || s[i] == '[') {
+      bool obj = s[i] == '{';
       i++;
-    } else {
-      while (true) {
-        ws();
-        if (i >= n || s[i] != '"') return false;
-        uint32_t k, v;
-        if (!string(k)) return false;
-        ws();
-        if (i >= n || s[i] != ':') return false;
+      if (fr.size() >= MAX_DEPTH) return false;
+      fr.push_back(((uint64_t)tmp.size() << 1) | (obj ? 1u : 0u));
+      ws();
+      if (i < n && s[i] == (obj ? '}' : ']')) {
         i++;
-        if (!value(v)) return false;
-        tmp.push_back(k);
-        tmp.push_back(v);
-        ws();
-        if (i >= n) return false;
-        if (s[i] == ',') {
-          i++;
-          continue;
-        }
-        if (s[i] == '}') {
-          i++;
-          break;
-        }
-        return false;
+        goto close;
       }
+      if (obj) goto key;
+      goto value;
     }
-    node = (uint32_t)d->nodes.size();
-    d->nodes.push_back({J_OBJ, 0, (uint32_t)d->kids.size(), (uint32_t)(tmp.size() / 2)});
-    d->kids.insert(d->kids.end(), tmp.begin(), tmp.end());
-    return true;
-  }
-
-  bool array(uint32_t& node) {
-    i++;
-    std::vector<uint32_t> tmp;
+    if (!scalar(v)) return false;
+    goto after;
+  key:
     ws();
-    if (i < n && s[i] == ']') {
-      i++;
-    } else {
-      while (true) {
-        uint32_t v;
-        if (!value(v)) return false;
-        tmp.push_back(v);
-        ws();
-        if (i >= n) return false;
-        if (s[i] == ',') {
-          i++;
-          continue;
-        }
-        if (s[i] == ']') {
-          i++;
-          break;
-        }
-        return false;
+    if (i >= n || s[i] != '"') return false;
+    {
+      uint32_t k;
+      if (!string(k)) return false;
+      tmp.push_back(k);
+    }
+    ws();
+    if (i >= n || s[i] != ':') return false;
+    i++;
+    goto value;
+  close : {
+    uint64_t f = fr.back();
+    fr.pop_back();
+    bool obj = f & 1;
+    size_t t0 = (size_t)(f >> 1);
+    v = (uint32_t)d->nodes.size();
+    uint32_t cnt = (uint32_t)(tmp.size() - t0);
+    d->nodes.push_back({obj ? J_OBJ : J_ARR, 0, (uint32_t)d->kids.size(), obj ? cnt / 2 : cnt});
+    d->kids.insert(d->kids.end(), tmp.begin() + t0, tmp.end());
+    tmp.resize(t0);
+  }
+  after:
+    if (fr.empty()) {
+      root = v;
+      return true;
+    }
+    tmp.push_back(v);
+    ws();
+    if (i >= n) return false;
+    {
+      bool obj = fr.back() & 1;
+      if (s[i] == ',') {
+        i++;
+        if (obj) goto key;
+        goto value;
+      }
+      if (s[i] == (obj ? '}' : ']')) {
+        i++;
+        goto close;
       }
     }
-    node = (uint32_t)d->nodes.size();
-    d->nodes.push_back({J_ARR, 0, (uint32_t)d->kids.size(), (uint32_t)tmp.size()});
-    d->kids.insert(d->kids.end(), tmp.begin(), tmp.end());
-    return true;
+    return false;
   }
 };
-
-// ASCII-only case fold (Go's EqualFold on ASCII field names)
-bool fold_eq(const char* a, uint32_t alen, const char* b) {
-  size_t blen = strlen(b);
-  if (alen != blen) return false;
-  for (uint32_t k = 0; k < alen; k++) {
-    char x = a[k], y = b[k];
-    if (x >= 'A' && x <= 'Z') x += 32;
-    if (y >= 'A' && y <= 'Z') y += 32;
-    if (x != y) return false;
-  }
-  return true;
-}
 
 int8_t B64_TAB[256];
 struct B64Init {
@@ -276,56 +330,144 @@ bool JDoc::parse(const uint8_t* p, size_t n) {
   nodes.clear();
   kids.clear();
   pool.clear();
-  nodes.reserve(n / 8 + 8);
-  pool.reserve(n);
-  Parser ps{p, n, 0, this, 0};
+  src = p;
+  Parser ps{p, n, 0, this};
   uint32_t root;
-  if (!ps.value(root)) return false;
+  if (!ps.run(root)) return false;
   ps.ws();
   if (ps.i != n) return false;
-  // root must be the last node pushed; move it to index 0 by convention
-  if (root != nodes.size() - 1) return false;
-  return true;
+  return root == nodes.size() - 1;  // containers close after their children: the root is the last node
+}
+
+// encoding/json fold.go: foldFunc(name) picks equalFoldRight when the name holds
+// k/K/s/S (the key may then spell them U+212A / U+017F), else ASCII case folding
+// (asciiEqualFold == simpleLetterEqualFold on letter-only names).
+bool go_key_matches(const char* key, size_t klen, const char* name, size_t nlen) {
+  if (klen == nlen) {
+    // equal lengths: a match can only be ASCII (U+017F / U+212A are multi-byte),
+    // where every fold function reduces to ASCII case folding of the letters
+    for (size_t k = 0; k < nlen; k++) {
+      uint8_t sb = (uint8_t)name[k], tb = (uint8_t)key[k];
+      if (sb == tb) continue;
+      uint8_t su = sb & 0xDF;
+      if (!(su >= 'A' && su <= 'Z') || su != (tb & 0xDF)) return false;
+    }
+    return true;
+  }
+  if (klen < nlen) return false;
+  bool special = false;
+  for (size_t k = 0; k < nlen; k++) {
+    char c = name[k];
+    special |= (c == 'k' || c == 'K' || c == 's' || c == 'S');
+  }
+  if (!special) return false;
+  // equalFoldRight(name, key)
+  const uint8_t* t = (const uint8_t*)key;
+  size_t tl = klen;
+  for (size_t k = 0; k < nlen; k++) {
+    uint8_t sb = (uint8_t)name[k];
+    if (tl == 0) return false;
+    uint8_t tb = t[0];
+    if (tb < 0x80) {
+      if (sb != tb) {
+        uint8_t su = sb & 0xDF;
+        if (!(su >= 'A' && su <= 'Z') || su != (tb & 0xDF)) return false;
+      }
+      t++;
+      tl--;
+      continue;
+    }
+    size_t sz;
+    uint32_t r = decode_rune(t, tl, sz);
+    if (sb == 's' || sb == 'S') {
+      if (r != 0x017F) return false;
+    } else if (sb == 'k' || sb == 'K') {
+      if (r != 0x212A) return false;
+    } else {
+      return false;
+    }
+    t += sz;
+    tl -= sz;
+  }
+  return tl == 0;
 }
 
 int64_t JDoc::field(uint32_t obj, const char* name) const {
   const JNode& o = nodes[obj];
   if (o.type != J_OBJ) return -1;
+  size_t nlen = strlen(name);
   int64_t found = -1;
   for (uint32_t k = 0; k < o.count; k++) {
     uint32_t key = kids[o.first + 2 * k];
-    if (fold_eq(str(key), nodes[key].count, name)) found = kids[o.first + 2 * k + 1];
+    if (go_key_matches(str(key), nodes[key].count, name, nlen)) found = kids[o.first + 2 * k + 1];
   }
   return found;
 }
 
+bool b64_decode_append(const char* s, size_t n, std::vector<uint8_t>& out) {
+  size_t base = out.size();
+  out.resize(base + n / 4 * 3 + 3);
+  uint8_t* w = out.data() + base;
+  uint32_t q[4];
+  int nq = 0;
+  size_t k = 0;
+  bool done = false;
+  // fast path: whole quanta of alphabet characters
+  while (k + 4 <= n) {
+    int32_t a = B64_TAB[(uint8_t)s[k]], b = B64_TAB[(uint8_t)s[k + 1]], c = B64_TAB[(uint8_t)s[k + 2]],
+            e = B64_TAB[(uint8_t)s[k + 3]];
+    if ((a | b | c | e) < 0) break;
+    uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)e;
+    w[0] = (uint8_t)(v >> 16);
+    w[1] = (uint8_t)(v >> 8);
+    w[2] = (uint8_t)v;
+    w += 3;
+    k += 4;
+  }
+  for (; k < n; k++) {
+    uint8_t c = (uint8_t)s[k];
+    if (c == '\r' || c == '\n') continue;
+    if (c == '=') {
+      // padding: quantum position 2 needs "==", position 3 one '='; then only newlines may follow
+      if (nq < 2) return false;
+      if (nq == 2) {
+        size_t m = k + 1;
+        while (m < n && (s[m] == '\r' || s[m] == '\n')) m++;
+        if (m >= n || s[m] != '=') return false;
+        k = m;
+      }
+      done = true;
+      k++;
+      break;
+    }
+    int8_t v = B64_TAB[c];
+    if (v < 0) return false;
+    q[nq++] = (uint32_t)v;
+    if (nq == 4) {
+      uint32_t a = (q[0] << 18) | (q[1] << 12) | (q[2] << 6) | q[3];
+      w[0] = (uint8_t)(a >> 16);
+      w[1] = (uint8_t)(a >> 8);
+      w[2] = (uint8_t)a;
+      w += 3;
+      nq = 0;
+    }
+  }
+  if (done) {
+    for (; k < n; k++)
+      if (s[k] != '\r' && s[k] != '\n') return false;
+    uint32_t a = (q[0] << 18) | (q[1] << 12) | (nq == 3 ? q[2] << 6 : 0);
+    *w++ = (uint8_t)(a >> 16);
+    if (nq == 3) *w++ = (uint8_t)(a >> 8);
+  } else if (nq != 0) {
+    return false;  // unpadded tail
+  }
+  out.resize((size_t)(w - out.data()));
+  return true;
+}
+
 bool b64_decode(const char* s, size_t n, std::vector<uint8_t>& out) {
   out.clear();
-  std::string t;
-  t.reserve(n);
-  for (size_t k = 0; k < n; k++)
-    if (s[k] != '\r' && s[k] != '\n') t.push_back(s[k]);
-  if (t.size() % 4 != 0) return false;
-  out.reserve(t.size() / 4 * 3);
-  for (size_t q = 0; q < t.size(); q += 4) {
-    bool last = q + 4 == t.size();
-    int pad = 0;
-    if (t[q + 3] == '=') {
-      if (!last) return false;
-      pad = (t[q + 2] == '=') ? 2 : 1;
-    }
-    uint32_t acc = 0;
-    for (int k = 0; k < 4 - pad; k++) {
-      int8_t v = B64_TAB[(uint8_t)t[q + k]];
-      if (v < 0) return false;
-      acc = (acc << 6) | (uint32_t)v;
-    }
-    acc <<= 6 * pad;
-    out.push_back((uint8_t)(acc >> 16));
-    if (pad < 2) out.push_back((uint8_t)(acc >> 8));
-    if (pad < 1) out.push_back((uint8_t)acc);
-  }
-  return true;
+  return b64_decode_append(s, n, out);
 }
 
 void b64_encode(const uint8_t* p, size_t n, std::string& out) {
@@ -396,33 +538,46 @@ DecStatus dec_string(const JDoc& d, int64_t node, std::string& out) {
   return D_OK;
 }
 
+// curve and element of a mathlib element object; D_OK / D_NIL / D_ERR / D_PANIC
+static DecStatus elem_fields(const JDoc& d, int64_t node, int64_t& elem) {
+  if (node < 0 || d.at((uint32_t)node).type == J_NULL) return D_NIL;
+  if (d.at((uint32_t)node).type != J_OBJ) return D_ERR;
+  int64_t curve = 0;
+  if (dec_int(d, d.field((uint32_t)node, "curve"), curve) == D_ERR) return D_ERR;
+  elem = d.field((uint32_t)node, "element");
+  if (elem >= 0 && d.at((uint32_t)elem).type != J_NULL && d.at((uint32_t)elem).type != J_STR) return D_ERR;
+  return curve == 1 ? D_OK : D_PANIC;
+}
+
 ElemBytes dec_elem(const JDoc& d, int64_t node) {
   ElemBytes r;
-  if (node < 0 || d.at((uint32_t)node).type == J_NULL) {
-    r.st = D_NIL;
-    return r;
-  }
-  if (d.at((uint32_t)node).type != J_OBJ) {
-    r.st = D_ERR;
-    return r;
-  }
-  int64_t curve = 0;
-  DecStatus cs = dec_int(d, d.field((uint32_t)node, "curve"), curve);
-  if (cs == D_ERR) {
-    r.st = D_ERR;
-    return r;
-  }
-  DecStatus bs = dec_bytes(d, d.field((uint32_t)node, "element"), r.raw);
-  if (bs == D_ERR) {
-    r.st = D_ERR;
-    return r;
-  }
-  if (curve != 1) {
-    r.st = D_PANIC;
-    return r;
-  }
-  r.st = D_OK;
+  int64_t el = -1;
+  r.st = elem_fields(d, node, el);
+  if (r.st == D_NIL || r.st == D_ERR) return r;
+  DecStatus bs = dec_bytes(d, el, r.raw);
+  if (bs == D_ERR) r.st = D_ERR;  // a bad element string fails Unmarshal before the curve id is used
   return r;
+}
+
+DecStatus dec_elem_into(const JDoc& d, int64_t node, std::vector<uint8_t>& dst, size_t& off, uint32_t& len) {
+  int64_t el = -1;
+  DecStatus st = elem_fields(d, node, el);
+  if (st == D_NIL || st == D_ERR) return st;
+  size_t mark = dst.size();
+  size_t a = (mark + 15) & ~(size_t)15;
+  dst.resize(a, 0);
+  if (el >= 0 && d.at((uint32_t)el).type == J_STR &&
+      !b64_decode_append(d.str((uint32_t)el), d.len((uint32_t)el), dst)) {
+    dst.resize(mark);
+    return D_ERR;
+  }
+  if (st == D_PANIC) {
+    dst.resize(mark);
+    return D_PANIC;
+  }
+  off = a;
+  len = (uint32_t)(dst.size() - a);
+  return D_OK;
 }
 
 }  // namespace ftsh

@@ -1,13 +1,23 @@
 // Go encoding/json restated for the zkatdlog proof wire format (host side of
-// the product boundary).  Semantics reproduced:
-//   * struct fields match object keys exactly or case-insensitively; a later
-//     duplicate key overwrites an earlier one; unknown keys are ignored;
+// the product boundary).  Semantics reproduced (Go 1.18, go.mod:3; SURVEY
+// Appendix C.2):
+//   * struct fields match object keys exactly, else by Go's foldFunc for the
+//     field name (encoding/json/fold.go: ASCII case folding, plus U+017F 'ſ'
+//     for s/S and U+212A Kelvin sign for k/K when the name holds those letters);
+//     a later duplicate key overwrites an earlier one; unknown keys are ignored;
+//   * strings are unquoted as encoding/json unquoteBytes does: escapes decoded,
+//     unpaired surrogates and invalid UTF-8 bytes become U+FFFD (one per byte);
 //   * JSON null leaves pointers / slices nil;
 //   * []byte is standard base64 with padding, '\r' and '\n' skipped;
 //   * mathlib elements are {"curve": <int>, "element": <[]byte>}.
-// The parser builds a flat DOM (node indices into one vector) per document.
+// The parser is iterative (nesting up to Go's maxNestingDepth = 10000) and
+// builds a flat DOM (node indices into one vector) per document; a JDoc keeps
+// its buffers between documents, so a planner thread parses without
+// allocating once warm.
 #pragma once
 #include <stdint.h>
+#include <string.h>
+
 #include <string>
 #include <vector>
 
@@ -18,7 +28,8 @@ enum JType : uint8_t { J_NULL, J_BOOL, J_NUM, J_STR, J_ARR, J_OBJ };
 struct JNode {
   JType type;
   uint8_t bval;
-  uint32_t first;   // ARR/OBJ: index of first child in kids[]; STR/NUM: offset into text pool
+  uint32_t first;   // ARR/OBJ: index of first child in kids[]; NUM, STR: offset into the text pool
+                    // (STR with bval = 1: offset into the parsed source text)
   uint32_t count;   // ARR/OBJ: number of children; STR/NUM: length
 };
 
@@ -26,19 +37,30 @@ struct JDoc {
   std::vector<JNode> nodes;
   std::vector<uint32_t> kids;      // OBJ: pairs (key node, value node); ARR: value nodes
   std::string pool;                // unescaped strings and number tokens
+  std::vector<uint32_t> tmp;       // parser scratch (children of open containers)
+  std::vector<uint64_t> frames;    // parser scratch (open containers)
   bool parse(const uint8_t* p, size_t n);  // false on syntax error
 
   uint32_t root() const { return (uint32_t)nodes.size() - 1; }
   const JNode& at(uint32_t i) const { return nodes[i]; }
   // Go struct-field lookup on an object node: returns node index or -1
   int64_t field(uint32_t obj, const char* name) const;
-  const char* str(uint32_t i) const { return pool.data() + nodes[i].first; }
+  const uint8_t* src = nullptr;    // text of the last parse (plain strings point into it)
+  const char* str(uint32_t i) const {
+    return nodes[i].type == J_STR && nodes[i].bval ? (const char*)src + nodes[i].first : pool.data() + nodes[i].first;
+  }
   uint32_t len(uint32_t i) const { return nodes[i].count; }
   uint32_t elem(uint32_t arr, uint32_t k) const { return kids[nodes[arr].first + k]; }
 };
 
-// base64.StdEncoding.DecodeString ('\r','\n' skipped); false if illegal
+// Go encoding/json field matching of an (unescaped) object key against an
+// ASCII struct field name.
+bool go_key_matches(const char* key, size_t klen, const char* name, size_t nlen);
+
+// base64.StdEncoding.DecodeString ('\r','\n' skipped); false if illegal.
+// b64_decode_append appends to `out` (which keeps its earlier contents).
 bool b64_decode(const char* s, size_t n, std::vector<uint8_t>& out);
+bool b64_decode_append(const char* s, size_t n, std::vector<uint8_t>& out);
 void b64_encode(const uint8_t* p, size_t n, std::string& out);
 
 // Result of decoding a JSON value into a Go field of the given kind.
@@ -52,6 +74,9 @@ struct ElemBytes {
 // mathlib element (Zr/G1/G2) UnmarshalJSON: curve must be BN254 (= 1); any
 // other id makes the reference panic on first use (driver type assertion).
 ElemBytes dec_elem(const JDoc& d, int64_t node);
+// Same, decoding the element bytes straight into `dst` at a 16-byte aligned
+// offset (returned in off/len; dst is restored on error).
+DecStatus dec_elem_into(const JDoc& d, int64_t node, std::vector<uint8_t>& dst, size_t& off, uint32_t& len);
 // []byte field
 DecStatus dec_bytes(const JDoc& d, int64_t node, std::vector<uint8_t>& out);
 // int field (Go: number without fraction/exponent)

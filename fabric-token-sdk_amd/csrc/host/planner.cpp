@@ -16,7 +16,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
+#include <type_traits>
 
 #include "gojson.h"
 
@@ -61,14 +65,15 @@ struct Ref {
 // syntax errors are reported before any element is decoded; an element whose
 // UnmarshalJSON would panic (foreign curve) marks `panic`; element / type
 // errors mark `err` (the reference's Unmarshal returns the first error).
+// The JDoc is borrowed from the builder so its buffers are reused.
 struct Doc {
-  JDoc d;
+  JDoc& d;
   bool ok = false;
   bool panic = false;
   bool err = false;
   Plan* pl;
 
-  explicit Doc(Plan* p) : pl(p) {}
+  Doc(Plan* p, JDoc& jd) : d(jd), pl(p) {}
 
   bool parse(const std::vector<uint8_t>& b, bool nil) {
     if (nil) return ok = false;  // json.Unmarshal(nil) -> "unexpected end of JSON input"
@@ -79,23 +84,25 @@ struct Doc {
   Ref elem(int64_t node) {
     Ref r;
     if (node < 0 || d.at((uint32_t)node).type == J_NULL) return r;
-    ElemBytes e = dec_elem(d, node);
-    if (e.st == D_ERR) {
+    size_t off = 0;
+    uint32_t len = 0;
+    // element bytes land 16-byte aligned in the wire pool (device vector loads)
+    DecStatus st = dec_elem_into(d, node, pl->wire, off, len);
+    if (st == D_ERR) {
       err = true;
       return r;
     }
-    if (e.st == D_PANIC) {
+    if (st == D_PANIC) {
       panic = true;
       return r;
     }
-    if (e.raw.size() > ZR_MAX_LEN) {  // beyond the device decoder's range
+    if (len > ZR_MAX_LEN) {  // beyond the device decoder's range
+      pl->wire.resize(off);
       err = true;
       return r;
     }
-    pl->wire.resize((pl->wire.size() + 15) & ~(size_t)15, 0);  // 16-byte aligned element (vector loads)
-    r.off = (int64_t)pl->wire.size();
-    r.len = (uint32_t)e.raw.size();
-    pl->wire.insert(pl->wire.end(), e.raw.begin(), e.raw.end());
+    r.off = (int64_t)off;
+    r.len = len;
     return r;
   }
 
@@ -173,6 +180,8 @@ class Builder {
  private:
   Plan& pl;
   const PPInfo& pp;
+  JDoc jtop, jwf, jrc;                 // parse buffers, reused across proofs
+  std::vector<uint8_t> wfb, rcb;       // base64-decoded inner documents
   TxChecks tc;
   int part = 0;  // 0: WF part, 1: range part
   uint32_t ncheck[2];
@@ -414,7 +423,7 @@ static constexpr uint32_t DIGIT_SLOT = 64 + 64 + 384 + SIG_JSON_LEN;       // 74
 void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t out_pt, uint32_t out_bytes,
                          uint32_t n) {
   begin_range();
-  Doc doc(&pl);
+  Doc doc(&pl, jrc);
   if (!doc.parse(rc, rc_nil)) {
     fail(E_PARSE);
     return;
@@ -604,10 +613,9 @@ void Builder::transfer(const TransferIn& t) {
   if (t.n_in + t.n_out) check(CK_PTS, E_PARSE, tok_pt, t.n_in + t.n_out);
 
   // transfer.Proof JSON (transfer.go:125-129)
-  std::vector<uint8_t> wfb, rcb;
   bool wf_nil = true, rc_nil = true;
   {
-    JDoc top;
+    JDoc& top = jtop;
     if (!top.parse(t.proof, t.proof_len)) {
       fail(E_PARSE);
       end_tx();
@@ -632,7 +640,7 @@ void Builder::transfer(const TransferIn& t) {
   }
   // WellFormednessVerifier.Verify (wellformedness.go:311-351)
   {
-    Doc doc(&pl);
+    Doc doc(&pl, jwf);
     if (!doc.parse(wfb, wf_nil)) {
       fail(E_PARSE);
     } else {
@@ -681,10 +689,9 @@ void Builder::issue(const IssueIn& t) {
   uint32_t tok_pt = tokens(t.outputs, t.n_out, tok_bytes);
   if (t.n_out) check(CK_PTS, E_PARSE, tok_pt, t.n_out);
   uint32_t n = t.n_out;
-  std::vector<uint8_t> wfb, rcb;
   bool wf_nil = true, rc_nil = true;
   {
-    JDoc top;
+    JDoc& top = jtop;
     if (!top.parse(t.proof, t.proof_len)) {
       fail(E_PARSE);
       end_tx();
@@ -708,7 +715,7 @@ void Builder::issue(const IssueIn& t) {
     }
   }
   // issue WellFormednessVerifier.Verify (issue/wellformedness.go:206-265)
-  Doc doc(&pl);
+  Doc doc(&pl, jwf);
   if (!doc.parse(wfb, wf_nil)) {
     fail(E_PARSE);
     end_tx();
@@ -793,28 +800,152 @@ void Builder::issue(const IssueIn& t) {
 
 }  // namespace
 
-// Append piece `b` (local indices) to plan `a`, relocating every index.
-void plan_merge(Plan& a, const Plan& b) {
-  a.arena.resize((a.arena.size() + 15) & ~(size_t)15, 0);  // keep the pieces' 16-byte alignment
-  a.wire.resize((a.wire.size() + 15) & ~(size_t)15, 0);
-  uint32_t o_wire = (uint32_t)a.wire.size(), o_arena = (uint32_t)a.arena.size();
-  uint32_t o_pts = a.n_pts, o_scal = a.n_scal, o_g1 = a.n_g1out, o_g2 = a.n_g2out;
-  uint32_t o_list = (uint32_t)a.sclist.size(), o_vt = (uint32_t)a.vt.size(), o_seg = (uint32_t)a.seg.size();
-  uint32_t o_hmain = (uint32_t)a.hmain.size(), o_ck = (uint32_t)a.ck.size();
-  auto rel = [](uint32_t v, uint32_t o) { return v == NONE ? NONE : v + o; };
-  a.wire.insert(a.wire.end(), b.wire.begin(), b.wire.end());
-  a.arena.insert(a.arena.end(), b.arena.begin(), b.arena.end());
+// ------------------------------------------------------------------ work pool
+struct WorkPool::State {
+  std::mutex run_mu;  // one run() at a time
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  const std::function<void(size_t)>* fn = nullptr;
+  size_t n = 0;
+  std::atomic<size_t> next{0};
+  size_t gen = 0, active = 0;
+  bool stop = false;
+  std::vector<std::thread> th;
+};
+
+WorkPool::WorkPool(int threads) : st_(new State()), nthreads_(std::max(0, threads - 1)) {
+  for (int t = 0; t < nthreads_; t++) {
+    st_->th.emplace_back([this]() {
+      State& s = *st_;
+      size_t seen = 0;
+      while (true) {
+        std::unique_lock<std::mutex> lk(s.mu);
+        s.cv.wait(lk, [&]() { return s.stop || s.gen != seen; });
+        if (s.stop) return;
+        seen = s.gen;
+        const std::function<void(size_t)>* f = s.fn;
+        size_t n = s.n;
+        lk.unlock();
+        for (size_t i; (i = s.next.fetch_add(1)) < n;) (*f)(i);
+        lk.lock();
+        if (--s.active == 0) s.done_cv.notify_all();
+      }
+    });
+  }
+}
+
+WorkPool::~WorkPool() {
+  {
+    std::lock_guard<std::mutex> lk(st_->mu);
+    st_->stop = true;
+  }
+  st_->cv.notify_all();
+  for (auto& t : st_->th) t.join();
+  delete st_;
+}
+
+void WorkPool::run(size_t n, const std::function<void(size_t)>& f) {
+  if (n == 0) return;
+  State& s = *st_;
+  std::lock_guard<std::mutex> rl(s.run_mu);
+  if (nthreads_ == 0 || n == 1) {
+    for (size_t i = 0; i < n; i++) f(i);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(s.mu);
+    s.fn = &f;
+    s.n = n;
+    s.next.store(0);
+    s.active = (size_t)nthreads_;
+    s.gen++;
+  }
+  s.cv.notify_all();
+  for (size_t i; (i = s.next.fetch_add(1)) < n;) f(i);
+  std::unique_lock<std::mutex> lk(s.mu);
+  s.done_cv.wait(lk, [&]() { return s.active == 0; });
+}
+
+// ------------------------------------------------------------------ flat plans
+namespace {
+
+constexpr size_t SEC_ALIGN = 256;
+constexpr size_t IDX_LIMIT = (size_t)1 << 31;  // Seg.off uses bit 31 (CONST_FLAG); NONE is 2^32 - 1
+
+size_t elem_size(int s) {
+  switch (s) {
+    case PS_WIRE: case PS_ARENA: case PS_OUT: return 1;
+    case PS_DEC: return sizeof(DecodeJob);
+    case PS_ZR: return sizeof(ZrJob);
+    case PS_SC: case PS_SC1: case PS_SCPOST: return sizeof(ScalJob);
+    case PS_SCLIST: return sizeof(uint32_t);
+    case PS_VT: return sizeof(VTerm);
+    case PS_G1: case PS_G1P: return sizeof(G1Job);
+    case PS_G2: return sizeof(G2Job);
+    case PS_PR: return sizeof(PairJob);
+    case PS_SEG: return sizeof(Seg);
+    case PS_HPRE: case PS_HMAIN: return sizeof(HashJob);
+    case PS_CK: return sizeof(Check);
+    case PS_TX: return sizeof(TxChecks);
+    case PS_RND: return sizeof(RandJob);
+    case PS_EMIT: return sizeof(EmitJob);
+    case PS_B64: return sizeof(B64Job);
+  }
+  return 1;
+}
+
+size_t piece_count(const Plan& p, int s) {
+  switch (s) {
+    case PS_WIRE: return p.wire.size();
+    case PS_ARENA: return p.arena.size();
+    case PS_DEC: return p.dec.size();
+    case PS_ZR: return p.zr.size();
+    case PS_SC: return p.sc.size();
+    case PS_SCLIST: return p.sclist.size();
+    case PS_VT: return p.vt.size();
+    case PS_G1: return p.g1.size();
+    case PS_G1P: return p.g1p.size();
+    case PS_G2: return p.g2.size();
+    case PS_PR: return p.pr.size();
+    case PS_SEG: return p.seg.size();
+    case PS_HPRE: return p.hpre.size();
+    case PS_HMAIN: return p.hmain.size();
+    case PS_CK: return p.ck.size();
+    case PS_TX: return p.tx.size();
+    case PS_RND: return p.rnd.size();
+    case PS_SC1: return p.sc1.size();
+    case PS_SCPOST: return p.sc_post.size();
+    case PS_EMIT: return p.emit.size();
+    case PS_B64: return p.b64.size();
+    case PS_OUT: return p.out.size();
+  }
+  return 0;
+}
+
+// Piece `b` (indices local to b) written at its place in the flat plan with
+// every index relocated.
+void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8_t* blob) {
+  const uint32_t o_wire = (uint32_t)o.sec[PS_WIRE], o_arena = (uint32_t)o.sec[PS_ARENA];
+  const uint32_t o_pts = o.pts, o_scal = o.scal, o_g1 = o.g1out, o_g2 = o.g2out;
+  const uint32_t o_list = (uint32_t)o.sec[PS_SCLIST], o_vt = (uint32_t)o.sec[PS_VT], o_seg = (uint32_t)o.sec[PS_SEG];
+  const uint32_t o_hmain = (uint32_t)o.sec[PS_HMAIN], o_ck = (uint32_t)o.sec[PS_CK], o_out = (uint32_t)o.sec[PS_OUT];
+  auto rel = [](uint32_t v, uint32_t off) { return v == NONE ? NONE : v + off; };
+  if (!b.wire.empty()) memcpy(blob + fp.off[PS_WIRE] + o_wire, b.wire.data(), b.wire.size());
+  if (!b.arena.empty()) memcpy(blob + fp.off[PS_ARENA] + o_arena, b.arena.data(), b.arena.size());
+  if (!b.out.empty()) memcpy(blob + fp.off[PS_OUT] + o_out, b.out.data(), b.out.size());
+  DecodeJob* dec = fp.ptr<DecodeJob>(blob, PS_DEC) + o.sec[PS_DEC];
   for (DecodeJob j : b.dec) {
     j.raw += o_wire;
     j.out += o_pts;
     j.bytes = rel(j.bytes, o_arena);
     j.b64 = rel(j.b64, o_arena);
-    a.dec.push_back(j);
+    *dec++ = j;
   }
+  ZrJob* zr = fp.ptr<ZrJob>(blob, PS_ZR) + o.sec[PS_ZR];
   for (ZrJob j : b.zr) {
     j.raw += o_wire;
     j.out += o_scal;
-    a.zr.push_back(j);
+    *zr++ = j;
   }
   auto rel_sc = [&](ScalJob j) {
     if (j.op == SOP_SUM) {
@@ -827,15 +958,22 @@ void plan_merge(Plan& a, const Plan& b) {
     j.out += o_scal;
     return j;
   };
-  for (const ScalJob& j : b.sc) a.sc.push_back(rel_sc(j));
-  for (const ScalJob& j : b.sc1) a.sc1.push_back(rel_sc(j));
-  for (const ScalJob& j : b.sc_post) a.sc_post.push_back(rel_sc(j));
-  for (uint32_t v : b.sclist) a.sclist.push_back(v + o_scal);
+  const int scs[3] = {PS_SC, PS_SC1, PS_SCPOST};
+  const std::vector<ScalJob>* scv[3] = {&b.sc, &b.sc1, &b.sc_post};
+  for (int k = 0; k < 3; k++) {
+    ScalJob* d = fp.ptr<ScalJob>(blob, (PlanSec)scs[k]) + o.sec[scs[k]];
+    for (const ScalJob& j : *scv[k]) *d++ = rel_sc(j);
+  }
+  uint32_t* sl = fp.ptr<uint32_t>(blob, PS_SCLIST) + o.sec[PS_SCLIST];
+  for (uint32_t v : b.sclist) *sl++ = v + o_scal;
+  VTerm* vt = fp.ptr<VTerm>(blob, PS_VT) + o.sec[PS_VT];
   for (VTerm v : b.vt) {
     v.pt += o_pts;
-    a.vt.push_back(v);
+    *vt++ = v;
   }
   for (int side = 0; side < 2; side++) {
+    int sec = side ? PS_G1P : PS_G1;
+    G1Job* d = fp.ptr<G1Job>(blob, (PlanSec)sec) + o.sec[sec];
     for (G1Job j : (side ? b.g1p : b.g1)) {
       for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
       j.vstart += o_vt;
@@ -843,105 +981,233 @@ void plan_merge(Plan& a, const Plan& b) {
       j.out += o_g1;
       j.bytes = rel(j.bytes, o_arena);
       j.b64 = rel(j.b64, o_arena);
-      (side ? a.g1p : a.g1).push_back(j);
+      *d++ = j;
     }
   }
+  G2Job* g2 = fp.ptr<G2Job>(blob, PS_G2) + o.sec[PS_G2];
   for (G2Job j : b.g2) {
     for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
     j.out += o_g2;
-    a.g2.push_back(j);
+    *g2++ = j;
   }
+  PairJob* pr = fp.ptr<PairJob>(blob, PS_PR) + o.sec[PS_PR];
   for (PairJob j : b.pr) {
     j.p1 += o_g1;
-    j.p2 += a.p2_g1out ? o_g1 : o_pts;
+    j.p2 += fp.p2_g1out ? o_g1 : o_pts;
     j.q2 += o_g2;
     j.bytes += o_arena;
-    a.pr.push_back(j);
+    *pr++ = j;
   }
+  Seg* sg = fp.ptr<Seg>(blob, PS_SEG) + o.sec[PS_SEG];
   for (Seg s : b.seg) {
     if (s.off & CONST_FLAG)
       s.off &= ~CONST_FLAG;  // const region sits at absolute offset 0
     else
       s.off += o_arena;
-    a.seg.push_back(s);
+    *sg++ = s;
   }
-  for (HashJob h : b.hpre) {
-    h.seg_start += o_seg;
-    h.expect = rel(h.expect, o_scal);
-    h.out_scal = rel(h.out_scal, o_scal);
-    a.hpre.push_back(h);
+  const int hs[2] = {PS_HPRE, PS_HMAIN};
+  const std::vector<HashJob>* hv[2] = {&b.hpre, &b.hmain};
+  for (int k = 0; k < 2; k++) {
+    HashJob* d = fp.ptr<HashJob>(blob, (PlanSec)hs[k]) + o.sec[hs[k]];
+    for (HashJob h : *hv[k]) {
+      h.seg_start += o_seg;
+      h.expect = rel(h.expect, o_scal);
+      h.out_scal = rel(h.out_scal, o_scal);
+      *d++ = h;
+    }
   }
-  for (HashJob h : b.hmain) {
-    h.seg_start += o_seg;
-    h.expect = rel(h.expect, o_scal);
-    h.out_scal = rel(h.out_scal, o_scal);
-    a.hmain.push_back(h);
-  }
+  Check* ck = fp.ptr<Check>(blob, PS_CK) + o.sec[PS_CK];
   for (Check c : b.ck) {
     if (c.kind == CK_PTS) c.a += o_pts;
     if (c.kind == CK_HASH) c.a += o_hmain;
-    a.ck.push_back(c);
+    *ck++ = c;
   }
+  TxChecks* tx = fp.ptr<TxChecks>(blob, PS_TX) + o.sec[PS_TX];
   for (TxChecks t : b.tx) {
     t.wf_start += o_ck;
     t.rg_start += o_ck;
-    a.tx.push_back(t);
+    *tx++ = t;
   }
-  // prover pieces
+  RandJob* rnd = fp.ptr<RandJob>(blob, PS_RND) + o.sec[PS_RND];
   for (RandJob j : b.rnd) {
     j.seed += o_arena;
     j.tag += o_arena;
     j.out += o_scal;
-    a.rnd.push_back(j);
+    *rnd++ = j;
   }
+  EmitJob* em = fp.ptr<EmitJob>(blob, PS_EMIT) + o.sec[PS_EMIT];
   for (EmitJob j : b.emit) {
     j.dst += o_arena;
     j.src += j.kind == EM_ZR ? o_scal : o_arena;
-    a.emit.push_back(j);
+    *em++ = j;
   }
-  uint32_t o_out = (uint32_t)a.out.size();
+  B64Job* bj = fp.ptr<B64Job>(blob, PS_B64) + o.sec[PS_B64];
   for (B64Job j : b.b64) {
     j.src += o_arena;
     j.dst += o_out;
-    a.b64.push_back(j);
+    *bj++ = j;
   }
-  a.out.insert(a.out.end(), b.out.begin(), b.out.end());
-  for (uint32_t v : b.out_off) a.out_off.push_back(v + o_out);
-  a.n_pts += b.n_pts;
-  a.n_scal += b.n_scal;
-  a.n_g1out += b.n_g1out;
-  a.n_g2out += b.n_g2out;
+}
+
+}  // namespace
+
+std::string flat_layout(const PlanWork& w, bool p2_g1out, FlatPlan& fp) {
+  fp.p2_g1out = p2_g1out;
+  fp.base.assign(w.used, PieceBase{});
+  fp.out_off.clear();
+  fp.n_items = 0;
+  size_t cur[PS_COUNT] = {};
+  cur[PS_ARENA] = C_SIZE;
+  uint64_t pts = 0, scal = 0, g1 = 0, g2 = 0;
+  for (size_t k = 0; k < w.used; k++) {
+    const Plan& p = w.pieces[k];
+    PieceBase& b = fp.base[k];
+    cur[PS_WIRE] = (cur[PS_WIRE] + 15) & ~(size_t)15;  // keep the pieces' 16-byte alignment
+    cur[PS_ARENA] = (cur[PS_ARENA] + 15) & ~(size_t)15;
+    for (int s = 0; s < PS_COUNT; s++) {
+      b.sec[s] = cur[s];
+      cur[s] += piece_count(p, s);
+    }
+    b.pts = (uint32_t)pts;
+    b.scal = (uint32_t)scal;
+    b.g1out = (uint32_t)g1;
+    b.g2out = (uint32_t)g2;
+    pts += p.n_pts;
+    scal += p.n_scal;
+    g1 += p.n_g1out;
+    g2 += p.n_g2out;
+    for (uint32_t v : p.out_off) fp.out_off.push_back((uint32_t)(v + b.sec[PS_OUT]));
+    fp.n_items += p.tx.size();
+  }
+  if (!fp.out_off.empty() || cur[PS_OUT]) fp.out_off.push_back((uint32_t)cur[PS_OUT]);
+  for (int s = 0; s < PS_COUNT; s++)
+    if (cur[s] >= IDX_LIMIT) return "batch too large for 32-bit job indices (split it into smaller batches)";
+  if (pts >= IDX_LIMIT || scal >= IDX_LIMIT || g1 >= IDX_LIMIT || g2 >= IDX_LIMIT)
+    return "batch too large for 32-bit job indices (split it into smaller batches)";
+  fp.n_pts = (uint32_t)pts;
+  fp.n_scal = (uint32_t)scal;
+  fp.n_g1out = (uint32_t)g1;
+  fp.n_g2out = (uint32_t)g2;
+  size_t off = 0;
+  for (int s = 0; s < PS_COUNT; s++) {
+    fp.cnt[s] = cur[s];
+    fp.off[s] = off;
+    size_t bytes = cur[s] * elem_size(s) + (s == PS_WIRE ? WIRE_TAIL : 0);
+    off = (off + bytes + SEC_ALIGN - 1) & ~(SEC_ALIGN - 1);
+  }
+  fp.bytes = std::max<size_t>(off, SEC_ALIGN);
+  return "";
+}
+
+void flat_write(const PlanWork& w, const FlatPlan& fp, uint8_t* blob, const uint8_t* const_bytes, WorkPool& pool) {
+  memcpy(blob + fp.off[PS_ARENA], const_bytes, C_SIZE);
+  memset(blob + fp.off[PS_WIRE] + fp.cnt[PS_WIRE], 0, WIRE_TAIL);
+  pool.run(w.used, [&](size_t k) {
+    const Plan& p = w.pieces[k];
+    const PieceBase& b = fp.base[k];
+    // zero the alignment gap in front of the piece's byte pools
+    size_t prev_w = k ? fp.base[k - 1].sec[PS_WIRE] + w.pieces[k - 1].wire.size() : 0;
+    size_t prev_a = k ? fp.base[k - 1].sec[PS_ARENA] + w.pieces[k - 1].arena.size() : C_SIZE;
+    memset(blob + fp.off[PS_WIRE] + prev_w, 0, b.sec[PS_WIRE] - prev_w);
+    memset(blob + fp.off[PS_ARENA] + prev_a, 0, b.sec[PS_ARENA] - prev_a);
+    relocate_piece(p, b, fp, blob);
+  });
+}
+
+void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out) {
+  out.clear();
+  auto take = [&](auto& v, PlanSec s) {
+    using T = typename std::remove_reference<decltype(v)>::type::value_type;
+    const T* p = reinterpret_cast<const T*>(blob + fp.off[s]);
+    v.assign(p, p + fp.cnt[s]);
+  };
+  take(out.wire, PS_WIRE);
+  out.wire.insert(out.wire.end(), blob + fp.off[PS_WIRE] + fp.cnt[PS_WIRE],
+                  blob + fp.off[PS_WIRE] + fp.cnt[PS_WIRE] + WIRE_TAIL);
+  take(out.arena, PS_ARENA);
+  take(out.dec, PS_DEC);
+  take(out.zr, PS_ZR);
+  take(out.sc, PS_SC);
+  take(out.sclist, PS_SCLIST);
+  take(out.vt, PS_VT);
+  take(out.g1, PS_G1);
+  take(out.g1p, PS_G1P);
+  take(out.g2, PS_G2);
+  take(out.pr, PS_PR);
+  take(out.seg, PS_SEG);
+  take(out.hpre, PS_HPRE);
+  take(out.hmain, PS_HMAIN);
+  take(out.ck, PS_CK);
+  take(out.tx, PS_TX);
+  take(out.rnd, PS_RND);
+  take(out.sc1, PS_SC1);
+  take(out.sc_post, PS_SCPOST);
+  take(out.emit, PS_EMIT);
+  take(out.b64, PS_B64);
+  take(out.out, PS_OUT);
+  out.out_off = fp.out_off;
+  out.p2_g1out = fp.p2_g1out;
+  out.n_pts = fp.n_pts;
+  out.n_scal = fp.n_scal;
+  out.n_g1out = fp.n_g1out;
+  out.n_g2out = fp.n_g2out;
+}
+
+// items per piece: at least 32, at most one piece per pool thread
+size_t plan_piece_count(size_t n, int threads) {
+  return std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), n / 32));
+}
+
+void plan_items(const PPInfo& pp, size_t n, const PlanItem* items, PlanWork& w, WorkPool& pool) {
+  size_t np = plan_piece_count(n, pool.size());
+  if (w.pieces.size() < np) w.pieces.resize(np);
+  w.used = np;
+  pool.run(np, [&](size_t c) {
+    Plan& p = w.pieces[c];
+    p.clear();
+    size_t lo = n * c / np, hi = n * (c + 1) / np;
+    Builder b(p, pp);
+    for (size_t i = lo; i < hi; i++) {
+      if (items[i].kind == 0)
+        b.transfer(items[i].t);
+      else
+        b.issue(items[i].i);
+    }
+  });
 }
 
 namespace {
 
-template <class In, class Fn>
-void plan_batch(const PPInfo& pp, size_t n, const In* in, Plan& out, int threads, Fn fn) {
-  out.clear();
-  out.arena.resize(C_SIZE, 0);
-  if (threads < 1) threads = 1;
-  size_t chunks = std::min<size_t>((size_t)threads, std::max<size_t>(1, n / 64));
-  std::vector<Plan> pieces(chunks);
-  std::vector<std::thread> th;
-  for (size_t c = 0; c < chunks; c++) {
-    size_t lo = n * c / chunks, hi = n * (c + 1) / chunks;
-    th.emplace_back([&, c, lo, hi]() {
-      Builder b(pieces[c], pp);
-      for (size_t i = lo; i < hi; i++) fn(b, in[i]);
-    });
+template <class In>
+void plan_merged(const PPInfo& pp, size_t n, const In* in, Plan& out, int threads, uint8_t kind) {
+  std::vector<PlanItem> items(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&items[i], 0, sizeof(PlanItem));
+    items[i].kind = kind;
+    if constexpr (std::is_same<In, TransferIn>::value)
+      items[i].t = in[i];
+    else
+      items[i].i = in[i];
   }
-  for (auto& t : th) t.join();
-  for (auto& p : pieces) plan_merge(out, p);
+  WorkPool pool(threads);
+  PlanWork w;
+  plan_items(pp, n, items.data(), w, pool);
+  FlatPlan fp;
+  flat_layout(w, false, fp);
+  std::vector<uint8_t> blob(fp.bytes);
+  flat_write(w, fp, blob.data(), std::vector<uint8_t>(C_SIZE, 0).data(), pool);
+  plan_unflatten(fp, blob.data(), out);
 }
 
 }  // namespace
 
 void plan_transfers(const PPInfo& pp, size_t n, const TransferIn* tx, Plan& out, int threads) {
-  plan_batch(pp, n, tx, out, threads, [](Builder& b, const TransferIn& t) { b.transfer(t); });
+  plan_merged(pp, n, tx, out, threads, 0);
 }
 
 void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int threads) {
-  plan_batch(pp, n, is, out, threads, [](Builder& b, const IssueIn& t) { b.issue(t); });
+  plan_merged(pp, n, is, out, threads, 1);
 }
 
 // ------------------------------------------------------------------ public params

@@ -2,6 +2,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -82,13 +83,86 @@ struct IssueIn {
   uint8_t anonymous;
 };
 
-// Build a plan for a batch (multi-threaded over proofs).  Arena offsets in the
-// plan are absolute: the const region occupies [0, C_SIZE).
+// One proof of a (possibly mixed) verification batch: a block of a ledger
+// carries transfer and issue actions side by side.
+struct PlanItem {
+  uint8_t kind;  // 0: transfer, 1: issue
+  TransferIn t;
+  IssueIn i;
+};
+
+// A small persistent pool of host threads; run(n, f) calls f(0..n-1) across
+// the pool and the caller and returns when all calls are done.  Concurrent
+// run() calls are serialised.
+class WorkPool {
+ public:
+  explicit WorkPool(int threads);
+  ~WorkPool();
+  WorkPool(const WorkPool&) = delete;
+  WorkPool& operator=(const WorkPool&) = delete;
+  void run(size_t n, const std::function<void(size_t)>& f);
+  int size() const { return nthreads_ + 1; }
+
+ private:
+  struct State;
+  State* st_;
+  int nthreads_;
+};
+
+// Sections of a flattened plan: every job array and byte pool of a batch at a
+// 256-byte aligned offset of ONE blob, so that a batch is one host->device copy
+// (from pinned memory) and the device pointers are blob + offset.
+enum PlanSec : int {
+  PS_WIRE, PS_ARENA, PS_DEC, PS_ZR, PS_SC, PS_SCLIST, PS_VT, PS_G1, PS_G1P, PS_G2, PS_PR, PS_SEG, PS_HPRE,
+  PS_HMAIN, PS_CK, PS_TX, PS_RND, PS_SC1, PS_SCPOST, PS_EMIT, PS_B64, PS_OUT, PS_COUNT
+};
+static constexpr size_t WIRE_TAIL = 64;  // zero bytes after the wire pool (decode jobs may read past a short element)
+
+// Where each per-thread piece lands in the flat plan.
+struct PieceBase {
+  size_t sec[PS_COUNT];               // element index (bytes for WIRE/ARENA/OUT) within each section
+  uint32_t pts, scal, g1out, g2out;   // value-index bases
+};
+
+struct FlatPlan {
+  size_t off[PS_COUNT] = {};  // byte offset of each section in the blob
+  size_t cnt[PS_COUNT] = {};  // elements (bytes for WIRE / ARENA / OUT)
+  size_t bytes = 0;           // blob size
+  size_t n_items = 0;
+  uint32_t n_pts = 0, n_scal = 0, n_g1out = 0, n_g2out = 0;
+  bool p2_g1out = false;      // prover plans: PairJob.p2 indexes g1out
+  std::vector<PieceBase> base;
+  std::vector<uint32_t> out_off;  // prover: per item start in OUT, plus the end
+  template <class T>
+  T* ptr(uint8_t* blob, PlanSec s) const { return reinterpret_cast<T*>(blob + off[s]); }
+};
+
+// Reusable planning state of one batch slot: per-thread pieces keep their
+// buffers between batches, so steady-state planning does not allocate.
+struct PlanWork {
+  std::vector<Plan> pieces;
+  std::vector<std::string> errs;
+  size_t used = 0;  // pieces of the current batch
+};
+
+// pieces a batch of n items is planned in (one per pool thread, >= 32 items each)
+size_t plan_piece_count(size_t n, int threads);
+// Plan n items into w's pieces (items split into contiguous ranges, one per
+// piece, run on the pool).
+void plan_items(const PPInfo& pp, size_t n, const PlanItem* items, PlanWork& w, WorkPool& pool);
+// Offsets of every section and piece.  Returns "" or an error when a pool of
+// the batch would overflow the 32-bit indices the device jobs use.
+std::string flat_layout(const PlanWork& w, bool p2_g1out, FlatPlan& fp);
+// Write the relocated pieces into blob (fp.bytes), the const region first:
+// the caller's C_SIZE const bytes, the zero wire tail.  Parallel over pieces.
+void flat_write(const PlanWork& w, const FlatPlan& fp, uint8_t* blob, const uint8_t* const_bytes, WorkPool& pool);
+
+// Merged single-Plan form (test-only host emulation): plan, flatten and copy
+// the sections back into `out`'s vectors (same relocation code as the device
+// path).  Arena offsets are absolute: the const region occupies [0, C_SIZE).
 void plan_transfers(const PPInfo& pp, size_t n, const TransferIn* tx, Plan& out, int threads);
 void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int threads);
-
-// Append piece b (indices local to b) to a, relocating every index.
-void plan_merge(Plan& a, const Plan& b);
+void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out);
 
 // ------------------------------------------------------------------ prover
 // Witness of one transfer / issue (token.TokenDataWitness: Type, Value,
@@ -120,5 +194,9 @@ struct IssueWit {
 // error ("proof i: ...", e.g. a value outside [0, base^exponent)).
 std::string plan_prove_transfers(const PPInfo& pp, size_t n, const TransferWit* w, Plan& out, int threads);
 std::string plan_prove_issues(const PPInfo& pp, size_t n, const IssueWit* w, Plan& out, int threads);
+// Piece form (the runtime's slots): returns "" or the first witness error.
+std::string plan_prove_items_transfers(const PPInfo& pp, size_t n, const TransferWit* wit, PlanWork& w,
+                                       WorkPool& pool);
+std::string plan_prove_items_issues(const PPInfo& pp, size_t n, const IssueWit* wit, PlanWork& w, WorkPool& pool);
 
 }  // namespace ftsh

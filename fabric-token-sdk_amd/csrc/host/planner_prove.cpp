@@ -602,27 +602,36 @@ void PB::issue(const IssueWit& w, size_t idx) {
 }
 
 template <class W, class Fn>
-std::string plan_prove(const PPInfo& pp, size_t n, const W* w, Plan& out, int threads, Fn fn) {
-  out.clear();
-  out.arena.resize(C_SIZE, 0);
-  out.p2_g1out = true;
-  if (threads < 1) threads = 1;
-  size_t chunks = std::min<size_t>((size_t)threads, std::max<size_t>(1, n / 64));
-  std::vector<Plan> pieces(chunks);
-  std::vector<std::string> errs(chunks);
-  std::vector<std::thread> th;
-  for (size_t c = 0; c < chunks; c++) {
-    size_t lo = n * c / chunks, hi = n * (c + 1) / chunks;
-    th.emplace_back([&, c, lo, hi]() {
-      PB b(pieces[c], pp);
-      for (size_t i = lo; i < hi; i++) fn(b, w[i], i);
-      errs[c] = b.err;
-    });
-  }
-  for (auto& t : th) t.join();
-  for (auto& e : errs)
+std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& work, WorkPool& pool, Fn fn) {
+  size_t np = plan_piece_count(n, pool.size());
+  if (work.pieces.size() < np) work.pieces.resize(np);
+  work.errs.assign(np, std::string());
+  work.used = np;
+  pool.run(np, [&](size_t c) {
+    Plan& p = work.pieces[c];
+    p.clear();
+    size_t lo = n * c / np, hi = n * (c + 1) / np;
+    PB b(p, pp);
+    for (size_t i = lo; i < hi; i++) fn(b, w[i], i);
+    work.errs[c] = b.err;
+  });
+  for (auto& e : work.errs)
     if (!e.empty()) return e;
-  for (auto& p : pieces) plan_merge(out, p);
+  return "";
+}
+
+template <class W, class Fn>
+std::string plan_prove(const PPInfo& pp, size_t n, const W* w, Plan& out, int threads, Fn fn) {
+  WorkPool pool(threads);
+  PlanWork work;
+  std::string e = plan_prove_pieces(pp, n, w, work, pool, fn);
+  if (!e.empty()) return e;
+  FlatPlan fp;
+  e = flat_layout(work, true, fp);
+  if (!e.empty()) return e;
+  std::vector<uint8_t> blob(fp.bytes);
+  flat_write(work, fp, blob.data(), std::vector<uint8_t>(C_SIZE, 0).data(), pool);
+  plan_unflatten(fp, blob.data(), out);
   return "";
 }
 
@@ -634,6 +643,15 @@ std::string plan_prove_transfers(const PPInfo& pp, size_t n, const TransferWit* 
 
 std::string plan_prove_issues(const PPInfo& pp, size_t n, const IssueWit* w, Plan& out, int threads) {
   return plan_prove(pp, n, w, out, threads, [](PB& b, const IssueWit& x, size_t i) { b.issue(x, i); });
+}
+
+std::string plan_prove_items_transfers(const PPInfo& pp, size_t n, const TransferWit* wit, PlanWork& w,
+                                       WorkPool& pool) {
+  return plan_prove_pieces(pp, n, wit, w, pool, [](PB& b, const TransferWit& x, size_t i) { b.transfer(x, i); });
+}
+
+std::string plan_prove_items_issues(const PPInfo& pp, size_t n, const IssueWit* wit, PlanWork& w, WorkPool& pool) {
+  return plan_prove_pieces(pp, n, wit, w, pool, [](PB& b, const IssueWit& x, size_t i) { b.issue(x, i); });
 }
 
 }  // namespace ftsh

@@ -61,6 +61,7 @@ __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines
                          const G1Dev* g1out, F12Dev* fbuf);
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
+__global__ void k_fexp_exact(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 
 // prover (k_light.hip)
 __global__ void k_rand(const RandJob* jobs, uint32_t n, const uint8_t* arena, uint32_t (*scal)[8]);

@@ -1,10 +1,15 @@
-// Host-runtime internals shared by runtime.hip (verification batches) and
-// msm_rt.hip (standalone MSM): device buffers, the per-GPU context, errors.
+// Host-runtime internals shared by runtime.hip (contexts, batch slots, the
+// staged batch API), engine.hip (the job engine / micro-batcher behind
+// ftz_verify_*) and msm_rt.hip (standalone MSM): device buffers, the per-GPU
+// context, errors.
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ftsamd.h"
@@ -45,6 +50,46 @@ struct DBuf {
   }
 };
 
+// Grow-only device / pinned-host byte buffers (batch slots are reused, so
+// steady-state batches neither hipMalloc nor page-lock).
+struct DevMem {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+};
+struct PinnedMem {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  ~PinnedMem() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n + n / 4 + 4096;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+};
+
+struct Engine;
+struct ftz_prover;
+
 struct ftz_ctx {
   int device = 0;
   hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
@@ -53,7 +98,68 @@ struct ftz_ctx {
   DBuf<G1Dev> g1tab;
   DBuf<G2Dev> g2tab;
   DBuf<LineCoef> qlines;
-  int threads = 8;
-  std::mutex mu;
+  ftz_options opt;                   // resolved options (ftz_ctx_create_ex)
+  int serial = 0;                    // profiling: every kernel of a batch on one stream
+  WorkPool* pool = nullptr;          // host planning threads
+  std::mutex mu;                     // context-level device work (MSM, setup)
+  // job engine behind ftz_verify_* (created on first use)
+  std::mutex eng_mu;
+  Engine* eng = nullptr;
+  // reusable prover slots behind ftz_prove_* (one one-shot prove call at a time)
+  std::mutex prove_mu;
+  std::vector<ftz_prover*> pslots;
 };
 
+// ------------------------------------------------------------------ batch slots
+// Device scratch of a batch (values the kernels produce), sub-allocated from
+// one grow-only buffer.
+struct ScratchLayout {
+  size_t pts, pt_ok, scal, canon, g1out, g2out, fbuf, lines2, part1, part1p, vtab1, vtab1p, hash_ok, hash_ok_pre,
+      codes, bitmap, total;
+};
+
+// One batch: its planning state, pinned staging blob, device blob + scratch,
+// its three HIP streams and events.  The staged API hands one out per
+// ftz_batch_load_*; the engine cycles a fixed set of them.
+struct ftz_batch {
+  ftz_ctx* ctx = nullptr;
+  bool prover = false;
+  size_t n = 0;
+  PlanWork work;
+  FlatPlan fp;
+  ScratchLayout sl{};
+  PinnedMem h_blob, h_res;  // staging (host -> device) and results (device -> host)
+  DevMem d_blob, d_scr;
+  hipEvent_t ev[20];
+  bool ev_init = false;
+  hipStream_t st[3] = {nullptr, nullptr, nullptr};
+  bool pending = false;
+  uint64_t jobs_last[FTZ_NKERNELS] = {};
+  ftz_stats stats{};
+  // engine bookkeeping: which caller requests this batch's items belong to
+  struct Part {
+    struct Request* req;
+    size_t start, count;
+  };
+  std::vector<Part> parts;
+  std::vector<PlanItem> items;
+};
+struct ftz_prover : ftz_batch {};
+
+int slot_init(ftz_batch* b);                                      // streams + events (once)
+int slot_plan_items(ftz_batch* b, size_t n, const PlanItem* items);  // plan + flatten into pinned staging
+int slot_submit(ftz_batch* b, bool upload, bool fetch_codes);      // enqueue (optionally the H2D copy first)
+int slot_wait(ftz_batch* b);                                       // block, collect stats
+void slot_free(ftz_batch* b);                                      // sync + release everything
+int prover_plan(ftz_batch* b, size_t n, const void* wit, int kind);  // kind 0 transfer / 1 issue
+int prover_submit(ftz_batch* b, bool upload, bool fetch);
+int prover_wait(ftz_batch* b);
+// results of the last submission that fetched them (valid after slot_wait)
+inline const int32_t* slot_codes(const ftz_batch* b) { return reinterpret_cast<const int32_t*>(b->h_res.p); }
+inline const uint8_t* slot_out(const ftz_batch* b) {
+  return b->h_res.p + ((b->n * sizeof(int32_t) + 255) & ~(size_t)255);
+}
+
+// ------------------------------------------------------------------ engine (engine.hip)
+int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue* is, int32_t* codes);
+void engine_destroy(ftz_ctx* c);

@@ -1,11 +1,14 @@
-// ftsamd: HIP runtime + kernels + C ABI (include/ftsamd.h).
+// ftsamd: HIP runtime + C ABI (include/ftsamd.h) -- contexts, batch slots and
+// the staged batch / prover API.  The job engine behind ftz_verify_* is in
+// engine.hip, the standalone MSM in msm_rt.hip.
 //
 // One context per GPU holds the public parameters in device form: fixed-base
-// tables (8-bit windows) for Ped0..2, PedGen, the G1 generator and PK0..2, Q;
-// the precomputed Miller lines of Q; and the canonical RawBytes of the PP
-// points that every transcript hashes.  A batch is planned on the host
-// (host/planner.cpp), uploaded once, and executed as a fixed sequence of
-// job kernels on one HIP stream (see dev/jobs.h for the job model).
+// tables for Ped0..2, PedGen, the G1 generator and PK0..2, Q; the precomputed
+// Miller lines of Q; and the canonical RawBytes of the PP points that every
+// transcript hashes.  A batch is planned on host threads (host/planner.cpp)
+// straight into a pinned staging blob, copied to the device in ONE transfer,
+// and executed as a fixed sequence of job kernels on the batch's own three
+// HIP streams (see dev/jobs.h for the job model).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -33,67 +36,39 @@ int set_err(int code, const std::string& msg) {
   return code;
 }
 
-struct ftz_batch {
-  ftz_ctx* ctx = nullptr;
-  size_t n = 0;
-  Plan plan;
-  DBuf<uint8_t> wire, arena, pt_ok, canon, hash_ok_pre, hash_ok;
-  DBuf<DecodeJob> dec;
-  DBuf<ZrJob> zr;
-  DBuf<ScalJob> sc;
-  DBuf<uint32_t> sclist;
-  DBuf<VTerm> vt;
-  DBuf<G1Job> g1, g1p;
-  DBuf<G2Job> g2;
-  DBuf<PairJob> pr;
-  DBuf<Seg> seg;
-  DBuf<HashJob> hpre, hmain;
-  DBuf<Check> ck;
-  DBuf<TxChecks> tx;
-  DBuf<G1Dev> pts, g1out;
-  DBuf<G2Dev> g2out;
-  DBuf<uint32_t> scal;  // 8 limbs per scalar
-  DBuf<F12Dev> fbuf;
-  DBuf<EvLineDev> lines2;  // pair-2 Miller lines, [line][pair job]
-  DBuf<G1JDev> part1, part1p;  // G1 job parts (4 per job) of the side / pairing G1 jobs
-  DBuf<G1Dev> vtab1, vtab1p;   // window tables of their variable parts (16 entries per job)
-  DBuf<int32_t> codes;
-  DBuf<uint32_t> bitmap;
-  // prover
-  DBuf<RandJob> rnd;
-  DBuf<ScalJob> sc1, sc_post;
-  DBuf<EmitJob> emit;
-  DBuf<B64Job> b64;
-  DBuf<uint8_t> out;
-  hipEvent_t ev[20];
-  bool ev_init = false;
-  ftz_stats stats;
-  // the batch's own streams (pairing chain, side G1 jobs, G2 jobs + lines), so
-  // that several batches can be in flight at once (ftz_batch_submit)
-  hipStream_t st[3] = {nullptr, nullptr, nullptr};
-  bool pending = false;
-  uint64_t jobs_last[FTZ_NKERNELS] = {};
-};
-
-// Same priorities as the context streams: the pairing chain high, the side G1
-// jobs low.
-static int batch_streams(ftz_batch* b) {
-  if (b->st[0]) return FTZ_SUCCESS;
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  HC(hipStreamCreateWithPriority(&b->st[0], hipStreamNonBlocking, prio_hi));
-  HC(hipStreamCreateWithPriority(&b->st[1], hipStreamNonBlocking, prio_lo));
-  HC(hipStreamCreateWithPriority(&b->st[2], hipStreamNonBlocking, prio_hi));
-  return FTZ_SUCCESS;
-}
-
 static int blocks_for(uint32_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
 extern "C" const char* ftz_last_error(void) { return g_err.c_str(); }
 
+extern "C" void ftz_options_default(ftz_options* o) {
+  if (!o) return;
+  memset(o, 0, sizeof(*o));
+  o->struct_size = sizeof(ftz_options);
+  o->batch = 4096;
+  o->slots = 4;
+  o->window_us = 2000;
+  o->threads = 0;
+  o->fexp = FTZ_FEXP_EXACT;
+}
+
 extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {
+  return ftz_ctx_create_ex(pp, pp_len, device, nullptr, out);
+}
+
+extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, const ftz_options* opt,
+                                 ftz_ctx** out) {
   if (!pp || !out) return set_err(FTZ_E_INVALID, "null argument");
   *out = nullptr;
+  ftz_options o;
+  ftz_options_default(&o);
+  if (opt) {
+    if (opt->struct_size != sizeof(ftz_options)) return set_err(FTZ_E_INVALID, "ftz_options.struct_size mismatch");
+    o = *opt;
+    if (o.batch == 0) o.batch = 4096;
+    if (o.slots == 0) o.slots = 4;
+    if (o.fexp != FTZ_FEXP_EXACT && o.fexp != FTZ_FEXP_FUENTES) return set_err(FTZ_E_INVALID, "unknown fexp variant");
+    if (o.batch > (1u << 20) || o.slots > 64) return set_err(FTZ_E_INVALID, "batch / slots out of range");
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
     return set_err(FTZ_E_DEVICE, "no HIP device available (ftsamd requires an MI355X / gfx950 GPU)");
@@ -106,21 +81,20 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
                                      " (code objects are built for gfx950)");
   ftz_ctx* c = new ftz_ctx();
   c->device = device;
+  c->opt = o;
   unsigned hc = std::thread::hardware_concurrency();
-  c->threads = (int)std::max(1u, std::min(16u, hc ? hc : 8u));
+  int threads = o.threads ? (int)o.threads : (int)std::max(1u, std::min(16u, hc ? hc : 8u));
+  c->opt.threads = (uint32_t)threads;
+  c->pool = new WorkPool(threads);
   std::string e = parse_pp(pp, pp_len, "zkatdlog", c->pp);
   if (!e.empty()) {
-    delete c;
+    ftz_ctx_destroy(c);
     return set_err(FTZ_E_PP, e);
   }
-  // The pairing chain (stream, stream3) gets the higher priority: the G1 jobs
-  // no pairing depends on (stream2) fill the SIMDs the chain leaves idle.
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream2, hipStreamNonBlocking, prio_lo) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, prio_hi) != hipSuccess) {
-    delete c;
+  if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+    ftz_ctx_destroy(c);
     return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
   }
   // decode PP points on the GPU: G1 [PedGen, Ped0, Ped1, Ped2, G1 generator], G2 [PK0, PK1, PK2, Q]
@@ -140,7 +114,14 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
   push(gen, 64, g1off);
   for (int k = 0; k < 3; k++) push(c->pp.pk[k], 128, g2off);
   push(c->pp.q, 128, g2off);
+  // SignedValues (setup.go:168-184): decoded to check Validate's point rules
+  size_t nsig = c->pp.sig_r.size();
+  for (size_t k = 0; k < nsig; k++) {
+    push(c->pp.sig_r[k], 64, g1off);
+    push(c->pp.sig_s[k], 64, g1off);
+  }
   raw.resize(raw.size() + 128, 0);
+  const uint32_t n1 = (uint32_t)g1off.size();
   DBuf<uint8_t> d_raw, d_g1b, d_g2b, d_ok;
   DBuf<uint32_t> d_g1off, d_g2off;
   DBuf<G1Dev> d_g1;
@@ -152,17 +133,17 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
   };
   do {
     if (d_raw.upload(raw, c->stream) != hipSuccess || d_g1off.upload(g1off, c->stream) != hipSuccess ||
-        d_g2off.upload(g2off, c->stream) != hipSuccess || d_g1.alloc(5) != hipSuccess ||
-        d_g2.alloc(4) != hipSuccess || d_g1b.alloc(64 * 5) != hipSuccess || d_g2b.alloc(128 * 4) != hipSuccess ||
-        d_ok.alloc(9) != hipSuccess) {
+        d_g2off.upload(g2off, c->stream) != hipSuccess || d_g1.alloc(n1) != hipSuccess ||
+        d_g2.alloc(4) != hipSuccess || d_g1b.alloc(64 * (size_t)n1) != hipSuccess ||
+        d_g2b.alloc(128 * 4) != hipSuccess || d_ok.alloc(n1 + 4) != hipSuccess) {
       fail(FTZ_E_NOMEM, "device allocation failed");
       break;
     }
-    k_pp_decode<<<1, 64, 0, c->stream>>>(d_raw.p, d_g1off.p, 5, d_g2off.p, 4, d_g1.p, d_g2.p, d_g1b.p, d_g2b.p,
-                                         d_ok.p);
-    uint8_t ok[9];
-    std::vector<uint8_t> g1b(64 * 5), g2b(128 * 4);
-    if (hipMemcpyAsync(ok, d_ok.p, 9, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+    k_pp_decode<<<blocks_for(n1 + 4, 64), 64, 0, c->stream>>>(d_raw.p, d_g1off.p, n1, d_g2off.p, 4, d_g1.p, d_g2.p,
+                                                               d_g1b.p, d_g2b.p, d_ok.p);
+    std::vector<uint8_t> ok(n1 + 4);
+    std::vector<uint8_t> g1b(64 * (size_t)n1), g2b(128 * 4);
+    if (hipMemcpyAsync(ok.data(), d_ok.p, ok.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipMemcpyAsync(g1b.data(), d_g1b.p, g1b.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipMemcpyAsync(g2b.data(), d_g2b.p, g2b.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess) {
@@ -170,7 +151,7 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
       break;
     }
     bool allok = true;
-    for (int k = 0; k < 9; k++) allok = allok && ok[k];
+    for (size_t k = 0; k < ok.size(); k++) allok = allok && ok[k];
     if (!allok) {
       fail(FTZ_E_PP, "public parameters hold an invalid curve point");
       break;
@@ -198,8 +179,8 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
       fail(FTZ_E_NOMEM, "alloc");
       break;
     }
-    uint32_t n1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, n2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
-    if (c->g1tab.alloc(n1) != hipSuccess || c->g2tab.alloc(n2) != hipSuccess ||
+    uint32_t t1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, t2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
+    if (c->g1tab.alloc(t1) != hipSuccess || c->g2tab.alloc(t2) != hipSuccess ||
         c->qlines.alloc(MILLER_LINES) != hipSuccess) {
       fail(FTZ_E_NOMEM, "table allocation failed");
       break;
@@ -208,11 +189,11 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
     DBuf<G1JDev> d_jt;
     DBuf<uint32_t> d_zs;
     if (G1TAB_C <= 8) {
-      k_tab_g1<<<blocks_for(n1, 64), 64, 0, c->stream>>>(d_b1.p, n1, c->g1tab.p);
+      k_tab_g1<<<blocks_for(t1, 64), 64, 0, c->stream>>>(d_b1.p, t1, c->g1tab.p);
     } else {
       const uint32_t chunk = 128, lanes = G1B_COUNT * G1TAB_WINDOWS * (G1TAB_DIGITS / chunk);
-      if (d_bw.alloc(G1B_COUNT * G1TAB_WINDOWS) != hipSuccess || d_jt.alloc(n1) != hipSuccess ||
-          d_zs.alloc(8 * (size_t)n1) != hipSuccess) {
+      if (d_bw.alloc(G1B_COUNT * G1TAB_WINDOWS) != hipSuccess || d_jt.alloc(t1) != hipSuccess ||
+          d_zs.alloc(8 * (size_t)t1) != hipSuccess) {
         fail(FTZ_E_NOMEM, "table scratch allocation failed");
         break;
       }
@@ -223,11 +204,11 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
     DBuf<G2Dev> d_bw2;
     DBuf<uint32_t> d_jt2, d_zs2;
     if (G2TAB_C <= 8) {
-      k_tab_g2<<<blocks_for(n2, 64), 64, 0, c->stream>>>(d_g2.p, n2, c->g2tab.p);  // PK0, PK1, PK2, Q
+      k_tab_g2<<<blocks_for(t2, 64), 64, 0, c->stream>>>(d_g2.p, t2, c->g2tab.p);  // PK0, PK1, PK2, Q
     } else {
       const uint32_t chunk = 64, lanes = G2B_COUNT * G2TAB_WINDOWS * (G2TAB_DIGITS / chunk);
-      if (d_bw2.alloc(G2B_COUNT * G2TAB_WINDOWS) != hipSuccess || d_jt2.alloc(48 * (size_t)n2) != hipSuccess ||
-          d_zs2.alloc(16 * (size_t)n2) != hipSuccess) {
+      if (d_bw2.alloc(G2B_COUNT * G2TAB_WINDOWS) != hipSuccess || d_jt2.alloc(48 * (size_t)t2) != hipSuccess ||
+          d_zs2.alloc(16 * (size_t)t2) != hipSuccess) {
         fail(FTZ_E_NOMEM, "table scratch allocation failed");
         break;
       }
@@ -260,19 +241,34 @@ extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_
 extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  engine_destroy(c);
+  for (ftz_prover* p : c->pslots) {
+    slot_free(p);
+    delete p;
+  }
+  c->pslots.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->g1tab.alloc(0);
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
-  if (c->stream2) (void)hipStreamDestroy(c->stream2);
-  if (c->stream3) (void)hipStreamDestroy(c->stream3);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c->pool;
   delete c;
 }
 
 extern "C" int ftz_ctx_set_threads(ftz_ctx* c, int threads) {
-  if (!c || threads < 1) return set_err(FTZ_E_INVALID, "bad argument");
-  c->threads = threads;
+  if (!c || threads < 1 || threads > 256) return set_err(FTZ_E_INVALID, "bad argument");
+  std::lock_guard<std::mutex> lk(c->eng_mu);
+  if (c->eng) return set_err(FTZ_E_INVALID, "ftz_ctx_set_threads: the context's engine is already running");
+  delete c->pool;
+  c->pool = new WorkPool(threads);
+  c->opt.threads = (uint32_t)threads;
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  c->serial = serial ? 1 : 0;
   return FTZ_SUCCESS;
 }
 
@@ -283,220 +279,364 @@ extern "C" int ftz_ctx_info(const ftz_ctx* c, uint32_t* base, uint32_t* exponent
   return FTZ_SUCCESS;
 }
 
-static int batch_upload(ftz_batch* b) {
+// ------------------------------------------------------------------ batch slots
+int slot_init(ftz_batch* b) {
+  if (b->st[0]) return FTZ_SUCCESS;
+  // Same priorities as the context streams: the pairing chain and the G2 /
+  // line jobs high, the side G1 jobs (which fill the SIMDs the chain leaves
+  // idle) low.
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  HC(hipStreamCreateWithPriority(&b->st[0], hipStreamNonBlocking, prio_hi));
+  HC(hipStreamCreateWithPriority(&b->st[1], hipStreamNonBlocking, prio_lo));
+  HC(hipStreamCreateWithPriority(&b->st[2], hipStreamNonBlocking, prio_hi));
+  for (int k = 0; k < 20; k++)
+    HC(hipEventCreateWithFlags(&b->ev[k], k == 17 ? (hipEventBlockingSync | hipEventDisableTiming) : 0));
+  b->ev_init = true;
+  return FTZ_SUCCESS;
+}
+
+void slot_free(ftz_batch* b) {
+  if (!b) return;
+  for (int k = 0; k < 3; k++)
+    if (b->st[k]) (void)hipStreamSynchronize(b->st[k]);
+  if (b->ev_init)
+    for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
+  b->ev_init = false;
+  for (int k = 0; k < 3; k++)
+    if (b->st[k]) (void)hipStreamDestroy(b->st[k]);
+  b->st[0] = b->st[1] = b->st[2] = nullptr;
+}
+
+static void scratch_layout(ftz_batch* b) {
+  const FlatPlan& f = b->fp;
+  ScratchLayout& s = b->sl;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    size_t r = o;
+    o = (o + std::max<size_t>(bytes, 1) + 255) & ~(size_t)255;
+    return r;
+  };
+  size_t n_pr = f.cnt[PS_PR], n_g1 = f.cnt[PS_G1], n_g1p = f.cnt[PS_G1P];
+  s.pts = take(sizeof(G1Dev) * (size_t)f.n_pts);
+  s.pt_ok = take(f.n_pts);
+  s.scal = take(32 * (size_t)f.n_scal);
+  s.canon = take(f.n_scal);
+  s.g1out = take(sizeof(G1Dev) * (size_t)f.n_g1out);
+  s.g2out = take(sizeof(G2Dev) * (size_t)f.n_g2out);
+  s.fbuf = take(sizeof(F12Dev) * n_pr);
+  s.lines2 = take(sizeof(EvLineDev) * n_pr * MILLER_LINES);
+  s.part1 = take(sizeof(G1JDev) * 4 * n_g1);
+  s.part1p = take(sizeof(G1JDev) * 4 * n_g1p);
+  s.vtab1 = take(sizeof(G1Dev) * 16 * n_g1);
+  s.vtab1p = take(sizeof(G1Dev) * 16 * n_g1p);
+  s.hash_ok = take(f.cnt[PS_HMAIN]);
+  s.hash_ok_pre = take(f.cnt[PS_HPRE]);
+  s.codes = take(sizeof(int32_t) * b->n);
+  s.bitmap = take(sizeof(uint32_t) * ((b->n + 31) / 32 + 1));
+  s.total = o;
+}
+
+// Flattened plan -> pinned staging blob; device blob and scratch sized.
+static int slot_finish_plan(ftz_batch* b, size_t n, bool p2_g1out) {
   ftz_ctx* c = b->ctx;
-  Plan& p = b->plan;
-  int rc = batch_streams(b);
-  if (rc != FTZ_SUCCESS) return rc;
-  hipStream_t s = b->st[0];
-  memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
-  std::vector<uint8_t> wire = p.wire;
-  wire.resize(wire.size() + 64, 0);  // decode jobs may look at 64 bytes past a short element
-  HC(b->wire.upload(wire, s));
-  HC(b->arena.upload(p.arena, s));
-  HC(b->dec.upload(p.dec, s));
-  HC(b->zr.upload(p.zr, s));
-  HC(b->sc.upload(p.sc, s));
-  HC(b->sclist.upload(p.sclist, s));
-  HC(b->vt.upload(p.vt, s));
-  HC(b->g1.upload(p.g1, s));
-  HC(b->g1p.upload(p.g1p, s));
-  HC(b->g2.upload(p.g2, s));
-  HC(b->pr.upload(p.pr, s));
-  HC(b->seg.upload(p.seg, s));
-  HC(b->hpre.upload(p.hpre, s));
-  HC(b->hmain.upload(p.hmain, s));
-  HC(b->ck.upload(p.ck, s));
-  HC(b->tx.upload(p.tx, s));
-  HC(b->pts.alloc(std::max<uint32_t>(p.n_pts, 1)));
-  HC(b->pt_ok.alloc(std::max<uint32_t>(p.n_pts, 1)));
-  HC(b->scal.alloc(8 * (size_t)std::max<uint32_t>(p.n_scal, 1)));
-  HC(b->canon.alloc(std::max<uint32_t>(p.n_scal, 1)));
-  HC(b->g1out.alloc(std::max<uint32_t>(p.n_g1out, 1)));
-  HC(b->g2out.alloc(std::max<uint32_t>(p.n_g2out, 1)));
-  HC(b->fbuf.alloc(std::max<size_t>(p.pr.size(), 1)));
-  HC(b->lines2.alloc(std::max<size_t>(p.pr.size(), 1) * MILLER_LINES));
-  HC(b->part1.alloc(4 * std::max<size_t>(p.g1.size(), 1)));
-  HC(b->part1p.alloc(4 * std::max<size_t>(p.g1p.size(), 1)));
-  HC(b->vtab1.alloc(16 * std::max<size_t>(p.g1.size(), 1)));
-  HC(b->vtab1p.alloc(16 * std::max<size_t>(p.g1p.size(), 1)));
-  if (p.g2.size() != p.pr.size()) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
-  for (size_t i = 0; i < p.pr.size(); i++)
-    if (p.pr[i].q2 != p.g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
-  HC(b->rnd.upload(p.rnd, s));
-  HC(b->sc1.upload(p.sc1, s));
-  HC(b->sc_post.upload(p.sc_post, s));
-  HC(b->emit.upload(p.emit, s));
-  HC(b->b64.upload(p.b64, s));
-  HC(b->out.upload(p.out, s));
-  HC(b->hash_ok.alloc(std::max<size_t>(p.hmain.size(), 1)));
-  HC(b->hash_ok_pre.alloc(std::max<size_t>(p.hpre.size(), 1)));
-  HC(b->codes.alloc(std::max<size_t>(b->n, 1)));
-  HC(b->bitmap.alloc((b->n + 31) / 32 + 1));
-  HC(hipMemsetAsync(b->pt_ok.p, 1, std::max<uint32_t>(p.n_pts, 1), s));
-  HC(hipStreamSynchronize(s));
-  if (!b->ev_init) {
-    for (int k = 0; k < 20; k++) HC(hipEventCreate(&b->ev[k]));
-    b->ev_init = true;
-  }
-  return FTZ_SUCCESS;
-}
-
-extern "C" int ftz_batch_load_transfers(ftz_ctx* c, size_t n, const ftz_transfer* tx, ftz_batch** out) {
-  if (!c || !out || (n && !tx)) return set_err(FTZ_E_INVALID, "null argument");
-  for (size_t i = 0; i < n; i++)
-    if ((tx[i].n_in && !tx[i].inputs) || (tx[i].n_out && !tx[i].outputs) || (tx[i].proof_len && !tx[i].proof))
-      return set_err(FTZ_E_INVALID, "null buffer in transfer");
-  std::lock_guard<std::mutex> lk(c->mu);
-  HC(hipSetDevice(c->device));
-  ftz_batch* b = new ftz_batch();
-  b->ctx = c;
+  std::string e = flat_layout(b->work, p2_g1out, b->fp);
+  if (!e.empty()) return set_err(FTZ_E_INVALID, e);
+  if (b->fp.n_items != n) return set_err(FTZ_E_INVALID, "planner: item count mismatch");
+  if (b->fp.cnt[PS_G2] != b->fp.cnt[PS_PR]) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   b->n = n;
-  std::vector<TransferIn> t(n);
-  for (size_t i = 0; i < n; i++)
-    t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
-  plan_transfers(c->pp, n, t.data(), b->plan, c->threads);
-  int rc = batch_upload(b);
-  if (rc != FTZ_SUCCESS) {
-    ftz_batch_destroy(b);
-    return rc;
-  }
-  *out = b;
+  HC(b->h_blob.reserve(b->fp.bytes));
+  flat_write(b->work, b->fp, b->h_blob.p, c->const_bytes.data(), *c->pool);
+  // pairing job i consumes G2 job i's output (k_g2lines computes both)
+  const PairJob* pr = b->fp.ptr<PairJob>(b->h_blob.p, PS_PR);
+  const G2Job* g2 = b->fp.ptr<G2Job>(b->h_blob.p, PS_G2);
+  for (size_t i = 0; i < b->fp.cnt[PS_PR]; i++)
+    if (pr[i].q2 != g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
+  scratch_layout(b);
+  HC(b->d_blob.reserve(b->fp.bytes));
+  HC(b->d_scr.reserve(b->sl.total));
+  size_t res = ((n * sizeof(int32_t) + 255) & ~(size_t)255) + b->fp.cnt[PS_OUT] + 256;
+  HC(b->h_res.reserve(res));
   return FTZ_SUCCESS;
 }
 
-extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, ftz_batch** out) {
-  if (!c || !out || (n && !is)) return set_err(FTZ_E_INVALID, "null argument");
-  for (size_t i = 0; i < n; i++)
-    if ((is[i].n_out && !is[i].outputs) || (is[i].proof_len && !is[i].proof))
-      return set_err(FTZ_E_INVALID, "null buffer in issue");
-  std::lock_guard<std::mutex> lk(c->mu);
-  HC(hipSetDevice(c->device));
-  ftz_batch* b = new ftz_batch();
-  b->ctx = c;
-  b->n = n;
-  std::vector<IssueIn> t(n);
-  for (size_t i = 0; i < n; i++) t[i] = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
-  plan_issues(c->pp, n, t.data(), b->plan, c->threads);
-  int rc = batch_upload(b);
-  if (rc != FTZ_SUCCESS) {
-    ftz_batch_destroy(b);
-    return rc;
-  }
-  *out = b;
-  return FTZ_SUCCESS;
+int slot_plan_items(ftz_batch* b, size_t n, const PlanItem* items) {
+  plan_items(b->ctx->pp, n, items, b->work, *b->ctx->pool);
+  return slot_finish_plan(b, n, false);
 }
 
-// Three streams after the light decode/scalar kernels:
-//   stream3: G2 jobs t' and the pair-2 Miller lines evaluated at R (k_g2lines)
-//   stream : G1 jobs feeding the pairings (P1 = sbf*P - c*S), then, after
-//            stream3, the sextet Miller loops and final exponentiations
-//   stream2: the G1 jobs no pairing depends on (well-formedness, range
-//            equality, membership Schnorr commitments)
+int prover_plan(ftz_batch* b, size_t n, const void* wit, int kind) {
+  ftz_ctx* c = b->ctx;
+  std::string e = kind == 0
+                      ? plan_prove_items_transfers(c->pp, n, static_cast<const TransferWit*>(wit), b->work, *c->pool)
+                      : plan_prove_items_issues(c->pp, n, static_cast<const IssueWit*>(wit), b->work, *c->pool);
+  if (!e.empty()) return set_err(FTZ_E_INVALID, e);
+  return slot_finish_plan(b, n, true);
+}
+
+// Device pointers of a slot (blob sections + scratch).
+struct SlotPtrs {
+  uint8_t *wire, *arena, *out;
+  const DecodeJob* dec;
+  const ZrJob* zr;
+  const ScalJob *sc, *sc1, *sc_post;
+  const uint32_t* sclist;
+  const VTerm* vt;
+  const G1Job *g1, *g1p;
+  const G2Job* g2;
+  const PairJob* pr;
+  const Seg* seg;
+  const HashJob *hpre, *hmain;
+  const Check* ck;
+  const TxChecks* tx;
+  const RandJob* rnd;
+  const EmitJob* emit;
+  const B64Job* b64;
+  G1Dev* pts;
+  uint8_t *pt_ok, *canon, *hash_ok, *hash_ok_pre;
+  uint32_t (*scal)[8];
+  G1Dev* g1out;
+  G2Dev* g2out;
+  F12Dev* fbuf;
+  EvLineDev* lines2;
+  G1JDev *part1, *part1p;
+  G1Dev *vtab1, *vtab1p;
+  int32_t* codes;
+  uint32_t* bitmap;
+  uint32_t n_dec, n_zr, n_sc, n_sc1, n_sp, n_rnd, n_em, n_b64, n_g1, n_g1p, n_g2, n_pr, n_hp, n_hm, n_tx;
+};
+
+static SlotPtrs slot_ptrs(ftz_batch* b) {
+  SlotPtrs p;
+  const FlatPlan& f = b->fp;
+  uint8_t* d = b->d_blob.p;
+  uint8_t* s = b->d_scr.p;
+  p.wire = d + f.off[PS_WIRE];
+  p.arena = d + f.off[PS_ARENA];
+  p.out = d + f.off[PS_OUT];
+  p.dec = f.ptr<DecodeJob>(d, PS_DEC);
+  p.zr = f.ptr<ZrJob>(d, PS_ZR);
+  p.sc = f.ptr<ScalJob>(d, PS_SC);
+  p.sc1 = f.ptr<ScalJob>(d, PS_SC1);
+  p.sc_post = f.ptr<ScalJob>(d, PS_SCPOST);
+  p.sclist = f.ptr<uint32_t>(d, PS_SCLIST);
+  p.vt = f.ptr<VTerm>(d, PS_VT);
+  p.g1 = f.ptr<G1Job>(d, PS_G1);
+  p.g1p = f.ptr<G1Job>(d, PS_G1P);
+  p.g2 = f.ptr<G2Job>(d, PS_G2);
+  p.pr = f.ptr<PairJob>(d, PS_PR);
+  p.seg = f.ptr<Seg>(d, PS_SEG);
+  p.hpre = f.ptr<HashJob>(d, PS_HPRE);
+  p.hmain = f.ptr<HashJob>(d, PS_HMAIN);
+  p.ck = f.ptr<Check>(d, PS_CK);
+  p.tx = f.ptr<TxChecks>(d, PS_TX);
+  p.rnd = f.ptr<RandJob>(d, PS_RND);
+  p.emit = f.ptr<EmitJob>(d, PS_EMIT);
+  p.b64 = f.ptr<B64Job>(d, PS_B64);
+  const ScratchLayout& l = b->sl;
+  p.pts = reinterpret_cast<G1Dev*>(s + l.pts);
+  p.pt_ok = s + l.pt_ok;
+  p.scal = reinterpret_cast<uint32_t (*)[8]>(s + l.scal);
+  p.canon = s + l.canon;
+  p.g1out = reinterpret_cast<G1Dev*>(s + l.g1out);
+  p.g2out = reinterpret_cast<G2Dev*>(s + l.g2out);
+  p.fbuf = reinterpret_cast<F12Dev*>(s + l.fbuf);
+  p.lines2 = reinterpret_cast<EvLineDev*>(s + l.lines2);
+  p.part1 = reinterpret_cast<G1JDev*>(s + l.part1);
+  p.part1p = reinterpret_cast<G1JDev*>(s + l.part1p);
+  p.vtab1 = reinterpret_cast<G1Dev*>(s + l.vtab1);
+  p.vtab1p = reinterpret_cast<G1Dev*>(s + l.vtab1p);
+  p.hash_ok = s + l.hash_ok;
+  p.hash_ok_pre = s + l.hash_ok_pre;
+  p.codes = reinterpret_cast<int32_t*>(s + l.codes);
+  p.bitmap = reinterpret_cast<uint32_t*>(s + l.bitmap);
+  p.n_dec = (uint32_t)f.cnt[PS_DEC];
+  p.n_zr = (uint32_t)f.cnt[PS_ZR];
+  p.n_sc = (uint32_t)f.cnt[PS_SC];
+  p.n_sc1 = (uint32_t)f.cnt[PS_SC1];
+  p.n_sp = (uint32_t)f.cnt[PS_SCPOST];
+  p.n_rnd = (uint32_t)f.cnt[PS_RND];
+  p.n_em = (uint32_t)f.cnt[PS_EMIT];
+  p.n_b64 = (uint32_t)f.cnt[PS_B64];
+  p.n_g1 = (uint32_t)f.cnt[PS_G1];
+  p.n_g1p = (uint32_t)f.cnt[PS_G1P];
+  p.n_g2 = (uint32_t)f.cnt[PS_G2];
+  p.n_pr = (uint32_t)f.cnt[PS_PR];
+  p.n_hp = (uint32_t)f.cnt[PS_HPRE];
+  p.n_hm = (uint32_t)f.cnt[PS_HMAIN];
+  p.n_tx = (uint32_t)f.cnt[PS_TX];
+  return p;
+}
+
+static void launch_fexp(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
+  if (!p.n_pr) return;
+  if (c->opt.fexp == FTZ_FEXP_FUENTES)
+    k_fexp<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, p.fbuf, p.arena);
+  else
+    k_fexp_exact<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, p.fbuf, p.arena);
+}
+
+// Verification pipeline.  Three streams after the light decode/scalar kernels:
+//   st[2]: G2 jobs t' and the pair-2 Miller lines evaluated at R (k_g2lines)
+//   st[0]: G1 jobs feeding the pairings (P1 = sbf*P - c*S), then, after st[2],
+//          the sextet Miller loops and final exponentiations
+//   st[1]: the G1 jobs no pairing depends on (well-formedness, range equality,
+//          membership Schnorr commitments)
 // The transcript hashes wait for all three.
-extern "C" int ftz_batch_submit(ftz_batch* b) {
-  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   ftz_ctx* c = b->ctx;
-  std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
-  Plan& p = b->plan;
+  SlotPtrs p = slot_ptrs(b);
   hipStream_t s = b->st[0], s2 = b->st[1], s3 = b->st[2];
-  // FTZ_SERIAL=1: run every kernel on one stream (per-kernel timings without
-  // overlap, for profiling)
-  const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
-  // FTZ_BATCH_STREAMS=1: the whole batch on its pairing-chain stream (several
-  // batches in flight then overlap each other instead)
-  const bool one = getenv("FTZ_BATCH_STREAMS") && getenv("FTZ_BATCH_STREAMS")[0] == '1';
-  if (serial || one) s2 = s3 = s;
-  uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
-  uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
-  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
-  uint32_t n_pr = (uint32_t)p.pr.size();
-  uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
-  const uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1, n_hm, n_tx, n_tx};
+  if (c->serial) s2 = s3 = s;
+  const uint64_t jobs[FTZ_NKERNELS] = {p.n_dec, p.n_zr, p.n_hp, p.n_sc, p.n_g1p, p.n_g2,
+                                       p.n_pr,  p.n_pr, p.n_g1, p.n_hm, p.n_tx, p.n_tx};
   for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
-  HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
+  if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
+  HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
+  if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));
   HC(hipEventRecord(e[0], s));
-  if (n_dec) k_decode<<<blocks_for(n_dec, 256), 256, 0, s>>>(b->dec.p, n_dec, b->wire.p, b->pts.p, b->pt_ok.p, b->arena.p);
+  if (p.n_dec) k_decode<<<blocks_for(p.n_dec, 256), 256, 0, s>>>(p.dec, p.n_dec, p.wire, p.pts, p.pt_ok, p.arena);
   HC(hipEventRecord(e[1], s));
-  if (n_zr) k_zr<<<blocks_for(n_zr, 256), 256, 0, s>>>(b->zr.p, n_zr, b->wire.p, scal, b->canon.p);
+  if (p.n_zr) k_zr<<<blocks_for(p.n_zr, 256), 256, 0, s>>>(p.zr, p.n_zr, p.wire, p.scal, p.canon);
   HC(hipEventRecord(e[2], s));
-  if (n_hp)
-    k_hash<<<blocks_for(n_hp, 128), 128, 0, s>>>(b->hpre.p, n_hp, b->seg.p, b->arena.p, scal, b->canon.p,
-                                                 b->hash_ok_pre.p);
+  if (p.n_hp)
+    k_hash<<<blocks_for(p.n_hp, 128), 128, 0, s>>>(p.hpre, p.n_hp, p.seg, p.arena, p.scal, p.canon, p.hash_ok_pre);
   HC(hipEventRecord(e[3], s));
-  if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
+  if (p.n_sc) k_scalar<<<blocks_for(p.n_sc, 256), 256, 0, s>>>(p.sc, p.n_sc, p.scal, p.sclist);
   HC(hipEventRecord(e[4], s));
-  // stream3: G2 jobs + pair-2 lines
+  // st[2]: G2 jobs + pair-2 lines
   HC(hipStreamWaitEvent(s3, e[4], 0));
   HC(hipEventRecord(e[14], s3));
-  if (n_g2)
-    k_g2lines<<<blocks_for(n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p, b->g2out.p, b->pts.p,
-                                                   b->lines2.p);
+  if (p.n_g2)
+    k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out,
+                                                                   p.pts, p.lines2);
   HC(hipEventRecord(e[15], s3));
-  // main stream: pairing chain
+  // st[0]: pairing chain
   HC(hipEventRecord(e[16], s));
-  if (n_g1p) {
-    k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1p.p, b->vtab1p.p);
-    k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
+  if (p.n_g1p) {
+    k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, c->g1tab.p, p.part1p,
+                                                           p.vtab1p);
+    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena);
   }
   HC(hipEventRecord(e[5], s));
-  // stream2: pairing-independent G1 jobs, started after the jobs the pairing
-  // chain waits for (FTZ_G1_AFTER: 0 with them, 1 after the pairing G1 jobs,
-  // 2 after the G2 jobs and lines)
-  const char* ga = getenv("FTZ_G1_AFTER");
-  const int g1_after = ga ? atoi(ga) : 0;
-  HC(hipStreamWaitEvent(s2, g1_after == 1 ? e[5] : (g1_after == 2 ? e[15] : e[4]), 0));
+  // st[1]: pairing-independent G1 jobs, started with the jobs the chain waits for
+  HC(hipStreamWaitEvent(s2, e[4], 0));
   HC(hipEventRecord(e[11], s2));
-  if (n_g1) {
-    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1.p, b->vtab1.p);
-    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
+  if (p.n_g1) {
+    k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, c->g1tab.p, p.part1,
+                                                           p.vtab1);
+    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena);
   }
   HC(hipEventRecord(e[12], s2));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
-  if (n_pr)
-    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->lines2.p, b->g1out.p,
-                                                               b->fbuf.p);
+  if (p.n_pr)
+    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines.p, p.lines2, p.g1out,
+                                                                 p.fbuf);
   HC(hipEventRecord(e[7], s));
-  if (n_pr) k_fexp<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
+  launch_fexp(c, p, s);
   HC(hipEventRecord(e[8], s));
   HC(hipStreamWaitEvent(s, e[12], 0));
   HC(hipEventRecord(e[9], s));
-  if (n_hm)
-    k_hash<<<blocks_for(n_hm, 128), 128, 0, s>>>(b->hmain.p, n_hm, b->seg.p, b->arena.p, scal, b->canon.p,
-                                                 b->hash_ok.p);
+  if (p.n_hm)
+    k_hash<<<blocks_for(p.n_hm, 128), 128, 0, s>>>(p.hmain, p.n_hm, p.seg, p.arena, p.scal, p.canon, p.hash_ok);
   HC(hipEventRecord(e[10], s));
-  if (n_tx)
-    k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
-                                                    b->bitmap.p);
+  if (p.n_tx)
+    k_verdict<<<blocks_for(p.n_tx, 256), 256, 0, s>>>(p.tx, p.n_tx, p.ck, p.pt_ok, p.hash_ok, p.codes, p.bitmap);
   HC(hipEventRecord(e[13], s));
+  if (fetch_codes && b->n) HC(hipMemcpyAsync(b->h_res.p, p.codes, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  HC(hipEventRecord(e[17], s));
   HC(hipGetLastError());
   b->pending = true;
   return FTZ_SUCCESS;
 }
 
-// Wait for the batch's last submission and collect its per-kernel timings.
-extern "C" int ftz_batch_wait(ftz_batch* b) {
-  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+// stats slots: decode zr hash_pre scalar g1p g2+lines miller fexp g1(side) hash verdict total
+static const int ST_FROM[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
+static const int ST_TO[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
+
+int slot_wait(ftz_batch* b) {
   if (!b->pending) return FTZ_SUCCESS;
   HC(hipSetDevice(b->ctx->device));
-  HC(hipStreamSynchronize(b->st[0]));
+  HC(hipEventSynchronize(b->ev[17]));
   b->pending = false;
-  hipEvent_t* e = b->ev;
-  // stats order: decode zr hash_pre scalar g1p g2+lines miller fexp g1(side) hash verdict total
-  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
-  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
   for (int k = 0; k < FTZ_NKERNELS; k++) {
     float ms = 0;
-    HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
+    HC(hipEventElapsedTime(&ms, b->ev[ST_FROM[k]], b->ev[ST_TO[k]]));
     b->stats.ms[k] = ms;
     b->stats.jobs[k] = b->jobs_last[k];
   }
   return FTZ_SUCCESS;
+}
+
+// ------------------------------------------------------------------ staged batch API
+static int staged_load(ftz_ctx* c, size_t n, const PlanItem* items, ftz_batch** out) {
+  HC(hipSetDevice(c->device));
+  ftz_batch* b = new ftz_batch();
+  b->ctx = c;
+  int rc = slot_init(b);
+  if (rc == FTZ_SUCCESS) rc = slot_plan_items(b, n, items);
+  if (rc == FTZ_SUCCESS) {
+    hipError_t e = hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, b->st[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(b->st[0]);
+    if (e != hipSuccess) rc = set_err(FTZ_E_DEVICE, std::string("batch upload failed: ") + hipGetErrorString(e));
+  }
+  if (rc != FTZ_SUCCESS) {
+    slot_free(b);
+    delete b;
+    return rc;
+  }
+  *out = b;
+  return FTZ_SUCCESS;
+}
+
+static bool transfer_args_ok(size_t n, const ftz_transfer* tx) {
+  for (size_t i = 0; i < n; i++)
+    if ((tx[i].n_in && !tx[i].inputs) || (tx[i].n_out && !tx[i].outputs) || (tx[i].proof_len && !tx[i].proof))
+      return false;
+  return true;
+}
+static bool issue_args_ok(size_t n, const ftz_issue* is) {
+  for (size_t i = 0; i < n; i++)
+    if ((is[i].n_out && !is[i].outputs) || (is[i].proof_len && !is[i].proof)) return false;
+  return true;
+}
+
+extern "C" int ftz_batch_load_transfers(ftz_ctx* c, size_t n, const ftz_transfer* tx, ftz_batch** out) {
+  if (!c || !out || (n && !tx)) return set_err(FTZ_E_INVALID, "null argument");
+  if (!transfer_args_ok(n, tx)) return set_err(FTZ_E_INVALID, "null buffer in transfer");
+  std::vector<PlanItem> items(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&items[i], 0, sizeof(PlanItem));
+    items[i].kind = 0;
+    items[i].t = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+  }
+  return staged_load(c, n, items.data(), out);
+}
+
+extern "C" int ftz_batch_load_issues(ftz_ctx* c, size_t n, const ftz_issue* is, ftz_batch** out) {
+  if (!c || !out || (n && !is)) return set_err(FTZ_E_INVALID, "null argument");
+  if (!issue_args_ok(n, is)) return set_err(FTZ_E_INVALID, "null buffer in issue");
+  std::vector<PlanItem> items(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&items[i], 0, sizeof(PlanItem));
+    items[i].kind = 1;
+    items[i].i = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
+  }
+  return staged_load(c, n, items.data(), out);
+}
+
+extern "C" int ftz_batch_submit(ftz_batch* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+  if (b->pending) return set_err(FTZ_E_INVALID, "batch resubmitted before ftz_batch_wait");
+  return slot_submit(b, false, false);
+}
+
+extern "C" int ftz_batch_wait(ftz_batch* b) {
+  if (!b) return set_err(FTZ_E_INVALID, "null batch");
+  return slot_wait(b);
 }
 
 extern "C" int ftz_batch_run(ftz_batch* b) {
@@ -506,24 +646,20 @@ extern "C" int ftz_batch_run(ftz_batch* b) {
 
 extern "C" int ftz_batch_codes(ftz_batch* b, int32_t* codes) {
   if (!b || (b->n && !codes)) return set_err(FTZ_E_INVALID, "null argument");
-  if (b->pending) {
-    int rc = ftz_batch_wait(b);
-    if (rc != FTZ_SUCCESS) return rc;
-  }
+  int rc = slot_wait(b);
+  if (rc != FTZ_SUCCESS) return rc;
   HC(hipSetDevice(b->ctx->device));
-  if (b->n) HC(hipMemcpy(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (b->n) HC(hipMemcpy(codes, b->d_scr.p + b->sl.codes, b->n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return FTZ_SUCCESS;
 }
 
 extern "C" int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits) {
   if (!b || (b->n && !bits)) return set_err(FTZ_E_INVALID, "null argument");
-  if (b->pending) {
-    int rc = ftz_batch_wait(b);
-    if (rc != FTZ_SUCCESS) return rc;
-  }
+  int rc = slot_wait(b);
+  if (rc != FTZ_SUCCESS) return rc;
   HC(hipSetDevice(b->ctx->device));
   std::vector<uint32_t> w((b->n + 31) / 32);
-  if (!w.empty()) HC(hipMemcpy(w.data(), b->bitmap.p, w.size() * 4, hipMemcpyDeviceToHost));
+  if (!w.empty()) HC(hipMemcpy(w.data(), b->d_scr.p + b->sl.bitmap, w.size() * 4, hipMemcpyDeviceToHost));
   for (size_t i = 0; i < (b->n + 7) / 8; i++) bits[i] = (uint8_t)(w[i / 4] >> (8 * (i % 4)));
   return FTZ_SUCCESS;
 }
@@ -539,56 +675,125 @@ extern "C" size_t ftz_batch_size(const ftz_batch* b) { return b ? b->n : 0; }
 extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
-  for (int k = 0; k < 3; k++)
-    if (b->st[k]) (void)hipStreamSynchronize(b->st[k]);
-  if (b->ev_init)
-    for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
-  for (int k = 0; k < 3; k++)
-    if (b->st[k]) (void)hipStreamDestroy(b->st[k]);
+  slot_free(b);
   delete b;
 }
 
 extern "C" int ftz_verify_transfers(ftz_ctx* c, size_t n, const ftz_transfer* tx, int32_t* codes) {
+  if (!c || (n && (!tx || !codes))) return set_err(FTZ_E_INVALID, "null argument");
   if (n == 0) return FTZ_SUCCESS;
-  ftz_batch* b = nullptr;
-  int rc = ftz_batch_load_transfers(c, n, tx, &b);
-  if (rc == FTZ_SUCCESS) rc = ftz_batch_run(b);
-  if (rc == FTZ_SUCCESS) rc = ftz_batch_codes(b, codes);
-  ftz_batch_destroy(b);
-  return rc;
+  if (!transfer_args_ok(n, tx)) return set_err(FTZ_E_INVALID, "null buffer in transfer");
+  return engine_verify(c, n, tx, nullptr, codes);
 }
 
 extern "C" int ftz_verify_issues(ftz_ctx* c, size_t n, const ftz_issue* is, int32_t* codes) {
+  if (!c || (n && (!is || !codes))) return set_err(FTZ_E_INVALID, "null argument");
   if (n == 0) return FTZ_SUCCESS;
-  ftz_batch* b = nullptr;
-  int rc = ftz_batch_load_issues(c, n, is, &b);
-  if (rc == FTZ_SUCCESS) rc = ftz_batch_run(b);
-  if (rc == FTZ_SUCCESS) rc = ftz_batch_codes(b, codes);
-  ftz_batch_destroy(b);
-  return rc;
+  if (!issue_args_ok(n, is)) return set_err(FTZ_E_INVALID, "null buffer in issue");
+  return engine_verify(c, n, nullptr, is, codes);
 }
 
 // ------------------------------------------------------------------ prover
-// Plans from host/planner_prove.cpp; the pipeline of ftz_batch_run with the
+// Plans from host/planner_prove.cpp; the pipeline of slot_submit with the
 // prover's extra stages: randomness before the group work, responses, JSON
 // hole filling and base64 of the inner documents after the transcript hashes.
-struct ftz_prover : ftz_batch {};
+int prover_submit(ftz_batch* b, bool upload, bool fetch) {
+  ftz_ctx* c = b->ctx;
+  HC(hipSetDevice(c->device));
+  SlotPtrs p = slot_ptrs(b);
+  hipStream_t s = b->st[0], s2 = b->st[1], s3 = b->st[2];
+  if (c->serial) s2 = s3 = s;
+  uint64_t jobs[FTZ_NKERNELS] = {p.n_dec, p.n_zr, (uint64_t)p.n_rnd + p.n_hp, p.n_sc, p.n_g1p, p.n_g2, p.n_pr, p.n_pr,
+                                 p.n_g1, (uint64_t)p.n_hm + p.n_sp, (uint64_t)p.n_em + p.n_b64, p.n_tx};
+  for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
+  hipEvent_t* e = b->ev;
+  if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
+  HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
+  if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));
+  HC(hipEventRecord(e[0], s));
+  if (p.n_dec) k_decode<<<blocks_for(p.n_dec, 256), 256, 0, s>>>(p.dec, p.n_dec, p.wire, p.pts, p.pt_ok, p.arena);
+  HC(hipEventRecord(e[1], s));
+  if (p.n_zr) k_zr<<<blocks_for(p.n_zr, 256), 256, 0, s>>>(p.zr, p.n_zr, p.wire, p.scal, p.canon);
+  HC(hipEventRecord(e[2], s));
+  if (p.n_rnd) k_rand<<<blocks_for(p.n_rnd, 128), 128, 0, s>>>(p.rnd, p.n_rnd, p.arena, p.scal);
+  if (p.n_hp)
+    k_hash<<<blocks_for(p.n_hp, 128), 128, 0, s>>>(p.hpre, p.n_hp, p.seg, p.arena, p.scal, p.canon, p.hash_ok_pre);
+  HC(hipEventRecord(e[3], s));
+  if (p.n_sc) k_scalar<<<blocks_for(p.n_sc, 256), 256, 0, s>>>(p.sc, p.n_sc, p.scal, p.sclist);
+  if (p.n_sc1) k_scalar<<<blocks_for(p.n_sc1, 256), 256, 0, s>>>(p.sc1, p.n_sc1, p.scal, p.sclist);
+  HC(hipEventRecord(e[4], s));
+  // st[1]: G1 jobs no pairing depends on
+  HC(hipStreamWaitEvent(s2, e[4], 0));
+  HC(hipEventRecord(e[11], s2));
+  if (p.n_g1) {
+    k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, c->g1tab.p, p.part1,
+                                                           p.vtab1);
+    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena);
+  }
+  HC(hipEventRecord(e[12], s2));
+  // st[0]: R' = rr R and rsbf P (the pairing inputs)
+  HC(hipEventRecord(e[16], s));
+  if (p.n_g1p) {
+    k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, c->g1tab.p, p.part1p,
+                                                           p.vtab1p);
+    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena);
+  }
+  HC(hipEventRecord(e[5], s));
+  // st[2]: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)
+  HC(hipStreamWaitEvent(s3, e[5], 0));
+  HC(hipEventRecord(e[14], s3));
+  if (p.n_g2)
+    k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out,
+                                                                   p.g1out, p.lines2);
+  HC(hipEventRecord(e[15], s3));
+  HC(hipStreamWaitEvent(s, e[15], 0));
+  HC(hipEventRecord(e[6], s));
+  if (p.n_pr)
+    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines.p, p.lines2, p.g1out,
+                                                                 p.fbuf);
+  HC(hipEventRecord(e[7], s));
+  launch_fexp(c, p, s);
+  HC(hipEventRecord(e[8], s));
+  HC(hipStreamWaitEvent(s, e[12], 0));
+  HC(hipEventRecord(e[9], s));
+  if (p.n_hm)
+    k_hash<<<blocks_for(p.n_hm, 128), 128, 0, s>>>(p.hmain, p.n_hm, p.seg, p.arena, p.scal, p.canon, p.hash_ok);
+  if (p.n_sp) k_scalar<<<blocks_for(p.n_sp, 256), 256, 0, s>>>(p.sc_post, p.n_sp, p.scal, p.sclist);
+  HC(hipEventRecord(e[10], s));
+  if (p.n_em) k_emit<<<blocks_for(p.n_em, 256), 256, 0, s>>>(p.emit, p.n_em, p.scal, p.arena);
+  if (p.n_b64) k_b64<<<p.n_b64, 256, 0, s>>>(p.b64, p.n_b64, p.arena, p.out);
+  if (p.n_tx)
+    k_verdict<<<blocks_for(p.n_tx, 256), 256, 0, s>>>(p.tx, p.n_tx, p.ck, p.pt_ok, p.hash_ok, p.codes, p.bitmap);
+  HC(hipEventRecord(e[13], s));  // total includes the verdict kernel
+  if (fetch) {
+    if (b->n) HC(hipMemcpyAsync(b->h_res.p, p.codes, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (b->fp.cnt[PS_OUT])
+      HC(hipMemcpyAsync(const_cast<uint8_t*>(slot_out(b)), p.out, b->fp.cnt[PS_OUT], hipMemcpyDeviceToHost, s));
+  }
+  HC(hipEventRecord(e[17], s));
+  HC(hipGetLastError());
+  b->pending = true;
+  return FTZ_SUCCESS;
+}
 
-template <class W, class In, class Plan_fn>
-static int prover_load(ftz_ctx* c, size_t n, const W* w, ftz_prover** out, Plan_fn plan) {
+int prover_wait(ftz_batch* b) { return slot_wait(b); }
+
+template <class W>
+static int prover_load(ftz_ctx* c, size_t n, const W* w, int kind, ftz_prover** out) {
   if (!c || !out || (n && !w)) return set_err(FTZ_E_INVALID, "null argument");
-  std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   ftz_prover* b = new ftz_prover();
   b->ctx = c;
-  b->n = n;
-  std::string e = plan(b->plan);
-  if (!e.empty()) {
-    delete b;
-    return set_err(FTZ_E_INVALID, e);
+  b->prover = true;
+  int rc = slot_init(b);
+  if (rc == FTZ_SUCCESS) rc = prover_plan(b, n, w, kind);
+  if (rc == FTZ_SUCCESS) {
+    hipError_t e = hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, b->st[0]);
+    if (e == hipSuccess) e = hipStreamSynchronize(b->st[0]);
+    if (e != hipSuccess) rc = set_err(FTZ_E_DEVICE, std::string("prover upload failed: ") + hipGetErrorString(e));
   }
-  int rc = batch_upload(b);
   if (rc != FTZ_SUCCESS) {
+    slot_free(b);
     delete b;
     return rc;
   }
@@ -596,138 +801,63 @@ static int prover_load(ftz_ctx* c, size_t n, const W* w, ftz_prover** out, Plan_
   return FTZ_SUCCESS;
 }
 
-static bool seeds_ok(const uint8_t* seed) { return seed != nullptr; }
+static bool transfer_wit_ok(size_t n, const ftz_transfer_witness* w, std::string& e) {
+  for (size_t i = 0; i < n; i++)
+    if ((w[i].n_in && (!w[i].inputs || !w[i].in_values || !w[i].in_bfs)) ||
+        (w[i].n_out && (!w[i].outputs || !w[i].out_values || !w[i].out_bfs)) || !w[i].seed ||
+        (w[i].type_len && !w[i].type)) {
+      e = "null buffer in witness " + std::to_string(i);
+      return false;
+    }
+  return true;
+}
+static bool issue_wit_ok(size_t n, const ftz_issue_witness* w, std::string& e) {
+  for (size_t i = 0; i < n; i++)
+    if ((w[i].n_out && (!w[i].outputs || !w[i].values || !w[i].bfs)) || !w[i].seed ||
+        (w[i].type_len && !w[i].type)) {
+      e = "null buffer in witness " + std::to_string(i);
+      return false;
+    }
+  return true;
+}
+
+static std::vector<TransferWit> to_wit(size_t n, const ftz_transfer_witness* w) {
+  std::vector<TransferWit> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {w[i].inputs,     w[i].n_in,    w[i].outputs, w[i].n_out,    w[i].in_values, w[i].in_bfs,
+            w[i].out_values, w[i].out_bfs, w[i].type,    w[i].type_len, w[i].seed};
+  return t;
+}
+static std::vector<IssueWit> to_wit(size_t n, const ftz_issue_witness* w) {
+  std::vector<IssueWit> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {w[i].outputs, w[i].n_out, w[i].values, w[i].bfs, w[i].type, w[i].type_len, w[i].anonymous, w[i].seed};
+  return t;
+}
 
 extern "C" int ftz_prover_load_transfers(ftz_ctx* c, size_t n, const ftz_transfer_witness* w, ftz_prover** out) {
-  for (size_t i = 0; i < n && w; i++)
-    if ((w[i].n_in && (!w[i].inputs || !w[i].in_values || !w[i].in_bfs)) ||
-        (w[i].n_out && (!w[i].outputs || !w[i].out_values || !w[i].out_bfs)) || !seeds_ok(w[i].seed) ||
-        (w[i].type_len && !w[i].type))
-      return set_err(FTZ_E_INVALID, "null buffer in witness " + std::to_string(i));
-  return prover_load<ftz_transfer_witness, TransferWit>(c, n, w, out, [&](Plan& p) {
-    std::vector<TransferWit> t(n);
-    for (size_t i = 0; i < n; i++)
-      t[i] = {w[i].inputs, w[i].n_in, w[i].outputs, w[i].n_out, w[i].in_values, w[i].in_bfs,
-              w[i].out_values, w[i].out_bfs, w[i].type, w[i].type_len, w[i].seed};
-    return plan_prove_transfers(c->pp, n, t.data(), p, c->threads);
-  });
+  std::string e;
+  if (w && !transfer_wit_ok(n, w, e)) return set_err(FTZ_E_INVALID, e);
+  std::vector<TransferWit> t = w ? to_wit(n, w) : std::vector<TransferWit>();
+  return prover_load(c, n, w ? t.data() : (const TransferWit*)nullptr, 0, out);
 }
 
 extern "C" int ftz_prover_load_issues(ftz_ctx* c, size_t n, const ftz_issue_witness* w, ftz_prover** out) {
-  for (size_t i = 0; i < n && w; i++)
-    if ((w[i].n_out && (!w[i].outputs || !w[i].values || !w[i].bfs)) || !seeds_ok(w[i].seed) ||
-        (w[i].type_len && !w[i].type))
-      return set_err(FTZ_E_INVALID, "null buffer in witness " + std::to_string(i));
-  return prover_load<ftz_issue_witness, IssueWit>(c, n, w, out, [&](Plan& p) {
-    std::vector<IssueWit> t(n);
-    for (size_t i = 0; i < n; i++)
-      t[i] = {w[i].outputs, w[i].n_out, w[i].values, w[i].bfs, w[i].type, w[i].type_len, w[i].anonymous, w[i].seed};
-    return plan_prove_issues(c->pp, n, t.data(), p, c->threads);
-  });
+  std::string e;
+  if (w && !issue_wit_ok(n, w, e)) return set_err(FTZ_E_INVALID, e);
+  std::vector<IssueWit> t = w ? to_wit(n, w) : std::vector<IssueWit>();
+  return prover_load(c, n, w ? t.data() : (const IssueWit*)nullptr, 1, out);
 }
 
 extern "C" int ftz_prover_submit(ftz_prover* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null prover");
-  ftz_ctx* c = b->ctx;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HC(hipSetDevice(c->device));
-  Plan& p = b->plan;
-  hipStream_t s = b->st[0], s2 = b->st[1], s3 = b->st[2];
-  const bool serial = getenv("FTZ_SERIAL") && getenv("FTZ_SERIAL")[0] == '1';  // read per run (bench toggles it)
-  if (serial) s2 = s3 = s;
-  uint32_t (*scal)[8] = reinterpret_cast<uint32_t (*)[8]>(b->scal.p);
-  uint32_t n_dec = (uint32_t)p.dec.size(), n_zr = (uint32_t)p.zr.size(), n_sc = (uint32_t)p.sc.size();
-  uint32_t n_rnd = (uint32_t)p.rnd.size(), n_sp = (uint32_t)p.sc_post.size(), n_em = (uint32_t)p.emit.size();
-  uint32_t n_b64 = (uint32_t)p.b64.size();
-  uint32_t n_g1 = (uint32_t)p.g1.size(), n_g1p = (uint32_t)p.g1p.size(), n_g2 = (uint32_t)p.g2.size();
-  uint32_t n_pr = (uint32_t)p.pr.size();
-  uint32_t n_hp = (uint32_t)p.hpre.size(), n_hm = (uint32_t)p.hmain.size(), n_tx = (uint32_t)p.tx.size();
-  uint64_t jobs[FTZ_NKERNELS] = {n_dec, n_zr, (uint64_t)n_rnd + n_hp, n_sc, n_g1p, n_g2, n_pr, n_pr, n_g1,
-                                 (uint64_t)n_hm + n_sp, (uint64_t)n_em + n_b64, n_tx};
-  hipEvent_t* e = b->ev;
-  HC(hipMemsetAsync(b->bitmap.p, 0, b->bitmap.n * sizeof(uint32_t), s));
-  HC(hipEventRecord(e[0], s));
-  if (n_dec) k_decode<<<blocks_for(n_dec, 256), 256, 0, s>>>(b->dec.p, n_dec, b->wire.p, b->pts.p, b->pt_ok.p, b->arena.p);
-  HC(hipEventRecord(e[1], s));
-  if (n_zr) k_zr<<<blocks_for(n_zr, 256), 256, 0, s>>>(b->zr.p, n_zr, b->wire.p, scal, b->canon.p);
-  HC(hipEventRecord(e[2], s));
-  if (n_rnd) k_rand<<<blocks_for(n_rnd, 128), 128, 0, s>>>(b->rnd.p, n_rnd, b->arena.p, scal);
-  if (n_hp)
-    k_hash<<<blocks_for(n_hp, 128), 128, 0, s>>>(b->hpre.p, n_hp, b->seg.p, b->arena.p, scal, b->canon.p,
-                                                 b->hash_ok_pre.p);
-  HC(hipEventRecord(e[3], s));
-  if (n_sc) k_scalar<<<blocks_for(n_sc, 256), 256, 0, s>>>(b->sc.p, n_sc, scal, b->sclist.p);
-  uint32_t n_sc1 = (uint32_t)p.sc1.size();
-  if (n_sc1) k_scalar<<<blocks_for(n_sc1, 256), 256, 0, s>>>(b->sc1.p, n_sc1, scal, b->sclist.p);
-  HC(hipEventRecord(e[4], s));
-  // stream2: G1 jobs no pairing depends on
-  HC(hipStreamWaitEvent(s2, e[4], 0));
-  HC(hipEventRecord(e[11], s2));
-  if (n_g1) {
-    k_g1_part<<<blocks_for(4 * n_g1, 128), 128, 0, s2>>>(b->g1.p, n_g1, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1.p, b->vtab1.p);
-    k_g1_combine<<<blocks_for(n_g1, 256), 256, 0, s2>>>(b->g1.p, n_g1, b->part1.p, b->g1out.p, b->arena.p);
-  }
-  HC(hipEventRecord(e[12], s2));
-  // main: R' = rr R and rsbf P (the pairing inputs)
-  HC(hipEventRecord(e[16], s));
-  if (n_g1p) {
-    k_g1_part<<<blocks_for(4 * n_g1p, 128), 128, 0, s>>>(b->g1p.p, n_g1p, b->vt.p, b->pts.p, scal, c->g1tab.p,
-                                                         b->part1p.p, b->vtab1p.p);
-    k_g1_combine<<<blocks_for(n_g1p, 256), 256, 0, s>>>(b->g1p.p, n_g1p, b->part1p.p, b->g1out.p, b->arena.p);
-  }
-  HC(hipEventRecord(e[5], s));
-  // stream3: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)
-  HC(hipStreamWaitEvent(s3, e[5], 0));
-  HC(hipEventRecord(e[14], s3));
-  if (n_g2)
-    k_g2lines<<<blocks_for(n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(b->g2.p, b->pr.p, n_g2, scal, c->g2tab.p,
-                                                                 b->g2out.p, b->g1out.p, b->lines2.p);
-  HC(hipEventRecord(e[15], s3));
-  HC(hipStreamWaitEvent(s, e[15], 0));
-  HC(hipEventRecord(e[6], s));
-  if (n_pr)
-    k_miller<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, c->qlines.p, b->lines2.p, b->g1out.p,
-                                                               b->fbuf.p);
-  HC(hipEventRecord(e[7], s));
-  if (n_pr) k_fexp<<<blocks_for(n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(b->pr.p, n_pr, b->fbuf.p, b->arena.p);
-  HC(hipEventRecord(e[8], s));
-  HC(hipStreamWaitEvent(s, e[12], 0));
-  HC(hipEventRecord(e[9], s));
-  if (n_hm)
-    k_hash<<<blocks_for(n_hm, 128), 128, 0, s>>>(b->hmain.p, n_hm, b->seg.p, b->arena.p, scal, b->canon.p,
-                                                 b->hash_ok.p);
-  if (n_sp) k_scalar<<<blocks_for(n_sp, 256), 256, 0, s>>>(b->sc_post.p, n_sp, scal, b->sclist.p);
-  HC(hipEventRecord(e[10], s));
-  if (n_em) k_emit<<<blocks_for(n_em, 256), 256, 0, s>>>(b->emit.p, n_em, scal, b->arena.p);
-  if (n_b64) k_b64<<<n_b64, 256, 0, s>>>(b->b64.p, n_b64, b->arena.p, b->out.p);
-  HC(hipEventRecord(e[13], s));
-  if (n_tx)
-    k_verdict<<<blocks_for(n_tx, 256), 256, 0, s>>>(b->tx.p, n_tx, b->ck.p, b->pt_ok.p, b->hash_ok.p, b->codes.p,
-                                                    b->bitmap.p);
-  HC(hipGetLastError());
-  for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
-  b->pending = true;
-  return FTZ_SUCCESS;
+  if (b->pending) return set_err(FTZ_E_INVALID, "prover resubmitted before ftz_prover_wait");
+  return prover_submit(b, false, false);
 }
 
 extern "C" int ftz_prover_wait(ftz_prover* b) {
   if (!b) return set_err(FTZ_E_INVALID, "null prover");
-  if (!b->pending) return FTZ_SUCCESS;
-  HC(hipSetDevice(b->ctx->device));
-  HC(hipStreamSynchronize(b->st[0]));
-  b->pending = false;
-  hipEvent_t* e = b->ev;
-  // stats order: decode zr rand+hash_pre scalar g1p g2+lines miller fexp g1(side) hash+responses emit+b64 total
-  const int from[FTZ_NKERNELS] = {0, 1, 2, 3, 16, 14, 6, 7, 11, 9, 10, 0};
-  const int to[FTZ_NKERNELS] = {1, 2, 3, 4, 5, 15, 7, 8, 12, 10, 13, 13};
-  for (int k = 0; k < FTZ_NKERNELS; k++) {
-    float ms = 0;
-    HC(hipEventElapsedTime(&ms, e[from[k]], e[to[k]]));
-    b->stats.ms[k] = ms;
-    b->stats.jobs[k] = b->jobs_last[k];
-  }
-  return FTZ_SUCCESS;
+  return prover_wait(b);
 }
 
 extern "C" int ftz_prover_run(ftz_prover* b) {
@@ -735,24 +865,22 @@ extern "C" int ftz_prover_run(ftz_prover* b) {
   return rc == FTZ_SUCCESS ? ftz_prover_wait(b) : rc;
 }
 
-extern "C" size_t ftz_prover_bytes(const ftz_prover* b) { return b ? b->plan.out.size() : 0; }
+extern "C" size_t ftz_prover_bytes(const ftz_prover* b) { return b ? b->fp.cnt[PS_OUT] : 0; }
 
 extern "C" int ftz_prover_proofs(ftz_prover* b, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes) {
   if (!b) return set_err(FTZ_E_INVALID, "null prover");
-  const Plan& p = b->plan;
-  if (cap < p.out.size() || (p.out.size() && !buf)) return set_err(FTZ_E_INVALID, "proof buffer too small");
-  if (b->pending) {
-    int rc = ftz_prover_wait(b);
-    if (rc != FTZ_SUCCESS) return rc;
-  }
+  size_t nb = b->fp.cnt[PS_OUT];
+  if (cap < nb || (nb && !buf)) return set_err(FTZ_E_INVALID, "proof buffer too small");
+  int rc = slot_wait(b);
+  if (rc != FTZ_SUCCESS) return rc;
   HC(hipSetDevice(b->ctx->device));
   hipStream_t s = b->st[0];
-  if (p.out.size()) HC(hipMemcpyAsync(buf, b->out.p, p.out.size(), hipMemcpyDeviceToHost, s));
-  if (codes && b->n) HC(hipMemcpyAsync(codes, b->codes.p, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (nb) HC(hipMemcpyAsync(buf, b->d_blob.p + b->fp.off[PS_OUT], nb, hipMemcpyDeviceToHost, s));
+  if (codes && b->n) HC(hipMemcpyAsync(codes, b->d_scr.p + b->sl.codes, b->n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   HC(hipStreamSynchronize(s));
   if (offsets) {
-    for (size_t i = 0; i < b->n; i++) offsets[i] = p.out_off[i];
-    offsets[b->n] = p.out.size();
+    for (size_t i = 0; i < b->n; i++) offsets[i] = b->fp.out_off[i];
+    offsets[b->n] = nb;
   }
   return FTZ_SUCCESS;
 }
@@ -766,29 +894,94 @@ extern "C" int ftz_prover_stats(const ftz_prover* b, ftz_stats* out) {
 extern "C" void ftz_prover_destroy(ftz_prover* b) {
   if (!b) return;
   (void)hipSetDevice(b->ctx->device);
-  if (b->ev_init)
-    for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
+  slot_free(b);  // syncs and destroys the streams and events (no leak per prove call)
   delete b;
 }
 
-template <class W, class Load>
-static int prove_once(ftz_ctx* c, size_t n, const W* w, uint8_t* buf, size_t cap, size_t* offsets, int32_t* codes,
-                      Load load) {
-  ftz_prover* p = nullptr;
-  int rc = load(c, n, w, &p);
-  if (rc != FTZ_SUCCESS) return rc;
-  rc = ftz_prover_run(p);
-  if (rc == FTZ_SUCCESS) rc = ftz_prover_proofs(p, buf, cap, offsets, codes);
-  ftz_prover_destroy(p);
+// One-shot proving of any n: batches of opt.batch witnesses pipelined through
+// the context's reusable prover slots (plan batch k+1 on the host while batch
+// k runs), proofs concatenated into buf in witness order.
+template <class W>
+static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* buf, size_t cap, size_t* offsets,
+                         int32_t* codes) {
+  std::lock_guard<std::mutex> lk(c->prove_mu);
+  HC(hipSetDevice(c->device));
+  const size_t K = 3, B = c->opt.batch;
+  while (c->pslots.size() < K) {
+    ftz_prover* p = new ftz_prover();
+    p->ctx = c;
+    p->prover = true;
+    int rc = slot_init(p);
+    if (rc != FTZ_SUCCESS) {
+      slot_free(p);
+      delete p;
+      return rc;
+    }
+    c->pslots.push_back(p);
+  }
+  size_t nchunks = (n + B - 1) / B, written = 0;
+  int rc = FTZ_SUCCESS;
+  auto finish = [&](size_t k) {
+    ftz_prover* p = c->pslots[k % K];
+    int r = prover_wait(p);
+    if (r != FTZ_SUCCESS) return r;
+    size_t lo = k * B, nb = p->fp.cnt[PS_OUT];
+    if (written + nb > cap) return set_err(FTZ_E_INVALID, "proof buffer too small");
+    if (nb) memcpy(buf + written, slot_out(p), nb);
+    for (size_t i = 0; i < p->n; i++) {
+      if (offsets) offsets[lo + i] = written + p->fp.out_off[i];
+      if (codes) codes[lo + i] = slot_codes(p)[i];
+    }
+    written += nb;
+    return FTZ_SUCCESS;
+  };
+  size_t done = 0;
+  for (size_t k = 0; k < nchunks && rc == FTZ_SUCCESS; k++) {
+    if (k >= K) {
+      rc = finish(done++);
+      if (rc != FTZ_SUCCESS) break;
+    }
+    ftz_prover* p = c->pslots[k % K];
+    size_t lo = k * B, cnt = std::min(B, n - lo);
+    rc = prover_plan(p, cnt, w + lo, kind);
+    if (rc == FTZ_SUCCESS) rc = prover_submit(p, true, true);
+  }
+  // drain what is in flight (also after an error, so no slot stays pending)
+  int rc2 = FTZ_SUCCESS;
+  while (done < nchunks) {
+    ftz_prover* p = c->pslots[done % K];
+    if (!p->pending) break;
+    int r = rc == FTZ_SUCCESS ? finish(done) : prover_wait(p);
+    if (r != FTZ_SUCCESS && rc2 == FTZ_SUCCESS) rc2 = r;
+    done++;
+  }
+  if (rc == FTZ_SUCCESS) rc = rc2;
+  if (rc == FTZ_SUCCESS && offsets) offsets[n] = written;
   return rc;
 }
 
 extern "C" int ftz_prove_transfers(ftz_ctx* c, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,
                                    size_t* offsets, int32_t* codes) {
-  return prove_once(c, n, w, buf, cap, offsets, codes, ftz_prover_load_transfers);
+  if (!c || (n && !w)) return set_err(FTZ_E_INVALID, "null argument");
+  std::string e;
+  if (!transfer_wit_ok(n, w, e)) return set_err(FTZ_E_INVALID, e);
+  if (n == 0) {
+    if (offsets) offsets[0] = 0;
+    return FTZ_SUCCESS;
+  }
+  std::vector<TransferWit> t = to_wit(n, w);
+  return prove_chunked(c, n, t.data(), 0, buf, cap, offsets, codes);
 }
 
 extern "C" int ftz_prove_issues(ftz_ctx* c, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap,
                                 size_t* offsets, int32_t* codes) {
-  return prove_once(c, n, w, buf, cap, offsets, codes, ftz_prover_load_issues);
+  if (!c || (n && !w)) return set_err(FTZ_E_INVALID, "null argument");
+  std::string e;
+  if (!issue_wit_ok(n, w, e)) return set_err(FTZ_E_INVALID, e);
+  if (n == 0) {
+    if (offsets) offsets[0] = 0;
+    return FTZ_SUCCESS;
+  }
+  std::vector<IssueWit> t = to_wit(n, w);
+  return prove_chunked(c, n, t.data(), 1, buf, cap, offsets, codes);
 }

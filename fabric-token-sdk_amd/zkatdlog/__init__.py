@@ -50,14 +50,22 @@ class Context:
     its validator once per process (token/services/network/fabric/tcc/tcc.go:170-182);
     so does this."""
 
-    def __init__(self, pp_bytes, device=0, threads=None):
+    def __init__(self, pp_bytes, device=0, threads=None, fexp="exact", batch=None, slots=None, window_us=None):
+        """fexp: "exact" (FTZ_FEXP_EXACT, gnark-crypto v0.6.0) or "fuentes";
+        batch / slots / window_us / threads: job-engine options (ftz_options)."""
         self._lib = _abi.load()
         h = ctypes.c_void_p()
         pp_bytes = bytes(pp_bytes)
-        _check(self._lib.ftz_ctx_create(pp_bytes, len(pp_bytes), int(device), ctypes.byref(h)), self._lib)
+        o = _abi.Options()
+        self._lib.ftz_options_default(ctypes.byref(o))
+        o.fexp = _abi.FEXP[fexp]
+        for k, v in (("batch", batch), ("slots", slots), ("window_us", window_us), ("threads", threads)):
+            if v is not None:
+                setattr(o, k, int(v))
+        _check(self._lib.ftz_ctx_create_ex(pp_bytes, len(pp_bytes), int(device), ctypes.byref(o), ctypes.byref(h)),
+               self._lib)
         self._h = h
-        if threads:
-            _check(self._lib.ftz_ctx_set_threads(h, int(threads)), self._lib)
+        self.options = {k: getattr(o, k) for k, _ in _abi.Options._fields_[1:]}
         b, e = ctypes.c_uint32(), ctypes.c_uint32()
         _check(self._lib.ftz_ctx_info(h, ctypes.byref(b), ctypes.byref(e)), self._lib)
         self.base, self.exponent = b.value, e.value
@@ -84,6 +92,30 @@ class Context:
         codes = (ctypes.c_int32 * max(1, n))()
         _check(self._lib.ftz_verify_transfers(self._h, n, arr, codes), self._lib)
         return list(codes)[:n]
+
+    def verify_transfers_flat(self, inputs, in_off, outputs, out_off, proofs, proof_off):
+        """Zero-copy verification of n transfers held in flat buffers (see
+        _abi.pack_transfers_flat); returns a numpy int32 array of codes."""
+        import numpy as np
+        ptr, n, keep = _abi.pack_transfers_flat(inputs, in_off, outputs, out_off, proofs, proof_off)
+        codes = np.zeros(max(1, n), dtype=np.int32)
+        _check(self._lib.ftz_verify_transfers(self._h, n, ptr,
+                                              codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), self._lib)
+        del keep
+        return codes[:n]
+
+    def verify_issues_flat(self, outputs, out_off, proofs, proof_off, anonymous):
+        import numpy as np
+        ptr, n, keep = _abi.pack_issues_flat(outputs, out_off, proofs, proof_off, anonymous)
+        codes = np.zeros(max(1, n), dtype=np.int32)
+        _check(self._lib.ftz_verify_issues(self._h, n, ptr,
+                                           codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), self._lib)
+        del keep
+        return codes[:n]
+
+    def set_serial(self, serial):
+        """profiling: every kernel of a batch on one stream (ftz_ctx_set_serial)"""
+        _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)
 
     def verify_issues(self, issues):
         """issues: iterable of (outputs, proof, anonymous)."""

@@ -33,6 +33,16 @@ MESSAGES = {
 }
 
 
+FTZ_FEXP_EXACT = 0
+FTZ_FEXP_FUENTES = 1
+FEXP = {"exact": FTZ_FEXP_EXACT, "fuentes": FTZ_FEXP_FUENTES}
+
+
+class Options(ctypes.Structure):
+    _fields_ = [("struct_size", ctypes.c_uint32), ("batch", ctypes.c_uint32), ("slots", ctypes.c_uint32),
+                ("window_us", ctypes.c_uint32), ("threads", ctypes.c_uint32), ("fexp", ctypes.c_uint32)]
+
+
 class Transfer(ctypes.Structure):
     _fields_ = [("inputs", ctypes.c_void_p), ("n_in", ctypes.c_uint32),
                 ("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
@@ -108,7 +118,8 @@ class Stats(ctypes.Structure):
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libftsamd.so")
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
-SYMBOLS = ["ftz_ctx_create", "ftz_ctx_destroy", "ftz_last_error", "ftz_ctx_set_threads", "ftz_ctx_info",
+SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
+           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_info",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
@@ -128,7 +139,11 @@ def load():
                            "-- there is no CPU fallback for the zkatdlog GPU verifier" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int32
+    lib.ftz_options_default.argtypes = [ctypes.POINTER(Options)]
+    lib.ftz_options_default.restype = None
     lib.ftz_ctx_create.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
+    lib.ftz_ctx_create_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(vp)]
+    lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
     lib.ftz_ctx_destroy.argtypes = [vp]
     lib.ftz_ctx_destroy.restype = None
     lib.ftz_last_error.restype = ctypes.c_char_p
@@ -187,6 +202,65 @@ def pack_transfers(items):
         arr[k] = Transfer(ctypes.addressof(bi), len(ins) // 64, ctypes.addressof(bo), len(outs) // 64,
                           ctypes.addressof(bp), len(proof))
     return arr, keep
+
+
+def _np_struct(dtype_fields, ctype):
+    import numpy as np
+    dt = np.dtype(dtype_fields, align=True)
+    assert dt.itemsize == ctypes.sizeof(ctype), (dt.itemsize, ctypes.sizeof(ctype))
+    return dt
+
+
+def _addr(buf):
+    """(address, keep) of a bytes-like / numpy uint8 buffer, without copying numpy arrays."""
+    import numpy as np
+    if isinstance(buf, np.ndarray):
+        a = np.ascontiguousarray(buf, dtype=np.uint8)
+        return a.ctypes.data, a
+    b = bytes(buf)
+    c = ctypes.create_string_buffer(b, max(1, len(b)))
+    return ctypes.addressof(c), c
+
+
+def pack_transfers_flat(inputs, in_off, outputs, out_off, proofs, proof_off):
+    """Zero-copy ftz_transfer array over flat buffers (a block as it arrives):
+    transfer i has inputs[in_off[i]:in_off[i+1]] (64-byte RawBytes each),
+    outputs[out_off[i]:out_off[i+1]] and proof proofs[proof_off[i]:proof_off[i+1]];
+    offsets are byte offsets, n+1 of each.  Returns (pointer, n, keepalive)."""
+    import numpy as np
+    in_off, out_off, proof_off = (np.asarray(o, dtype=np.int64) for o in (in_off, out_off, proof_off))
+    n = len(proof_off) - 1
+    dt = _np_struct([("inputs", "<u8"), ("n_in", "<u4"), ("outputs", "<u8"), ("n_out", "<u4"), ("proof", "<u8"),
+                     ("proof_len", "<u8")], Transfer)
+    ai, ki = _addr(inputs)
+    ao, ko = _addr(outputs)
+    ap, kp = _addr(proofs)
+    arr = np.zeros(max(1, n), dtype=dt)
+    arr["inputs"][:n] = ai + in_off[:-1]
+    arr["n_in"][:n] = (in_off[1:] - in_off[:-1]) // 64
+    arr["outputs"][:n] = ao + out_off[:-1]
+    arr["n_out"][:n] = (out_off[1:] - out_off[:-1]) // 64
+    arr["proof"][:n] = ap + proof_off[:-1]
+    arr["proof_len"][:n] = proof_off[1:] - proof_off[:-1]
+    return ctypes.cast(arr.ctypes.data, ctypes.POINTER(Transfer)), n, (arr, ki, ko, kp)
+
+
+def pack_issues_flat(outputs, out_off, proofs, proof_off, anonymous):
+    """As pack_transfers_flat for issues; anonymous: n flags."""
+    import numpy as np
+    out_off, proof_off = (np.asarray(o, dtype=np.int64) for o in (out_off, proof_off))
+    n = len(proof_off) - 1
+    dt = _np_struct([("outputs", "<u8"), ("n_out", "<u4"), ("proof", "<u8"), ("proof_len", "<u8"),
+                     ("anonymous", "u1")], Issue)
+    ao, ko = _addr(outputs)
+    ap, kp = _addr(proofs)
+    arr = np.zeros(max(1, n), dtype=dt)
+    arr["outputs"][:n] = ao + out_off[:-1]
+    arr["n_out"][:n] = (out_off[1:] - out_off[:-1]) // 64
+    arr["proof"][:n] = ap + proof_off[:-1]
+    arr["proof_len"][:n] = proof_off[1:] - proof_off[:-1]
+    arr["anonymous"][:n] = np.asarray(anonymous, dtype=np.uint8)[:n]
+    return ctypes.cast(arr.ctypes.data, ctypes.POINTER(Issue)), n, (arr, ko, kp)
 
 
 def pack_issues(items):

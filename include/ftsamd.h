@@ -16,8 +16,14 @@
  * reference would panic (nil dereference, foreign curve id) is reported as
  * FTZ_ERR_PANIC (reject) instead of crashing the process.
  *
- * Thread-safety: a context may be used from several threads; calls on one
- * context are serialised internally.  Every entry point is synchronous.
+ * Thread-safety and batching: a context may be used from any number of
+ * threads.  ftz_verify_transfers / ftz_verify_issues are synchronous for the
+ * caller but go through one job engine per context: a call of any size is cut
+ * into device batches of at most `batch` proofs (planned on host threads while
+ * earlier batches run on the GPU, `slots` batches in flight), and concurrent
+ * small calls -- the Go shim verifies one TransferAction per call
+ * (validator_transfer.go:84-98) -- are coalesced into shared batches
+ * (micro-batching).  Results are delivered per call.
  */
 #ifndef FTSAMD_H
 #define FTSAMD_H
@@ -75,24 +81,56 @@ typedef struct {
   uint64_t jobs[FTZ_NKERNELS];
 } ftz_stats;
 
+/* Final exponentiation variant [EXT] (GT bytes feed every
+ * membership transcript, sigproof/membership.go:247,260-277):
+ *   FTZ_FEXP_EXACT    f^((p^12-1)/r) -- the Scott et al. (ePrint 2008/490) hard
+ *                     part of gnark-crypto v0.6.0 (go.mod:53), the default;
+ *   FTZ_FEXP_FUENTES  f^(2x(6x^2+3x+1)(p^12-1)/r) -- the Fuentes-Castaneda et al.
+ *                     chain later gnark-crypto releases use. */
+#define FTZ_FEXP_EXACT 0
+#define FTZ_FEXP_FUENTES 1
+
+typedef struct {
+  uint32_t struct_size; /* sizeof(ftz_options)                                          */
+  uint32_t batch;       /* max proofs per device batch (default 4096)                   */
+  uint32_t slots;       /* device batches in flight in the job engine (default 4)       */
+  uint32_t window_us;   /* micro-batching: how long a partial batch may wait for more
+                           callers while the GPU is busy (default 2000)                 */
+  uint32_t threads;     /* host planning threads (0: min(16, hardware threads))         */
+  uint32_t fexp;        /* FTZ_FEXP_EXACT (default) or FTZ_FEXP_FUENTES                 */
+} ftz_options;
+void ftz_options_default(ftz_options* opt);
+
 /* pp: json(driver.SerializedPublicParameters{Identifier:"zkatdlog", Raw}) as
- * produced by crypto.PublicParams.Serialize (setup.go:335-344).
+ * produced by crypto.PublicParams.Serialize (setup.go:119-128) and read by
+ * PublicParams.Deserialize (setup.go:134-151) + Validate (setup.go:238-273).
  * device: HIP device ordinal (the local rank in a multi-GPU job). */
 int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out);
+int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, const ftz_options* opt, ftz_ctx** out);
+/* Call only when no other call on the context is running. */
 void ftz_ctx_destroy(ftz_ctx* ctx);
 /* last error message of the calling thread (empty string if none) */
 const char* ftz_last_error(void);
-/* number of host threads used to plan a batch (default: min(16, cores)) */
+/* number of host threads used to plan a batch; only before the first
+ * ftz_verify_* call on the context (FTZ_E_INVALID afterwards) */
 int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
+/* profiling: 1 = run every kernel of a batch on one stream (per-kernel times
+ * without overlap), 0 = the normal three-stream schedule */
+int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
 /* PP properties: base (len(SignedValues)) and exponent */
 int ftz_ctx_info(const ftz_ctx* ctx, uint32_t* base, uint32_t* exponent);
 
-/* Verify n proofs; codes[i] receives FTZ_OK or an FTZ_ERR_* class. */
+/* Verify n proofs (any n: large calls are split into device batches and
+ * pipelined, small concurrent calls share batches); codes[i] receives FTZ_OK
+ * or an FTZ_ERR_* class. */
 int ftz_verify_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, int32_t* codes);
 int ftz_verify_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, int32_t* codes);
 
 /* Staged form: plan + upload once, then run the GPU pipeline on resident
- * inputs any number of times (used by bench.py to time the device path). */
+ * inputs any number of times (used by bench.py to time the device path).
+ * One staged batch is one device pass: n must keep every job pool of the
+ * batch below 2^31 entries / bytes (FTZ_E_INVALID otherwise; a 2-in/2-out
+ * PP-A transfer uses ~4 KB of arena, so up to ~500k transfers). */
 int ftz_batch_load_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, ftz_batch** out);
 int ftz_batch_load_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, ftz_batch** out);
 int ftz_batch_run(ftz_batch* b); /* = ftz_batch_submit + ftz_batch_wait */

@@ -10,9 +10,11 @@ from /root/reference, see SURVEY.md section 8c and Appendix C:
 * optimal-ate Miller loop (loop count 6x+2, two Frobenius lines) -- the value
   after final exponentiation does not depend on line scaling,
 * final exponentiation  f^((p^6-1)(p^2+1) * H) where the hard exponent H is
-  selectable: ``FE_FUENTES`` (default, H = 2x(6x^2+3x+1)(p^4-p^2+1)/r, the
-  Fuentes-Castaneda et al. variant gnark's bn254 uses) or ``FE_EXACT``
-  (H = (p^4-p^2+1)/r).  [EXT] unpinned -- see DESIGN.md.
+  selectable: ``FE_EXACT`` (default, H = (p^4-p^2+1)/r: gnark-crypto v0.6.0,
+  the version IBM/mathlib 0a7378db6912 pins (reference go.mod:7,53), computes
+  it with the Scott et al. ePrint 2008/490 chain) or ``FE_FUENTES`` (H =
+  2x(6x^2+3x+1)(p^4-p^2+1)/r, the Fuentes-Castaneda et al. chain of later
+  gnark-crypto releases).  [EXT] unpinned -- see DESIGN.md section 4.
 * encodings: G1 RawBytes (64 B X||Y), G2 RawBytes (X.A1|X.A0|Y.A1|Y.A0),
   E12.Bytes (C1.B2.A1 first ... C0.B0.A0 last), HashToZr = SHA-256 mod r.
 
@@ -29,7 +31,7 @@ ATE = 6 * X + 2                  # optimal-ate loop count
 
 FE_FUENTES = "fuentes"
 FE_EXACT = "exact"
-FE_VARIANT = FE_FUENTES          # default [EXT] assumption, see module doc
+FE_VARIANT = FE_EXACT            # default [EXT] assumption, see module doc
 
 # ---------------------------------------------------------------- Fp2
 def f2(a0, a1=0):

@@ -5,10 +5,15 @@ whitespace, ``[]byte`` as standard base64 with padding, nil slices/pointers as
 ``null``, HTML-safe string escaping.  mathlib's G1/G2/Zr elements marshal as
 ``{"curve":<CurveID>,"element":<base64(Bytes())>}`` ([EXT]).
 
-Decoding follows ``json.Unmarshal``: object keys match struct fields exactly
-or case-insensitively, unknown keys are ignored, a later duplicate overwrites
-an earlier one, ``null`` leaves a nil pointer/slice, ``[]byte`` is decoded by
-``base64.StdEncoding`` (``\\r``/``\\n`` ignored, padding required).
+Decoding follows ``json.Unmarshal`` of Go 1.18 (reference go.mod:3): object
+keys match struct fields exactly, else by encoding/json fold.go's foldFunc
+for the field name (ASCII case folding; when the name holds k/K/s/S the key
+may also spell them U+212A KELVIN SIGN / U+017F LATIN SMALL LETTER LONG S),
+unknown keys are ignored, a later duplicate overwrites an earlier one,
+``null`` leaves a nil pointer/slice, strings are unquoted as unquoteBytes does
+(invalid UTF-8 bytes and unpaired surrogates become U+FFFD, one per byte),
+``[]byte`` is decoded by ``base64.StdEncoding`` (``\\r``/``\\n`` ignored,
+padding required).
 """
 import base64
 import json
@@ -52,22 +57,55 @@ def enc_struct(fields):
 
 
 # ------------------------------------------------------------------ decoding
+def _decode_rune(b, i):
+    """unicode/utf8.DecodeRune on bytes b at i -> (rune, size); invalid -> (0xFFFD, 1)."""
+    n = len(b)
+    b0 = b[i]
+    if b0 < 0x80:
+        return b0, 1
+
+    def cont(k, lo=0x80, hi=0xBF):
+        return i + k < n and lo <= b[i + k] <= hi
+    if 0xC2 <= b0 <= 0xDF:
+        if cont(1):
+            return ((b0 & 0x1F) << 6) | (b[i + 1] & 0x3F), 2
+        return 0xFFFD, 1
+    if 0xE0 <= b0 <= 0xEF:
+        lo = 0xA0 if b0 == 0xE0 else 0x80
+        hi = 0x9F if b0 == 0xED else 0xBF
+        if cont(1, lo, hi) and cont(2):
+            return ((b0 & 0x0F) << 12) | ((b[i + 1] & 0x3F) << 6) | (b[i + 2] & 0x3F), 3
+        return 0xFFFD, 1
+    if 0xF0 <= b0 <= 0xF4:
+        lo = 0x90 if b0 == 0xF0 else 0x80
+        hi = 0x8F if b0 == 0xF4 else 0xBF
+        if cont(1, lo, hi) and cont(2) and cont(3):
+            return (((b0 & 0x07) << 18) | ((b[i + 1] & 0x3F) << 12) | ((b[i + 2] & 0x3F) << 6)
+                    | (b[i + 3] & 0x3F)), 4
+        return 0xFFFD, 1
+    return 0xFFFD, 1
+
+
+_HEX = b"0123456789abcdefABCDEF"
+_WS = b" \t\r\n"
+MAX_DEPTH = 10000  # encoding/json scanner.go maxNestingDepth
+
+
 class _Parser:
-    """Minimal RFC 8259 parser that keeps object members as an ordered list of
-    (key, value) pairs, so duplicate keys survive to the typed decoder."""
+    """RFC 8259 parser over BYTES (as encoding/json's scanner) that keeps object
+    members as an ordered list of (key, value) pairs, so duplicate keys survive
+    to the typed decoder.  Strings come out unquoted as Go's unquoteBytes."""
 
     def __init__(self, text):
-        if isinstance(text, (bytes, bytearray)):
-            try:
-                text = bytes(text).decode("utf-8")
-            except UnicodeDecodeError as e:
-                raise GoJSONError("invalid utf-8") from e
-        self.s = text
+        if isinstance(text, str):
+            text = text.encode("utf-8")
+        self.s = bytes(text)
         self.i = 0
+        self.depth = 0
 
     def ws(self):
         s, i = self.s, self.i
-        while i < len(s) and s[i] in " \t\r\n":
+        while i < len(s) and s[i] in _WS:
             i += 1
         self.i = i
 
@@ -84,19 +122,22 @@ class _Parser:
         if self.i >= len(self.s):
             raise GoJSONError("unexpected end of JSON input")
         c = self.s[self.i]
-        if c == "{":
-            return self.obj()
-        if c == "[":
-            return self.arr()
-        if c == '"':
+        if c in b"{[":
+            self.depth += 1
+            if self.depth > MAX_DEPTH:
+                raise GoJSONError("exceeded max depth")
+            v = self.obj() if c == ord("{") else self.arr()
+            self.depth -= 1
+            return v
+        if c == ord('"'):
             return ("str", self.string())
-        if self.s.startswith("null", self.i):
+        if self.s.startswith(b"null", self.i):
             self.i += 4
             return ("null", None)
-        if self.s.startswith("true", self.i):
+        if self.s.startswith(b"true", self.i):
             self.i += 4
             return ("bool", True)
-        if self.s.startswith("false", self.i):
+        if self.s.startswith(b"false", self.i):
             self.i += 5
             return ("bool", False)
         return self.number()
@@ -105,16 +146,16 @@ class _Parser:
         self.i += 1
         pairs = []
         self.ws()
-        if self.i < len(self.s) and self.s[self.i] == "}":
+        if self.i < len(self.s) and self.s[self.i] == ord("}"):
             self.i += 1
             return ("obj", pairs)
         while True:
             self.ws()
-            if self.i >= len(self.s) or self.s[self.i] != '"':
+            if self.i >= len(self.s) or self.s[self.i] != ord('"'):
                 raise GoJSONError("expected object key")
             k = self.string()
             self.ws()
-            if self.i >= len(self.s) or self.s[self.i] != ":":
+            if self.i >= len(self.s) or self.s[self.i] != ord(":"):
                 raise GoJSONError("expected ':'")
             self.i += 1
             v = self.value()
@@ -122,10 +163,10 @@ class _Parser:
             self.ws()
             if self.i >= len(self.s):
                 raise GoJSONError("unexpected end")
-            if self.s[self.i] == ",":
+            if self.s[self.i] == ord(","):
                 self.i += 1
                 continue
-            if self.s[self.i] == "}":
+            if self.s[self.i] == ord("}"):
                 self.i += 1
                 return ("obj", pairs)
             raise GoJSONError("expected ',' or '}'")
@@ -134,7 +175,7 @@ class _Parser:
         self.i += 1
         items = []
         self.ws()
-        if self.i < len(self.s) and self.s[self.i] == "]":
+        if self.i < len(self.s) and self.s[self.i] == ord("]"):
             self.i += 1
             return ("arr", items)
         while True:
@@ -142,90 +183,95 @@ class _Parser:
             self.ws()
             if self.i >= len(self.s):
                 raise GoJSONError("unexpected end")
-            if self.s[self.i] == ",":
+            if self.s[self.i] == ord(","):
                 self.i += 1
                 continue
-            if self.s[self.i] == "]":
+            if self.s[self.i] == ord("]"):
                 self.i += 1
                 return ("arr", items)
             raise GoJSONError("expected ',' or ']'")
+
+    def _u4(self, i):
+        h = self.s[i:i + 4]
+        if len(h) != 4 or any(ch not in _HEX for ch in h):
+            return None
+        return int(h, 16)
 
     def string(self):
         s = self.s
         i = self.i + 1
         out = []
+        esc = {ord('"'): '"', ord("\\"): "\\", ord("/"): "/", ord("b"): "\b", ord("f"): "\f",
+               ord("n"): "\n", ord("r"): "\r", ord("t"): "\t"}
         while True:
             if i >= len(s):
                 raise GoJSONError("unterminated string")
             c = s[i]
-            if c == '"':
+            if c == ord('"'):
                 self.i = i + 1
                 return "".join(out)
-            if c == "\\":
+            if c == ord("\\"):
                 i += 1
                 if i >= len(s):
                     raise GoJSONError("bad escape")
                 e = s[i]
-                m = {'"': '"', "\\": "\\", "/": "/", "b": "\b", "f": "\f",
-                     "n": "\n", "r": "\r", "t": "\t"}
-                if e in m:
-                    out.append(m[e])
+                if e in esc:
+                    out.append(esc[e])
                     i += 1
-                elif e == "u":
-                    h = s[i + 1:i + 5]
-                    if len(h) != 4 or any(ch not in "0123456789abcdefABCDEF" for ch in h):
+                elif e == ord("u"):
+                    cp = self._u4(i + 1)
+                    if cp is None:
                         raise GoJSONError("bad \\u escape")
-                    cp = int(h, 16)
                     i += 5
-                    if 0xD800 <= cp < 0xDC00 and s[i:i + 2] == "\\u":
-                        h2 = s[i + 2:i + 6]
-                        try:
-                            lo = int(h2, 16)
-                        except ValueError:
-                            lo = -1
-                        if 0xDC00 <= lo < 0xE000:
+                    if 0xD800 <= cp < 0xE000:
+                        lo = self._u4(i + 2) if s[i:i + 2] == b"\\u" else None
+                        if cp < 0xDC00 and lo is not None and 0xDC00 <= lo < 0xE000:
                             cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00)
                             i += 6
                         else:
                             cp = 0xFFFD
-                    elif 0xD800 <= cp < 0xE000:
-                        cp = 0xFFFD
                     out.append(chr(cp))
                 else:
                     raise GoJSONError("bad escape")
                 continue
-            if ord(c) < 0x20:
+            if c < 0x20:
                 raise GoJSONError("control character in string")
-            out.append(c)
-            i += 1
+            if c < 0x80:
+                out.append(chr(c))
+                i += 1
+                continue
+            r, size = _decode_rune(s, i)
+            out.append(chr(r))
+            i += size
 
     def number(self):
         s = self.s
         j = self.i
-        if j < len(s) and s[j] == "-":
+        dig = b"0123456789"
+        if j < len(s) and s[j] == ord("-"):
             j += 1
-        if j < len(s) and s[j] == "0":
+        if j < len(s) and s[j] == ord("0"):
             j += 1
-        elif j < len(s) and s[j].isdigit():
-            while j < len(s) and s[j].isdigit():
+        elif j < len(s) and s[j] in dig:
+            while j < len(s) and s[j] in dig:
                 j += 1
         else:
             raise GoJSONError("invalid character")
-        if j < len(s) and s[j] == ".":
+        if j < len(s) and s[j] == ord("."):
             j += 1
-            if not (j < len(s) and s[j].isdigit()):
+            if not (j < len(s) and s[j] in dig):
                 raise GoJSONError("bad number")
-            while j < len(s) and s[j].isdigit():
+            while j < len(s) and s[j] in dig:
                 j += 1
-        if j < len(s) and s[j] in "eE":
+        if j < len(s) and s[j] in b"eE":
             j += 1
-            if j < len(s) and s[j] in "+-":
+            if j < len(s) and s[j] in b"+-":
                 j += 1
-            if not (j < len(s) and s[j].isdigit()):
+            if not (j < len(s) and s[j] in dig):
                 raise GoJSONError("bad number")
-            while j < len(s) and s[j].isdigit():
+            while j < len(s) and s[j] in dig:
                 j += 1
-        tok = s[self.i:j]
+        tok = s[self.i:j].decode()
         self.i = j
         return ("num", tok)
 
@@ -234,16 +280,38 @@ def parse(text):
     return _Parser(text).parse()
 
 
+def key_matches(key, name):
+    """encoding/json: key selects the struct field ``name`` (ASCII) when equal,
+    else under foldFunc(name): every name letter matches the same letter in
+    either ASCII case, and -- only for names holding k/K/s/S (equalFoldRight) --
+    s/S also matches U+017F and k/K matches U+212A."""
+    if key == name:
+        return True
+    special = any(ch in "kKsS" for ch in name)
+    if len(key) != len(name):
+        return False
+    for kc, nc in zip(key, name):
+        if kc == nc:
+            continue
+        if nc.isascii() and nc.isalpha() and kc.isascii() and kc.lower() == nc.lower():
+            continue
+        if special and nc in "sS" and kc == "\u017f":
+            continue
+        if special and nc in "kK" and kc == "\u212a":
+            continue
+        return False
+    return True
+
+
 def field(obj, name):
-    """Go struct-field lookup: the LAST member whose key equals ``name`` exactly
-    or case-insensitively (Go applies members in order, so the last wins).
-    Returns None when the key is absent (zero value)."""
+    """Go struct-field lookup: the LAST member whose key selects ``name``
+    (key_matches; Go applies members in order, so the last wins).  Returns None
+    when the key is absent (zero value)."""
     if obj[0] != "obj":
         raise GoJSONError("cannot unmarshal %s into struct" % obj[0])
     found = None
-    lname = name.lower()
     for k, v in obj[1]:
-        if k == name or k.lower() == lname:
+        if key_matches(k, name):
             found = v
     return found
 

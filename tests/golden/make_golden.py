@@ -87,20 +87,66 @@ def transfer_case(pp, rnd, tag, in_vals, out_vals, ttype="ABC"):
     return ins, outs, proof
 
 
-def main():
-    out = {}
-    # ---------------------------------------------------------------- PP-A
-    pp, rnd = make_pp(100, 2, b"golden-pp-A")
+# [EXT] behaviours of IBM/mathlib 0a7378db6912 / gnark-crypto v0.6.0 the
+# expected verdicts assume; recorded in the fixture.
+EXT_ASSUMPTIONS = {
+    "final_exponentiation": "exact: f^((p^12-1)/r) (Scott et al. ePrint 2008/490 chain of gnark-crypto v0.6.0 "
+                            "bn254.FinalExponentiation); the 'pp_a_fuentes' section holds proofs made under the "
+                            "Fuentes-Castaneda multiple 2x(6x^2+3x+1)(p^12-1)/r for the FTZ_FEXP_FUENTES option",
+    "gt_bytes": "E12.Bytes: C1.B2.A1 first ... C0.B0.A0 last, 32-byte big-endian canonical coefficients",
+    "g1_rawbytes": "X||Y big-endian canonical; infinity = 64 zero bytes (gnark bn254 has no uncompressed-infinity "
+                   "flag)",
+    "g1_decode": "flags 00 uncompressed (coordinates reduced mod p, must be on the curve; (0,0) = infinity), "
+                 "01 infinity, 10/11 compressed (smallest / largest root); anything else rejects",
+    "g2_rawbytes": "X.A1||X.A0||Y.A1||Y.A0",
+    "zr_equals": "raw big.Int comparison: a challenge c+r is not equal to c (rejects); responses are reduced "
+                 "mod r when used",
+    "element_json": "{\"curve\":<CurveID>,\"element\":<base64 Bytes()>}, BN254 = 1; a foreign curve id panics "
+                    "(reported as FTZ_ERR_PANIC)",
+    "hash_to_zr": "SHA-256(bytes) as a big-endian integer mod r",
+    "json_field_matching": "Go 1.18 encoding/json: exact, else foldFunc (ASCII case folding; U+017F for s/S and "
+                           "U+212A for k/K in names holding those letters); last duplicate wins",
+    "json_strings": "unquoteBytes: invalid UTF-8 bytes / unpaired surrogates become U+FFFD (one per byte)",
+}
+
+_POOL_PP = {}
+
+
+def _verify(args):
+    """(pp_json, variant, kind, ins_hex, outs_hex, proof, anonymous) -> (code, message); process-pool worker."""
+    pp_json, variant, kind, ins, outs, proof, anon = args
+    C.FE_VARIANT = variant
+    pp = _POOL_PP.get(pp_json)
+    if pp is None:
+        pp = _POOL_PP[pp_json] = Z.PublicParams.from_json(pp_json)
+    dec = lambda h: [C.g1_from_bytes(bytes.fromhex(h)[64 * i:64 * i + 64]) for i in range(len(h) // 128)]
+    if kind == "transfer":
+        ok, code, msg = Z.transfer_verify(pp, dec(ins), dec(outs), proof)
+    else:
+        ok, code, msg = Z.issue_verify(pp, dec(outs), proof, anon)
+    return code, msg
+
+
+def verify_all(pp, cases, variant):
+    from concurrent.futures import ProcessPoolExecutor
+    js = pp.to_json()
+    args = [(js, variant, c["kind"], c["inputs"], c["outputs"], unb64(c["proof"]), c["anonymous"]) for c in cases]
+    with ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        res = list(ex.map(_verify, args, chunksize=1))
+    for c, (code, msg) in zip(cases, res):
+        c["expect"], c["message"] = code, msg
+        print("%-48s code=%d %s" % (c["name"], code, msg), flush=True)
+    return cases
+
+
+def corpus(pp, rnd, extras=True):
+    """The reference's own test classes plus the SURVEY C.3 tamper corpus, for one PP.
+    Returns case dicts without verdicts (verify_all adds them)."""
     cases = []
 
     def add(name, ins, outs, proof, kind="transfer", anonymous=False):
-        if kind == "transfer":
-            ok, code, msg = Z.transfer_verify(pp, ins, outs, proof)
-        else:
-            ok, code, msg = Z.issue_verify(pp, outs, proof, anonymous)
         cases.append({"name": name, "kind": kind, "inputs": g1cat(ins).hex(), "outputs": g1cat(outs).hex(),
-                      "proof": b64(proof), "anonymous": anonymous, "expect": code, "message": msg})
-        print("%-40s code=%d %s" % (name, code, msg), flush=True)
+                      "proof": b64(proof), "anonymous": anonymous})
 
     # valid transfers (transfer/transfer_test.go:53-59 uses in (90,60) / out (50,100))
     ins, outs, proof = transfer_case(pp, rnd, "t0", [90, 60], [50, 100])
@@ -160,6 +206,20 @@ def main():
     add("wf_unknown_field", ins, outs, join_transfer(top, w, rc))
     add("wf_pretty_printed", ins, outs,
         join_transfer(top, None, rc, raw_wf=json.dumps(wf, indent=2).encode()))
+    if extras:
+        # encoding/json foldFunc: U+017F matches s/S in names holding s (equalFoldRight), ...
+        add("wf_key_long_s_matches_sum", ins, outs,
+            join_transfer(top, None, rc, raw_wf=raw.replace(b'"Sum"', '"\u017fum"'.encode())))
+        add("wf_key_long_s_escaped_matches_sum", ins, outs,
+            join_transfer(top, None, rc, raw_wf=raw.replace(b'"Sum"', b'"\\u017fUM"')))
+        dup3 = raw[:-1] + ',"\u017fum":'.encode() + jdump(zr_elem(777)) + b"}"
+        add("wf_key_long_s_duplicate_last_wins_bad", ins, outs, join_transfer(top, None, rc, raw_wf=dup3))
+        # ... but not in names without s/k ("Type": simple ASCII folding) -> Type missing -> nil panic
+        add("wf_key_long_s_in_type_no_match", ins, outs,
+            join_transfer(top, None, rc, raw_wf=raw.replace(b'"Type"', '"\u017fype"'.encode())))
+        # non-ASCII key bytes that are not a rune (invalid UTF-8) never match
+        add("wf_key_invalid_utf8_no_match", ins, outs,
+            join_transfer(top, None, rc, raw_wf=raw.replace(b'"Sum"', b'"S\xffm"')))
     add("swapped_outputs", ins, list(reversed(outs)), proof)
     add("swapped_inputs", list(reversed(ins)), outs, proof)
     add("truncated_proof_json", ins, outs, proof[:-7])
@@ -174,6 +234,11 @@ def main():
     add("range_null_equality", ins, outs, join_transfer(top, wf, r))
     r = copy.deepcopy(rc); r["EqualityProofs"]["CommitmentBlindingFactor"] = r["EqualityProofs"]["CommitmentBlindingFactor"][:1]
     add("range_equality_length", ins, outs, join_transfer(top, wf, r))
+    if extras:
+        rr = jdump(rc)
+        add("range_key_kelvin_matches_token_bf", ins, outs,
+            join_transfer(top, wf, None, raw_rc=rr.replace(b'"TokenBlindingFactor"',
+                                                           '"To\u212aenBlindingFactor"'.encode())))
     mp = lambda rr, k, i: rr["MembershipProofs"][k]["SignatureProofs"][i]
     r = copy.deepcopy(rc); mp(r, 0, 1)["Challenge"] = zr_elem(zr_val(mp(r, 0, 1)["Challenge"]) ^ 2)
     add("membership_challenge_bitflip", ins, outs, join_transfer(top, wf, r))
@@ -200,7 +265,6 @@ def main():
     y = int.from_bytes(cb[32:], "big")
     r = copy.deepcopy(rc); mp(r, 0, 1)["Commitment"]["element"] = b64(cb[:32] + (y + C.P).to_bytes(32, "big"))
     add("g1_noncanonical_y_accepts", ins, outs, join_transfer(top, wf, r))
-    x = int.from_bytes(cb[:32], "big")
     ny = (-y) % C.P
     flag = 0xC0 if y > ny else 0x80
     comp = bytes([flag | cb[0]]) + cb[1:32]
@@ -250,29 +314,79 @@ def main():
             ti = dict(top_i); ti["RangeCorrectness"] = b64(jdump(rci))
             add("issue_range_challenge", [], toks, jdump(ti), kind="issue")
             add("issue_as_anonymous_mismatch", [], toks, ip, kind="issue", anonymous=True)
+    if extras:
+        # TypeInTheClear is hashed as Go unquotes it: a raw invalid UTF-8 byte is U+FFFD
+        wit = [(42, rnd.zr("isu/bf/0"))]
+        ttype = "AB\ufffdC"
+        toks = [Z.token_commitment(pp, ttype, v, b) for v, b in wit]
+        ip = Z.issue_prove(pp, rnd, toks, wit, ttype, anonymous=False, tag="issue-utf8")
+        top_i = jload(ip)
+        wraw = unb64(top_i["WellFormedness"])
+        fffd = "\ufffd".encode()  # json.Marshal writes U+FFFD as raw UTF-8
+        assert fffd in wraw
+        ti = dict(top_i); ti["WellFormedness"] = b64(wraw.replace(fffd, b"\xff"))
+        add("issue_type_in_clear_invalid_utf8_is_fffd", [], toks, jdump(ti), kind="issue")
+        ti = dict(top_i); ti["WellFormedness"] = b64(wraw.replace(fffd, b"\xff\xfe"))
+        add("issue_type_in_clear_two_invalid_bytes", [], toks, jdump(ti), kind="issue")
     # value out of range: the prover refuses (transfer_test.go:74-84)
     try:
-        transfer_case(pp, rnd, "toor", [10000, 0], [10000, 0])
+        big = pp.base ** pp.exponent
+        transfer_case(pp, rnd, "toor", [big, 0], [big, 0])
         raise AssertionError("prover accepted an out-of-range value")
     except ValueError:
         pass
-    out["pp_a"] = {"base": 100, "exponent": 2, "pp": pp.to_json().decode(), "cases": cases}
+    return cases
 
-    # ---------------------------------------------------------------- PP-B (64-bit-class)
+
+def main():
+    out = {"ext_assumptions": EXT_ASSUMPTIONS,
+           "generator": "tests/golden/make_golden.py (oracle/py/ftsoracle, FE_VARIANT per section)"}
+    # ---------------------------------------------------------------- PP-A (b=100, e=2: reference default)
+    C.FE_VARIANT = C.FE_EXACT
+    pp, rnd = make_pp(100, 2, b"golden-pp-A")
+    out["pp_a"] = {"base": 100, "exponent": 2, "fexp": "exact", "pp": pp.to_json().decode(),
+                   "cases": verify_all(pp, corpus(pp, rnd), C.FE_EXACT)}
+
+    # ---------------------------------------------------------------- PP-A, Fuentes variant proofs
+    C.FE_VARIANT = C.FE_FUENTES
+    rf = Z.Rand(b"golden-pp-A-fuentes")
+    fc = []
+    for k, (iv, ov) in enumerate([([90, 60], [50, 100]), ([9999, 0], [5000, 4999])]):
+        i2, o2, p2 = transfer_case(pp, rf, "tf%d" % k, iv, ov)
+        fc.append({"name": "fuentes_valid_transfer_%d" % k, "kind": "transfer", "inputs": g1cat(i2).hex(),
+                   "outputs": g1cat(o2).hex(), "proof": b64(p2), "anonymous": False})
+    wit = [(10, rf.zr("if/bf/0")), (20, rf.zr("if/bf/1"))]
+    toks = [Z.token_commitment(pp, "ABC", v, b) for v, b in wit]
+    ip = Z.issue_prove(pp, rf, toks, wit, "ABC", anonymous=False, tag="issue-f")
+    fc.append({"name": "fuentes_valid_issue", "kind": "issue", "inputs": "", "outputs": g1cat(toks).hex(),
+               "proof": b64(ip), "anonymous": False})
+    fc = verify_all(pp, fc, C.FE_FUENTES)
+    # the same proofs under the exact variant: every membership transcript differs
+    for c in fc:
+        c["expect_exact"] = _verify((pp.to_json(), C.FE_EXACT, c["kind"], c["inputs"], c["outputs"],
+                                     unb64(c["proof"]), c["anonymous"]))[0]
+    out["pp_a_fuentes"] = {"fexp": "fuentes", "cases": fc}
+    C.FE_VARIANT = C.FE_EXACT
+
+    # ---------------------------------------------------------------- PP-B (b=16, e=16: "64-bit" class)
     if os.environ.get("GOLDEN_PPB", "1") == "1":
         ppb, rndb = make_pp(16, 16, b"golden-pp-B")
-        pp_save = pp
-        pp = ppb
         cases = []
         ib_, ob_, pb_ = transfer_case(ppb, rndb, "b0", [2 ** 62, 12345], [2 ** 61, 2 ** 61 + 12345])
-        add("ppb_valid_2in_2out", ib_, ob_, pb_)
+        cases.append({"name": "ppb_valid_2in_2out_64bit_values", "kind": "transfer", "inputs": g1cat(ib_).hex(),
+                      "outputs": g1cat(ob_).hex(), "proof": b64(pb_), "anonymous": False})
         top_b, wf_b, rc_b = split_transfer(pb_)
         r = copy.deepcopy(rc_b)
         r["MembershipProofs"][1]["SignatureProofs"][15]["Challenge"] = zr_elem(
             zr_val(r["MembershipProofs"][1]["SignatureProofs"][15]["Challenge"]) ^ 1)
-        add("ppb_membership_last_digit", ib_, ob_, join_transfer(top_b, wf_b, r))
-        out["pp_b"] = {"base": 16, "exponent": 16, "pp": ppb.to_json().decode(), "cases": cases}
-        pp = pp_save
+        cases.append({"name": "ppb_membership_last_digit", "kind": "transfer", "inputs": g1cat(ib_).hex(),
+                      "outputs": g1cat(ob_).hex(), "proof": b64(join_transfer(top_b, wf_b, r)), "anonymous": False})
+        # the full PP-A corpus replayed at e = 16
+        for c in corpus(ppb, rndb, extras=False):
+            c["name"] = "ppb_" + c["name"]
+            cases.append(c)
+        out["pp_b"] = {"base": 16, "exponent": 16, "fexp": "exact", "pp": ppb.to_json().decode(),
+                       "cases": verify_all(ppb, cases, C.FE_EXACT)}
 
     path = os.path.join(HERE, "zkatdlog_golden.json")
     with open(path, "w") as f:

@@ -25,11 +25,14 @@ struct EmuCtx {
   std::vector<G1Dev> g1tab;
   std::vector<G2Dev> g2tab;
   std::vector<LineCoef> qlines;
+  int fexp = 0;  // 0: exact (FTZ_FEXP_EXACT), 1: Fuentes
 };
+
+static unsigned g_threads = 0;  // 0: all hardware threads
 
 template <class F>
 static void par_for(uint32_t n, F f) {
-  unsigned t = std::max(1u, std::thread::hardware_concurrency());
+  unsigned t = g_threads ? g_threads : std::max(1u, std::thread::hardware_concurrency());
   std::vector<std::thread> th;
   for (unsigned k = 0; k < t; k++)
     th.emplace_back([&, k]() {
@@ -105,6 +108,8 @@ void* emu_ctx_create(const uint8_t* pp, size_t len, char* err, size_t errlen) {
 }
 
 void emu_ctx_destroy(void* c) { delete (EmuCtx*)c; }
+void emu_ctx_set_fexp(void* c, int variant) { ((EmuCtx*)c)->fexp = variant; }
+void emu_set_threads(int t) { g_threads = t > 0 ? (unsigned)t : 0; }
 
 static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
@@ -141,7 +146,7 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
     job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), i);
   });
-  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data()); });
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data(), c->fexp); });
   par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   for (size_t i = 0; i < n; i++) codes[i] = job_verdict(p.tx[i], p.ck.data(), pt_ok.data(), hok.data());
 }
@@ -184,7 +189,7 @@ int emu_opcount_transfers(void* ctx, size_t n, const ftz_transfer* tx, unsigned 
   stage(4, all.size(), [&](size_t i) { job_g1(all[i], p.vt.data(), pts.data(), scal, c->g1tab.data(), g1out.data(), p.arena.data()); });
   stage(5, p.g2.size(), [&](size_t i) { job_g2(p.g2[i], scal, c->g2tab.data(), g2out.data()); });
   stage(6, p.pr.size(), [&](size_t i) { job_miller(p.pr[i], c->qlines.data(), g1out.data(), pts.data(), g2out.data(), fbuf.data(), (uint32_t)i); });
-  stage(7, p.pr.size(), [&](size_t i) { job_fexp(p.pr[i], fbuf.data(), (uint32_t)i, p.arena.data()); });
+  stage(7, p.pr.size(), [&](size_t i) { job_fexp(p.pr[i], fbuf.data(), (uint32_t)i, p.arena.data(), c->fexp); });
   stage(8, p.hmain.size(), [&](size_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   per_stage[9] = 0;
   jobs[9] = n;
@@ -230,7 +235,7 @@ static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t ca
   par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
     job_miller(p.pr[i], c->qlines.data(), g1out.data(), g1out.data(), g2out.data(), fbuf.data(), i);
   });
-  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data()); });
+  par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data(), c->fexp); });
   par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   par_for((uint32_t)p.sc_post.size(), [&](uint32_t i) { job_scalar(p.sc_post[i], scal, p.sclist.data()); });
   par_for((uint32_t)p.emit.size(), [&](uint32_t i) { job_emit(p.emit[i], scal, p.arena.data()); });
@@ -281,7 +286,7 @@ int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* c
   for (size_t i = 0; i < n; i++)
     t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
   Plan p;
-  plan_transfers(c->pp, n, t.data(), p, 4);
+  plan_transfers(c->pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
   run_plan(c, p, n, codes);
   return 0;
 }
@@ -291,7 +296,7 @@ int emu_verify_issues(void* ctx, size_t n, const ftz_issue* is, int32_t* codes) 
   std::vector<IssueIn> t(n);
   for (size_t i = 0; i < n; i++) t[i] = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
   Plan p;
-  plan_issues(c->pp, n, t.data(), p, 4);
+  plan_issues(c->pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
   run_plan(c, p, n, codes);
   return 0;
 }

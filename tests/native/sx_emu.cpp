@@ -134,13 +134,14 @@ int sxe_ops(uint32_t seed, int iters) {
   return bad;
 }
 
-// final exponentiation of a random Fp12: sextet vs one-lane (GT bytes)
-int sxe_fexp(uint32_t seed, uint8_t* out_sx, uint8_t* out_ref) {
+// final exponentiation of a random Fp12: sextet vs one-lane (GT bytes);
+// variant 0 = exact (k_fexp_exact), 1 = Fuentes (k_fexp)
+int sxe_fexp(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
   uint32_t s = seed | 1;
   fp12 f = rnd_f12(s);
-  f12_to_bytes(out_ref, final_exp(f));
+  f12_to_bytes(out_ref, final_exp(f, variant));
   run6([&](const SxH& x) {
-    fp2 g = sx_final_exp(x, f12_coef(f, x.k));
+    fp2 g = variant == 1 ? sx_final_exp(x, f12_coef(f, x.k)) : sx_final_exp_exact(x, f12_coef(f, x.k));
     sx_gt_bytes(out_sx, x.k, g);
   });
   return memcmp(out_sx, out_ref, 384) != 0;

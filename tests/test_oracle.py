@@ -44,8 +44,8 @@ def test_pairing_bilinear_nondegenerate():
     a, b = 0x1234567, 0xABCDEF
     assert C.pairing(C.g1_mul(C.G1_GEN, a), C.g2_mul(C.G2_GEN, b)) == C.f12_pow(e, a * b)
     # both variants are pairings; they differ by the exponent s = 2x(6x^2+3x+1)
-    ee = C.pairing(C.G1_GEN, C.G2_GEN, C.FE_EXACT)
-    assert C.f12_pow(ee, 2 * C.X * (6 * C.X ** 2 + 3 * C.X + 1)) == e
+    ef = C.pairing(C.G1_GEN, C.G2_GEN, C.FE_FUENTES)
+    assert C.f12_pow(e, 2 * C.X * (6 * C.X ** 2 + 3 * C.X + 1)) == ef  # default is FE_EXACT
 
 
 def test_g1_codec_rules():

@@ -20,10 +20,11 @@ def test_sextet_field_ops(sx):
     assert sx.sxe_ops(20241016, 4) == 0
 
 
+@pytest.mark.parametrize("variant", [0, 1], ids=["exact", "fuentes"])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_sextet_final_exp(sx, seed):
+def test_sextet_final_exp(sx, seed, variant):
     a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
-    assert sx.sxe_fexp(seed, a, b) == 0
+    assert sx.sxe_fexp(seed, variant, a, b) == 0
     assert bytes(a) == bytes(b)
 
 
