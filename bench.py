@@ -1,29 +1,28 @@
 #!/usr/bin/env python3
 """zkatdlog batch-verification benchmark (BASELINE.json configs[1] / [3]).
 
-One step = one pass of the GPU verification pipeline over a batch of
-`--batch` (default 4096) synthetic 2-in/2-out zkatdlog transfers resident in
-HBM (BASELINE configs[1]); with N GPUs every rank verifies its own contiguous
-shard of the same size (weak scaling, BASELINE configs[3]) and the verdict
-bitmaps are gathered over RCCL.  Prints ONE JSON line on rank 0.
+One step = one pass of the verification path over a batch of `--batch`
+(default 4096) synthetic 2-in/2-out zkatdlog transfers (BASELINE configs[1]),
+END TO END: proof bytes in host memory -> Go-encoding/json parse + base64 +
+structural checks on host threads -> one H2D copy -> the HIP kernel pipeline
+-> verdict codes back in host memory.  The timed region is ONE
+ftz_verify_transfers call over steps x batch transfers (the job engine cuts it
+into device batches and pipelines host planning with device execution), so
+`value` includes parsing and upload.  Inputs: distinct proofs made by the GPU
+batch prover (a fresh seed per proof; made and checked before timing) with
+~1/64 rows replaced by tampered golden-corpus proofs; every verdict is checked
+against its expected code.
+
+With N GPUs (torchrun, one process per GPU) the job is N x steps x batch
+transfers sharded contiguously by transaction (zkatdlog.dist.verify_shard,
+weak scaling: each rank verifies steps x batch); the only collective is the
+verdict-bitmap all-gather over RCCL (configs[3]).  Prints ONE JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-    torchrun --nproc-per-node N bench.py --gpus N ...
-
-Verdicts are checked bit-exactly against the oracle's expected codes on
-every run (1/64 of the batch is tampered).
 """
-import os as _os
-
-# Hardware queues per process: 4 batches in flight x 3 streams need more than
-# HIP's default of 4 (set before the HIP runtime initialises; <= 32).
-if int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import argparse
-import base64
 import json
 import os
-import random
 import sys
 import time
 
@@ -34,59 +33,51 @@ METRIC = "zkatdlog transfer proofs verified/sec (node) + BN254 G1 MSM 2^20 laten
 MAD_PER_M = 136  # u32 MADs per 254-bit CIOS Montgomery product (8x8 + 8x8 + 8)
 
 
-def load_workload(batch, rank, seed=2024):
-    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
-    bs = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_transfers.json")))["transfers"]
-    good = [(bytes.fromhex(t["inputs"]), bytes.fromhex(t["outputs"]), base64.b64decode(t["proof"])) for t in bs]
-    good += [(bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"]))
-             for c in g["cases"] if c["kind"] == "transfer" and c["expect"] == 0
-             and len(c["inputs"]) == 256 and len(c["outputs"]) == 256]
-    bad = [((bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"])), c["expect"])
-           for c in g["cases"] if c["kind"] == "transfer" and c["expect"] != 0
-           and len(c["inputs"]) == 256 and len(c["outputs"]) == 256]
-    rng = random.Random(seed + rank)
-    items, expect = [], []
-    for i in range(batch):
-        if rng.random() < 1 / 64:
-            t, e = rng.choice(bad)
-        else:
-            t, e = good[rng.randrange(len(good))], 0
-        items.append(t)
-        expect.append(e)
-    return g["pp"].encode(), items, expect, len(good)
+def cpu_baseline(pp_json, job, sample=2048, reps=5):
+    """The C++ CPU restatement (oracle/cpu/libftscpu.so: the host build of the
+    verifier's planner and job code with 4 x 64-bit Montgomery products) on
+    one thread per core of this process's CPU share, over the first `sample`
+    transfers of the bench job: one warm-up, median of `reps` runs."""
+    import ctypes
 
-
-def cpu_baseline(pp_json, items, expect, seconds=15.0):
-    """The CPU oracle (oracle/py, kind "port") verifying a bounded sample of the
-    same workload on all host cores (one process per core)."""
-    from concurrent.futures import ProcessPoolExecutor
-    sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
-    cores = min(os.cpu_count() or 1, int(os.environ.get("FTS_CPU_BASELINE_CORES", "16")))
-    # one proof takes ~1-1.5 s in the pure-Python oracle: size the sample to ~seconds * cores
-    n = max(cores, int(seconds * cores / 1.3))
-    sample = [(pp_json, items[i], expect[i]) for i in range(min(n, len(items)))]
-    t0 = time.time()
-    with ProcessPoolExecutor(max_workers=cores) as ex:
-        res = list(ex.map(_oracle_verify, sample, chunksize=1))
-    dt = time.time() - t0
-    assert all(r == e for r, (_, _, e) in zip(res, sample)), "oracle disagrees with expected verdicts"
-    return {"value": round(len(sample) / dt, 3), "unit": "transfers/s", "cores": cores, "kind": "port",
-            "sample": "%d transfers of the bench batch verified by oracle/py (pure-Python restatement, "
-                      "one process per core) in %.1f s" % (len(sample), dt)}
-
-
-_PP_CACHE = {}
-
-
-def _oracle_verify(arg):
-    pp_json, (ins, outs, proof), _ = arg
-    from ftsoracle import bn254 as C
-    from ftsoracle import zkat as Z
-    pp = _PP_CACHE.get(pp_json)
-    if pp is None:
-        pp = _PP_CACHE[pp_json] = Z.PublicParams.from_json(pp_json)
-    dec = lambda b: [C.g1_from_bytes(b[64 * i:64 * i + 64]) for i in range(len(b) // 64)]
-    return Z.transfer_verify(pp, dec(ins), dec(outs), proof)[1]
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
+    import build_cpu
+    lib = ctypes.CDLL(build_cpu.build())
+    from zkatdlog import _abi as A
+    lib.emu_ctx_create.restype = ctypes.c_void_p
+    lib.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    lib.emu_ctx_destroy.argtypes = [ctypes.c_void_p]
+    lib.emu_verify_transfers.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Transfer),
+                                         ctypes.POINTER(ctypes.c_int32)]
+    lib.emu_set_threads.argtypes = [ctypes.c_int]
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cores = min(cores, int(os.environ.get("FTS_CPU_BASELINE_CORES", "16")))  # the box's CPU share per GPU
+    lib.emu_set_threads(cores)
+    err = ctypes.create_string_buffer(256)
+    c = lib.emu_ctx_create(pp_json, len(pp_json), err, 256)
+    if not c:
+        raise RuntimeError(err.value.decode())
+    try:
+        n = min(sample, job.n)
+        codes = np.zeros(n, dtype=np.int32)
+        cp = codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        lib.emu_verify_transfers(c, min(n, 4 * cores), job.ptr(), cp)  # warm-up
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            lib.emu_verify_transfers(c, n, job.ptr(), cp)
+            times.append(time.perf_counter() - t0)
+        assert np.array_equal(codes, job.expect[:n]), "CPU restatement disagrees with the expected verdicts"
+    finally:
+        lib.emu_ctx_destroy(c)
+    times.sort()
+    med = times[reps // 2]
+    return {"value": round(n / med, 2), "unit": "transfers/s", "cores": cores, "kind": "port",
+            "impl": "cpp-restatement",
+            "sample": "%d transfers of the bench job (same proofs, same verdicts) verified by the C++ CPU restatement "
+                      "(oracle/cpu: host build of the planner + job code, 4x64-bit Montgomery) on %d threads; "
+                      "median of %d runs after a warm-up: %.2f s" % (n, cores, reps, med)}
 
 
 def madpeak(device):
@@ -102,9 +93,10 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     in HBM (P_i = (i + 1) G generated on the device, random 256-bit scalars),
     median wall-clock of `reps` synchronous runs after one warm-up; the result
     must be identical on every run (tests/test_msm.py checks it bit-exactly)."""
+    import numpy as np
+
     import zkatdlog
     n = 1 << lg
-    import numpy as np
     scal = np.random.default_rng(seed + lg).bytes(32 * n)
     m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
     try:
@@ -125,92 +117,138 @@ def msm_latency(ctx, lg, reps=5, seed=7):
             "window_bits": info["window_bits"]}
 
 
-def prover_bench(ctx, batch, steps, warmup, inflight=1):
-    """BASELINE configs[4] (batch prover) at the configs[1] shape: `batch`
-    2-in/2-out transfer proofs per pass from HBM-resident witnesses (64 distinct
-    witnesses of tests/golden/bench_transfers.json tiled, a distinct 32-byte
-    seed per proof).  The proofs of the last pass are re-verified by the GPU
-    verifier (all must be accepted)."""
-    import hashlib
+def prover_bench(ctx, batch, steps):
+    """BASELINE configs[4] at the configs[1] shape: ONE ftz_prove_transfers call
+    of steps x batch 2-in/2-out transfer proofs (witness bases tiled, a fresh
+    seed per proof), end to end (witness structs in host memory -> proof JSON
+    bytes in host memory).  Every proof is then re-verified by the GPU
+    verifier."""
+    import ctypes
 
-    import zkatdlog
-    bs = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_transfers.json")))["transfers"]
-    ws = []
-    for i in range(batch):
-        t = bs[i % len(bs)]
-        ws.append({"inputs": bytes.fromhex(t["inputs"]), "outputs": bytes.fromhex(t["outputs"]),
-                   "in_values": t["in_values"], "in_bfs": [int(x) for x in t["in_bfs"]],
-                   "out_values": t["out_values"], "out_bfs": [int(x) for x in t["out_bfs"]],
-                   "type": t["type"], "seed": hashlib.sha256(b"bench-prover/%d" % i).digest()})
-    provers = [zkatdlog.Prover(ctx, ws, "transfer") for _ in range(max(1, inflight))]
-    p = provers[0]
-    try:
-        for _ in range(warmup):
-            for q in provers:
-                q.run()
+    import numpy as np
+
+    from zkatdlog import _abi as A
+    from zkatdlog import workload as W
+    bases = W.witness_bases()
+    n = batch * steps
+    sel = np.arange(n) % len(bases)
+    wp, wn, keep = A.pack_transfer_witnesses_tiled(bases, sel, W.seeds(n, b"bench-prover"))
+    t0 = time.perf_counter()
+    blob, offs, codes = ctx.prove_packed("transfer", wp, wn)
+    dt = time.perf_counter() - t0
+    ins = np.frombuffer(b"".join(b["inputs"] for b in bases), dtype=np.uint8)
+    outs = np.frombuffer(b"".join(b["outputs"] for b in bases), dtype=np.uint8)
+    rows = np.zeros(n, dtype=A.transfer_dtype())
+    ia, ik = A.buffer_address(ins)
+    oa, ok_ = A.buffer_address(outs)
+    pa, pk = A.buffer_address(blob)
+    rows["inputs"], rows["n_in"] = ia + 128 * sel, 2
+    rows["outputs"], rows["n_out"] = oa + 128 * sel, 2
+    rows["proof"], rows["proof_len"] = pa + offs[:-1], offs[1:] - offs[:-1]
+    v = ctx.verify_transfers_packed(ctypes.cast(rows.ctypes.data, ctypes.POINTER(A.Transfer)), n)
+    return {"proofs_per_s": round(n / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3), "batch": batch,
+            "proofs": n, "bytes_per_proof": round(float(offs[-1]) / n, 1),
+            "all_accepted_by_gpu_verifier": bool((codes == 0).all() and (v == 0).all())}
+
+
+def device_only(ctx, job, batch, steps, inflight=4):
+    """Device-resident rate (the round-1 headline, kept as a secondary figure):
+    `inflight` batches planned + uploaded once (ftz_batch_load_transfers), then
+    re-run; no host parsing or upload in the timed region."""
+    import numpy as np
+
+    from zkatdlog import workload as W
+    batches = []
+    for k in range(inflight):
+        sub = W.Job(job.rows[k * batch:(k + 1) * batch], job.expect[k * batch:(k + 1) * batch], [job])
+        batches.append((ctx.load_packed(sub.ptr(), sub.n), sub))
+    for b, _ in batches:
+        b.run()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b, _ = batches[k % len(batches)]
+        if k >= len(batches):
+            b.wait()
+        b.submit()
+    for b, _ in batches:
+        b.wait()
+    dt = time.perf_counter() - t0
+    ok = all(np.array_equal(np.asarray(b.codes()), s.expect) for b, s in batches)
+    stats = batches[0][0].stats()
+    t1 = time.perf_counter()
+    batches[0][0].run()
+    lat = (time.perf_counter() - t1) * 1e3
+    for b, _ in batches:
+        b.close()
+    return {"transfers_per_s": round(batch * steps / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3),
+            "batches_in_flight": inflight, "batch_latency_ms": round(lat, 3), "verdicts_ok": ok,
+            "kernel_ms": {k: round(v[0], 3) for k, v in stats.items()}}
+
+
+def plan_rate(ctx, job, batch, reps=3):
+    """Host planning of one batch (JSON parse, base64, structural checks, job
+    layout into the pinned staging blob on the context's planning threads) plus
+    its one H2D copy, via the staged load: best of `reps`, seconds."""
+    from zkatdlog import workload as W
+    sub = W.Job(job.rows[:batch], job.expect[:batch], [job])
+    best = 1e9
+    for _ in range(reps):
         t0 = time.perf_counter()
-        for k in range(steps):  # `inflight` provers on their own streams, as the verifier batches
-            q = provers[k % len(provers)]
-            if k >= len(provers):
-                q.wait()
-            q.submit()
-        for q in provers:
-            q.wait()
-        dt = time.perf_counter() - t0
-        proofs, codes = p.proofs()
-        stats = p.stats()
-        same = all(q.proofs()[0] == proofs for q in provers[1:])  # deterministic seeds: identical bytes
-    finally:
-        for q in provers:
-            q.close()
-    verdicts = ctx.verify_transfers([(w["inputs"], w["outputs"], pr) for w, pr in zip(ws, proofs)])
-    return {"proofs_per_s": round(batch * steps / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3),
-            "batch": batch, "in_flight": len(provers),
-            "all_accepted_by_gpu_verifier": bool(same and all(c == 0 for c in codes) and all(v == 0 for v in verdicts)),
-            "stage_ms": {k: round(v[0], 3) for k, v in stats.items()}}
+        b = ctx.load_packed(sub.ptr(), sub.n)
+        best = min(best, time.perf_counter() - t0)
+        b.close()
+    return best
 
 
-def roofline(batch, device, tx_per_s):
+def roofline(ctx, job, batch, device, tx_per_s):
     """Integer-VALU roofline of the dominant kernel.  The timed steps overlap
     three streams, so per-kernel wall times there include shared SIMDs; the
-    roofline pass re-runs 3 steps with every kernel on one stream (FTZ_SERIAL=1,
-    same kernels, same inputs) and takes each kernel's HIP-event time there.
-    achieved = counted Montgomery products per job (profiles/opcounts.json, the
-    oracle-checked job code run with an op counter) x jobs x 136 MAD / time."""
-    os.environ["FTZ_SERIAL"] = "1"
+    roofline pass re-runs 3 steps of one batch with every kernel on one stream
+    (ftz_ctx_set_serial, same kernels, same inputs) and takes each kernel's
+    HIP-event time there.  achieved = counted Montgomery products per job
+    (profiles/opcounts.json, the oracle-checked job code run with an op
+    counter) x jobs x 136 MAD / time."""
+    from zkatdlog import workload as W
+    sub = W.Job(job.rows[:batch], job.expect[:batch], [job])
+    b = ctx.load_packed(sub.ptr(), sub.n)
+    ctx.set_serial(True)
     try:
+        b.run()
         acc = None
         for _ in range(3):
-            batch.run()
-            st = batch.stats()
+            b.run()
+            st = b.stats()
             acc = st if acc is None else {k: (acc[k][0] + st[k][0], st[k][1]) for k in st}
     finally:
-        del os.environ["FTZ_SERIAL"]
+        ctx.set_serial(False)
+        b.close()
     kern = {k: (v[0] / 3, v[1]) for k, v in acc.items() if k != "total"}
     peak = madpeak(device)
     opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["pp_a"]
-    # k_g1_part + k_g1_combine run the job_g1 work of "g1" (side) / "g1p" (pairing inputs)
     names = {"g1": "k_g1_part+k_g1_combine (side stream)", "g1p": "k_g1_part+k_g1_combine (pairing inputs)",
-             "g2": "k_g2lines", "miller": "k_miller", "fexp": "k_fexp", "hash": "k_hash", "decode": "k_decode"}
-    dom = max((k for k in kern if k in names), key=lambda k: kern[k][0])
-    m_job = opc["m_per_job"]["g1" if dom == "g1p" else dom]
+             "g2": "k_g2lines", "miller": "k_miller", "fexp": "k_fexp_exact", "hash": "k_hash", "decode": "k_decode"}
+    mjob = dict(opc["m_per_job"])
+    mjob["g1p"] = mjob["g1"]  # the pairing-input G1 jobs run the same job code
+    dom = max((k for k in kern if k in names and mjob.get(k)), key=lambda k: kern[k][0])
+    m_job = mjob[dom]
     achieved = m_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_fetch.json")
     if os.path.exists(pmc):
-        t = json.load(open(pmc)).get("per_launch_bytes", {})
-        traffic = t.get(dom)
+        traffic = json.load(open(pmc)).get("per_launch_bytes", {}).get(dom)
     step_mad = opc["m_per_tx"] * tx_per_s * MAD_PER_M
     return {"bound": "valu", "kernel": names[dom], "achieved": round(achieved / 1e12, 4),
             "peak": round(peak / 1e12, 4), "unit": "TMAD/s", "frac": round(achieved / peak, 4),
             "traffic": traffic, "kernel_ms_serial": round(kern[dom][0], 3), "jobs": kern[dom][1],
             "m_per_job": round(m_job, 1),
             "serial_ms": {k: round(v[0], 3) for k, v in kern.items()},
+            "per_kernel_frac": {k: round(mjob[k] * kern[k][1] * MAD_PER_M / (kern[k][0] * 1e-3) / peak, 4)
+                                for k in kern if k in mjob and kern[k][0] > 0},
             "pipeline": {"achieved": round(step_mad / 1e12, 4), "frac": round(step_mad / peak, 4),
-                         "note": "whole step: counted products per transfer x 136 x transfers/s"},
+                         "note": "whole step, end to end: counted products per transfer x 136 x transfers/s"},
             "note": "integer VALU roofline (v_mad_u64_u32, peak = measured madpeak); per-kernel time from a "
-                    "serial pass (FTZ_SERIAL=1) of the same batch; traffic = HBM bytes per launch from "
-                    "rocprofv3 FETCH_SIZE (profiles/pmc_fetch.json, x1024 B, x2 gfx950 correction)"}
+                    "serial pass (ftz_ctx_set_serial) of one batch of the bench job; traffic = HBM bytes per "
+                    "launch from rocprofv3 FETCH_SIZE (profiles/pmc_fetch.json)"}
 
 
 def main():
@@ -218,13 +256,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="transfers per GPU per step")
+    ap.add_argument("--batch", type=int, default=4096, help="transfers per step (per GPU)")
+    ap.add_argument("--distinct", type=int, default=16384, help="distinct GPU-made proofs in the workload")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
     ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
-    ap.add_argument("--inflight", type=int, default=4,
-                    help="batches in flight (ftz_batch_submit on per-batch streams; 1 = one synchronous batch per step)")
+    ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,19 +274,24 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")  # RCCL over xGMI
 
+    import numpy as np
+
     import zkatdlog
-    pp_json, items, expect, ndistinct = load_workload(args.batch, rank)
-    ctx = zkatdlog.Context(pp_json, device=local)
-    t_plan = time.time()
-    batch = ctx.load_transfers(items)  # host planning + H2D upload (outside the timed region)
-    t_plan = time.time() - t_plan
-    # further device-resident copies of the same 4096-transfer batch, so that
-    # consecutive steps overlap as a validator pipelines blocks (each step is
-    # still one full pass over one batch)
-    batches = [batch] + [ctx.load_transfers(items) for _ in range(max(1, args.inflight) - 1)]
-    for _ in range(args.warmup):
-        for b in batches:
-            b.run()
+    from zkatdlog import workload as W
+    from zkatdlog.dist import bitmap_of, verify_shard
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
+    pp_json = g["pp"].encode()
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch)
+    t_setup = time.time()
+    valid = W.prove_distinct(ctx, args.distinct, tag=b"bench/%d" % rank)
+    bad = W.golden_tampered()
+    n_total = world * args.steps * args.batch
+    job = W.mixed_job(valid, bad, n_total, seed=2024)  # the whole N-GPU job (rows are cheap)
+    warm = W.mixed_job(valid, bad, args.warmup * args.batch, seed=7, offset=5)
+    t_setup = time.time() - t_setup
+    if warm.n:
+        wc = ctx.verify_transfers_packed(warm.ptr(), warm.n)
+        assert np.array_equal(wc, warm.expect), "warm-up verdicts differ from the expected codes"
 
     def barrier():
         if dist is not None:
@@ -259,62 +301,49 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        b = batches[k % len(batches)]
-        if k >= len(batches):
-            b.wait()  # its previous step
-        b.submit()
-    for b in batches:
-        b.wait()
+    start, stop, codes = verify_shard(ctx, job.rows, n_total, rank, world)  # ONE call, end to end
     barrier()
     elapsed = time.perf_counter() - t0
-    # one batch alone (latency of a step without overlap)
-    t1 = time.perf_counter()
-    for _ in range(3):
-        batch.run()
-    latency_ms = (time.perf_counter() - t1) / 3 * 1e3
-    # verdicts: exact per-proof codes, and the gathered accept bitmap
-    codes = batch.codes()
-    ok_local = codes == expect and all(b.codes() == expect for b in batches)
-    bits = batch.bitmap()
+    ok_local = bool(np.array_equal(codes, job.expect[start:stop]))
+    bits = bitmap_of(codes)
     if dist is not None:
         from zkatdlog.dist import gather_verdicts, max_elapsed
         elapsed = max_elapsed(elapsed, dist)
-        _, n_accept, verdict_ok = gather_verdicts(bits, len(items), ok_local, dist)  # RCCL over xGMI
+        _, n_accept, verdict_ok = gather_verdicts(bits, stop - start, ok_local, dist)  # RCCL over xGMI
     else:
-        verdict_ok = ok_local
-        n_accept = sum(bin(b).count("1") for b in bits)
+        verdict_ok, n_accept = ok_local, int((codes == 0).sum())
 
-    stats = batch.stats()
     if rank == 0:
-        total = args.batch * world * args.steps
-        value = total / elapsed
-        roof = roofline(batch, local, value)
+        value = n_total / elapsed
+        extras = {}
+        if not args.no_extras:
+            extras["plan_upload_s_per_batch"] = round(plan_rate(ctx, job, args.batch), 4)
+            extras["device_only"] = device_only(ctx, job, args.batch, args.steps)
+            extras["roofline"] = roofline(ctx, job, args.batch, local, value)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
-        prover = None if args.no_prover else prover_bench(ctx, args.batch, args.steps, args.warmup, args.inflight)
+        prover = None if args.no_prover else prover_bench(ctx, args.batch, min(args.steps, 16))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(pp_json, items, expect, args.cpu_seconds)
+            cpu = cpu_baseline(pp_json, job)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "transfers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp/Fr Montgomery)",
-            "data": "synthetic: %d distinct oracle-generated 2-in/2-out transfers (PP-A b=100 e=2) tiled to the "
-                    "batch, 1/64 tampered" % ndistinct,
-            "config": {"workload": "batch verify %d zkatdlog transfers per GPU (BASELINE configs[1]); "
-                                   "%d GPUs sharded by tx (configs[3])" % (args.batch, world),
-                       "batch_per_gpu": args.batch, "pp": "b=100,e=2", "parallelism": "tx-sharded x%d" % world},
-            "verdicts_bit_exact": verdict_ok, "accepted": n_accept,
-            "batches_in_flight": len(batches), "batch_latency_ms": round(latency_ms, 3),
-            "kernel_ms": {k: round(v[0], 3) for k, v in stats.items()},
-            "plan_upload_s": round(t_plan, 3),
-            "roofline": roof, "cpu_baseline": cpu,
+            "data": "synthetic: %d distinct GPU-prover-made 2-in/2-out transfers (PP-A b=100 e=2, fresh seed per "
+                    "proof) tiled over the job, ~1/64 rows tampered golden-corpus proofs; end to end from host "
+                    "proof bytes (parse + upload + kernels + verdicts in the timed region)" % args.distinct,
+            "config": {"workload": "batch verify %d zkatdlog transfers per GPU per step (BASELINE configs[1]); "
+                                   "%d-GPU job of %d transfers sharded by tx (configs[3])"
+                                   % (args.batch, world, n_total),
+                       "batch_per_gpu": args.batch, "pp": "b=100,e=2", "fexp": "exact",
+                       "parallelism": "tx-sharded x%d" % world},
+            "verdicts_bit_exact": verdict_ok, "accepted": n_accept, "setup_s": round(t_setup, 2),
+            "roofline": extras.pop("roofline", None), "cpu_baseline": cpu,
             "msm_2^20_latency_ms": msm20, "msm": msm, "prover": prover,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
-    for b in batches:
-        b.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -113,6 +113,30 @@ class Context:
         del keep
         return codes[:n]
 
+    def verify_transfers_packed(self, ptr, n):
+        """Verify an already packed ftz_transfer array (e.g. a numpy selection
+        of _abi.pack_transfers_flat rows); returns numpy int32 codes."""
+        import numpy as np
+        codes = np.zeros(max(1, n), dtype=np.int32)
+        _check(self._lib.ftz_verify_transfers(self._h, n, ptr,
+                                              codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), self._lib)
+        return codes[:n]
+
+    def prove_packed(self, kind, ptr, n, bytes_per_proof=12288):
+        """One-shot ftz_prove_transfers / ftz_prove_issues on a packed witness
+        array (_abi.pack_*_witnesses_tiled).  Returns (proof blob as a numpy
+        uint8 array, offsets int64[n + 1], codes int32[n])."""
+        import numpy as np
+        fn = self._lib.ftz_prove_transfers if kind == "transfer" else self._lib.ftz_prove_issues
+        cap = max(1, n * bytes_per_proof)
+        buf = np.empty(cap, dtype=np.uint8)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        codes = np.zeros(max(1, n), dtype=np.int32)
+        _check(fn(self._h, n, ptr, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), cap,
+                  offs.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
+                  codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), self._lib)
+        return buf[:int(offs[n])], offs.astype(np.int64), codes[:n]
+
     def set_serial(self, serial):
         """profiling: every kernel of a batch on one stream (ftz_ctx_set_serial)"""
         _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)
@@ -157,6 +181,13 @@ class Context:
         n = len(keep) // 3
         h = ctypes.c_void_p()
         _check(self._lib.ftz_batch_load_transfers(self._h, n, arr, ctypes.byref(h)), self._lib)
+        return Batch(self, h, n)
+
+    def load_packed(self, ptr, n):
+        """Staged batch (ftz_batch_load_transfers) of an already packed
+        ftz_transfer array."""
+        h = ctypes.c_void_p()
+        _check(self._lib.ftz_batch_load_transfers(self._h, n, ptr, ctypes.byref(h)), self._lib)
         return Batch(self, h, n)
 
     def load_issues(self, issues):

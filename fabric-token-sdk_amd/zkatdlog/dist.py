@@ -18,6 +18,27 @@ def shard_range(n_total, rank, world):
     return start, start + base + (1 if rank < extra else 0)
 
 
+def verify_shard(ctx, rows, n_total, rank, world):
+    """BASELINE configs[3]: this rank's contiguous slice [start, stop) of an
+    n_total-transfer job, verified through the context's job engine (which cuts
+    it into device batches and pipelines them).  rows: the job as a packed
+    numpy ftz_transfer array (_abi.pack_transfers_flat rows, or a selection of
+    them).  Returns (start, stop, codes)."""
+    import ctypes
+
+    from . import _abi
+    start, stop = shard_range(n_total, rank, world)
+    part = rows[start:stop]
+    codes = ctx.verify_transfers_packed(ctypes.cast(part.ctypes.data, ctypes.POINTER(_abi.Transfer)), stop - start)
+    return start, stop, codes
+
+
+def bitmap_of(codes):
+    """verdict bitmap (bit i <=> transfer i accepted, LSB first) of a code array"""
+    import numpy as np
+    return np.packbits(np.asarray(codes) == 0, bitorder="little").tobytes()
+
+
 def _device(dist):
     import torch
     return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")

@@ -1,0 +1,148 @@
+"""Synthetic zkatdlog workloads for the bench and the GPU tests.
+
+Distinct transfer proofs are made by the GPU batch prover (ftz_prove_transfers)
+from a few witness bases -- the 2-in/2-out PP-A transfers of
+tests/golden/bench_transfers.json, whose commitments the oracle computed -- with
+a fresh 32-byte seed per proof, so every proof's randomness, commitments to
+randomness, challenges and bytes differ (values uniform
+in [1, (b^e-1)/2], outputs re-split).  Tampered proofs are taken from the golden
+corpus (tests/golden/zkatdlog_golden.json) with their expected codes.
+
+A TransferSet keeps the proof bytes in flat buffers and the job as a packed
+numpy ftz_transfer array (zero-copy: rows point into the buffers), so a
+1M-transfer job is a numpy selection of rows, not 1M Python objects.
+"""
+import base64
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from . import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def witness_bases(path=None):
+    """The bench witness bases (dicts for _abi.pack_transfer_witnesses_tiled)."""
+    bs = json.load(open(path or os.path.join(GOLDEN, "bench_transfers.json")))["transfers"]
+    return [{"inputs": bytes.fromhex(t["inputs"]), "outputs": bytes.fromhex(t["outputs"]),
+             "in_values": t["in_values"], "in_bfs": [int(x) for x in t["in_bfs"]],
+             "out_values": t["out_values"], "out_bfs": [int(x) for x in t["out_bfs"]], "type": t["type"]}
+            for t in bs]
+
+
+def seeds(n, tag=b"bench"):
+    """n distinct 32-byte prover seeds"""
+    out = bytearray(32 * n)
+    for i in range(n):
+        out[32 * i:32 * i + 32] = hashlib.sha256(tag + b"/%d" % i).digest()
+    return bytes(out)
+
+
+class TransferSet:
+    """n transfers whose bytes live in buffers kept alive by this object;
+    rows = packed ftz_transfer numpy array pointing into them; expect = the
+    expected verdict code of each row."""
+
+    def __init__(self, rows, expect, keep):
+        self.rows = rows
+        self.n = len(rows)
+        self.expect = np.asarray(expect, dtype=np.int32)
+        self._keep = keep
+
+    @staticmethod
+    def from_flat(inputs, in_off, outputs, out_off, proofs, proof_off, expect):
+        ptr, n, keep = _abi.pack_transfers_flat(inputs, in_off, outputs, out_off, proofs, proof_off)
+        return TransferSet(keep[0][:n], expect, keep)
+
+    @staticmethod
+    def from_items(items, expect):
+        """items: (inputs, outputs, proof) byte triples"""
+        def flat(parts):
+            off = np.zeros(len(parts) + 1, dtype=np.int64)
+            off[1:] = np.cumsum([len(p) for p in parts])
+            return np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8), off
+        ib, io = flat([t[0] for t in items])
+        ob, oo = flat([t[1] for t in items])
+        pb, po = flat([t[2] for t in items])
+        return TransferSet.from_flat(ib, io, ob, oo, pb, po, expect)
+
+    def proof(self, i):
+        r = self.rows[i]
+        return ctypes.string_at(int(r["proof"]), int(r["proof_len"]))
+
+    def item(self, i):
+        r = self.rows[i]
+        return (ctypes.string_at(int(r["inputs"]), 64 * int(r["n_in"])),
+                ctypes.string_at(int(r["outputs"]), 64 * int(r["n_out"])), self.proof(i))
+
+
+class Job:
+    """A verification job: a row selection over one or more TransferSets
+    (which must stay alive as long as the job)."""
+
+    def __init__(self, rows, expect, sets):
+        self.rows = np.ascontiguousarray(rows)
+        self.expect = np.asarray(expect, dtype=np.int32)
+        self.n = len(self.rows)
+        self._sets = sets
+
+    def ptr(self, start=0):
+        return ctypes.cast(self.rows.ctypes.data + start * self.rows.itemsize, ctypes.POINTER(_abi.Transfer))
+
+
+def prove_distinct(ctx, n, tag=b"bench", bases=None):
+    """n distinct valid 2-in/2-out transfer proofs made on the GPU (witness
+    bases tiled, a fresh seed per proof).  Returns a TransferSet."""
+    bases = bases or witness_bases()
+    sel = np.arange(n) % len(bases)
+    wptr, wn, wkeep = _abi.pack_transfer_witnesses_tiled(bases, sel, seeds(n, tag))
+    blob, offs, codes = ctx.prove_packed("transfer", wptr, wn)
+    if not (codes == 0).all():
+        raise RuntimeError("prover rejected a bench witness")
+    ins = np.frombuffer(b"".join(b["inputs"] for b in bases), dtype=np.uint8)
+    outs = np.frombuffer(b"".join(b["outputs"] for b in bases), dtype=np.uint8)
+    ia, ik = _abi.buffer_address(ins)
+    oa, ok = _abi.buffer_address(outs)
+    pa, pk = _abi.buffer_address(blob)
+    rows = np.zeros(n, dtype=_abi.transfer_dtype())
+    rows["inputs"] = ia + 128 * sel
+    rows["n_in"] = 2
+    rows["outputs"] = oa + 128 * sel
+    rows["n_out"] = 2
+    rows["proof"] = pa + offs[:-1]
+    rows["proof_len"] = offs[1:] - offs[:-1]
+    return TransferSet(rows, np.zeros(n, dtype=np.int32), [ik, ok, pk, blob])
+
+
+def golden_tampered(pp_key="pp_a", shape=(2, 2)):
+    """The golden corpus' rejected transfers of the given shape, with codes."""
+    g = json.load(open(os.path.join(GOLDEN, "zkatdlog_golden.json")))[pp_key]
+    items, codes = [], []
+    for c in g["cases"]:
+        if c["kind"] != "transfer" or c["expect"] == 0:
+            continue
+        if len(c["inputs"]) != 128 * shape[0] or len(c["outputs"]) != 128 * shape[1]:
+            continue
+        items.append((bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"])))
+        codes.append(c["expect"])
+    return TransferSet.from_items(items, codes)
+
+
+def mixed_job(valid, bad, n, rate=1 / 64, seed=2024, offset=0):
+    """A job of n rows: row i is valid[(offset + i) % valid.n] except a
+    pseudo-random ~rate of rows, which are tampered corpus cases."""
+    rng = np.random.default_rng(seed)
+    idx = (offset + np.arange(n)) % valid.n
+    rows = valid.rows[idx].copy()
+    expect = valid.expect[idx].copy()
+    if bad is not None and bad.n and rate > 0:
+        pick = rng.random(n) < rate
+        which = rng.integers(0, bad.n, size=n)
+        rows[pick] = bad.rows[which[pick]]
+        expect[pick] = bad.expect[which[pick]]
+    return Job(rows, expect, [valid, bad])
