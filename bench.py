@@ -20,6 +20,13 @@ verdict-bitmap all-gather over RCCL (configs[3]).  Prints ONE JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
+import os as _os
+
+# Hardware queues per process: the engine keeps 4 batches in flight on 3 streams
+# each; HIP's default of 4 queues would serialise them (set before the HIP
+# runtime initialises; <= 32).
+if int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import argparse
 import json
 import os
@@ -300,10 +307,12 @@ def main():
             dist.barrier()
 
     barrier()
+    ctx.engine_stats(reset=True)
     t0 = time.perf_counter()
     start, stop, codes = verify_shard(ctx, job.rows, n_total, rank, world)  # ONE call, end to end
     barrier()
     elapsed = time.perf_counter() - t0
+    est = ctx.engine_stats()
     ok_local = bool(np.array_equal(codes, job.expect[start:stop]))
     bits = bitmap_of(codes)
     if dist is not None:
@@ -339,6 +348,12 @@ def main():
                        "batch_per_gpu": args.batch, "pp": "b=100,e=2", "fexp": "exact",
                        "parallelism": "tx-sharded x%d" % world},
             "verdicts_bit_exact": verdict_ok, "accepted": n_accept, "setup_s": round(t_setup, 2),
+            "engine": {"batches": est["batches"], "max_in_flight": est["max_in_flight"],
+                       "host_plan_ms_per_batch": round(est["plan_ms"] / max(1, est["batches"]), 3),
+                       "enqueue_ms_per_batch": round(est["submit_ms"] / max(1, est["batches"]), 3),
+                       "device_ms_per_batch": round(est["device_ms"] / max(1, est["batches"]), 3),
+                       "parse_rate_transfers_per_s": round(est["proofs"] / max(1e-9, est["plan_ms"] * 1e-3), 1),
+                       "planning_threads": ctx.options["threads"]},
             "roofline": extras.pop("roofline", None), "cpu_baseline": cpu,
             "msm_2^20_latency_ms": msm20, "msm": msm, "prover": prover,
         }

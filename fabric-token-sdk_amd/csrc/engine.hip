@@ -60,6 +60,8 @@ struct Engine {
   std::deque<Request*> q;
   std::vector<ftz_batch*> slots;
   std::deque<ftz_batch*> free_slots, inflight;
+  ftz_engine_stats st{};
+  Clock::time_point first, last;
   bool stop = false;
   bool disp_done = false;  // the dispatcher has exited (nothing more will be put in flight)
   std::thread disp, comp;
@@ -147,10 +149,19 @@ void Engine::dispatcher() {
       if (bytes >= BATCH_PROOF_BYTES) break;
     }
     lk.unlock();
+    Clock::time_point t0 = Clock::now();
     int rc = slot_plan_items(b, b->items.size(), b->items.data());
+    Clock::time_point t1 = Clock::now();
     if (rc == FTZ_SUCCESS) rc = slot_submit(b, true, true);
+    Clock::time_point t2 = Clock::now();
     std::string err = rc == FTZ_SUCCESS ? std::string() : g_err;
     lk.lock();
+    if (st.batches == 0 && inflight.empty()) first = t1;
+    st.batches++;
+    st.proofs += b->items.size();
+    st.plan_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st.submit_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    st.max_in_flight = std::max<uint32_t>(st.max_in_flight, (uint32_t)inflight.size() + 1);
     if (rc != FTZ_SUCCESS) {
       if (b->pending) {  // enqueued part of the work before failing: let it drain first
         lk.unlock();
@@ -185,7 +196,12 @@ void Engine::completer() {
         off += p.count;
       }
     }
+    float dev_ms = 0;
+    if (rc == FTZ_SUCCESS) (void)hipEventElapsedTime(&dev_ms, b->ev[18], b->ev[13]);
     lk.lock();
+    st.device_ms += dev_ms;
+    last = Clock::now();
+    st.wall_ms = std::chrono::duration<double, std::milli>(last - first).count();
     inflight.pop_front();
     if (rc != FTZ_SUCCESS) {
       fail_parts(b, rc, err);
@@ -273,4 +289,16 @@ void engine_destroy(ftz_ctx* c) {
     delete b;
   }
   delete e;
+}
+
+extern "C" int ftz_ctx_engine_stats(ftz_ctx* c, ftz_engine_stats* out, int reset) {
+  if (!c || !out) return set_err(FTZ_E_INVALID, "null argument");
+  memset(out, 0, sizeof(*out));
+  std::lock_guard<std::mutex> lk(c->eng_mu);
+  Engine* e = c->eng;
+  if (!e) return FTZ_SUCCESS;
+  std::lock_guard<std::mutex> lk2(e->mu);
+  *out = e->st;
+  if (reset) e->st = ftz_engine_stats{};
+  return FTZ_SUCCESS;
 }

@@ -465,6 +465,37 @@ bool b64_decode_append(const char* s, size_t n, std::vector<uint8_t>& out) {
   return true;
 }
 
+bool b64_decode_strict_append(const char* s, size_t n, std::vector<uint8_t>& out) {
+  if (n % 4) return false;
+  size_t base = out.size();
+  out.resize(base + n / 4 * 3);
+  uint8_t* w = out.data() + base;
+  size_t k = 0;
+  for (; k + 4 < n; k += 4) {  // every quantum but the last: 4 alphabet characters
+    int32_t a = B64_TAB[(uint8_t)s[k]], b = B64_TAB[(uint8_t)s[k + 1]], c = B64_TAB[(uint8_t)s[k + 2]],
+            e = B64_TAB[(uint8_t)s[k + 3]];
+    if ((a | b | c | e) < 0) return false;
+    uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)e;
+    w[0] = (uint8_t)(v >> 16);
+    w[1] = (uint8_t)(v >> 8);
+    w[2] = (uint8_t)v;
+    w += 3;
+  }
+  if (n) {  // last quantum: "xxxx", "xxx=" or "xx=="
+    int pad = s[n - 1] == '=' ? (s[n - 2] == '=' ? 2 : 1) : 0;
+    int32_t a = B64_TAB[(uint8_t)s[k]], b = B64_TAB[(uint8_t)s[k + 1]];
+    int32_t c = pad == 2 ? 0 : B64_TAB[(uint8_t)s[k + 2]], e = pad ? 0 : B64_TAB[(uint8_t)s[k + 3]];
+    if ((a | b | c | e) < 0) return false;
+    uint32_t v = ((uint32_t)a << 18) | ((uint32_t)b << 12) | ((uint32_t)c << 6) | (uint32_t)e;
+    w[0] = (uint8_t)(v >> 16);
+    if (pad < 2) w[1] = (uint8_t)(v >> 8);
+    if (pad < 1) w[2] = (uint8_t)v;
+    w += 3 - pad;
+  }
+  out.resize((size_t)(w - out.data()));
+  return true;
+}
+
 bool b64_decode(const char* s, size_t n, std::vector<uint8_t>& out) {
   out.clear();
   return b64_decode_append(s, n, out);

@@ -62,6 +62,9 @@ bool go_key_matches(const char* key, size_t klen, const char* name, size_t nlen)
 bool b64_decode(const char* s, size_t n, std::vector<uint8_t>& out);
 bool b64_decode_append(const char* s, size_t n, std::vector<uint8_t>& out);
 void b64_encode(const uint8_t* p, size_t n, std::string& out);
+// strict form for the canonical fast path: alphabet only, length % 4 == 0,
+// padding only at the end (no '\r' / '\n'); false otherwise
+bool b64_decode_strict_append(const char* s, size_t n, std::vector<uint8_t>& out);
 
 // Result of decoding a JSON value into a Go field of the given kind.
 enum DecStatus : uint8_t { D_OK = 0, D_NIL = 1, D_ERR = 2, D_PANIC = 3 };

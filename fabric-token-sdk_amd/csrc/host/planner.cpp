@@ -151,6 +151,102 @@ struct Doc {
   }
 };
 
+// Reader for the canonical json.Marshal bytes of the proof structs: fields in
+// declaration order, no whitespace, elements as {"curve":1,"element":"<b64>"},
+// pointers / slices null or present.  A document that matches this grammar
+// exactly decodes to the same values under Go's rules as under the general
+// path (Doc), which it skips: no DOM, element bytes decoded straight from the
+// source into the wire pool.  Anything else -- whitespace, case-folded,
+// duplicate or unknown keys, escapes, another curve id, bad base64 -- makes a
+// reader call return false; the caller then rolls the wire pool back and
+// re-parses the document with the general path, which owns every error.
+struct Canon {
+  const uint8_t* s;
+  size_t n, i;
+  Plan* pl;
+
+  Canon(const uint8_t* p, size_t len, Plan* plan) : s(p), n(len), i(0), pl(plan) {}
+
+  bool lit(const char* L, size_t len) {
+    if (i + len > n || memcmp(s + i, L, len) != 0) return false;
+    i += len;
+    return true;
+  }
+  template <size_t N>
+  bool lit(const char (&L)[N]) {
+    return lit(L, N - 1);
+  }
+  bool at(char c) const { return i < n && s[i] == (uint8_t)c; }
+  bool end() const { return i == n; }
+
+  // string body up to the closing quote (validated by the strict base64
+  // decoder, which rejects anything but the alphabet and final padding)
+  bool b64span(size_t& a, size_t& b) {
+    a = i;
+    const void* q = memchr(s + i, '"', n - i);
+    if (!q) return false;
+    b = (size_t)((const uint8_t*)q - s);
+    i = b + 1;
+    return true;
+  }
+
+  // *Elem: null or {"curve":1,"element":"<b64>"}
+  bool elem(Ref& r) {
+    r = Ref();
+    if (at('n')) return lit("null");
+    if (!lit("{\"curve\":1,\"element\":\"")) return false;
+    size_t a, b;
+    if (!b64span(a, b)) return false;
+    std::vector<uint8_t>& w = pl->wire;
+    size_t off = (w.size() + 15) & ~(size_t)15;  // 16-byte aligned element (device vector loads)
+    w.resize(off, 0);
+    if (!b64_decode_strict_append((const char*)s + a, b - a, w) || w.size() - off > ZR_MAX_LEN) return false;
+    r.off = (int64_t)off;
+    r.len = (uint32_t)(w.size() - off);
+    return lit("}");
+  }
+
+  // []*Elem: null or [E,...]
+  bool list(std::vector<Ref>& out) {
+    out.clear();
+    if (at('n')) return lit("null");
+    if (!lit("[")) return false;
+    if (lit("]")) return true;
+    while (true) {
+      Ref r;
+      if (!elem(r)) return false;
+      out.push_back(r);
+      if (lit(",")) continue;
+      return lit("]");
+    }
+  }
+
+  // []byte: null (nil) or "<b64>" decoded into out
+  bool bytes(std::vector<uint8_t>& out, bool& nil) {
+    out.clear();
+    nil = at('n');
+    if (nil) return lit("null");
+    if (!lit("\"")) return false;
+    size_t a, b;
+    if (!b64span(a, b)) return false;
+    return b64_decode_strict_append((const char*)s + a, b - a, out);
+  }
+
+  // string without escapes or non-ASCII bytes
+  bool plain_string(std::string& out) {
+    if (!lit("\"")) return false;
+    size_t a = i;
+    while (i < n && s[i] != '"') {
+      if (s[i] == '\\' || s[i] < 0x20 || s[i] >= 0x80) return false;
+      i++;
+    }
+    if (i >= n) return false;
+    out.assign((const char*)s + a, i - a);
+    i++;
+    return true;
+  }
+};
+
 struct Membership {
   bool nil = true;
   Ref chal, value, combf, sigbf, hash;
@@ -285,7 +381,78 @@ class Builder {
                uint32_t& s_chal, uint32_t wfout_bytes);
   void range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t out_pt, uint32_t out_bytes, uint32_t n);
   static void decode_range(Doc& doc, RangeDoc& r);
+  bool fast_range(const std::vector<uint8_t>& rc, RangeDoc& r);
 };
+
+// RangeProof (range/proof.go:25-57) in canonical form
+bool Builder::fast_range(const std::vector<uint8_t>& rc, RangeDoc& r) {
+  Canon c(rc.data(), rc.size(), &pl);
+  if (!c.lit("{\"Challenge\":") || !c.elem(r.chal) || !c.lit(",\"EqualityProofs\":")) return false;
+  r.eq_nil = c.at('n');
+  if (r.eq_nil) {
+    if (!c.lit("null")) return false;
+  } else if (!c.lit("{\"Type\":") || !c.elem(r.eq_type) || !c.lit(",\"Value\":") || !c.list(r.eq_val) ||
+             !c.lit(",\"TokenBlindingFactor\":") || !c.list(r.eq_tbf) || !c.lit(",\"CommitmentBlindingFactor\":") ||
+             !c.list(r.eq_cbf) || !c.lit("}")) {
+    return false;
+  }
+  if (!c.lit(",\"MembershipProofs\":")) return false;
+  r.mps.clear();
+  if (c.at('n')) {
+    if (!c.lit("null")) return false;
+  } else {
+    if (!c.lit("[")) return false;
+    if (!c.lit("]")) {
+      while (true) {
+        r.mps.emplace_back();
+        MP& mp = r.mps.back();
+        mp.nil = c.at('n');
+        if (mp.nil) {
+          if (!c.lit("null")) return false;
+        } else {
+          if (!c.lit("{\"Commitments\":") || !c.list(mp.coms) || !c.lit(",\"SignatureProofs\":")) return false;
+          if (c.at('n')) {
+            if (!c.lit("null")) return false;
+          } else {
+            if (!c.lit("[")) return false;
+            if (!c.lit("]")) {
+              while (true) {
+                mp.sps.emplace_back();
+                Membership& m = mp.sps.back();
+                m.nil = c.at('n');
+                if (m.nil) {
+                  if (!c.lit("null")) return false;
+                } else {
+                  if (!c.lit("{\"Challenge\":") || !c.elem(m.chal) || !c.lit(",\"Signature\":")) return false;
+                  m.sig_nil = c.at('n');
+                  if (m.sig_nil) {
+                    if (!c.lit("null")) return false;
+                  } else if (!c.lit("{\"R\":") || !c.elem(m.R) || !c.lit(",\"S\":") || !c.elem(m.S) || !c.lit("}")) {
+                    return false;
+                  }
+                  if (!c.lit(",\"Value\":") || !c.elem(m.value) || !c.lit(",\"ComBlindingFactor\":") ||
+                      !c.elem(m.combf) || !c.lit(",\"SigBlindingFactor\":") || !c.elem(m.sigbf) ||
+                      !c.lit(",\"Hash\":") || !c.elem(m.hash) || !c.lit(",\"Commitment\":") || !c.elem(m.commitment) ||
+                      !c.lit("}")) {
+                    return false;
+                  }
+                }
+                if (c.lit(",")) continue;
+                if (!c.lit("]")) return false;
+                break;
+              }
+            }
+          }
+          if (!c.lit("}")) return false;
+        }
+        if (c.lit(",")) continue;
+        if (!c.lit("]")) return false;
+        break;
+      }
+    }
+  }
+  return c.lit("}") && c.end();
+}
 
 uint32_t Builder::tokens(const uint8_t* p, uint32_t n, uint32_t& bytes_off) {
   bytes_off = arena_alloc(64 * n);
@@ -423,22 +590,26 @@ static constexpr uint32_t DIGIT_SLOT = 64 + 64 + 384 + SIG_JSON_LEN;       // 74
 void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t out_pt, uint32_t out_bytes,
                          uint32_t n) {
   begin_range();
-  Doc doc(&pl, jrc);
-  if (!doc.parse(rc, rc_nil)) {
-    fail(E_PARSE);
-    return;
-  }
   RangeDoc r;
   size_t wire_mark = pl.wire.size();
-  decode_range(doc, r);
-  if (doc.panic) {
-    fail(E_PANIC);
-    return;
-  }
-  if (doc.err) {
+  if (rc_nil || !fast_range(rc, r)) {
     pl.wire.resize(wire_mark);
-    fail(E_PARSE);
-    return;
+    r = RangeDoc();
+    Doc doc(&pl, jrc);
+    if (!doc.parse(rc, rc_nil)) {
+      fail(E_PARSE);
+      return;
+    }
+    decode_range(doc, r);
+    if (doc.panic) {
+      fail(E_PANIC);
+      return;
+    }
+    if (doc.err) {
+      pl.wire.resize(wire_mark);
+      fail(E_PARSE);
+      return;
+    }
   }
   // decode every G1 of the document (json.Unmarshal -> mathlib NewG1FromBytes)
   uint32_t e = (uint32_t)pp.exponent;
@@ -614,7 +785,10 @@ void Builder::transfer(const TransferIn& t) {
 
   // transfer.Proof JSON (transfer.go:125-129)
   bool wf_nil = true, rc_nil = true;
-  {
+  Canon oc(t.proof, t.proof_len, &pl);
+  bool outer_fast = oc.lit("{\"WellFormedness\":") && oc.bytes(wfb, wf_nil) && oc.lit(",\"RangeCorrectness\":") &&
+                    oc.bytes(rcb, rc_nil) && oc.lit("}") && oc.end();
+  if (!outer_fast) {
     JDoc& top = jtop;
     if (!top.parse(t.proof, t.proof_len)) {
       fail(E_PARSE);
@@ -638,21 +812,31 @@ void Builder::transfer(const TransferIn& t) {
       return;
     }
   }
-  // WellFormednessVerifier.Verify (wellformedness.go:311-351)
+  // WellFormednessVerifier.Verify (wellformedness.go:157-197, parseProof :200-240)
   {
     Doc doc(&pl, jwf);
-    if (!doc.parse(wfb, wf_nil)) {
+    size_t mark = pl.wire.size();
+    std::vector<Ref> ibf, obf, ivl, ovl;
+    Ref type, sum, chal;
+    Canon c(wfb.data(), wfb.size(), &pl);
+    bool fast = !wf_nil && c.lit("{\"InputBlindingFactors\":") && c.list(ibf) &&
+                c.lit(",\"OutputBlindingFactors\":") && c.list(obf) && c.lit(",\"InputValues\":") && c.list(ivl) &&
+                c.lit(",\"OutputValues\":") && c.list(ovl) && c.lit(",\"Type\":") && c.elem(type) &&
+                c.lit(",\"Sum\":") && c.elem(sum) && c.lit(",\"Challenge\":") && c.elem(chal) && c.lit("}") && c.end();
+    if (!fast) pl.wire.resize(mark);
+    if (!fast && !doc.parse(wfb, wf_nil)) {
       fail(E_PARSE);
     } else {
-      size_t mark = pl.wire.size();
-      int64_t top = doc.top();
-      std::vector<Ref> ibf = doc.list(doc.f(top, "InputBlindingFactors"));
-      std::vector<Ref> obf = doc.list(doc.f(top, "OutputBlindingFactors"));
-      std::vector<Ref> ivl = doc.list(doc.f(top, "InputValues"));
-      std::vector<Ref> ovl = doc.list(doc.f(top, "OutputValues"));
-      Ref type = doc.elem(doc.f(top, "Type"));
-      Ref sum = doc.elem(doc.f(top, "Sum"));
-      Ref chal = doc.elem(doc.f(top, "Challenge"));
+      if (!fast) {
+        int64_t top = doc.top();
+        ibf = doc.list(doc.f(top, "InputBlindingFactors"));
+        obf = doc.list(doc.f(top, "OutputBlindingFactors"));
+        ivl = doc.list(doc.f(top, "InputValues"));
+        ovl = doc.list(doc.f(top, "OutputValues"));
+        type = doc.elem(doc.f(top, "Type"));
+        sum = doc.elem(doc.f(top, "Sum"));
+        chal = doc.elem(doc.f(top, "Challenge"));
+      }
       if (doc.panic) {
         fail(E_PANIC);
       } else if (doc.err) {
@@ -690,7 +874,10 @@ void Builder::issue(const IssueIn& t) {
   if (t.n_out) check(CK_PTS, E_PARSE, tok_pt, t.n_out);
   uint32_t n = t.n_out;
   bool wf_nil = true, rc_nil = true;
-  {
+  Canon oc(t.proof, t.proof_len, &pl);
+  bool outer_fast = oc.lit("{\"WellFormedness\":") && oc.bytes(wfb, wf_nil) && oc.lit(",\"RangeCorrectness\":") &&
+                    oc.bytes(rcb, rc_nil) && oc.lit("}") && oc.end();
+  if (!outer_fast) {
     JDoc& top = jtop;
     if (!top.parse(t.proof, t.proof_len)) {
       fail(E_PARSE);
@@ -714,22 +901,32 @@ void Builder::issue(const IssueIn& t) {
       return;
     }
   }
-  // issue WellFormednessVerifier.Verify (issue/wellformedness.go:206-265)
+  // issue WellFormednessVerifier.Verify (issue/wellformedness.go:206-236, parseProof :239-265)
   Doc doc(&pl, jwf);
-  if (!doc.parse(wfb, wf_nil)) {
-    fail(E_PARSE);
-    end_tx();
-    return;
-  }
   size_t mark = pl.wire.size();
-  int64_t top = doc.top();
-  Ref type = doc.elem(doc.f(top, "Type"));
-  std::vector<Ref> vals = doc.list(doc.f(top, "Values"));
-  std::vector<Ref> bfs = doc.list(doc.f(top, "BlindingFactors"));
+  Ref type, chal;
+  std::vector<Ref> vals, bfs;
   std::string clear;
-  DecStatus cs = dec_string(doc.d, doc.f(top, "TypeInTheClear"), clear);
-  if (cs == D_ERR) doc.err = true;
-  Ref chal = doc.elem(doc.f(top, "Challenge"));
+  Canon c(wfb.data(), wfb.size(), &pl);
+  bool fast = !wf_nil && c.lit("{\"Type\":") && c.elem(type) && c.lit(",\"Values\":") && c.list(vals) &&
+              c.lit(",\"BlindingFactors\":") && c.list(bfs) && c.lit(",\"TypeInTheClear\":") &&
+              c.plain_string(clear) && c.lit(",\"Challenge\":") && c.elem(chal) && c.lit("}") && c.end();
+  if (!fast) {
+    pl.wire.resize(mark);
+    clear.clear();
+    if (!doc.parse(wfb, wf_nil)) {
+      fail(E_PARSE);
+      end_tx();
+      return;
+    }
+    int64_t top = doc.top();
+    type = doc.elem(doc.f(top, "Type"));
+    vals = doc.list(doc.f(top, "Values"));
+    bfs = doc.list(doc.f(top, "BlindingFactors"));
+    DecStatus cs = dec_string(doc.d, doc.f(top, "TypeInTheClear"), clear);
+    if (cs == D_ERR) doc.err = true;
+    chal = doc.elem(doc.f(top, "Challenge"));
+  }
   if (doc.panic) {
     fail(E_PANIC);
     end_tx();

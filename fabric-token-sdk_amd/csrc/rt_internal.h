@@ -5,6 +5,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <array>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -92,7 +94,7 @@ struct ftz_prover;
 
 struct ftz_ctx {
   int device = 0;
-  hipStream_t stream = nullptr, stream2 = nullptr, stream3 = nullptr;
+  hipStream_t stream = nullptr;  // context-level work (setup, MSM)
   PPInfo pp;
   std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
   DBuf<G1Dev> g1tab;
@@ -102,6 +104,12 @@ struct ftz_ctx {
   int serial = 0;                    // profiling: every kernel of a batch on one stream
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
+  // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every
+  // batch slot of the context round-robin, so the number of HIP streams -- and
+  // of hardware queues they need (GPU_MAX_HW_QUEUES) -- stays 3 x opt.slots + 1
+  // however many staged batches, prover slots and engine slots exist.
+  std::vector<std::array<hipStream_t, 3>> triples;
+  std::atomic<uint32_t> next_triple{0};
   // job engine behind ftz_verify_* (created on first use)
   std::mutex eng_mu;
   Engine* eng = nullptr;

@@ -97,6 +97,17 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     ftz_ctx_destroy(c);
     return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
   }
+  for (uint32_t k = 0; k < c->opt.slots; k++) {
+    std::array<hipStream_t, 3> t{};
+    bool ok = hipStreamCreateWithPriority(&t[0], hipStreamNonBlocking, prio_hi) == hipSuccess &&
+              hipStreamCreateWithPriority(&t[1], hipStreamNonBlocking, prio_lo) == hipSuccess &&
+              hipStreamCreateWithPriority(&t[2], hipStreamNonBlocking, prio_hi) == hipSuccess;
+    c->triples.push_back(t);
+    if (!ok) {
+      ftz_ctx_destroy(c);
+      return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
+    }
+  }
   // decode PP points on the GPU: G1 [PedGen, Ped0, Ped1, Ped2, G1 generator], G2 [PK0, PK1, PK2, Q]
   std::vector<uint8_t> raw;
   std::vector<uint32_t> g1off, g2off;
@@ -248,6 +259,13 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   }
   c->pslots.clear();
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& t : c->triples)
+    for (hipStream_t x : t)
+      if (x) {
+        (void)hipStreamSynchronize(x);
+        (void)hipStreamDestroy(x);
+      }
+  c->triples.clear();
   c->g1tab.alloc(0);
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
@@ -272,6 +290,12 @@ extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_ctx_options(const ftz_ctx* c, ftz_options* out) {
+  if (!c || !out) return set_err(FTZ_E_INVALID, "null argument");
+  *out = c->opt;
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_ctx_info(const ftz_ctx* c, uint32_t* base, uint32_t* exponent) {
   if (!c) return set_err(FTZ_E_INVALID, "null context");
   if (base) *base = c->pp.base;
@@ -282,14 +306,12 @@ extern "C" int ftz_ctx_info(const ftz_ctx* c, uint32_t* base, uint32_t* exponent
 // ------------------------------------------------------------------ batch slots
 int slot_init(ftz_batch* b) {
   if (b->st[0]) return FTZ_SUCCESS;
-  // Same priorities as the context streams: the pairing chain and the G2 /
-  // line jobs high, the side G1 jobs (which fill the SIMDs the chain leaves
-  // idle) low.
-  int prio_lo = 0, prio_hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  HC(hipStreamCreateWithPriority(&b->st[0], hipStreamNonBlocking, prio_hi));
-  HC(hipStreamCreateWithPriority(&b->st[1], hipStreamNonBlocking, prio_lo));
-  HC(hipStreamCreateWithPriority(&b->st[2], hipStreamNonBlocking, prio_hi));
+  // the next of the context's shared stream triples (pairing chain and G2 /
+  // line jobs high priority, side G1 jobs -- which fill the SIMDs the chain
+  // leaves idle -- low)
+  ftz_ctx* c = b->ctx;
+  const auto& t = c->triples[c->next_triple.fetch_add(1) % c->triples.size()];
+  for (int k = 0; k < 3; k++) b->st[k] = t[k];
   for (int k = 0; k < 20; k++)
     HC(hipEventCreateWithFlags(&b->ev[k], k == 17 ? (hipEventBlockingSync | hipEventDisableTiming) : 0));
   b->ev_init = true;
@@ -298,13 +320,12 @@ int slot_init(ftz_batch* b) {
 
 void slot_free(ftz_batch* b) {
   if (!b) return;
-  for (int k = 0; k < 3; k++)
-    if (b->st[k]) (void)hipStreamSynchronize(b->st[k]);
+  // the streams are the context's: wait for this slot's last submission only
+  if (b->ev_init && b->pending) (void)hipEventSynchronize(b->ev[17]);
+  b->pending = false;
   if (b->ev_init)
     for (int k = 0; k < 20; k++) (void)hipEventDestroy(b->ev[k]);
   b->ev_init = false;
-  for (int k = 0; k < 3; k++)
-    if (b->st[k]) (void)hipStreamDestroy(b->st[k]);
   b->st[0] = b->st[1] = b->st[2] = nullptr;
 }
 
@@ -493,6 +514,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
                                        p.n_pr,  p.n_pr, p.n_g1, p.n_hm, p.n_tx, p.n_tx};
   for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
+  HC(hipEventRecord(e[18], s));
   if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
   HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
   if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));
@@ -707,6 +729,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
                                  p.n_g1, (uint64_t)p.n_hm + p.n_sp, (uint64_t)p.n_em + p.n_b64, p.n_tx};
   for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
+  HC(hipEventRecord(e[18], s));
   if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
   HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
   if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));

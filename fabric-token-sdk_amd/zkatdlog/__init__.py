@@ -65,6 +65,7 @@ class Context:
         _check(self._lib.ftz_ctx_create_ex(pp_bytes, len(pp_bytes), int(device), ctypes.byref(o), ctypes.byref(h)),
                self._lib)
         self._h = h
+        _check(self._lib.ftz_ctx_options(h, ctypes.byref(o)), self._lib)
         self.options = {k: getattr(o, k) for k, _ in _abi.Options._fields_[1:]}
         b, e = ctypes.c_uint32(), ctypes.c_uint32()
         _check(self._lib.ftz_ctx_info(h, ctypes.byref(b), ctypes.byref(e)), self._lib)
@@ -136,6 +137,12 @@ class Context:
                   offs.ctypes.data_as(ctypes.POINTER(ctypes.c_size_t)),
                   codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), self._lib)
         return buf[:int(offs[n])], offs.astype(np.int64), codes[:n]
+
+    def engine_stats(self, reset=False):
+        """job-engine counters (ftz_ctx_engine_stats)"""
+        st = _abi.EngineStats()
+        _check(self._lib.ftz_ctx_engine_stats(self._h, ctypes.byref(st), 1 if reset else 0), self._lib)
+        return {k: getattr(st, k) for k, _ in _abi.EngineStats._fields_}
 
     def set_serial(self, serial):
         """profiling: every kernel of a batch on one stream (ftz_ctx_set_serial)"""

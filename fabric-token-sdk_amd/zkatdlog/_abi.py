@@ -43,6 +43,12 @@ class Options(ctypes.Structure):
                 ("window_us", ctypes.c_uint32), ("threads", ctypes.c_uint32), ("fexp", ctypes.c_uint32)]
 
 
+class EngineStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("proofs", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
+                ("submit_ms", ctypes.c_double), ("device_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
+                ("max_in_flight", ctypes.c_uint32)]
+
+
 class Transfer(ctypes.Structure):
     _fields_ = [("inputs", ctypes.c_void_p), ("n_in", ctypes.c_uint32),
                 ("outputs", ctypes.c_void_p), ("n_out", ctypes.c_uint32),
@@ -119,7 +125,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
-           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_info",
+           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
@@ -144,6 +150,8 @@ def load():
     lib.ftz_ctx_create.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
     lib.ftz_ctx_create_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(vp)]
     lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
+    lib.ftz_ctx_options.argtypes = [vp, ctypes.POINTER(Options)]
+    lib.ftz_ctx_engine_stats.argtypes = [vp, ctypes.POINTER(EngineStats), ctypes.c_int]
     lib.ftz_ctx_destroy.argtypes = [vp]
     lib.ftz_ctx_destroy.restype = None
     lib.ftz_last_error.restype = ctypes.c_char_p

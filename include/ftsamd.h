@@ -117,6 +117,8 @@ int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
 /* profiling: 1 = run every kernel of a batch on one stream (per-kernel times
  * without overlap), 0 = the normal three-stream schedule */
 int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
+/* the context's resolved options (threads, batch, slots, window, fexp) */
+int ftz_ctx_options(const ftz_ctx* ctx, ftz_options* out);
 /* PP properties: base (len(SignedValues)) and exponent */
 int ftz_ctx_info(const ftz_ctx* ctx, uint32_t* base, uint32_t* exponent);
 
@@ -125,6 +127,22 @@ int ftz_ctx_info(const ftz_ctx* ctx, uint32_t* base, uint32_t* exponent);
  * or an FTZ_ERR_* class. */
 int ftz_verify_transfers(ftz_ctx* ctx, size_t n, const ftz_transfer* tx, int32_t* codes);
 int ftz_verify_issues(ftz_ctx* ctx, size_t n, const ftz_issue* is, int32_t* codes);
+
+/* Job-engine counters since context creation (or the last reset): device
+ * batches, proofs, host planning time (parse + layout into the pinned staging
+ * blob), enqueue time (H2D copy + kernel launches), device time per batch
+ * (HIP events from the H2D copy to the verdict download), and the caller-side
+ * wait of the completion thread. */
+typedef struct {
+  uint64_t batches;
+  uint64_t proofs;
+  double plan_ms;    /* sum over batches */
+  double submit_ms;  /* sum over batches */
+  double device_ms;  /* sum over batches, upload -> verdicts downloaded */
+  double wall_ms;    /* first submission -> last completion */
+  uint32_t max_in_flight;
+} ftz_engine_stats;
+int ftz_ctx_engine_stats(ftz_ctx* ctx, ftz_engine_stats* out, int reset);
 
 /* Staged form: plan + upload once, then run the GPU pipeline on resident
  * inputs any number of times (used by bench.py to time the device path).
