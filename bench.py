@@ -269,6 +269,7 @@ def main():
     ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
     ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
     ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
+    ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,7 +289,7 @@ def main():
     from zkatdlog.dist import bitmap_of, verify_shard
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
-    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch)
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch, slots=args.slots)
     t_setup = time.time()
     valid = W.prove_distinct(ctx, args.distinct, tag=b"bench/%d" % rank)
     bad = W.golden_tampered()

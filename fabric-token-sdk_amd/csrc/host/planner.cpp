@@ -3,7 +3,7 @@
 // compiles the arithmetic into GPU jobs.  Reference (paths under
 // token/core/zkatdlog/crypto/):
 //   transfer.Verifier.Verify             transfer/transfer.go:124-154
-//   WellFormednessVerifier.Verify        transfer/wellformedness.go:311-394
+//   WellFormednessVerifier.Verify        transfer/wellformedness.go:157-240
 //   rangeproof.Verifier.Verify           range/proof.go:211-284, 393-444
 //   MembershipVerifier.Verify            sigproof/membership.go:162-180, 260-305
 //   POKVerifier.recomputeCommitment      sigproof/pok.go:160-204
@@ -467,7 +467,7 @@ uint32_t Builder::tokens(const uint8_t* p, uint32_t n, uint32_t& bytes_off) {
 }
 
 // One side (inputs or outputs) of transfer WF verification:
-// parseProof (wellformedness.go:354-394) + RecomputeCommitments (common/schnorr.go:106-118).
+// parseProof (wellformedness.go:200-240) + RecomputeCommitments (common/schnorr.go:106-118).
 bool Builder::wf_side(uint32_t tok_pt, uint32_t n, const std::vector<Ref>& vals, const std::vector<Ref>& bfs,
                       const Ref& type, const Ref& sum, const Ref& chal, uint32_t& s_type, uint32_t& s_sum,
                       uint32_t& s_chal, uint32_t wfout_bytes) {
@@ -475,7 +475,7 @@ bool Builder::wf_side(uint32_t tok_pt, uint32_t n, const std::vector<Ref>& vals,
     fail(E_MALFORMED);
     return false;
   }
-  if (type.nil()) {  // ModMul(ttype, n) dereferences nil (wellformedness.go:381)
+  if (type.nil()) {  // ModMul(ttype, n) dereferences nil (wellformedness.go:227)
     fail(E_PANIC);
     return false;
   }
@@ -677,7 +677,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
     for (size_t i = 0; i < r.mps[k].sps.size(); i++) {
       const Membership& s = r.mps[k].sps[i];
       const DigitPts& d = dp[k][i];
-      // POKVerifier.recomputeCommitment (pok.go:465-509)
+      // POKVerifier.recomputeCommitment (pok.go:160-204)
       if (s.value.nil() || s.hash.nil() || s.sig_nil || s.R.nil() || s.S.nil() || s.chal.nil() ||
           s.sigbf.nil()) {
         fail(E_MALFORMED);
@@ -1408,8 +1408,69 @@ void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int t
 }
 
 // ------------------------------------------------------------------ public params
-// crypto.PublicParams.Deserialize (setup.go:350-367) + the structural subset
-// of Validate (setup.go:454-489) the verifier relies on.
+// crypto.PublicParams.Validate (setup.go:238-273, RangeProofParams.Validate
+// :56-80) after Deserialize (:134-151), on the serialized bytes: "" or the
+// reference's error text.  Point encodings are checked by ftz_ctx_create.
+static constexpr int64_t MATHLIB_CURVES = 3;  // [EXT] len(math.Curves) at IBM/mathlib 0a7378db6912
+
+std::string validate_pp(const uint8_t* p, size_t n, const char* label) {
+  JDoc outer;
+  if (!outer.parse(p, n) || outer.at(outer.root()).type != J_OBJ) return "invalid public parameters json";
+  std::string ident;
+  if (dec_string(outer, outer.field(outer.root(), "Identifier"), ident) == D_ERR) return "invalid identifier";
+  if (ident != label) return "invalid identifier, expecting [" + std::string(label) + "], got [" + ident + "]";
+  std::vector<uint8_t> raw;
+  if (dec_bytes(outer, outer.field(outer.root(), "Raw"), raw) == D_ERR) return "invalid Raw";
+  JDoc d;
+  if (!d.parse(raw.data(), raw.size())) return "failed unmarshalling public parameters";
+  uint32_t r = d.root();
+  if (d.at(r).type == J_NULL) r = NONE;
+  else if (d.at(r).type != J_OBJ) return "failed unmarshalling public parameters";
+  auto fld = [&](uint32_t o, const char* k) -> int64_t { return o == NONE ? -1 : d.field(o, k); };
+  auto isnull = [&](int64_t x) { return x < 0 || d.at((uint32_t)x).type == J_NULL; };
+  auto arrlen = [&](int64_t x) -> int64_t {
+    if (isnull(x)) return 0;
+    return d.at((uint32_t)x).type == J_ARR ? (int64_t)d.len((uint32_t)x) : -1;
+  };
+  int64_t curve = 0, icurve = 0, prec = 0;
+  std::vector<uint8_t> ipk;
+  if (dec_int(d, fld(r, "Curve"), curve) == D_ERR || dec_int(d, fld(r, "IdemixCurveID"), icurve) == D_ERR ||
+      dec_int(d, fld(r, "QuantityPrecision"), prec) == D_ERR || prec < 0 ||
+      dec_bytes(d, fld(r, "IdemixIssuerPK"), ipk) == D_ERR)
+    return "failed unmarshalling public parameters";
+  const std::string P = "invalid public parameters: ", W = P + "invalid range proof parameters: ";
+  if (curve > MATHLIB_CURVES - 1)
+    return P + "invalid curveID [" + std::to_string(curve) + " > " + std::to_string(MATHLIB_CURVES - 1) + "]";
+  if (icurve > MATHLIB_CURVES - 1)  // the reference prints pp.Curve here
+    return P + "invalid idemix curveID [" + std::to_string(curve) + " > " + std::to_string(MATHLIB_CURVES - 1) + "]";
+  if (isnull(fld(r, "PedGen"))) return P + "nil Pedersen generator";
+  int64_t ped = fld(r, "PedParams"), np = arrlen(ped);
+  if (np < 0) return "failed unmarshalling public parameters";
+  if (np != 3) return P + "length mismatch in Pedersen parameters [" + std::to_string(np) + " vs. 3]";
+  for (uint32_t i = 0; i < 3; i++)
+    if (isnull(d.elem((uint32_t)ped, i))) return P + "nil Pedersen parameter at index " + std::to_string(i);
+  int64_t rpp = fld(r, "RangeProofParams");
+  if (isnull(rpp)) return P + "nil range proof parameters";
+  if (d.at((uint32_t)rpp).type != J_OBJ) return "failed unmarshalling public parameters";
+  int64_t spk = d.field((uint32_t)rpp, "SignPK"), sv = d.field((uint32_t)rpp, "SignedValues");
+  int64_t nspk = arrlen(spk), nsv = arrlen(sv), e = 0;
+  if (nspk < 0 || nsv < 0 || dec_int(d, d.field((uint32_t)rpp, "Exponent"), e) == D_ERR)
+    return "failed unmarshalling public parameters";
+  if (nspk != 3) return W + "signature public key should be 3, instead it is " + std::to_string(nspk);
+  if (nsv < 2) return W + "signed values should be > 2";
+  if (isnull(d.field((uint32_t)rpp, "Q"))) return W + "generator Q is nil";
+  if (e == 0) return W + "exponent is 0";
+  for (int64_t i = 0; i < nsv; i++)
+    if (isnull(d.elem((uint32_t)sv, (uint32_t)i))) return W + "signed value at index " + std::to_string(i) + " is nil";
+  for (int64_t i = 0; i < nspk; i++)
+    if (isnull(d.elem((uint32_t)spk, (uint32_t)i))) return W + "public key at index " + std::to_string(i) + " is nil";
+  if (prec != 64) return P + "quantity precision should be 64 instead it is " + std::to_string(prec);
+  if (ipk.empty()) return P + "empty idemix issuer";
+  return "";
+}
+
+// crypto.PublicParams.Deserialize (setup.go:134-151) + the structural subset
+// of Validate (setup.go:238-273) the verifier relies on.
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out) {
   JDoc outer;
   if (!outer.parse(p, n)) return "invalid public parameters json";

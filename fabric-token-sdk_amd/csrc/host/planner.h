@@ -37,6 +37,8 @@ struct PPInfo {
 };
 // Returns empty string on success, else an error message.
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out);
+// PublicParams.Validate (setup.go:238-273) on serialized PP: "" or the error text
+std::string validate_pp(const uint8_t* p, size_t n, const char* label);
 
 struct Plan {
   std::vector<uint8_t> wire;   // raw element bytes (decode / zr job inputs)

@@ -97,7 +97,10 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     ftz_ctx_destroy(c);
     return set_err(FTZ_E_DEVICE, "hipStreamCreate failed");
   }
-  for (uint32_t k = 0; k < c->opt.slots; k++) {
+  // at most 4 triples (13 streams with the context's own: fits 16 hardware
+  // queues); engine slots beyond that share them round-robin, i.e. are planned
+  // ahead and queue behind the batch 4 slots earlier
+  for (uint32_t k = 0; k < std::min<uint32_t>(c->opt.slots, 4); k++) {
     std::array<hipStream_t, 3> t{};
     bool ok = hipStreamCreateWithPriority(&t[0], hipStreamNonBlocking, prio_hi) == hipSuccess &&
               hipStreamCreateWithPriority(&t[1], hipStreamNonBlocking, prio_lo) == hipSuccess &&
@@ -288,6 +291,12 @@ extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
   if (!c) return set_err(FTZ_E_INVALID, "null context");
   c->serial = serial ? 1 : 0;
   return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_pp_validate(const uint8_t* pp, size_t pp_len) {
+  if (!pp) return set_err(FTZ_E_INVALID, "null argument");
+  std::string e = validate_pp(pp, pp_len, "zkatdlog");
+  return e.empty() ? FTZ_SUCCESS : set_err(FTZ_E_PP, e);
 }
 
 extern "C" int ftz_ctx_options(const ftz_ctx* c, ftz_options* out) {

@@ -5,7 +5,7 @@ Host-side mirror of the reference's verifier interfaces (Go, paths relative to
 
     transfer.NewVerifier(inputs, outputs, pp).Verify(proof)   transfer/transfer.go:66,124
     issue.NewVerifier(tokens, anonymous, pp).Verify(proof)    issue/issue.go:194,202
-    validator TransferZKProofValidate(ctx)                    validator/validator_transfer.go:232
+    validator TransferZKProofValidate(ctx)                    validator/validator_transfer.go:84-98
 
 backed by libftsamd.so (include/ftsamd.h): every proof is parsed on the host
 and verified by HIP kernels on the GPU.  There is no CPU fallback: without
@@ -203,6 +203,15 @@ class Context:
         h = ctypes.c_void_p()
         _check(self._lib.ftz_batch_load_issues(self._h, n, arr, ctypes.byref(h)), self._lib)
         return Batch(self, h, n)
+
+
+def validate_public_params(pp_bytes):
+    """crypto.PublicParams.Validate (setup.go:238-273): "" or the error text
+    (host-side check; no GPU needed)."""
+    lib = _abi.load()
+    pp_bytes = bytes(pp_bytes)
+    rc = lib.ftz_pp_validate(pp_bytes, len(pp_bytes))
+    return "" if rc == 0 else lib.ftz_last_error().decode(errors="replace")
 
 
 class Msm:

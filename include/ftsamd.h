@@ -93,7 +93,8 @@ typedef struct {
 typedef struct {
   uint32_t struct_size; /* sizeof(ftz_options)                                          */
   uint32_t batch;       /* max proofs per device batch (default 4096)                   */
-  uint32_t slots;       /* device batches in flight in the job engine (default 4)       */
+  uint32_t slots;       /* batch slots of the job engine = batches in flight (default 4;
+                           measured best of 4/5/6/8, profiles/r02_slots_sweep.txt)      */
   uint32_t window_us;   /* micro-batching: how long a partial batch may wait for more
                            callers while the GPU is busy (default 2000)                 */
   uint32_t threads;     /* host planning threads (0: min(16, hardware threads))         */
@@ -117,6 +118,11 @@ int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
 /* profiling: 1 = run every kernel of a batch on one stream (per-kernel times
  * without overlap), 0 = the normal three-stream schedule */
 int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
+/* crypto.PublicParams.Validate (setup.go:238-273) on serialized public
+ * parameters, as the FSC node's loader runs it (nogh/loaders.go:133):
+ * FTZ_SUCCESS, or FTZ_E_PP with the reference's error text in
+ * ftz_last_error().  Point encodings are checked by ftz_ctx_create. */
+int ftz_pp_validate(const uint8_t* pp, size_t pp_len);
 /* the context's resolved options (threads, batch, slots, window, fexp) */
 int ftz_ctx_options(const ftz_ctx* ctx, ftz_options* out);
 /* PP properties: base (len(SignedValues)) and exponent */

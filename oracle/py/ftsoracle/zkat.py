@@ -196,6 +196,73 @@ class PublicParams:
         return pp
 
 
+MATHLIB_CURVES = 3  # [EXT] len(math.Curves) at IBM/mathlib 0a7378db6912: FP256BN_AMCL, BN254, FP256BN_AMCL_MIRACL
+
+
+def validate_json(data, label="zkatdlog"):
+    """setup.go:238-273 PublicParams.Validate (with RangeProofParams.Validate
+    :56-80) after Deserialize (:134-151), on the serialized bytes.  Returns ""
+    or the reference's error text.  Point encodings are not checked here (the
+    device decoder checks them when a context is created)."""
+    try:
+        outer = J.parse(data)
+        ident = J.dec_string(J.field(outer, "Identifier"))
+        if ident != label:
+            return "invalid identifier, expecting [%s], got [%s]" % (label, ident)
+        raw = J.dec_bytes(J.field(outer, "Raw"))
+        v = J.parse(raw if raw is not None else b"")
+        curve = J.dec_int(J.field(v, "Curve"))
+        idemix_curve = J.dec_int(J.field(v, "IdemixCurveID"))
+        prec = J.dec_int(J.field(v, "QuantityPrecision"))
+        if prec < 0:
+            raise J.GoJSONError("cannot unmarshal number into uint64")
+        ipk = J.dec_bytes(J.field(v, "IdemixIssuerPK"))
+    except J.GoJSONError as e:
+        return "failed unmarshalling public parameters: %s" % e
+
+    def isnull(x):
+        return x is None or x[0] == "null"
+
+    def arr(x):
+        return [] if isnull(x) else x[1]
+    if curve > MATHLIB_CURVES - 1:
+        return "invalid public parameters: invalid curveID [%d > %d]" % (curve, MATHLIB_CURVES - 1)
+    if idemix_curve > MATHLIB_CURVES - 1:  # the reference prints pp.Curve here
+        return "invalid public parameters: invalid idemix curveID [%d > %d]" % (curve, MATHLIB_CURVES - 1)
+    if isnull(J.field(v, "PedGen")):
+        return "invalid public parameters: nil Pedersen generator"
+    ped = arr(J.field(v, "PedParams"))
+    if len(ped) != 3:
+        return "invalid public parameters: length mismatch in Pedersen parameters [%d vs. 3]" % len(ped)
+    for i, x in enumerate(ped):
+        if isnull(x):
+            return "invalid public parameters: nil Pedersen parameter at index %d" % i
+    rpp = J.field(v, "RangeProofParams")
+    if isnull(rpp):
+        return "invalid public parameters: nil range proof parameters"
+    spk, sv = arr(J.field(rpp, "SignPK")), arr(J.field(rpp, "SignedValues"))
+    w = "invalid public parameters: invalid range proof parameters: "
+    if len(spk) != 3:
+        return w + "signature public key should be 3, instead it is %d" % len(spk)
+    if len(sv) < 2:
+        return w + "signed values should be > 2"
+    if isnull(J.field(rpp, "Q")):
+        return w + "generator Q is nil"
+    if J.dec_int(J.field(rpp, "Exponent")) == 0:
+        return w + "exponent is 0"
+    for i, x in enumerate(sv):
+        if isnull(x):
+            return w + "signed value at index %d is nil" % i
+    for i, x in enumerate(spk):
+        if isnull(x):
+            return w + "public key at index %d is nil" % i
+    if prec != 64:
+        return "invalid public parameters: quantity precision should be 64 instead it is %d" % prec
+    if not ipk:
+        return "invalid public parameters: empty idemix issuer"
+    return ""
+
+
 def ps_hash(m):
     """pssign/sign.go:198-206 hashMessages for a single message."""
     return C.hash_to_zr(C.zr_bytes(m))
@@ -318,7 +385,7 @@ def membership_verify(pp, com_to_value, proof):
     the transcript uses the proof's own Commitment field (membership.go:170)."""
     if proof is None:
         raise Panic("nil membership proof")           # membership.go:285 p.Challenge on nil
-    # pok.go:472-508
+    # pok.go:160-204
     if proof["Value"] is None:
         raise VerifyError(ERR_MALFORMED, "nil elements")
     if proof["Hash"] is None:
@@ -510,7 +577,7 @@ def range_verify(pp, tokens, raw):
 
 # ------------------------------------------------------------------ transfer WF
 def wf_prove(pp, rnd, tag, ins, outs, in_w, out_w, ttype):
-    """transfer/wellformedness.go:284-308 Prove, computeCommitments :461-532,
+    """transfer/wellformedness.go:131-154 Prove, computeProof :243-304, computeCommitments :307-378,
     computeProof :397-458.  in_w/out_w: lists of (value, bf)."""
     ni, no = len(ins), len(outs)
     rt = rnd.zr(tag + "/r_type")
@@ -548,7 +615,7 @@ def wf_prove(pp, rnd, tag, ins, outs, in_w, out_w, ttype):
 
 
 def wf_verify(pp, ins, outs, raw):
-    """transfer/wellformedness.go:311-351 Verify with parseProof :354-394."""
+    """transfer/wellformedness.go:157-197 Verify with parseProof :200-240."""
     try:
         v = J.parse(raw if raw is not None else b"")
     except J.GoJSONError as ex:
@@ -566,7 +633,7 @@ def wf_verify(pp, ins, outs, raw):
         values, bfs = values or [], bfs or []
         if len(values) != len(tokens) or len(bfs) != len(tokens):
             raise VerifyError(ERR_MALFORMED, "failed to parse wellformedness proof")
-        # ModMul(ttype, n) dereferences ttype: nil Type panics (wellformedness.go:381)
+        # ModMul(ttype, n) dereferences ttype: nil Type panics (wellformedness.go:227)
         zk = []
         agg = None
         for i, t in enumerate(tokens):

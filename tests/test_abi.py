@@ -44,3 +44,21 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_abi, "_lib", None)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _abi.load()
+
+
+def test_pp_validate_matches_oracle():
+    """ftz_pp_validate (host side of the product library, no GPU) reproduces
+    PublicParams.Validate (setup.go:238-273) on every golden mutation: same
+    accept/reject and the same error text as the oracle restatement."""
+    import json
+    import os
+
+    import zkatdlog
+    cases = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pp_validate.json")))
+    for c in cases:
+        got = zkatdlog.validate_public_params(c["pp"].encode())
+        if c["error"].startswith("failed unmarshalling"):
+            assert got.startswith("failed unmarshalling"), (c["name"], got)
+        else:
+            assert got == c["error"], (c["name"], got, c["error"])
+    assert sum(1 for c in cases if not c["error"]) == 2

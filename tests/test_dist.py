@@ -63,3 +63,95 @@ def test_gather_verdicts_gloo_world2():
         assert n_acc == sum(want)
         assert ok is False  # rank 1 reported a mismatch: the MIN reduce must see it
         assert t == pytest.approx(1.5)
+
+
+class _EmuVerifier:
+    """TEST-ONLY stand-in for zkatdlog.Context on a CPU rank: the host build of
+    the same planner + job code (tests/native), behind the one method
+    zkatdlog.dist.verify_shard calls."""
+
+    def __init__(self, pp_json):
+        import ctypes
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import build_emu
+        from zkatdlog import _abi as A
+        self._A = A
+        self.lib = ctypes.CDLL(build_emu())
+        self.lib.emu_ctx_create.restype = ctypes.c_void_p
+        self.lib.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        self.lib.emu_verify_transfers.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Transfer),
+                                                  ctypes.POINTER(ctypes.c_int32)]
+        self.lib.emu_set_threads.argtypes = [ctypes.c_int]
+        self.lib.emu_set_threads(2)
+        self.h = self.lib.emu_ctx_create(pp_json, len(pp_json), ctypes.create_string_buffer(256), 256)
+
+    def verify_transfers_packed(self, ptr, n):
+        import ctypes
+
+        import numpy as np
+        codes = np.zeros(max(1, n), dtype=np.int32)
+        if n:
+            self.lib.emu_verify_transfers(self.h, n, ptr, codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        return codes[:n]
+
+
+def _golden_job():
+    import base64
+    import json
+
+    from zkatdlog import workload as W
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
+    cases = [c for c in g["cases"] if c["kind"] == "transfer"][:26]
+    items = [(bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"])) for c in cases]
+    return g["pp"].encode(), W.TransferSet.from_items(items, [c["expect"] for c in cases])
+
+
+def _worker_real(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+
+    from zkatdlog.dist import bitmap_of, gather_verdicts, shard_range, verify_shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pp, ts = _golden_job()
+    v = _EmuVerifier(pp)
+    start, stop, codes = verify_shard(v, ts.rows, ts.n, rank, world)
+    ok_local = bool(np.array_equal(codes, ts.expect[start:stop]))
+    maps, n_acc, ok = gather_verdicts(bitmap_of(codes), stop - start, ok_local, dist)
+    glob = []
+    for r, m in enumerate(maps):
+        ra, rb = shard_range(ts.n, r, world)
+        glob += [bool((m[i // 8] >> (i % 8)) & 1) for i in range(rb - ra)]
+    q.put((rank, (start, stop), glob, n_acc, ok))
+    dist.destroy_process_group()
+
+
+def test_verify_shards_real_proofs_gloo_world2():
+    """configs[3]'s job path on two CPU ranks: each rank verifies its
+    shard_range slice of real golden proofs (valid and tampered) with the host
+    build of the verifier, and the gathered verdict bitmaps equal the oracle's
+    verdicts for the whole job."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    _, ts = _golden_job()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_real, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = [int(e) == 0 for e in ts.expect]
+    assert any(want) and not all(want)
+    spans = sorted(r[1] for r in res)
+    assert spans[0][0] == 0 and spans[0][1] == spans[1][0] and spans[1][1] == ts.n
+    for rank, span, glob, n_acc, ok in res:
+        assert ok is True
+        assert glob == want
+        assert n_acc == sum(want)

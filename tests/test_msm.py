@@ -126,3 +126,50 @@ def test_gpu_msm_known_logs(ctx, lg, bits):
     assert got == C.g1_bytes(want)
     assert again == got
     assert info["window_bits"] == (lg + 1) // 2 + 7 and info["last_ms"] > 0
+
+
+def _known_log_sum(kb, n, off):
+    """sum_i k_i (i + off) mod r for n big-endian 32-byte scalars, in 16-bit
+    chunks with numpy (each chunk's dot product with i fits in uint64 for
+    n <= 2^24)."""
+    import numpy as np
+    k = np.frombuffer(kb, dtype=">u2").reshape(n, 16).astype(np.uint64)  # chunk 0 = most significant
+    idx = np.arange(n, dtype=np.uint64)
+    total = 0
+    for j in range(16):
+        c = k[:, j]
+        s = int(np.dot(c, idx)) + off * int(c.sum())
+        total += s << (16 * (15 - j))
+    return total % C.R
+
+
+@pytest.mark.gpu
+def test_gpu_msm_known_logs_2_24(ctx):
+    """BASELINE configs[2] at its largest size: 2^24 points P_i = (i + off) G
+    generated on the device, 2^24 uniform 256-bit scalars; the result must be
+    (sum_i k_i (i + off)) G exactly, and stable across runs."""
+    import numpy as np
+
+    import zkatdlog
+    n, off = 1 << 24, 777
+    kb = np.random.default_rng(24).bytes(32 * n)
+    want = C.g1_bytes(C.g1_mul(C.G1_GEN, _known_log_sum(kb, n, off)))
+    m = zkatdlog.Msm(ctx, scalars=kb, gen_offset=off)
+    try:
+        got = m.run()
+        again = m.run()
+        info = m.info()
+    finally:
+        m.close()
+    assert got == want
+    assert again == got
+    print("MSM 2^24: %.2f ms device, window %d bits" % (info["last_ms"], info["window_bits"]), flush=True)
+
+
+def test_known_log_sum_helper():
+    """the numpy chunked sum equals the big-int sum (CPU)"""
+    import numpy as np
+    n, off = 1000, 5
+    kb = np.random.default_rng(3).bytes(32 * n)
+    ks = [int.from_bytes(kb[32 * i:32 * i + 32], "big") for i in range(n)]
+    assert _known_log_sum(kb, n, off) == sum(k * (i + off) for i, k in enumerate(ks)) % C.R
