@@ -34,6 +34,7 @@ void Plan::clear() {
   b64.clear();
   out.clear();
   out_off.clear();
+  item_off.clear();
   wire.clear();
   arena.clear();
   dec.clear();
@@ -272,6 +273,7 @@ class Builder {
 
   void transfer(const TransferIn& t);
   void issue(const IssueIn& t);
+  void opening(const OpeningIn& o);
 
  private:
   Plan& pl;
@@ -867,6 +869,45 @@ void Builder::transfer(const TransferIn& t) {
   end_tx();
 }
 
+// Token commitment H(type)*Ped0 + value*Ped1 + bf*Ped2 (token/token.go:64-76,
+// common/schnorr.go:59-76); with a commitment given, the auditor's opening check
+// (audit/auditor.go:208-234): its canonical RawBytes land next to the
+// recomputed ones and the host compares them (G1 Equals on affine points).
+void Builder::opening(const OpeningIn& o) {
+  begin_tx(1);
+  uint32_t res = arena_alloc(128);
+  pl.item_off.push_back(res);
+  if (o.commitment) {
+    pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
+    uint32_t raw = (uint32_t)pl.wire.size();
+    pl.wire.insert(pl.wire.end(), o.commitment, o.commitment + 64);
+    uint32_t pt = point(raw, 64, res + 64, NONE);
+    check(CK_PTS, E_PARSE, pt, 1);
+  }
+  uint32_t str_off = arena_alloc((uint32_t)o.type_len);
+  if (o.type_len) memcpy(pl.arena.data() + str_off, o.type, o.type_len);
+  uint32_t s_h = pl.n_scal++;
+  HashJob h;
+  h.seg_start = (uint32_t)pl.seg.size();
+  seg(str_off, (uint32_t)o.type_len);
+  h.seg_count = 1;
+  h.expect = NONE;
+  h.out_scal = s_h;
+  pl.hpre.push_back(h);
+  Ref v, b;
+  for (int k = 0; k < 2; k++) {
+    pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
+    Ref& r = k ? b : v;
+    r.off = (int64_t)pl.wire.size();
+    r.len = 32;
+    const uint8_t* src = k ? o.bf : o.value;
+    pl.wire.insert(pl.wire.end(), src, src + 32);
+  }
+  uint32_t s_v = scalar(v), s_b = scalar(b);
+  g1job({{G1B_PED0, s_h}, {G1B_PED1, s_v}, {G1B_PED2, s_b}}, {}, NONE, res);
+  end_tx();
+}
+
 void Builder::issue(const IssueIn& t) {
   begin_tx(1);
   uint32_t tok_bytes;
@@ -1253,6 +1294,7 @@ std::string flat_layout(const PlanWork& w, bool p2_g1out, FlatPlan& fp) {
   fp.p2_g1out = p2_g1out;
   fp.base.assign(w.used, PieceBase{});
   fp.out_off.clear();
+  fp.item_off.clear();
   fp.n_items = 0;
   size_t cur[PS_COUNT] = {};
   cur[PS_ARENA] = C_SIZE;
@@ -1275,6 +1317,7 @@ std::string flat_layout(const PlanWork& w, bool p2_g1out, FlatPlan& fp) {
     g1 += p.n_g1out;
     g2 += p.n_g2out;
     for (uint32_t v : p.out_off) fp.out_off.push_back((uint32_t)(v + b.sec[PS_OUT]));
+    for (uint32_t v : p.item_off) fp.item_off.push_back((uint32_t)(v + b.sec[PS_ARENA]));
     fp.n_items += p.tx.size();
   }
   if (!fp.out_off.empty() || cur[PS_OUT]) fp.out_off.push_back((uint32_t)cur[PS_OUT]);
@@ -1344,6 +1387,7 @@ void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out) {
   take(out.b64, PS_B64);
   take(out.out, PS_OUT);
   out.out_off = fp.out_off;
+  out.item_off = fp.item_off;
   out.p2_g1out = fp.p2_g1out;
   out.n_pts = fp.n_pts;
   out.n_scal = fp.n_scal;
@@ -1368,10 +1412,23 @@ void plan_items(const PPInfo& pp, size_t n, const PlanItem* items, PlanWork& w, 
     for (size_t i = lo; i < hi; i++) {
       if (items[i].kind == 0)
         b.transfer(items[i].t);
-      else
+      else if (items[i].kind == 1)
         b.issue(items[i].i);
+      else
+        b.opening(items[i].o);
     }
   });
+}
+
+void plan_items_merged(const PPInfo& pp, size_t n, const PlanItem* items, Plan& out, int threads) {
+  WorkPool pool(threads);
+  PlanWork w;
+  plan_items(pp, n, items, w, pool);
+  FlatPlan fp;
+  flat_layout(w, false, fp);
+  std::vector<uint8_t> blob(fp.bytes);
+  flat_write(w, fp, blob.data(), std::vector<uint8_t>(C_SIZE, 0).data(), pool);
+  plan_unflatten(fp, blob.data(), out);
 }
 
 namespace {

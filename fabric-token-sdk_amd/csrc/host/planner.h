@@ -64,6 +64,7 @@ struct Plan {
   std::vector<B64Job> b64;
   std::vector<uint8_t> out;       // outer proof JSON templates, concatenated
   std::vector<uint32_t> out_off;  // per proof: start in `out` (plus a final end)
+  std::vector<uint32_t> item_off; // openings: arena offset of the 128-byte result (recomputed | decoded)
   bool p2_g1out = false;          // PairJob.p2 indexes g1out (prover) instead of pts
   uint32_t n_pts = 0, n_scal = 0, n_g1out = 0, n_g2out = 0;
   void clear();
@@ -85,12 +86,25 @@ struct IssueIn {
   uint8_t anonymous;
 };
 
-// One proof of a (possibly mixed) verification batch: a block of a ledger
-// carries transfer and issue actions side by side.
+// A token opening (token.TokenDataWitness / audit.AuditableToken data):
+// the commitment H(type)*P0 + value*P1 + bf*P2 is recomputed
+// (token/token.go:64-76 computeTokens; audit/auditor.go:208-234 InspectOutput
+// compares it with `commitment` when that is given).
+struct OpeningIn {
+  const char* type;
+  size_t type_len;
+  const uint8_t* value;       // 32-byte big-endian Zr
+  const uint8_t* bf;          // 32-byte big-endian Zr
+  const uint8_t* commitment;  // 64-byte RawBytes to check, or null (commit only)
+};
+
+// One item of a (possibly mixed) batch: a block of a ledger carries transfer
+// and issue actions side by side.
 struct PlanItem {
-  uint8_t kind;  // 0: transfer, 1: issue
+  uint8_t kind;  // 0: transfer, 1: issue, 2: token opening
   TransferIn t;
   IssueIn i;
+  OpeningIn o;
 };
 
 // A small persistent pool of host threads; run(n, f) calls f(0..n-1) across
@@ -135,6 +149,7 @@ struct FlatPlan {
   bool p2_g1out = false;      // prover plans: PairJob.p2 indexes g1out
   std::vector<PieceBase> base;
   std::vector<uint32_t> out_off;  // prover: per item start in OUT, plus the end
+  std::vector<uint32_t> item_off; // openings: arena offset of each item's 128-byte result
   template <class T>
   T* ptr(uint8_t* blob, PlanSec s) const { return reinterpret_cast<T*>(blob + off[s]); }
 };
@@ -165,6 +180,7 @@ void flat_write(const PlanWork& w, const FlatPlan& fp, uint8_t* blob, const uint
 void plan_transfers(const PPInfo& pp, size_t n, const TransferIn* tx, Plan& out, int threads);
 void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int threads);
 void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out);
+void plan_items_merged(const PPInfo& pp, size_t n, const PlanItem* items, Plan& out, int threads);
 
 // ------------------------------------------------------------------ prover
 // Witness of one transfer / issue (token.TokenDataWitness: Type, Value,

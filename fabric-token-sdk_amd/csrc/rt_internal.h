@@ -116,6 +116,9 @@ struct ftz_ctx {
   // reusable prover slots behind ftz_prove_* (one one-shot prove call at a time)
   std::mutex prove_mu;
   std::vector<ftz_prover*> pslots;
+  // slot behind ftz_commit_tokens / ftz_audit_openings
+  std::mutex aux_mu;
+  struct ftz_batch* aux = nullptr;
 };
 
 // ------------------------------------------------------------------ batch slots

@@ -261,6 +261,11 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
     delete p;
   }
   c->pslots.clear();
+  if (c->aux) {
+    slot_free(c->aux);
+    delete c->aux;
+    c->aux = nullptr;
+  }
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& t : c->triples)
     for (hipStream_t x : t)
@@ -1016,4 +1021,68 @@ extern "C" int ftz_prove_issues(ftz_ctx* c, size_t n, const ftz_issue_witness* w
   }
   std::vector<IssueWit> t = to_wit(n, w);
   return prove_chunked(c, n, t.data(), 1, buf, cap, offsets, codes);
+}
+
+// ------------------------------------------------------------------ token openings
+// Batches of up to 2^16 openings on the context's aux slot: H(type) (hash job),
+// value / bf (scalar jobs), the 3-base fixed-base G1 job writing RawBytes into
+// the arena, and -- for audits -- the commitment's decode job writing its
+// canonical RawBytes next to it; the host then compares the two.
+static int openings_run(ftz_ctx* c, size_t n, const ftz_token_opening* t, const uint8_t* coms, uint8_t* out,
+                        int32_t* codes) {
+  if (!c || (n && !t) || (n && !out && !codes)) return set_err(FTZ_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if (!t[i].value || !t[i].bf || (t[i].type_len && !t[i].type))
+      return set_err(FTZ_E_INVALID, "null buffer in opening " + std::to_string(i));
+  if (n == 0) return FTZ_SUCCESS;
+  std::lock_guard<std::mutex> lk(c->aux_mu);
+  HC(hipSetDevice(c->device));
+  if (!c->aux) {
+    ftz_batch* b = new ftz_batch();
+    b->ctx = c;
+    int rc = slot_init(b);
+    if (rc != FTZ_SUCCESS) {
+      slot_free(b);
+      delete b;
+      return rc;
+    }
+    c->aux = b;
+  }
+  ftz_batch* b = c->aux;
+  const size_t B = (size_t)1 << 16;
+  std::vector<PlanItem> items;
+  std::vector<uint8_t> arena;
+  for (size_t lo = 0; lo < n; lo += B) {
+    size_t cnt = std::min(B, n - lo);
+    items.assign(cnt, PlanItem{});
+    for (size_t i = 0; i < cnt; i++) {
+      const ftz_token_opening& o = t[lo + i];
+      items[i].kind = 2;
+      items[i].o = {o.type, o.type_len, o.value, o.bf, coms ? coms + 64 * (lo + i) : nullptr};
+    }
+    int rc = slot_plan_items(b, cnt, items.data());
+    if (rc == FTZ_SUCCESS) rc = slot_submit(b, true, true);
+    if (rc == FTZ_SUCCESS) rc = slot_wait(b);
+    if (rc != FTZ_SUCCESS) return rc;
+    arena.resize(b->fp.cnt[PS_ARENA]);
+    HC(hipMemcpy(arena.data(), b->d_blob.p + b->fp.off[PS_ARENA], arena.size(), hipMemcpyDeviceToHost));
+    const int32_t* vc = slot_codes(b);
+    for (size_t i = 0; i < cnt; i++) {
+      const uint8_t* r = arena.data() + b->fp.item_off[i];
+      if (out) memcpy(out + 64 * (lo + i), r, 64);
+      if (codes) codes[lo + i] = vc[i] != FTZ_OK ? vc[i] : (memcmp(r, r + 64, 64) == 0 ? FTZ_OK : FTZ_ERR_OPENING);
+    }
+  }
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_commit_tokens(ftz_ctx* c, size_t n, const ftz_token_opening* t, uint8_t* out) {
+  if (n && !out) return set_err(FTZ_E_INVALID, "null output");
+  return openings_run(c, n, t, nullptr, out, nullptr);
+}
+
+extern "C" int ftz_audit_openings(ftz_ctx* c, size_t n, const uint8_t* commitments, const ftz_token_opening* t,
+                                  int32_t* codes) {
+  if (n && (!commitments || !codes)) return set_err(FTZ_E_INVALID, "null argument");
+  return openings_run(c, n, t, commitments, nullptr, codes);
 }

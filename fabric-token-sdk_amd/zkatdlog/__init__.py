@@ -19,8 +19,8 @@ Batch form (the point of the port):
 import ctypes
 
 from . import _abi
-from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_PANIC, FTZ_ERR_PARSE, FTZ_ERR_RANGE,  # noqa: F401
-                   FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
+from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_OPENING, FTZ_ERR_PANIC,  # noqa: F401
+                   FTZ_ERR_PARSE, FTZ_ERR_RANGE, FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
 
 __all__ = ["Context", "Batch", "Msm", "Prover", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
            "FTZ_OK", "MESSAGES"]
@@ -173,6 +173,28 @@ class Context:
             return p.proofs()
         finally:
             p.close()
+
+    def commit_tokens(self, openings):
+        """token commitments H(type)*Ped0 + v*Ped1 + bf*Ped2 (computeTokens,
+        token/token.go:64-76) for (type, value, bf) openings: 64-byte RawBytes each."""
+        arr, keep = _abi.pack_openings(openings)
+        n = len(keep) // 3
+        out = (ctypes.c_uint8 * max(1, 64 * n))()
+        _check(self._lib.ftz_commit_tokens(self._h, n, arr, out), self._lib)
+        raw = bytes(out)
+        return [raw[64 * i:64 * i + 64] for i in range(n)]
+
+    def audit_openings(self, commitments, openings):
+        """auditor opening check (audit/auditor.go:208-234): codes, 0 = match,
+        FTZ_ERR_OPENING = mismatch, FTZ_ERR_PARSE = invalid commitment bytes."""
+        arr, keep = _abi.pack_openings(openings)
+        n = len(keep) // 3
+        coms = b"".join(bytes(c) for c in commitments)
+        if len(coms) != 64 * n:
+            raise ValueError("one 64-byte commitment per opening")
+        codes = (ctypes.c_int32 * max(1, n))()
+        _check(self._lib.ftz_audit_openings(self._h, n, coms, arr, codes), self._lib)
+        return list(codes)[:n]
 
     def msm_g1(self, points, scalars):
         """sum_i k_i P_i (gnark G1Jac.MultiExp semantics): points n x 64-byte

@@ -9,6 +9,7 @@ FTZ_ERR_WF = 3
 FTZ_ERR_RANGE = 4
 FTZ_ERR_MEMBERSHIP = 5
 FTZ_ERR_PANIC = 6
+FTZ_ERR_OPENING = 7
 
 FTZ_SUCCESS = 0
 FTZ_E_INVALID = -1
@@ -30,6 +31,7 @@ MESSAGES = {
     FTZ_ERR_RANGE: "invalid range proof",
     FTZ_ERR_MEMBERSHIP: "invalid membership proof",
     FTZ_ERR_PANIC: "proof would make the reference verifier panic",
+    FTZ_ERR_OPENING: "does not match the provided opening",
 }
 
 
@@ -41,6 +43,22 @@ FEXP = {"exact": FTZ_FEXP_EXACT, "fuentes": FTZ_FEXP_FUENTES}
 class Options(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("batch", ctypes.c_uint32), ("slots", ctypes.c_uint32),
                 ("window_us", ctypes.c_uint32), ("threads", ctypes.c_uint32), ("fexp", ctypes.c_uint32)]
+
+
+class TokenOpening(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_void_p), ("type_len", ctypes.c_size_t), ("value", ctypes.c_void_p),
+                ("bf", ctypes.c_void_p)]
+
+
+def pack_openings(openings):
+    """openings: iterable of (type str/bytes, value int, bf int)."""
+    openings = list(openings)
+    keep = []
+    arr = (TokenOpening * max(1, len(openings)))()
+    for i, (t, v, b) in enumerate(openings):
+        t = t.encode() if isinstance(t, str) else bytes(t)
+        arr[i] = TokenOpening(_buf(t, keep), len(t), _buf(_zr32([v]), keep), _buf(_zr32([b]), keep))
+    return arr, keep
 
 
 class EngineStats(ctypes.Structure):
@@ -126,6 +144,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
            "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate",
+           "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
@@ -152,6 +171,9 @@ def load():
     lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
     lib.ftz_ctx_options.argtypes = [vp, ctypes.POINTER(Options)]
     lib.ftz_pp_validate.argtypes = [ctypes.c_char_p, sz]
+    lib.ftz_commit_tokens.argtypes = [vp, sz, ctypes.POINTER(TokenOpening), ctypes.POINTER(ctypes.c_uint8)]
+    lib.ftz_audit_openings.argtypes = [vp, sz, ctypes.c_char_p, ctypes.POINTER(TokenOpening),
+                                       ctypes.POINTER(ctypes.c_int32)]
     lib.ftz_ctx_engine_stats.argtypes = [vp, ctypes.POINTER(EngineStats), ctypes.c_int]
     lib.ftz_ctx_destroy.argtypes = [vp]
     lib.ftz_ctx_destroy.restype = None

@@ -43,6 +43,7 @@ extern "C" {
 #define FTZ_ERR_RANGE 4      /* "invalid range proof"                               */
 #define FTZ_ERR_MEMBERSHIP 5 /* "invalid membership proof"                          */
 #define FTZ_ERR_PANIC 6      /* the reference would panic on this proof             */
+#define FTZ_ERR_OPENING 7    /* audit: "output ... does not match the provided opening" */
 
 /* API return codes */
 #define FTZ_SUCCESS 0
@@ -171,6 +172,29 @@ int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits);
 int ftz_batch_stats(const ftz_batch* b, ftz_stats* out);
 size_t ftz_batch_size(const ftz_batch* b);
 void ftz_batch_destroy(ftz_batch* b);
+
+/* ---- token commitments and auditor opening checks.
+ * A token opening is token.TokenDataWitness{Type, Value, BlindingFactor}
+ * (crypto/token/token.go): value and bf as 32-byte big-endian Zr.  The
+ * commitment is H(type)*Ped0 + value*Ped1 + bf*Ped2 with H = HashToZr
+ * (computeTokens, token/token.go:64-76; common/schnorr.go:59-76).  Note
+ * GetTokensWithWitness (token.go:78-98) takes uint64 values through
+ * NewZrFromInt(int64(v)): a caller passes that Zr (v mod r for v < 2^63). */
+typedef struct {
+  const char* type;
+  size_t type_len;
+  const uint8_t* value; /* 32 bytes */
+  const uint8_t* bf;    /* 32 bytes */
+} ftz_token_opening;
+/* out: n x 64-byte RawBytes commitments */
+int ftz_commit_tokens(ftz_ctx* ctx, size_t n, const ftz_token_opening* t, uint8_t* out);
+/* Auditor InspectOutput / InspectInputs commitment check (audit/auditor.go:208-234):
+ * codes[i] = FTZ_OK if commitments[i] (64-byte RawBytes, gnark decoding rules)
+ * equals the recomputed commitment of t[i], FTZ_ERR_OPENING if it does not,
+ * FTZ_ERR_PARSE if the bytes are not a valid G1 encoding.  (The owner
+ * identity check InspectTokenOwnerFunc is idemix, outside this library.) */
+int ftz_audit_openings(ftz_ctx* ctx, size_t n, const uint8_t* commitments, const ftz_token_opening* t,
+                       int32_t* codes);
 
 /* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE configs[2]):
  * out = sum_i k_i P_i as 64-byte gnark RawBytes.  Points: n x 64-byte

@@ -280,6 +280,28 @@ long emu_prove_issues(void* ctx, size_t n, const ftz_issue_witness* w, uint8_t* 
   return run_prove_plan(c, p, n, buf, cap, offsets, codes);
 }
 
+// token commitments / auditor opening checks (ftz_commit_tokens / ftz_audit_openings)
+int emu_openings(void* ctx, size_t n, const ftz_token_opening* t, const uint8_t* coms, uint8_t* out,
+                 int32_t* codes) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<PlanItem> items(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&items[i], 0, sizeof(PlanItem));
+    items[i].kind = 2;
+    items[i].o = {t[i].type, t[i].type_len, t[i].value, t[i].bf, coms ? coms + 64 * i : nullptr};
+  }
+  Plan p;
+  plan_items_merged(c->pp, n, items.data(), p, g_threads ? (int)g_threads : 4);
+  std::vector<int32_t> vc(std::max<size_t>(n, 1));
+  run_plan(c, p, n, vc.data());
+  for (size_t i = 0; i < n; i++) {
+    const uint8_t* r = p.arena.data() + p.item_off[i];
+    if (out) memcpy(out + 64 * i, r, 64);
+    if (codes) codes[i] = vc[i] != E_OK ? vc[i] : (!coms || memcmp(r, r + 64, 64) == 0 ? 0 : 7);
+  }
+  return 0;
+}
+
 int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* codes) {
   EmuCtx* c = (EmuCtx*)ctx;
   std::vector<TransferIn> t(n);
