@@ -124,6 +124,39 @@ def msm_latency(ctx, lg, reps=5, seed=7):
             "window_bits": info["window_bits"]}
 
 
+def msm_split_latency(ctx, lg, rank, world, dist, reps=5, seed=7):
+    """configs[2] over N GPUs: the 2^lg known-log points split
+    into contiguous rank slices (each rank stages its slice with its own
+    generator offset), every rank runs its partial MSM, the 64-byte partials
+    are all-gathered over RCCL and added on the device (zkatdlog.dist.msm_shard).
+    Median over reps of the max-over-ranks wall time, barrier to barrier."""
+    import numpy as np
+    import torch
+
+    import zkatdlog
+    from zkatdlog.dist import max_elapsed, msm_shard, shard_range
+    n = 1 << lg
+    scal = np.random.default_rng(seed + lg).bytes(32 * n)
+    a, b = shard_range(n, rank, world)
+    m = zkatdlog.Msm(ctx, scalars=scal[32 * a:32 * b], gen_offset=1 + a) if b > a else None
+    part = (lambda s, e: m.run()) if m else (lambda s, e: bytes(64))
+    try:
+        first = msm_shard(ctx, n, rank, world, dist, part)[2]
+        times = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            out = msm_shard(ctx, n, rank, world, dist, part)[2]
+            times.append(max_elapsed(time.perf_counter() - t0, dist))
+            assert out == first, "split MSM result changed between runs"
+    finally:
+        if m:
+            m.close()
+    times.sort()
+    return {"n": n, "ms": round(times[reps // 2] * 1e3, 3), "ranks": world, "points_per_rank": b - a}
+
+
 def prover_bench(ctx, batch, steps):
     """BASELINE configs[4] at the configs[1] shape: ONE ftz_prove_transfers call
     of steps x batch 2-in/2-out transfer proofs (witness bases tiled, a fresh
@@ -323,6 +356,11 @@ def main():
     else:
         verdict_ok, n_accept = ok_local, int((codes == 0).sum())
 
+    msm_split = None
+    if dist is not None and args.msm:
+        lg_split = 20 if "20" in args.msm.split(",") else int(args.msm.split(",")[-1])
+        msm_split = msm_split_latency(ctx, lg_split, rank, world, dist)
+
     if rank == 0:
         value = n_total / elapsed
         extras = {}
@@ -356,7 +394,7 @@ def main():
                        "parse_rate_transfers_per_s": round(est["proofs"] / max(1e-9, est["plan_ms"] * 1e-3), 1),
                        "planning_threads": ctx.options["threads"]},
             "roofline": extras.pop("roofline", None), "cpu_baseline": cpu,
-            "msm_2^20_latency_ms": msm20, "msm": msm, "prover": prover,
+            "msm_2^20_latency_ms": msm20, "msm": msm, "msm_split": msm_split, "prover": prover,
         }
         line.update(extras)
         print(json.dumps(line), flush=True)

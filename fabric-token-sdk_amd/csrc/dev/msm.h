@@ -250,4 +250,41 @@ FTS_HD g1j msm_job_segment(const MsmPlan& p, uint32_t w, uint32_t s, const uint3
   return jac_add_inl(acc, jac_mul_small(run, bl));
 }
 
+// Decode one 64-byte gnark RawBytes G1 point (uncompressed, big-endian; the
+// identity is 64 zero bytes) with the load rules of k_msm_load_pts: false when
+// it is not canonical (flag bits, coordinates >= p) or not on the curve.
+FTS_HD bool g1_from_raw(const uint8_t* b, g1a& a) {
+  uint32_t x[8], y[8], t[8], mm[8];
+  be32_to_limbs(x, b);
+  be32_to_limbs(y, b + 32);
+  for (int q = 0; q < 8; q++) mm[q] = P_MOD[q];
+  bool canon = ((b[0] & 0xC0) == 0) && sub8(t, x, mm) && sub8(t, y, mm);
+  a.x = fe_from_int<ModP>(x);
+  a.y = fe_from_int<ModP>(y);
+  a.inf = is_zero(a.x) && is_zero(a.y);
+  return canon && g1_on_curve(a);
+}
+
+// Sum of n RawBytes points into out (RawBytes): the final addition of a
+// point-split multi-GPU MSM, where each rank contributes the MSM of its slice
+// of the points ("each GPU returns one partial sum; one gather
+// and a final add").  Returns n, or the index of the first point that does not
+// decode (out untouched).  Exceptional cases (identity, P + P, P - P) go
+// through jac_add_aff.
+FTS_HDN uint32_t g1_sum_raw(uint32_t n, const uint8_t* raw, uint8_t out[64]) {
+  g1j acc = jac_inf<fp>();
+  for (uint32_t i = 0; i < n; i++) {
+    g1a a;
+    if (!g1_from_raw(raw + 64 * (size_t)i, a)) return i;
+    acc = jac_add_aff(acc, a);
+  }
+  g1a r;
+  r.inf = is_zero(acc.z);
+  fp zi = r.inf ? fe_one<ModP>() : fp_inv_var(acc.z), zi2 = sqr(zi);
+  r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
+  r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
+  g1_to_bytes(out, r);
+  return n;
+}
+
 }  // namespace fts

@@ -14,20 +14,18 @@ using namespace fts;
 // ok[i] = 0 for a point off the curve or not in canonical form.
 __global__ void __launch_bounds__(256) k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok) {
   LANE_PROLOGUE(n);
-  const uint8_t* b = raw_pts + 64 * (size_t)i;
-  uint32_t x[8], y[8], t[8], mm[8];
-  be32_to_limbs(x, b);
-  be32_to_limbs(y, b + 32);
-  for (int q = 0; q < 8; q++) mm[q] = P_MOD[q];
-  bool canon = ((b[0] & 0xC0) == 0) && sub8(t, x, mm) && sub8(t, y, mm);
   g1a a;
-  a.x = fe_from_int<ModP>(x);
-  a.y = fe_from_int<ModP>(y);
-  a.inf = is_zero(a.x) && is_zero(a.y);
-  ok[i] = (canon && g1_on_curve(a)) ? 1 : 0;
+  ok[i] = g1_from_raw(raw_pts + 64 * (size_t)i, a) ? 1 : 0;
   G1Dev d;
   g1_store(d, a);
   pts[i] = d;
+}
+
+// final add of a point-split MSM (dev/msm.h g1_sum_raw): one lane; status[0] =
+// n on success, else the index of the first bad point
+__global__ void __launch_bounds__(64) k_g1_sum(uint32_t n, const uint8_t* raw, uint8_t* out, uint32_t* status) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  status[0] = g1_sum_raw(n, raw, out);
 }
 
 // 32-byte big-endian scalars -> 8 limbs reduced mod r

@@ -244,6 +244,29 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
   delete m;
 }
 
+extern "C" int ftz_g1_sum(ftz_ctx* c, size_t n, const uint8_t* points, uint8_t out[64]) {
+  if (!c || !out || (n && !points)) return set_err(FTZ_E_INVALID, "null argument");
+  if (n > 4096) return set_err(FTZ_E_INVALID, "ftz_g1_sum takes at most 4096 points");
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  DBuf<uint8_t> buf;
+  HC(buf.alloc(64 * n + 64 + 16));
+  uint8_t* d_out = buf.p + 64 * n;
+  uint32_t* d_status = reinterpret_cast<uint32_t*>(buf.p + 64 * n + 64);
+  if (n) HC(hipMemcpyAsync(buf.p, points, 64 * n, hipMemcpyHostToDevice, s));
+  k_g1_sum<<<1, 64, 0, s>>>((uint32_t)n, buf.p, d_out, d_status);
+  HC(hipGetLastError());
+  uint8_t res[64 + 16];
+  HC(hipMemcpyAsync(res, d_out, sizeof(res), hipMemcpyDeviceToHost, s));
+  HC(hipStreamSynchronize(s));
+  uint32_t st;
+  memcpy(&st, res + 64, 4);
+  if (st != n) return set_err(FTZ_E_INVALID, "point " + std::to_string(st) + " is not a canonical BN254 G1 point");
+  memcpy(out, res, 64);
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_msm_g1(ftz_ctx* c, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[64]) {
   ftz_msm* m = nullptr;
   int rc = ftz_msm_load(c, n, points, scalars, &m);

@@ -205,6 +205,16 @@ class Context:
         finally:
             m.close()
 
+    def g1_sum(self, points):
+        """Sum of RawBytes G1 points (n x 64 bytes, the identity = 64 zero
+        bytes) on the device: the final add of a point-split MSM."""
+        points = bytes(points)
+        if len(points) % 64:
+            raise ValueError("points must be n x 64 bytes")
+        out = (ctypes.c_uint8 * 64)()
+        _check(self._lib.ftz_g1_sum(self._h, len(points) // 64, points, out), self._lib)
+        return bytes(out)
+
     def load_transfers(self, transfers):
         arr, keep = _abi.pack_transfers(transfers)
         n = len(keep) // 3

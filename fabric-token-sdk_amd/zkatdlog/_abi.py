@@ -147,7 +147,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
-           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy",
+           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
@@ -202,6 +202,7 @@ def load():
     lib.ftz_msm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     lib.ftz_msm_destroy.argtypes = [vp]
     lib.ftz_msm_destroy.restype = None
+    lib.ftz_g1_sum.argtypes = [vp, sz, ctypes.c_char_p, u8p]
     szp = ctypes.POINTER(ctypes.c_size_t)
     i32p = ctypes.POINTER(ctypes.c_int32)
     lib.ftz_prove_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), u8p, sz, szp, i32p]

@@ -5,7 +5,9 @@ slices, one per rank (one process per GPU).  There is no data-path collective:
 each rank verifies its slice on its own GPU; the only exchange is the gather
 of the per-rank verdict bitmaps (RCCL all-gather over xGMI when the process
 group backend is "nccl", gloo on CPU in the tests) and a MIN all-reduce of the
-per-rank "verdicts matched the expected codes" flag.
+per-rank "verdicts matched the expected codes" flag.  The standalone MSM is
+split by points instead (msm_shard): one 64-byte partial per rank is gathered
+and added.
 """
 
 
@@ -31,6 +33,23 @@ def verify_shard(ctx, rows, n_total, rank, world):
     part = rows[start:stop]
     codes = ctx.verify_transfers_packed(ctypes.cast(part.ctypes.data, ctypes.POINTER(_abi.Transfer)), stop - start)
     return start, stop, codes
+
+
+def msm_shard(ctx, n_total, rank, world, dist, partial):
+    """SURVEY 8(e) for the standalone MSM (BASELINE configs[2]): the n_total
+    points are split into contiguous slices, rank r computes the partial MSM of
+    its slice with partial(start, stop) -> 64-byte RawBytes (ctx.msm_g1 or a
+    staged Msm), the partials are all-gathered (one 64-byte collective per
+    rank, RCCL over xGMI) and every rank adds them on its own device
+    (ctx.g1_sum).  Returns (start, stop, 64-byte RawBytes of the whole sum)."""
+    import torch
+    start, stop = shard_range(n_total, rank, world)
+    part = partial(start, stop) if stop > start else bytes(64)
+    dev = _device(dist)
+    t = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return start, stop, ctx.g1_sum(b"".join(bytes(p.cpu().tolist()) for p in parts))
 
 
 def bitmap_of(codes):

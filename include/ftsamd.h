@@ -213,6 +213,11 @@ int ftz_msm_run(ftz_msm* m, uint8_t out[64]);
 /* device time of the last ftz_msm_run in ms (HIP events) and the window size */
 int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits);
 void ftz_msm_destroy(ftz_msm* m);
+/* Sum of n <= 4096 RawBytes G1 points (the identity = 64 zero bytes accepted):
+ * the final add of a point-split multi-GPU MSM: each rank runs
+ * ftz_msm_g1 on its contiguous slice of the points, the 64-byte partials are
+ * all-gathered (RCCL), and every rank sums them here (zkatdlog/dist.py msm_shard). */
+int ftz_g1_sum(ftz_ctx* ctx, size_t n, const uint8_t* points, uint8_t out[64]);
 
 /* ---- batch prover (BASELINE configs[4]).
  * Replaces transfer.NewProver(inW, outW, in, out, pp).Prove()

@@ -60,3 +60,8 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   g1_to_bytes(out, jac_to_aff(acc));
   return 0;
 }
+
+// host run of the multi-GPU MSM's final add (dev/msm.h g1_sum_raw)
+extern "C" int emu_g1_sum(size_t n, const uint8_t* points, uint8_t out[64]) {
+  return g1_sum_raw((uint32_t)n, points, out) == n ? 0 : -1;
+}

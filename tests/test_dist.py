@@ -155,3 +155,88 @@ def test_verify_shards_real_proofs_gloo_world2():
         assert ok is True
         assert glob == want
         assert n_acc == sum(want)
+
+
+class _EmuMsm:
+    """TEST-ONLY stand-in for zkatdlog.Context on a CPU rank for the
+    point-split MSM: the host build of dev/msm.h (tests/native/msm_emu.cpp)
+    behind the two methods zkatdlog.dist.msm_shard uses."""
+
+    def __init__(self):
+        import ctypes
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import build_emu
+        self.lib = ctypes.CDLL(build_emu())
+        self.lib.emu_msm.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+        self.lib.emu_g1_sum.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]
+
+    def msm_g1(self, points, scalars):
+        import ctypes
+        out = ctypes.create_string_buffer(64)
+        assert self.lib.emu_msm(len(points) // 64, points, scalars, 4, 0, 0, 1, out) == 0
+        return out.raw
+
+    def g1_sum(self, points):
+        import ctypes
+        out = ctypes.create_string_buffer(64)
+        assert self.lib.emu_g1_sum(len(points) // 64, points, out) == 0
+        return out.raw
+
+
+def _msm_case(n):
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
+    from ftsoracle import bn254 as C
+    rng = random.Random(99)
+    pts = [C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)) for _ in range(n)]
+    ks = [rng.randrange(1 << 256) for _ in range(n)]
+    if n > 3:
+        ks[3] = 0
+    pb = b"".join(C.g1_bytes(p) for p in pts)
+    kb = b"".join(k.to_bytes(32, "big") for k in ks)
+    want = C.G1_INF
+    for p, k in zip(pts, ks):
+        want = C.g1_add(want, C.g1_mul(p, k % C.R))
+    return pb, kb, C.g1_bytes(want)
+
+
+def _worker_msm(rank, world, port, q, n):
+    import torch.distributed as dist
+
+    from zkatdlog.dist import msm_shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pb, kb, _ = _msm_case(n)
+    ctx = _EmuMsm()
+    start, stop, out = msm_shard(ctx, n, rank, world, dist,
+                                 lambda a, b: ctx.msm_g1(pb[64 * a:64 * b], kb[32 * a:32 * b]))
+    q.put((rank, start, stop, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 21), (3, 2)])
+def test_msm_point_split_gloo(world, n):
+    """configs[2] split over ranks: each rank's partial MSM of
+    its point slice, one all-gather of the 64-byte partials, the final add on
+    every rank -- equal to the oracle's whole sum (world 3 with n = 2 leaves
+    one rank with no points: its partial is the identity)."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    _, _, want = _msm_case(n)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_msm, args=(r, world, port, q, n)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted((r[1], r[2]) for r in res)[-1][1] == n
+    for rank, start, stop, out in res:
+        assert out == want

@@ -173,3 +173,49 @@ def test_known_log_sum_helper():
     kb = np.random.default_rng(3).bytes(32 * n)
     ks = [int.from_bytes(kb[32 * i:32 * i + 32], "big") for i in range(n)]
     assert _known_log_sum(kb, n, off) == sum(k * (i + off) for i, k in enumerate(ks)) % C.R
+
+
+@pytest.mark.gpu
+def test_gpu_g1_sum_edge_cases(ctx):
+    """ftz_g1_sum (the split MSM's final add): identity entries, P + P,
+    P + (-P), the empty sum, and a rejected off-curve point."""
+    import zkatdlog
+    rng = random.Random(5)
+    p = C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))
+    q = C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))
+    inf = bytes(64)
+    cases = [[p, q], [p, p], [p, C.g1_neg(p)], [p, None, q, None], [None], []]
+    for pts in cases:
+        want = C.G1_INF
+        for x in pts:
+            want = C.g1_add(want, x)
+        got = ctx.g1_sum(b"".join(inf if x is None else C.g1_bytes(x) for x in pts))
+        assert got == (inf if want is None else C.g1_bytes(want))
+    bad = bytearray(C.g1_bytes(p))
+    bad[63] ^= 1
+    with pytest.raises(zkatdlog.DeviceError, match="point 1"):
+        ctx.g1_sum(C.g1_bytes(q) + bytes(bad))
+
+
+@pytest.mark.gpu
+def test_gpu_msm_point_split_2_20(ctx):
+    """The configs[2] multi-GPU split on one device: 2^20 known-log points cut
+    into 4 contiguous rank slices (zkatdlog.dist.shard_range), each slice's MSM
+    staged with its own generator offset, the 4 partials added by ftz_g1_sum:
+    equal to (sum_i k_i (i + off)) G."""
+    import numpy as np
+
+    import zkatdlog
+    from zkatdlog.dist import shard_range
+    n, off, world = 1 << 20, 4242, 4
+    kb = np.random.default_rng(20).bytes(32 * n)
+    parts = []
+    for r in range(world):
+        a, b = shard_range(n, r, world)
+        m = zkatdlog.Msm(ctx, scalars=kb[32 * a:32 * b], gen_offset=off + a)
+        try:
+            parts.append(m.run())
+        finally:
+            m.close()
+    got = ctx.g1_sum(b"".join(parts))
+    assert got == C.g1_bytes(C.g1_mul(C.G1_GEN, _known_log_sum(kb, n, off)))
