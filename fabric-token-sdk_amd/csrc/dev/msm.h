@@ -5,14 +5,14 @@
 // is the unique group element, so any correct bucket order gives the same bytes.
 //
 // Pipeline (k_msm.hip; every stage one lane per item):
-//   digits    k_i -> W signed digits d in [-2^(c-1), 2^(c-1)]; bucket |d|-1,
-//             counted per (window, bucket)
-//   scan      exclusive prefix sums of the bucket counts
+//   keys      k_i -> W signed digits d in [-2^(c-1), 2^(c-1)]; sort key = the
+//             global bucket w B + |d| - 1, value = virtual point | sign
+//   sort      stable LSD radix sort of the (key, value) pairs (rocPRIM)
+//   bounds    bucket ranges [start, end) read off the sorted keys
 //   slots     bucket b gets m_b = max(1, ceil(count_b / T)) slots of at most T
 //             points (scan of m_b -> slot offsets, slot -> bucket owner map), so
 //             that heavy buckets (the top window's few buckets, skewed scalars)
 //             are spread over several lanes
-//   scatter   (window, bucket)-sorted list of point indices (sign in bit 31)
 //   bucket    one lane per slot: Jacobian sum of its <= T points
 //   segment   one lane per run of S consecutive slots of one window: running
 //             sums give sum (b+1) S_b restricted to the run
@@ -34,12 +34,7 @@ struct MsmPlan {
   uint32_t seg_len;    // S: slots per segment
   uint32_t max_slots;  // per window: B + ceil(n / T) bounds sum_b m_b
   uint32_t segs;       // segments per window: ceil(max_slots / S)
-  uint32_t top_used;   // buckets the top window can reach (scalars < r < 2^254)
 };
-
-// LDS-aggregated counting / scattering for the top window when it reaches at
-// most this many buckets (its few buckets would otherwise serialise on atomics)
-static constexpr uint32_t MSM_TOP_LDS = 1024;
 
 // window bits for n (virtual) points: floor(log2 n / 2) + 7 clamped to [8, 20]
 // (measured on MI355X with GLV: 2^17 -> 15, 2^21 -> 17, 2^25 -> 19; the
@@ -82,8 +77,6 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   }
   p.seg_len = seg_len;
   p.segs = (p.max_slots + seg_len - 1) / seg_len;
-  int t = (int)(bits - 1) - (int)(p.c * (p.windows - 1));  // bits left for the top window
-  p.top_used = t <= 0 ? 1 : (t >= 31 || (1u << t) > p.buckets ? p.buckets : 1u << t);
   return p;
 }
 
@@ -101,36 +94,36 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
   return (int32_t)raw;
 }
 
-// digits of point i: key[w * n + i] = bucket | sign << 31, or NONE for a zero digit
-// key of one (window, virtual point): bucket | sign << 31, or NONE for a zero
-// digit; rank = the entry's position within its bucket (the count before it),
-// so the sorted position is start[bucket] + rank with no second atomic.  With
-// top_hist the top window counts in an LDS histogram (rank local to the block;
-// the caller adds the block's base).
-FTS_HD void msm_put_digit(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
-                          uint32_t* rank, uint32_t* count, bool atomic_count, uint32_t* top_hist) {
-  uint32_t kk = NONE, rk = 0;
-  if (d != 0) {
-    uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-    kk = b | (((d < 0) != neg) ? 0x80000000u : 0u);
-    uint32_t* ct = (top_hist && w == p.windows - 1) ? &top_hist[b] : &count[(size_t)w * p.buckets + b];
-#if defined(__HIP_DEVICE_COMPILE__)
-    (void)atomic_count;
-    rk = atomicAdd(ct, 1u);
-#else
-    if (atomic_count)
-      rk = __atomic_fetch_add(ct, 1u, __ATOMIC_RELAXED);
-    else
-      rk = (*ct)++;
-#endif
-  }
-  key[(size_t)w * p.nv + vi] = kk;
-  rank[(size_t)w * p.nv + vi] = rk;
+// Sort keys of point i (both GLV halves): for window w and virtual point vi the
+// entry t = w nv + vi gets key[t] = w B + |d| - 1 (= the global bucket index g)
+// and val[t] = vi | sign << 31, or key[t] = MSM_KEY_NONE for a zero digit.  A
+// stable radix sort of (key, val) over msm_key_bits(p) bits then lists every
+// bucket's points contiguously (zero digits last) and msm_job_bounds reads the
+// bucket ranges off the sorted keys: no atomics, coalesced writes.
+static constexpr uint32_t MSM_KEY_NONE = 0xFFFFFFFFu;
+
+// key bits the sort must look at: g < W B plus one bit so that NONE sorts last
+FTS_HD uint32_t msm_key_bits(const MsmPlan& p) {
+  uint64_t top = (uint64_t)p.windows * p.buckets;
+  uint32_t b = 0;
+  while ((1ull << b) < top) b++;
+  return b + 1;
 }
 
-// digits of point i (both GLV halves)
-FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key, uint32_t* rank,
-                           uint32_t* count, bool atomic_count, uint32_t* top_hist = nullptr) {
+FTS_HD void msm_put_key(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
+                        uint32_t* val) {
+  size_t t = (size_t)w * p.nv + vi;
+  if (d == 0) {
+    key[t] = MSM_KEY_NONE;
+    val[t] = 0;
+    return;
+  }
+  uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
+  key[t] = w * p.buckets + b;
+  val[t] = vi | (((d < 0) != neg) ? 0x80000000u : 0u);
+}
+
+FTS_HD void msm_job_keys(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val) {
   if (p.glv) {
     uint32_t k1[4], k2[4];
     bool n1, n2;
@@ -138,23 +131,22 @@ FTS_HD void msm_job_digits(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[
     uint32_t a[8] = {k1[0], k1[1], k1[2], k1[3], 0, 0, 0, 0}, b[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
     uint32_t ca = 0, cb = 0;
     for (uint32_t w = 0; w < p.windows; w++) {
-      msm_put_digit(p, w, i, msm_digit(a, p.c, w, ca), n1, key, rank, count, atomic_count, top_hist);
-      msm_put_digit(p, w, p.n + i, msm_digit(b, p.c, w, cb), n2, key, rank, count, atomic_count, top_hist);
+      msm_put_key(p, w, i, msm_digit(a, p.c, w, ca), n1, key, val);
+      msm_put_key(p, w, p.n + i, msm_digit(b, p.c, w, cb), n2, key, val);
     }
   } else {
     uint32_t carry = 0;
-    for (uint32_t w = 0; w < p.windows; w++)
-      msm_put_digit(p, w, i, msm_digit(scal[i], p.c, w, carry), false, key, rank, count, atomic_count, top_hist);
+    for (uint32_t w = 0; w < p.windows; w++) msm_put_key(p, w, i, msm_digit(scal[i], p.c, w, carry), false, key, val);
   }
 }
 
-// sorted position of one (window, virtual point) entry
-FTS_HD void msm_job_scatter(const MsmPlan& p, uint64_t t, const uint32_t* key, const uint32_t* rank,
-                            const uint32_t* start, uint32_t* perm) {
-  uint32_t k = key[t];
-  if (k == NONE) return;
-  uint32_t w = (uint32_t)(t / p.nv), vi = (uint32_t)(t - (uint64_t)w * p.nv);
-  perm[start[(size_t)w * p.buckets + (k & 0x7FFFFFFFu)] + rank[t]] = vi | (k & 0x80000000u);
+// sorted entry t: a bucket's first entry records start[g] = t, its last one
+// end[g] = t + 1 (start/end zeroed beforehand, so an empty bucket reads 0, 0)
+FTS_HD void msm_job_bounds(uint64_t t, uint64_t total, const uint32_t* skey, uint32_t* start, uint32_t* end) {
+  uint32_t k = skey[t];
+  if (k == MSM_KEY_NONE) return;
+  if (t == 0 || skey[t - 1] != k) start[k] = (uint32_t)t;
+  if (t + 1 == total || skey[t + 1] != k) end[k] = (uint32_t)(t + 1);
 }
 
 // virtual point v of the resident array: P_v for v < n, phi(P_(v-n)) =

@@ -36,33 +36,28 @@ __global__ void __launch_bounds__(256) k_msm_load_scal(uint32_t n, const uint8_t
   fe_to_int(scal[i], fe_from_int<ModR>(k));
 }
 
-__global__ void __launch_bounds__(256) k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
-                                                    uint32_t* rank, uint32_t* count) {
-  __shared__ uint32_t top[MSM_TOP_LDS];
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool lds = p.top_used <= MSM_TOP_LDS;  // uniform
-  if (lds) {
-    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x) top[b] = 0;
-    __syncthreads();
-  }
-  if (i < p.n) msm_job_digits(p, i, scal, key, rank, count, true, lds ? top : nullptr);
-  if (lds) {
-    // the block's top-window counts: one returning atomic per bucket gives the
-    // block's base; the entries' ranks were local to the block
-    __syncthreads();
-    uint32_t* gtop = count + (size_t)(p.windows - 1) * p.buckets;
-    for (uint32_t b = threadIdx.x; b < p.top_used; b += blockDim.x)
-      if (top[b]) top[b] = atomicAdd(&gtop[b], top[b]);
-    __syncthreads();
-    if (i < p.n) {
-      size_t base = (size_t)(p.windows - 1) * p.nv;
-      for (uint32_t h = 0; h < (p.glv ? 2u : 1u); h++) {
-        size_t t = base + i + h * p.n;
-        uint32_t k = key[t];
-        if (k != NONE) rank[t] += top[k & 0x7FFFFFFFu];
-      }
-    }
-  }
+// one lane per point: sort keys + values of every window (dev/msm.h msm_job_keys)
+__global__ void __launch_bounds__(256) k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
+                                                  uint32_t* val) {
+  LANE_PROLOGUE(p.n);
+  msm_job_keys(p, i, scal, key, val);
+}
+
+// one lane per sorted entry: bucket ranges
+__global__ void __launch_bounds__(256) k_msm_bounds(uint64_t total, const uint32_t* skey, uint32_t* start,
+                                                    uint32_t* end) {
+  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  msm_job_bounds(t, total, skey, start, end);
+}
+
+// count[g] = end[g] - start[g] and the bucket's slot count
+__global__ void __launch_bounds__(256) k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end,
+                                                    uint32_t* count, uint32_t* m) {
+  LANE_PROLOGUE(p.windows * p.buckets);
+  uint32_t c = end[i] - start[i];
+  count[i] = c;
+  m[i] = msm_bucket_slots(p, c);
 }
 
 // exclusive scan, 1024 elements per workgroup; block totals to `tot`
@@ -85,20 +80,6 @@ __global__ void __launch_bounds__(1024) k_scan_block(const uint32_t* in, uint32_
 __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add) {
   uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   if (i < n) out[i] += add[blockIdx.x];
-}
-
-// one lane per (window, point): lanes of a wave hit random buckets of one window
-// one lane per (window, virtual point): position = start + rank (no atomics)
-__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, const uint32_t* rank,
-                                                     const uint32_t* start, uint32_t* perm) {
-  uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (uint64_t)p.windows * p.nv) return;
-  msm_job_scatter(p, t, key, rank, start, perm);
-}
-
-__global__ void __launch_bounds__(256) k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m) {
-  LANE_PROLOGUE(p.windows * p.buckets);
-  m[i] = msm_bucket_slots(p, count[i]);
 }
 
 __global__ void __launch_bounds__(256) k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff,

@@ -72,12 +72,11 @@ __global__ void k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint
 __global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok);
 __global__ void k_g1_sum(uint32_t n, const uint8_t* raw, uint8_t* out, uint32_t* status);
 __global__ void k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]);
-__global__ void k_msm_digits(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* rank, uint32_t* count);
+__global__ void k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val);
+__global__ void k_msm_bounds(uint64_t total, const uint32_t* skey, uint32_t* start, uint32_t* end);
+__global__ void k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end, uint32_t* count, uint32_t* m);
 __global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tot);
 __global__ void k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add);
-__global__ void k_msm_scatter(MsmPlan p, const uint32_t* key, const uint32_t* rank, const uint32_t* start,
-                              uint32_t* perm);
-__global__ void k_msm_nslots(MsmPlan p, const uint32_t* count, uint32_t* m);
 __global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
                             uint32_t* whi);
 __global__ void k_msm_phi(MsmPlan p, G1Dev* pts);

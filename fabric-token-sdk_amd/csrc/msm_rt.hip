@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "launch.h"
 #include "rt_internal.h"
@@ -12,7 +13,10 @@ struct ftz_msm {
   ftz_ctx* ctx = nullptr;
   MsmPlan p{};
   DBuf<G1Dev> pts;
-  DBuf<uint32_t> scal, key, rank, count, start, perm, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
+  DBuf<uint32_t> scal, key, skey, val, perm, count, start, end, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
+  DBuf<uint8_t> sort_tmp;
+  size_t sort_tmp_bytes = 0;
+  uint32_t key_bits = 0;
   DBuf<G1JDev> slot_sum, part, tree;
   DBuf<G1Dev> res;
   DBuf<G1JDev> hacc, wsum;
@@ -30,10 +34,16 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->pts.alloc(p.nv));  // P_i, then phi(P_i) for GLV
   HC(m->scal.alloc(8 * n));
   HC(m->key.alloc(wn));
+  HC(m->skey.alloc(wn));
+  HC(m->val.alloc(wn));
   HC(m->perm.alloc(wn));
   HC(m->count.alloc(wb));
   HC(m->start.alloc(wb));
-  HC(m->rank.alloc(wn));
+  HC(m->end.alloc(wb));
+  m->key_bits = msm_key_bits(p);
+  HC(rocprim::radix_sort_pairs(nullptr, m->sort_tmp_bytes, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0,
+                               m->key_bits, m->ctx->stream));
+  HC(m->sort_tmp.alloc(m->sort_tmp_bytes ? m->sort_tmp_bytes : 1));
   HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
   HC(m->nsl.alloc(wb));
   HC(m->soff.alloc(wb));
@@ -183,17 +193,19 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   const MsmPlan& p = m->p;
   size_t wb = (size_t)p.windows * p.buckets;
   HC(hipEventRecord(m->ev[0], s));
-  HC(hipMemsetAsync(m->count.p, 0, wb * sizeof(uint32_t), s));
   const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
-  k_msm_digits<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->rank.p, m->count.p);
-  int rc = scan(m->count.p, m->start.p, wb, m->tot.p, s);
-  if (rc != FTZ_SUCCESS) return rc;
-  k_msm_nslots<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->nsl.p);
-  rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
+  size_t wn = (size_t)p.windows * p.nv;
+  // (window, bucket)-sorted point lists: keys, stable radix sort, bucket ranges
+  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
+  size_t tb = m->sort_tmp_bytes;
+  HC(rocprim::radix_sort_pairs(m->sort_tmp.p, tb, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s));
+  HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
+  HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
+  k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>((uint64_t)wn, m->skey.p, m->start.p, m->end.p);
+  k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start.p, m->end.p, m->count.p, m->nsl.p);
+  int rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
-  k_msm_scatter<<<blocks((size_t)p.windows * p.nv, 256), 256, 0, s>>>(p, m->key.p, m->rank.p, m->start.p,
-                                                                       m->perm.p);
   // bucket slots in length order, then one lane per slot
   size_t sl = (size_t)p.windows * p.max_slots;
   HC(hipMemsetAsync(m->lenhist.p, 0, 1024 * sizeof(uint32_t), s));

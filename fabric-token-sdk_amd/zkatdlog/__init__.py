@@ -177,8 +177,9 @@ class Context:
     def commit_tokens(self, openings):
         """token commitments H(type)*Ped0 + v*Ped1 + bf*Ped2 (computeTokens,
         token/token.go:64-76) for (type, value, bf) openings: 64-byte RawBytes each."""
+        openings = list(openings)
         arr, keep = _abi.pack_openings(openings)
-        n = len(keep) // 3
+        n = len(openings)
         out = (ctypes.c_uint8 * max(1, 64 * n))()
         _check(self._lib.ftz_commit_tokens(self._h, n, arr, out), self._lib)
         raw = bytes(out)
@@ -187,8 +188,9 @@ class Context:
     def audit_openings(self, commitments, openings):
         """auditor opening check (audit/auditor.go:208-234): codes, 0 = match,
         FTZ_ERR_OPENING = mismatch, FTZ_ERR_PARSE = invalid commitment bytes."""
+        openings = list(openings)
         arr, keep = _abi.pack_openings(openings)
-        n = len(keep) // 3
+        n = len(openings)
         coms = b"".join(bytes(c) for c in commitments)
         if len(coms) != 64 * n:
             raise ValueError("one 64-byte commitment per opening")

@@ -1,9 +1,10 @@
 // TEST-ONLY host run of the MSM pipeline (dev/msm.h) with the same stage order
-// as msm_rt.hip: digits -> counting sort -> bucket sums -> segment sums ->
+// as msm_rt.hip: sort keys -> stable sort -> bucket ranges -> bucket sums -> segment sums ->
 // window sums -> Horner.  Small window sizes exercise many windows and the
 // signed-digit carries; tests/test_msm.py compares with the Python oracle.
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../fabric-token-sdk_amd/csrc/dev/msm.h"
@@ -31,16 +32,20 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   }
   if (p.glv)
     for (uint32_t i = 0; i < n; i++) msm_job_phi(p, i, pts.data());
-  size_t wb = (size_t)p.windows * p.buckets;
-  std::vector<uint32_t> key((size_t)p.windows * p.nv), rank((size_t)p.windows * p.nv), count(wb, 0), start(wb),
-      perm((size_t)p.windows * p.nv);
-  for (uint32_t i = 0; i < n; i++) msm_job_digits(p, i, sc, key.data(), rank.data(), count.data(), false);
-  uint32_t run = 0;
-  for (size_t b = 0; b < wb; b++) start[b] = run, run += count[b];
-  for (uint64_t t = 0; t < (uint64_t)p.windows * p.nv; t++)
-    msm_job_scatter(p, t, key.data(), rank.data(), start.data(), perm.data());
+  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * p.nv;
+  std::vector<uint32_t> key(wn), val(wn), skey(wn), perm(wn), count(wb), start(wb, 0), end(wb, 0);
+  for (uint32_t i = 0; i < n; i++) msm_job_keys(p, i, sc, key.data(), val.data());
+  // the device's stable radix sort over msm_key_bits(p) bits
+  uint32_t kb = msm_key_bits(p);
+  uint32_t kmask = kb >= 32 ? 0xFFFFFFFFu : (1u << kb) - 1;
+  std::vector<uint32_t> idx(wn);
+  for (size_t t = 0; t < wn; t++) idx[t] = (uint32_t)t;
+  std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return (key[a] & kmask) < (key[b] & kmask); });
+  for (size_t t = 0; t < wn; t++) skey[t] = key[idx[t]], perm[t] = val[idx[t]];
+  for (uint64_t t = 0; t < wn; t++) msm_job_bounds(t, wn, skey.data(), start.data(), end.data());
+  for (size_t g = 0; g < wb; g++) count[g] = end[g] - start[g];
   std::vector<uint32_t> soff(wb), owner((size_t)p.windows * p.max_slots, 0xFFFFFFFFu), wlo(p.windows), whi(p.windows);
-  run = 0;
+  uint32_t run = 0;
   for (size_t b = 0; b < wb; b++) soff[b] = run, run += msm_bucket_slots(p, count[b]);
   if (run > (size_t)p.windows * p.max_slots) return -2;
   for (uint32_t g = 0; g < wb; g++) msm_job_owner(p, g, count.data(), soff.data(), owner.data(), wlo.data(), whi.data());
