@@ -27,7 +27,8 @@ DEFS = ["-DFTS_G1TAB_C=16", "-DFTS_G2TAB_C=13"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH] + DEFS
 
 SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip")))
-           + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "msm_rt.hip")]
+           + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "msm_rt.hip"),
+              os.path.join(CSRC, "request_rt.hip")]
            + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))))
 
 

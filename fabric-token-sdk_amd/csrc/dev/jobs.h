@@ -249,20 +249,19 @@ FTS_HD void b64_encode(uint8_t* out, const uint8_t* in, uint32_t len) {
 // ------------------------------------------------------------------ jobs
 // gnark G1Affine.SetBytes via mathlib NewG1FromBytes:
 // flags 00 uncompressed (coordinates reduced mod p, (0,0) = infinity, must be
-// on the curve), 01 infinity, 10/11 compressed (smallest/largest root).
-FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, uint8_t* arena) {
-  const uint8_t* b = wire + j.raw;
-  g1a a;
+// on the curve), 01 infinity, 10/11 compressed (smallest/largest root); false
+// when SetBytes returns an error (a is then the point at infinity).
+FTS_HD bool g1_setbytes(const uint8_t* b, uint32_t len, g1a& a) {
   a.inf = false;
   bool ok = true;
-  uint8_t m = j.len >= 1 ? (b[0] & 0xC0) : 0;
-  if (j.len < 32) {
+  uint8_t m = len >= 1 ? (b[0] & 0xC0) : 0;
+  if (len < 32) {
     ok = false;
     a.inf = true;
   } else if (m == 0x40) {
     a.inf = true;
   } else if (m == 0x00) {
-    if (j.len < 64) {
+    if (len < 64) {
       ok = false;
       a.inf = true;
     } else {
@@ -309,6 +308,12 @@ FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, u
       }
     }
   }
+  return ok;
+}
+
+FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, uint8_t* arena) {
+  g1a a;
+  bool ok = g1_setbytes(wire + j.raw, j.len, a);
   G1Dev d;
   g1_store(d, a);
   pts[j.out] = d;

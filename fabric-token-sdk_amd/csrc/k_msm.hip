@@ -21,6 +21,14 @@ __global__ void __launch_bounds__(256) k_msm_load_pts(uint32_t n, const uint8_t*
   pts[i] = d;
 }
 
+// gnark SetBytes check of n 64-byte element slots (dev/jobs.h g1_setbytes;
+// token-request actions, request.cpp)
+__global__ void __launch_bounds__(256) k_g1_check(uint32_t n, const uint8_t* slots, uint8_t* ok) {
+  LANE_PROLOGUE(n);
+  g1a a;
+  ok[i] = g1_setbytes(slots + 64 * (size_t)i, 64, a) ? 1 : 0;
+}
+
 // final add of a point-split MSM (dev/msm.h g1_sum_raw): one lane; status[0] =
 // n on success, else the index of the first bad point
 __global__ void __launch_bounds__(64) k_g1_sum(uint32_t n, const uint8_t* raw, uint8_t* out, uint32_t* status) {

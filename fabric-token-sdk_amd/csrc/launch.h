@@ -71,6 +71,7 @@ __global__ void k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint
 // standalone MSM (k_msm.hip)
 __global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok);
 __global__ void k_g1_sum(uint32_t n, const uint8_t* raw, uint8_t* out, uint32_t* status);
+__global__ void k_g1_check(uint32_t n, const uint8_t* slots, uint8_t* ok);
 __global__ void k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]);
 __global__ void k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val);
 __global__ void k_msm_bounds(uint64_t total, const uint32_t* skey, uint32_t* start, uint32_t* end);

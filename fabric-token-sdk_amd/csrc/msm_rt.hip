@@ -256,6 +256,22 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
   delete m;
 }
 
+// gnark SetBytes check of n 64-byte slots on the context's device (rt_internal.h)
+int g1_check_slots(ftz_ctx* c, size_t n, const uint8_t* slots, uint8_t* ok) {
+  if (!n) return FTZ_SUCCESS;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  DBuf<uint8_t> buf;
+  HC(buf.alloc(65 * n));
+  HC(hipMemcpyAsync(buf.p, slots, 64 * n, hipMemcpyHostToDevice, s));
+  k_g1_check<<<blocks(n, 256), 256, 0, s>>>((uint32_t)n, buf.p, buf.p + 64 * n);
+  HC(hipGetLastError());
+  HC(hipMemcpyAsync(ok, buf.p + 64 * n, n, hipMemcpyDeviceToHost, s));
+  HC(hipStreamSynchronize(s));
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_g1_sum(ftz_ctx* c, size_t n, const uint8_t* points, uint8_t out[64]) {
   if (!c || !out || (n && !points)) return set_err(FTZ_E_INVALID, "null argument");
   if (n > 4096) return set_err(FTZ_E_INVALID, "ftz_g1_sum takes at most 4096 points");

@@ -1,0 +1,46 @@
+// C ABI of the raw token-request path (include/ftsamd.h, host/request.h):
+// ASN.1 + action JSON decoding on the calling thread, element checks on the
+// device, ZK verification of every action through the context's job engine.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host/request.h"
+#include "rt_internal.h"
+
+extern "C" int ftz_token_request_decode(const uint8_t* raw, size_t len, size_t counts[4], ftz_bytes* elems,
+                                        size_t cap) {
+  if (!counts || (!raw && len)) return set_err(FTZ_E_INVALID, "null argument");
+  std::vector<ftsh::Slice> f[4];
+  std::string e = ftsh::der_token_request(raw, len, f);
+  if (!e.empty()) return set_err(FTZ_E_INVALID, e);
+  size_t tot = 0;
+  for (int k = 0; k < 4; k++) counts[k] = f[k].size(), tot += f[k].size();
+  if (tot > cap || (tot && !elems)) return set_err(FTZ_E_INVALID, "elems capacity " + std::to_string(cap) +
+                                                                      " < " + std::to_string(tot));
+  size_t o = 0;
+  for (int k = 0; k < 4; k++)
+    for (const ftsh::Slice& s : f[k]) elems[o++] = ftz_bytes{s.p, s.len};
+  return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
+                                         void* user, int32_t* codes, int32_t* failed_action) {
+  if (!ctx || (n && (!reqs || !codes))) return set_err(FTZ_E_INVALID, "null argument");
+  ftsh::RequestHooks h;
+  h.check = [ctx](size_t m, const uint8_t* slots, uint8_t* ok) { return g1_check_slots(ctx, m, slots, ok); };
+  h.verify_transfers = [ctx](size_t m, const ftz_transfer* tx, int32_t* c) { return ftz_verify_transfers(ctx, m, tx, c); };
+  h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return ftz_verify_issues(ctx, m, is, c); };
+  h.get_state = get_state;
+  h.user = user;
+  std::string err;
+  int rc = ftsh::verify_token_requests(n, reqs, h, codes, failed_action, err);
+  if (rc != FTZ_SUCCESS && !err.empty()) {
+    std::string last = ftz_last_error();
+    return set_err(rc, err + (last.empty() ? "" : ": " + last));
+  }
+  return rc;
+}

@@ -171,6 +171,9 @@ inline const uint8_t* slot_out(const ftz_batch* b) {
   return b->h_res.p + ((b->n * sizeof(int32_t) + 255) & ~(size_t)255);
 }
 
+// gnark SetBytes check of n 64-byte element slots on the device (msm_rt.hip)
+int g1_check_slots(ftz_ctx* c, size_t n, const uint8_t* slots, uint8_t* ok);
+
 // ------------------------------------------------------------------ engine (engine.hip)
 int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue* is, int32_t* codes);
 void engine_destroy(ftz_ctx* c);

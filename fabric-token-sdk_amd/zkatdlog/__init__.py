@@ -207,6 +207,19 @@ class Context:
         finally:
             m.close()
 
+    def verify_token_requests(self, requests, ledger):
+        """Raw token requests (asn1 TokenRequest bytes) validated as
+        Validator.VerifyTokenRequestFromRaw does minus the Go-side signature /
+        HTLC / metadata checks; ledger: dict key -> token.Token JSON bytes (or a
+        callable).  Returns (codes, failed_action) lists."""
+        arr, keep = _abi.pack_bytes(requests)
+        n = len(keep)
+        cb = _abi.get_state_callback(ledger)
+        codes = (ctypes.c_int32 * max(1, n))()
+        failed = (ctypes.c_int32 * max(1, n))()
+        _check(self._lib.ftz_verify_token_requests(self._h, n, arr, cb, None, codes, failed), self._lib)
+        return list(codes)[:n], list(failed)[:n]
+
     def g1_sum(self, points):
         """Sum of RawBytes G1 points (n x 64 bytes, the identity = 64 zero
         bytes) on the device: the final add of a point-split MSM."""
@@ -237,6 +250,27 @@ class Context:
         h = ctypes.c_void_p()
         _check(self._lib.ftz_batch_load_issues(self._h, n, arr, ctypes.byref(h)), self._lib)
         return Batch(self, h, n)
+
+
+def decode_token_request(raw):
+    """driver.TokenRequest.FromBytes (Go encoding/asn1; host-side, no GPU):
+    [issues, transfers, signatures, auditor_signatures] or ValueError."""
+    lib = _abi.load()
+    raw = bytes(raw)
+    counts = (ctypes.c_size_t * 4)()
+    cap = max(1, len(raw) // 2)
+    elems = (_abi.Bytes * cap)()
+    if lib.ftz_token_request_decode(raw, len(raw), counts, elems, cap) != 0:
+        raise ValueError(lib.ftz_last_error().decode(errors="replace"))
+    out, k = [], 0
+    for f in range(4):
+        items = []
+        for _ in range(counts[f]):
+            e = elems[k]
+            k += 1
+            items.append(ctypes.string_at(e.p, e.len) if e.len else b"")
+        out.append(items)
+    return out
 
 
 def validate_public_params(pp_bytes):

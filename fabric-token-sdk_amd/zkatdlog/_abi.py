@@ -50,6 +50,48 @@ class TokenOpening(ctypes.Structure):
                 ("bf", ctypes.c_void_p)]
 
 
+class Bytes(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_void_p), ("len", ctypes.c_size_t)]
+
+
+# int (*)(void* user, const char* key, size_t key_len, const uint8_t** val, size_t* val_len)
+GET_STATE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t))
+FTZ_ERR_INPUT = 8
+
+
+def pack_bytes(items):
+    """list of bytes -> (ftz_bytes array, keepalive)."""
+    items = [bytes(x) for x in items]
+    arr = (Bytes * max(1, len(items)))()
+    keep = []
+    for k, x in enumerate(items):
+        b = ctypes.create_string_buffer(x, max(1, len(x)))
+        keep.append(b)
+        arr[k] = Bytes(ctypes.addressof(b), len(x))
+    return arr, keep
+
+
+def get_state_callback(ledger):
+    """A GET_STATE_FN over a dict key(str) -> bytes (or a callable key -> bytes
+    or None); the returned object must stay referenced during the call."""
+    lookup = ledger.get if isinstance(ledger, dict) else ledger
+    hold = {}
+
+    def cb(user, key, key_len, val, val_len):
+        k = ctypes.string_at(key, key_len).decode("utf-8", errors="surrogateescape")
+        v = lookup(k)
+        if v is None:
+            return 1
+        buf = hold.get(k)
+        if buf is None:
+            buf = hold[k] = ctypes.create_string_buffer(bytes(v), max(1, len(v)))
+        val[0] = ctypes.addressof(buf)
+        val_len[0] = len(v)
+        return 0
+    return GET_STATE_FN(cb)
+
+
 def pack_openings(openings):
     """openings: iterable of (type str/bytes, value int, bf int)."""
     openings = list(openings)
@@ -148,6 +190,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
+           "ftz_token_request_decode", "ftz_verify_token_requests",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
@@ -203,6 +246,9 @@ def load():
     lib.ftz_msm_destroy.argtypes = [vp]
     lib.ftz_msm_destroy.restype = None
     lib.ftz_g1_sum.argtypes = [vp, sz, ctypes.c_char_p, u8p]
+    lib.ftz_token_request_decode.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(Bytes), sz]
+    lib.ftz_verify_token_requests.argtypes = [vp, sz, ctypes.POINTER(Bytes), GET_STATE_FN, vp,
+                                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     szp = ctypes.POINTER(ctypes.c_size_t)
     i32p = ctypes.POINTER(ctypes.c_int32)
     lib.ftz_prove_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), u8p, sz, szp, i32p]

@@ -44,6 +44,7 @@ extern "C" {
 #define FTZ_ERR_MEMBERSHIP 5 /* "invalid membership proof"                          */
 #define FTZ_ERR_PANIC 6      /* the reference would panic on this proof             */
 #define FTZ_ERR_OPENING 7    /* audit: "output ... does not match the provided opening" */
+/* 8 = FTZ_ERR_INPUT (token requests, below) */
 
 /* API return codes */
 #define FTZ_SUCCESS 0
@@ -195,6 +196,39 @@ int ftz_commit_tokens(ftz_ctx* ctx, size_t n, const ftz_token_opening* t, uint8_
  * identity check InspectTokenOwnerFunc is idemix, outside this library.) */
 int ftz_audit_openings(ftz_ctx* ctx, size_t n, const uint8_t* commitments, const ftz_token_opening* t,
                        int32_t* codes);
+
+/* ---- raw token requests (the wire format around the path).
+ * A request is asn1.Marshal(driver.TokenRequest{Issues, Transfers, Signatures,
+ * AuditorSignatures [][]byte}) (token/driver/request.go:24-38). */
+typedef struct {
+  const uint8_t* p;
+  size_t len;
+} ftz_bytes;
+/* Go encoding/asn1 decoding as TokenRequest.FromBytes does it (request.go:35-38):
+ * counts[0..3] = len(Issues), len(Transfers), len(Signatures), len(AuditorSignatures);
+ * elems[0 .. sum(counts)) receive the byte slices in that order, pointing into
+ * raw (when cap is large enough).  FTZ_SUCCESS, or FTZ_E_INVALID for bytes
+ * the reference rejects (message in ftz_last_error) or a too small cap. */
+int ftz_token_request_decode(const uint8_t* raw, size_t len, size_t counts[4], ftz_bytes* elems, size_t cap);
+/* Ledger lookup (driver.GetStateFnc, validator.go:45; the Go shim passes a cgo
+ * export over getState): 0 and *val / *val_len (valid until the next call on
+ * the same thread), or non-zero when the state cannot be read.  Called on the
+ * calling thread only, in the reference's order. */
+typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, const uint8_t** val, size_t* val_len);
+#define FTZ_ERR_INPUT 8 /* an input to spend is missing on the ledger or is not a token.Token */
+/* ZK validation of n raw token requests as Validator.VerifyTokenRequestFromRaw
+ * performs it (crypto/validator/validator.go:45-108) minus the checks that stay
+ * in Go (auditor / issuer / owner signatures, HTLC scripts, metadata counting):
+ * ASN.1 and action JSON decoding (a failure rejects the whole request with
+ * FTZ_ERR_PARSE, as unmarshalIssueActions / unmarshalTransferActions do), then
+ * every issue action (issue.Verifier) and every transfer action (inputs loaded
+ * through get_state and decoded as token.Token -- FTZ_ERR_INPUT --, then
+ * transfer.Verifier) in order; all actions of all requests are verified in
+ * shared device batches.  codes[i] = FTZ_OK or the first failing check of
+ * request i; failed_action (may be NULL) = that action's index (issues first,
+ * then transfers), -1 if none or request-level. */
+int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
+                              int32_t* codes, int32_t* failed_action);
 
 /* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE configs[2]):
  * out = sum_i k_i P_i as 64-byte gnark RawBytes.  Points: n x 64-byte

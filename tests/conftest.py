@@ -27,7 +27,8 @@ def build_emu():
     srcs = [os.path.join(ROOT, "tests", "native", "emu.cpp"), os.path.join(ROOT, "tests", "native", "emu_exec.cpp"),
             os.path.join(ROOT, "tests", "native", "sx_emu.cpp"), os.path.join(ROOT, "tests", "native", "msm_emu.cpp"),
             os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "planner.cpp"), os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "planner_prove.cpp"),
-            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "gojson.cpp")]
+            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "gojson.cpp"),
+            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "request.cpp")]
     deps = srcs + [os.path.join(d, f) for d in (os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "dev"),
                                               os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host"))
                    for f in os.listdir(d) if f.endswith(".h")]

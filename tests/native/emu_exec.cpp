@@ -10,6 +10,7 @@
 
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/host/planner.h"
+#include "../../fabric-token-sdk_amd/csrc/host/request.h"
 #include "../../include/ftsamd.h"
 
 using namespace fts;
@@ -321,5 +322,25 @@ int emu_verify_issues(void* ctx, size_t n, const ftz_issue* is, int32_t* codes) 
   plan_issues(c->pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
   run_plan(c, p, n, codes);
   return 0;
+}
+
+// host run of the raw token-request path (host/request.cpp) with the same
+// orchestration as ftz_verify_token_requests
+int emu_verify_token_requests(void* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
+                              int32_t* codes, int32_t* failed) {
+  ftsh::RequestHooks h;
+  h.check = [](size_t m, const uint8_t* slots, uint8_t* ok) {
+    for (size_t i = 0; i < m; i++) {
+      g1a a;
+      ok[i] = g1_setbytes(slots + 64 * i, 64, a) ? 1 : 0;
+    }
+    return 0;
+  };
+  h.verify_transfers = [ctx](size_t m, const ftz_transfer* tx, int32_t* c) { return emu_verify_transfers(ctx, m, tx, c); };
+  h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return emu_verify_issues(ctx, m, is, c); };
+  h.get_state = get_state;
+  h.user = user;
+  std::string err;
+  return ftsh::verify_token_requests(n, reqs, h, codes, failed, err);
 }
 }

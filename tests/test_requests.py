@@ -1,0 +1,129 @@
+"""Raw token requests: asn1 TokenRequest decoding, the
+action / ledger-token JSON and the request-level verdict order of
+Validator.VerifyTokenRequestFromRaw (crypto/validator/validator.go:45-108,
+minus the Go-side signature / HTLC / metadata checks).
+
+Fixtures: tests/golden/token_requests.json (tests/golden/make_requests.py, from
+the oracle ftsoracle.request over the golden proof corpus).  CPU tier: the
+oracle against the fixtures (structure everywhere, real ZK on a sample), the
+library's host-side ASN.1 decoder, and the host build of the whole request
+path (TEST-ONLY tests/native); GPU tier: ftz_verify_token_requests."""
+import base64
+import ctypes
+import json
+import os
+
+import pytest
+
+from ftsoracle import request as R
+from ftsoracle import zkat as Z
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def fx():
+    with open(os.path.join(HERE, "golden", "token_requests.json")) as f:
+        d = json.load(f)
+    d["ledger_b"] = {k: base64.b64decode(v) for k, v in d["ledger"].items()}
+    for r in d["requests"]:
+        r["raw_b"] = base64.b64decode(r["raw"])
+    return d
+
+
+def test_fixture_covers_classes(fx):
+    codes = {r["expect"] for r in fx["requests"]}
+    assert codes >= {Z.OK, Z.ERR_PARSE, Z.ERR_MALFORMED, Z.ERR_WF, Z.ERR_RANGE, Z.ERR_MEMBERSHIP, Z.ERR_PANIC,
+                     R.ERR_INPUT}
+    assert len(fx["requests"]) >= 40
+
+
+def test_oracle_asn1_round_trip(fx):
+    """der_encode -> der_token_request is the identity; the library's decoder
+    (host code, no GPU) accepts / rejects exactly as the oracle and returns
+    the same fields."""
+    import zkatdlog
+    fields = [[b"a", b""], [b"x" * 200], [], [b"\x00" * 70000]]
+    raw = R.der_encode_token_request(fields)
+    assert R.der_token_request(raw) == fields
+    assert zkatdlog.decode_token_request(raw) == fields
+    for r in fx["requests"]:
+        try:
+            want = R.der_token_request(r["raw_b"])
+        except R.Asn1Error:
+            want = None
+        try:
+            got = zkatdlog.decode_token_request(r["raw_b"])
+        except ValueError:
+            got = None
+        assert got == want, r["name"]
+
+
+def test_oracle_verdicts_real_zk_sample(fx):
+    """the oracle with its real ZK verifiers (not the corpus memo the maker
+    used) on requests with one cheap action each"""
+    pp = Z.PublicParams.from_json(fx["pp"].encode())
+    pick = {"issue_anonymous_mismatch", "input_missing", "transfer_action_null_json", "asn1_extra_field_inside_sequence_ignored",
+            "issue_nil_output_malformed"}
+    seen = 0
+    for r in fx["requests"]:
+        if r["name"] in pick:
+            got = R.verify_token_request(pp, r["raw_b"], fx["ledger_b"].get)
+            assert list(got) == [r["expect"], r["failed_action"]], r["name"]
+            seen += 1
+    assert seen == len(pick)
+
+
+def test_emu_request_path_matches_fixture(emu, fx):
+    """the product's request orchestration (host/request.cpp) over the host
+    build of the job code reproduces every fixture verdict and failing index"""
+    from zkatdlog import _abi as A
+    emu.emu_verify_token_requests.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Bytes),
+                                              A.GET_STATE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                              ctypes.POINTER(ctypes.c_int32)]
+    pp = fx["pp"].encode()
+    ctx = emu.emu_ctx_create(pp, len(pp), ctypes.create_string_buffer(256), 256)
+    try:
+        reqs = [r["raw_b"] for r in fx["requests"]]
+        arr, keep = A.pack_bytes(reqs)
+        cb = A.get_state_callback(fx["ledger_b"])
+        n = len(reqs)
+        codes = (ctypes.c_int32 * n)()
+        failed = (ctypes.c_int32 * n)()
+        assert emu.emu_verify_token_requests(ctx, n, arr, cb, None, codes, failed) == 0
+    finally:
+        emu.emu_ctx_destroy(ctx)
+    got = {r["name"]: (codes[k], failed[k]) for k, r in enumerate(fx["requests"])}
+    want = {r["name"]: (r["expect"], r["failed_action"]) for r in fx["requests"]}
+    assert got == want
+
+
+@pytest.fixture(scope="module")
+def gctx(fx):
+    import zkatdlog
+    c = zkatdlog.Context(fx["pp"].encode(), device=0)
+    yield c
+    c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_requests_match_fixture(gctx, fx):
+    codes, failed = gctx.verify_token_requests([r["raw_b"] for r in fx["requests"]], fx["ledger_b"])
+    got = {r["name"]: (codes[k], failed[k]) for k, r in enumerate(fx["requests"])}
+    want = {r["name"]: (r["expect"], r["failed_action"]) for r in fx["requests"]}
+    assert got == want
+
+
+@pytest.mark.gpu
+def test_gpu_requests_many(gctx, fx):
+    """2000 requests (the fixture tiled, ~5 actions per valid request): every
+    verdict as expected; prints the request rate end to end (ASN.1 + action
+    JSON + ledger callbacks + device batches)."""
+    import time
+    reqs = fx["requests"] * 44
+    t0 = time.perf_counter()
+    codes, failed = gctx.verify_token_requests([r["raw_b"] for r in reqs], fx["ledger_b"])
+    dt = time.perf_counter() - t0
+    assert codes == [r["expect"] for r in reqs]
+    assert failed == [r["failed_action"] for r in reqs]
+    print("%d token requests in %.3f s: %.0f requests/s" % (len(reqs), dt, len(reqs) / dt), flush=True)
