@@ -269,6 +269,10 @@ def roofline(ctx, job, batch, device, tx_per_s):
              "g2": "k_g2lines", "miller": "k_miller", "fexp": "k_fexp_exact", "hash": "k_hash", "decode": "k_decode"}
     mjob = dict(opc["m_per_job"])
     mjob["g1p"] = mjob["g1"]  # the pairing-input G1 jobs run the same job code
+    # device kernel split (tests/native/opcount.py): k_g2lines = t' + pair-2 lines, k_miller = f-chain only
+    mk = opc.get("m_per_kernel_job", {})
+    mjob["g2"] = mk.get("k_g2lines", mjob["g2"])
+    mjob["miller"] = mk.get("k_miller", mjob["miller"])
     dom = max((k for k in kern if k in names and mjob.get(k)), key=lambda k: kern[k][0])
     m_job = mjob[dom]
     achieved = m_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)

@@ -194,6 +194,14 @@ int emu_opcount_transfers(void* ctx, size_t n, const ftz_transfer* tx, unsigned 
   stage(8, p.hmain.size(), [&](size_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   per_stage[9] = 0;
   jobs[9] = n;
+  // stage 10: the device's k_g2lines split (t' by fixed-base tables + the 88
+  // pair-2 Miller lines evaluated at R), g2[i] paired with pr[i] as the kernel does
+  std::vector<G2Dev> g2o2(std::max<uint32_t>(p.n_g2out, 1));
+  std::vector<EvLineDev> lines(88 * std::max<size_t>(p.g2.size(), 1));
+  stage(10, p.g2.size(), [&](size_t i) {
+    job_g2lines(p.g2[i], p.pr[i], scal, c->g2tab.data(), g2o2.data(), pts.data(), lines.data(), (uint32_t)i,
+                (uint32_t)p.g2.size());
+  });
   return 0;
 }
 #endif

@@ -13,13 +13,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
 from zkatdlog import _abi as A  # noqa: E402
 
-NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "hash", "verdict"]
+NAMES = ["decode", "zr", "hash_pre", "scalar", "g1", "g2", "miller", "fexp", "hash", "verdict", "g2lines"]
 
 
 def main():
     lib = "/tmp/libftsemu_count.so"
     srcs = ["tests/native/emu.cpp", "tests/native/emu_exec.cpp", "fabric-token-sdk_amd/csrc/host/planner.cpp",
-            "fabric-token-sdk_amd/csrc/host/gojson.cpp", "fabric-token-sdk_amd/csrc/host/planner_prove.cpp"]
+            "fabric-token-sdk_amd/csrc/host/gojson.cpp", "fabric-token-sdk_amd/csrc/host/planner_prove.cpp",
+            "fabric-token-sdk_amd/csrc/host/request.cpp", "tests/native/sx_emu.cpp", "tests/native/msm_emu.cpp"]
     subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-Wno-unknown-pragmas", "-pthread",
                     "-DFTS_COUNT_OPS"] + [os.path.join(ROOT, s) for s in srcs] + ["-o", lib], check=True)
     L = ctypes.CDLL(lib)
@@ -39,12 +40,17 @@ def main():
             c = [x for x in g[key]["cases"] if x["name"] == sel][0]
             items = [(bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"]))]
         arr, keep = A.pack_transfers(items)
-        ps, js = (ctypes.c_ulonglong * 10)(), (ctypes.c_ulonglong * 10)()
+        ps, js = (ctypes.c_ulonglong * 11)(), (ctypes.c_ulonglong * 11)()
         L.emu_opcount_transfers(ctypes.c_void_p(ctx), len(items), arr, ps, js)
         out[key] = {"transfers": len(items),
-                    "m_per_tx": sum(ps) / 136 / len(items),
+                    "m_per_tx": sum(ps[:10]) / 136 / len(items),
                     "m_per_job": {n: (ps[i] / 136 / js[i] if js[i] else 0) for i, n in enumerate(NAMES)},
                     "jobs_per_tx": {n: js[i] / len(items) for i, n in enumerate(NAMES)}}
+        # per DEVICE kernel: k_g2lines = t' + the pair-2 lines (stage g2lines); k_miller = the one-lane
+        # Miller loop minus the pair-2 line computation it does inline (g2lines - g2)
+        mj = out[key]["m_per_job"]
+        out[key]["m_per_kernel_job"] = {"k_g2lines": mj["g2lines"], "k_miller": mj["miller"] - (mj["g2lines"] - mj["g2"]),
+                                        "k_fexp": mj["fexp"], "k_g1_part+k_g1_combine": mj["g1"]}
         print(key, json.dumps(out[key]))
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     json.dump(out, open(os.path.join(ROOT, "profiles", "opcounts.json"), "w"), indent=1)
