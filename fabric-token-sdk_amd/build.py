@@ -28,7 +28,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch="
 
 SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip")))
            + [os.path.join(CSRC, "runtime.hip"), os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "msm_rt.hip"),
-              os.path.join(CSRC, "request_rt.hip")]
+              os.path.join(CSRC, "request_rt.hip"), os.path.join(CSRC, "idemix_rt.hip")]
            + sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp"))))
 
 

@@ -1,0 +1,174 @@
+// Idemix owner-signature verification job: IBM/idemix
+// NymSignature.Ver on FP256BN, one lane per signature.  The reference calls it
+// per input token from TransferSignatureValidate
+// (zkatdlog/crypto/validator/validator_transfer.go:42-82) through
+// identity/msp/idemix/deserializer.go:155-167 Verifier.Verify.  [EXT] IBM/idemix
+// v0.0.0-20220113150823-80dd4cb2d74e (go.mod:6), restated:
+//   t = HSk^ProofSSk * HRand^ProofSRNym * Nym^-ProofC
+//   c = HashToZr("sign" || t || Nym || ipk.Hash || msg)     (G1 = 0x04||X||Y)
+//   accept  <=>  ProofC == HashToZr(c || Nonce)            (raw 32-byte integers)
+// The host (host/idemix.cpp) decodes the owner identity and the signature proto
+// and lays out per signature: the six 32-byte integers, a 176-byte transcript
+// prefix slot ("sign" and the IPK hash already in place) and the message.
+#pragma once
+#include "fp256bn.h"
+#include "sha256.h"
+
+namespace fts {
+
+// fixed-base tables of HSk and HRand: NYM_WINDOWS windows of 8 bits, entries
+// d * 2^(8w) * H for d = 1..255, Montgomery affine (never infinity: d 2^(8w) < n)
+static constexpr int NYM_WBITS = 8;
+static constexpr int NYM_WINDOWS = 32;
+static constexpr int NYM_TAB_PER_BASE = NYM_WINDOWS * 255;
+struct QDev {
+  uint32_t x[8], y[8];
+};
+
+struct NymJob {
+  uint32_t sc;       // blob offset (16-aligned): NymX, NymY, ProofC, ProofSSk, ProofSRNym, Nonce (32 bytes BE each)
+  uint32_t pre;      // blob offset (16-aligned) of the transcript prefix: "sign" | t (65) | Nym (65) | hash (32)
+  uint32_t msg;      // blob offset of the message, = 6 mod 16 so that stream byte 192 is 16-aligned
+  uint32_t msg_len;
+};
+static constexpr uint32_t NYM_PRE = 4 + 65 + 65 + 32;  // 166
+
+FTS_HD q1a q1_load(const QDev& d) {
+  q1a a;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    a.x.v[i] = d.x[i];
+    a.y.v[i] = d.y[i];
+  }
+  a.inf = false;
+  return a;
+}
+
+FTS_HD void q1_store(QDev& d, const q1a& a) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.x[i] = a.x.v[i];
+    d.y[i] = a.y.v[i];
+  }
+}
+
+// amcl ECP.ToBytes(b, false): 0x04 || X || Y; the point at infinity as amcl's
+// (0, 1) representative [EXT]
+FTS_HD void q1_bytes65(uint8_t* out, const q1a& a) {
+  uint32_t x[8], y[8];
+  if (a.inf) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      x[i] = 0;
+      y[i] = i == 0;
+    }
+  } else {
+    fq_to_int(x, a.x);
+    fq_to_int(y, a.y);
+  }
+  out[0] = 0x04;
+  limbs_to_be32(out + 1, x);
+  limbs_to_be32(out + 33, y);
+}
+
+// sum over the 32 byte-windows of k of tab[w][byte_w - 1]
+FTS_HD q1j q1_fixed_mul(const QDev* tab, const uint32_t k[8]) {
+  q1j acc = jac_inf<fq>();
+#pragma nounroll
+  for (int w = 0; w < NYM_WINDOWS; w++) {
+    uint32_t d = (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+    if (d) acc = jac_add_aff(acc, q1_load(tab[w * 255 + d - 1]));
+  }
+  return acc;
+}
+
+// one signature: 1 = accept, 0 = "pseudonym signature invalid".  The prefix
+// slot at blob + j.pre receives t and Nym (device-computed bytes).
+FTS_HD uint8_t job_nym(const NymJob& j, uint8_t* blob, const QDev* tab) {
+  uint32_t v[6][8];
+#pragma unroll
+  for (int q = 0; q < 6; q++) be32_to_limbs_g(v[q], blob + j.sc + 32 * q);
+  // the nym: NewECPbigs(x, y) -- coordinates mod q, off-curve -> infinity
+  q1a nym;
+  nym.x = fq_from_int(v[0]);
+  nym.y = fq_from_int(v[1]);
+  nym.inf = false;
+  if (!q1_on_curve(nym)) nym.inf = true;
+  // t = s_sk HSk + s_rnym HRand - c Nym
+  q1j acc = q1_fixed_mul(tab, v[3]);
+  acc = jac_add(acc, q1_fixed_mul(tab + NYM_TAB_PER_BASE, v[4]));
+  acc = jac_add(acc, aff_mul(aff_neg(nym), v[2]));
+  q1a t = jac_to_aff(acc);
+  uint8_t* pre = blob + j.pre;
+  q1_bytes65(pre + 4, t);
+  q1_bytes65(pre + 69, nym);
+  Sha256 s;
+  s.init();
+  s.update(pre, NYM_PRE);
+  uint32_t head = j.msg_len < 26 ? j.msg_len : 26;  // completes the third block
+  s.update(blob + j.msg, head);
+  s.update(blob + j.msg + head, j.msg_len - head);
+  uint8_t d[32];
+  s.final(d);
+  uint32_t c[8];
+  digest_mod_n(c, d);
+  // ProofC == HashToZr(c || Nonce), Nonce as its raw 32 bytes
+  uint8_t cb[64];
+  limbs_to_be32(cb, c);
+  limbs_to_be32(cb + 32, v[5]);
+  s.init();
+  s.update(cb, 64);
+  s.final(d);
+  digest_mod_n(c, d);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= c[i] ^ v[2][i];
+  return o == 0 ? 1 : 0;
+}
+
+// Host: the fixed-base tables of HSk and HRand (tab[b * NYM_TAB_PER_BASE +
+// w * 255 + d - 1] = d 2^(8w) H_b), built once per issuer key.  Window bases by
+// doublings, entries by mixed additions, one batch inversion per window.
+inline void nym_build_tables(const q1a bases[2], QDev* tab) {
+  for (int b = 0; b < 2; b++) {
+    q1a bw = bases[b];
+    for (int w = 0; w < NYM_WINDOWS; w++) {
+      q1j e[255];
+      e[0] = jac_from_aff(bw);
+      for (int d = 1; d < 255; d++) e[d] = jac_add_aff(e[d - 1], bw);
+      // batch inversion of the 255 Z coordinates (none is zero: d 2^(8w) < n)
+      fq pre[255];
+      pre[0] = e[0].z;
+      for (int d = 1; d < 255; d++) pre[d] = pre[d - 1] * e[d].z;
+      fq inv_all = inv(pre[254]);
+      for (int d = 254; d >= 0; d--) {
+        fq zi = d ? inv_all * pre[d - 1] : inv_all;
+        if (d) inv_all = inv_all * e[d].z;
+        fq zi2 = sqr(zi);
+        q1a a;
+        a.x = e[d].x * zi2;
+        a.y = e[d].y * zi2 * zi;
+        a.inf = false;
+        q1_store(tab[b * NYM_TAB_PER_BASE + w * 255 + d], a);
+      }
+      // next window base: 2^8 bw
+      q1j nb = jac_from_aff(bw);
+      for (int k = 0; k < NYM_WBITS; k++) nb = jac_dbl(nb);
+      bw = jac_to_aff(nb);
+    }
+  }
+}
+
+// 32 big-endian bytes -> Montgomery affine point (amcl NewECPbigs); false if
+// off the curve
+inline bool nym_point_from_be(const uint8_t* xb, const uint8_t* yb, q1a& out) {
+  uint32_t x[8], y[8];
+  be32_to_limbs(x, xb);
+  be32_to_limbs(y, yb);
+  out.x = fq_from_int(x);
+  out.y = fq_from_int(y);
+  out.inf = false;
+  return q1_on_curve(out);
+}
+
+}  // namespace fts

@@ -1,0 +1,432 @@
+// Host decoding for idemix owner-signature verification (idemix.h).
+#include "idemix.h"
+
+#include <string.h>
+
+#include <map>
+
+#include "../dev/idemix.h"
+
+namespace ftsh {
+
+// ---------------------------------------------------------------- protobuf
+// google.golang.org/protobuf v1.27.1 wire rules: tags are varints with field
+// number in [1, 2^29 - 1]; varints are at most 10 bytes (the 10th <= 1); wire
+// types 3/4 are groups (skipped with a matching end marker), 6/7 are reserved.
+namespace {
+
+bool pb_varint(const uint8_t* b, size_t n, size_t& i, uint64_t& v, std::string& err) {
+  v = 0;
+  for (int k = 0; k < 10; k++) {
+    if (i >= n) {
+      err = "unexpected EOF";
+      return false;
+    }
+    uint8_t c = b[i++];
+    if (k == 9 && c > 1) {
+      err = "variable length integer overflow";
+      return false;
+    }
+    v |= (uint64_t)(c & 0x7f) << (7 * k);
+    if (c < 0x80) return true;
+  }
+  err = "variable length integer overflow";
+  return false;
+}
+
+bool pb_tag(const uint8_t* b, size_t n, size_t& i, uint32_t& num, uint8_t& wt, std::string& err) {
+  uint64_t t;
+  if (!pb_varint(b, n, i, t, err)) return false;
+  uint64_t f = t >> 3;
+  if (f < 1 || f > (1u << 29) - 1) {
+    err = "invalid field number";
+    return false;
+  }
+  num = (uint32_t)f;
+  wt = (uint8_t)(t & 7);
+  return true;
+}
+
+bool pb_skip(const uint8_t* b, size_t n, size_t& i, uint32_t num, uint8_t wt, int depth, std::string& err) {
+  uint64_t v;
+  switch (wt) {
+    case 0:
+      return pb_varint(b, n, i, v, err);
+    case 1:
+      if (n - i < 8) {
+        err = "unexpected EOF";
+        return false;
+      }
+      i += 8;
+      return true;
+    case 5:
+      if (n - i < 4) {
+        err = "unexpected EOF";
+        return false;
+      }
+      i += 4;
+      return true;
+    case 2:
+      if (!pb_varint(b, n, i, v, err)) return false;
+      if (v > n - i) {
+        err = "unexpected EOF";
+        return false;
+      }
+      i += (size_t)v;
+      return true;
+    case 3:
+      if (depth > 10000) {
+        err = "exceeded maximum recursion depth";
+        return false;
+      }
+      for (;;) {
+        if (i >= n) {
+          err = "unexpected EOF";
+          return false;
+        }
+        uint32_t n2;
+        uint8_t w2;
+        if (!pb_tag(b, n, i, n2, w2, err)) return false;
+        if (w2 == 4) {
+          if (n2 != num) {
+            err = "mismatching end group marker";
+            return false;
+          }
+          return true;
+        }
+        if (!pb_skip(b, n, i, n2, w2, depth + 1, err)) return false;
+      }
+    default:
+      err = "cannot parse reserved wire type";
+      return false;
+  }
+}
+
+}  // namespace
+
+std::string pb_scan(const uint8_t* b, size_t n, std::vector<PbField>& out) {
+  out.clear();
+  size_t i = 0;
+  std::string err;
+  while (i < n) {
+    uint32_t num;
+    uint8_t wt;
+    if (!pb_tag(b, n, i, num, wt, err)) return err;
+    if (wt == 4) return "unexpected end group";
+    PbField f{num, wt, 0, nullptr, 0};
+    if (wt == 0) {
+      if (!pb_varint(b, n, i, f.v, err)) return err;
+    } else if (wt == 2) {
+      uint64_t L;
+      if (!pb_varint(b, n, i, L, err)) return err;
+      if (L > n - i) return "unexpected EOF";
+      f.p = b + i;
+      f.len = (size_t)L;
+      i += (size_t)L;
+    } else {
+      if (!pb_skip(b, n, i, num, wt, 0, err)) return err;
+      continue;  // fixed32/64, groups: no field of these messages uses them
+    }
+    out.push_back(f);
+  }
+  return "";
+}
+
+bool utf8_valid(const uint8_t* p, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    uint8_t c = p[i];
+    if (c < 0x80) {
+      i++;
+      continue;
+    }
+    int len;
+    uint32_t cp, lo_min;
+    if ((c & 0xe0) == 0xc0) {
+      len = 2, cp = c & 0x1f, lo_min = 0x80;
+    } else if ((c & 0xf0) == 0xe0) {
+      len = 3, cp = c & 0x0f, lo_min = 0x800;
+    } else if ((c & 0xf8) == 0xf0) {
+      len = 4, cp = c & 0x07, lo_min = 0x10000;
+    } else {
+      return false;
+    }
+    if (n - i < (size_t)len) return false;
+    for (int k = 1; k < len; k++) {
+      uint8_t d = p[i + k];
+      if ((d & 0xc0) != 0x80) return false;
+      cp = (cp << 6) | (d & 0x3f);
+    }
+    if (cp < lo_min || cp > 0x10ffff || (cp >= 0xd800 && cp <= 0xdfff)) return false;
+    i += len;
+  }
+  return true;
+}
+
+namespace {
+
+// proto3 field kinds of the messages read here
+enum PbKind { PK_BYTES, PK_STRING, PK_ENUM };
+
+// Decode a message whose known fields are all singular bytes / string / enum:
+// the last occurrence wins; a known field with another wire type is unknown.
+// present[k] / val[k] for field numbers 1..nf (kinds[k-1]).
+std::string pb_simple(const uint8_t* b, size_t n, int nf, const PbKind* kinds, bool* present, PbField* val) {
+  std::vector<PbField> fs;
+  std::string e = pb_scan(b, n, fs);
+  if (!e.empty()) return e;
+  for (int k = 0; k < nf; k++) present[k] = false;
+  for (const PbField& f : fs) {
+    if (f.num < 1 || (int)f.num > nf) continue;
+    PbKind kd = kinds[f.num - 1];
+    uint8_t want = kd == PK_ENUM ? 0 : 2;
+    if (f.wt != want) continue;
+    if (kd == PK_STRING && !utf8_valid(f.p, f.len)) return "string field contains invalid UTF-8";
+    present[f.num - 1] = true;
+    val[f.num - 1] = f;
+  }
+  return "";
+}
+
+// ---------------------------------------------------------------- ASN.1 RawOwner
+// Go 1.18 encoding/asn1: definite minimal lengths; a string field takes
+// PrintableString / IA5String / T61String / UTF8String / NumericString /
+// BMPString / GeneralString with that type's character rules.
+bool der_tlv(const uint8_t* b, size_t n, size_t& off, uint8_t& tag, size_t& len) {
+  if (off >= n) return false;
+  tag = b[off++];
+  if ((tag & 0x1f) == 0x1f) return false;  // high-tag-number form: no universal tag used here fits
+  if (off >= n) return false;
+  uint8_t c = b[off++];
+  size_t L = 0;
+  if (c & 0x80) {
+    int nb = c & 0x7f;
+    if (nb == 0) return false;
+    for (int k = 0; k < nb; k++) {
+      if (off >= n) return false;
+      if (L >= (1u << 23)) return false;
+      L = (L << 8) | b[off++];
+      if (L == 0) return false;
+    }
+    if (L < 0x80) return false;
+  } else {
+    L = c;
+  }
+  if (L > n - off) return false;
+  len = L;
+  return true;
+}
+
+bool printable(uint8_t c) {
+  return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || strchr(" '()+,-./:=?*&", c) != nullptr;
+}
+
+// decode an ASN.1 string of universal tag `tag` into UTF-8 (false: Go rejects it)
+bool asn1_string(uint8_t tag, const uint8_t* p, size_t n, std::string& out) {
+  out.clear();
+  switch (tag) {
+    case 0x13:  // PrintableString
+      for (size_t i = 0; i < n; i++)
+        if (!printable(p[i]) || p[i] == 0) return false;
+      out.assign((const char*)p, n);
+      return true;
+    case 0x16:  // IA5String
+      for (size_t i = 0; i < n; i++)
+        if (p[i] >= 0x80) return false;
+      out.assign((const char*)p, n);
+      return true;
+    case 0x14:  // T61String
+    case 0x1b:  // GeneralString: passed as 8-bit bytes
+      out.assign((const char*)p, n);
+      return true;
+    case 0x0c:  // UTF8String
+      if (!utf8_valid(p, n)) return false;
+      out.assign((const char*)p, n);
+      return true;
+    case 0x12:  // NumericString
+      for (size_t i = 0; i < n; i++)
+        if (!((p[i] >= '0' && p[i] <= '9') || p[i] == ' ')) return false;
+      out.assign((const char*)p, n);
+      return true;
+    case 0x1e: {  // BMPString: UTF-16BE, a trailing NUL pair stripped
+      if (n % 2) return false;
+      if (n >= 2 && p[n - 1] == 0 && p[n - 2] == 0) n -= 2;
+      for (size_t i = 0; i < n; i += 2) {
+        uint32_t u = ((uint32_t)p[i] << 8) | p[i + 1];
+        if (u >= 0xd800 && u < 0xdc00 && i + 2 < n) {
+          uint32_t u2 = ((uint32_t)p[i + 2] << 8) | p[i + 3];
+          if (u2 >= 0xdc00 && u2 < 0xe000) {
+            u = 0x10000 + ((u - 0xd800) << 10) + (u2 - 0xdc00);
+            i += 2;
+          } else {
+            u = 0xfffd;
+          }
+        } else if (u >= 0xd800 && u < 0xe000) {
+          u = 0xfffd;
+        }
+        if (u < 0x80) {
+          out.push_back((char)u);
+        } else if (u < 0x800) {
+          out.push_back((char)(0xc0 | (u >> 6)));
+          out.push_back((char)(0x80 | (u & 0x3f)));
+        } else if (u < 0x10000) {
+          out.push_back((char)(0xe0 | (u >> 12)));
+          out.push_back((char)(0x80 | ((u >> 6) & 0x3f)));
+          out.push_back((char)(0x80 | (u & 0x3f)));
+        } else {
+          out.push_back((char)(0xf0 | (u >> 18)));
+          out.push_back((char)(0x80 | ((u >> 12) & 0x3f)));
+          out.push_back((char)(0x80 | ((u >> 6) & 0x3f)));
+          out.push_back((char)(0x80 | (u & 0x3f)));
+        }
+      }
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
+// identity.UnmarshallRawOwner (identity/owner.go:30-37)
+bool raw_owner(const uint8_t* b, size_t n, std::string& type, const uint8_t*& ident, size_t& ident_len) {
+  size_t off = 0, len;
+  uint8_t tag;
+  if (!der_tlv(b, n, off, tag, len) || tag != 0x30) return false;
+  const uint8_t* s = b + off;
+  size_t k = 0, l1;
+  if (!der_tlv(s, len, k, tag, l1)) return false;
+  if (!asn1_string(tag, s + k, l1, type)) return false;
+  k += l1;
+  size_t l2;
+  if (!der_tlv(s, len, k, tag, l2) || tag != 0x04) return false;
+  ident = s + k;
+  ident_len = l2;
+  return true;  // trailing elements inside the SEQUENCE and bytes after it are ignored
+}
+
+}  // namespace
+
+std::string parse_ipk(const uint8_t* p, size_t n, IdemixIpk& out) {
+  std::vector<PbField> fs;
+  std::string e = pb_scan(p, n, fs);
+  if (!e.empty()) return "issuer public key: " + e;
+  bool have_hsk = false, have_hrand = false;
+  for (const PbField& f : fs) {
+    if (f.wt != 2) continue;
+    if (f.num == 1 && !utf8_valid(f.p, f.len)) return "issuer public key: invalid UTF-8 attribute name";
+    if (f.num == 2 || f.num == 3) {  // ECP{X = 1, Y = 2}; a repeated singular message merges
+      static const PbKind kinds[2] = {PK_BYTES, PK_BYTES};
+      bool pr[2];
+      PbField v[2];
+      e = pb_simple(f.p, f.len, 2, kinds, pr, v);
+      if (!e.empty()) return "issuer public key: " + e;
+      std::vector<uint8_t>& x = f.num == 2 ? out.hsk_x : out.hrand_x;
+      std::vector<uint8_t>& y = f.num == 2 ? out.hsk_y : out.hrand_y;
+      if (pr[0]) x.assign(v[0].p, v[0].p + v[0].len);
+      if (pr[1]) y.assign(v[1].p, v[1].p + v[1].len);
+      (f.num == 2 ? have_hsk : have_hrand) = true;
+    }
+    if (f.num == 10) out.hash.assign(f.p, f.p + f.len);
+  }
+  if (!have_hsk || !have_hrand) return "issuer public key: some part of the public key is undefined";
+  if (out.hsk_x.size() < 32 || out.hsk_y.size() < 32 || out.hrand_x.size() < 32 || out.hrand_y.size() < 32)
+    return "issuer public key: coordinate shorter than 32 bytes";
+  return "";
+}
+
+void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_t* sig, size_t sig_len,
+                            NymDecoded& out) {
+  out.code = 0;
+  out.why.clear();
+  auto fail = [&](int code, const char* why) {
+    out.code = code;
+    out.why = why;
+  };
+  // ---- GetOwnerVerifier: htlc.Deserializer -> RawOwnerIdentityDeserializer -> idemix
+  std::string type;
+  const uint8_t* ident;
+  size_t ident_len;
+  if (!raw_owner(owner, owner_len, type, ident, ident_len)) return fail(FTZ_ERR_OWNER, "failed to unmarshal RawOwner");
+  if (type == "htlc") return fail(FTZ_ERR_UNSUPPORTED, "htlc script owner: verified in Go");
+  if (type != "si") {
+    out.code = FTZ_ERR_OWNER;
+    out.why = "failed to deserialize RawOwner: Unknown owner type " + type;
+    return;
+  }
+  static const PbKind k_si[2] = {PK_STRING, PK_BYTES};
+  bool pr[5];
+  PbField v[5];
+  if (!pb_simple(ident, ident_len, 2, k_si, pr, v).empty())
+    return fail(FTZ_ERR_OWNER, "failed to unmarshal to msp.SerializedIdentity{}");
+  const uint8_t* idb = pr[1] ? v[1].p : nullptr;
+  size_t idn = pr[1] ? v[1].len : 0;
+  static const PbKind k_ser[5] = {PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES};
+  if (!pb_simple(idb, idn, 5, k_ser, pr, v).empty())
+    return fail(FTZ_ERR_OWNER, "could not deserialize a SerializedIdemixIdentity");
+  if (!pr[0] || !pr[1]) return fail(FTZ_ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid");
+  // NymPublicKey import: raw = NymX || NymY split in halves, FromBytes reads 32 bytes of each
+  size_t tot = v[0].len + v[1].len, half = tot / 2;
+  if (half < 32) return fail(FTZ_ERR_OWNER, "failed to import nym public key");
+  auto raw_at = [&](size_t i) { return i < v[0].len ? v[0].p[i] : v[1].p[i - v[0].len]; };
+  for (int i = 0; i < 32; i++) {
+    out.ints[0][i] = raw_at(i);
+    out.ints[1][i] = raw_at(half + i);
+  }
+  PbField ou = v[2], role = v[3];
+  bool has_ou = pr[2], has_role = pr[3];
+  static const PbKind k_ou[3] = {PK_STRING, PK_STRING, PK_BYTES};
+  if (!pb_simple(has_ou ? ou.p : nullptr, has_ou ? ou.len : 0, 3, k_ou, pr, v).empty())
+    return fail(FTZ_ERR_OWNER, "cannot deserialize the OU of the identity");
+  static const PbKind k_role[2] = {PK_STRING, PK_ENUM};
+  if (!pb_simple(has_role ? role.p : nullptr, has_role ? role.len : 0, 2, k_role, pr, v).empty())
+    return fail(FTZ_ERR_OWNER, "cannot deserialize the role of the identity");
+  // ---- Verifier.Verify: the NymSignature proto
+  if (sig_len == 0) return fail(FTZ_ERR_SIGNATURE, "invalid signature, it must not be empty");
+  static const PbKind k_sig[4] = {PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES};
+  std::string pe = pb_simple(sig, sig_len, 4, k_sig, pr, v);
+  if (!pe.empty()) {
+    out.code = FTZ_ERR_SIGNATURE;
+    out.why = "error unmarshalling signature: " + pe;
+    return;
+  }
+  for (int q = 0; q < 4; q++) {
+    if (!pr[q] || v[q].len < 32) return fail(FTZ_ERR_SIGNATURE, "failure [index out of range]");
+    memcpy(out.ints[2 + q], v[q].p, 32);
+  }
+}
+
+size_t nym_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
+                  const uint8_t hash_slot[32], uint8_t* blob) {
+  constexpr size_t SC_BYTES = 192, PRE_BYTES = 176;
+  size_t off = (m * sizeof(fts::NymJob) + 15) & ~(size_t)15;
+  std::map<std::pair<const uint8_t*, size_t>, size_t> msg_at;
+  size_t jobs_end = off + m * (SC_BYTES + PRE_BYTES);
+  size_t moff = jobs_end;
+  for (size_t k = 0; k < m; k++) {
+    const ftz_owner_sig& q = s[idx[k]];
+    auto key = std::make_pair(q.msg, q.msg_len);
+    auto it = msg_at.find(key);
+    if (it == msg_at.end()) {
+      moff = ((moff + 15) & ~(size_t)15) + 6;
+      it = msg_at.emplace(key, moff).first;
+      if (blob && q.msg_len) memcpy(blob + moff, q.msg, q.msg_len);
+      moff += q.msg_len;
+    }
+    if (blob) {
+      fts::NymJob j;
+      j.sc = (uint32_t)(off + k * (SC_BYTES + PRE_BYTES));
+      j.pre = (uint32_t)(j.sc + SC_BYTES);
+      j.msg = (uint32_t)it->second;
+      j.msg_len = (uint32_t)q.msg_len;
+      memcpy(blob + k * sizeof(fts::NymJob), &j, sizeof j);
+      memcpy(blob + j.sc, dec[idx[k]].ints, SC_BYTES);
+      uint8_t* pre = blob + j.pre;
+      memset(pre, 0, PRE_BYTES);
+      memcpy(pre, "sign", 4);
+      memcpy(pre + 134, hash_slot, 32);
+    }
+  }
+  return moff + 64;  // + slack: the hash reads whole 16-byte words
+}
+
+}  // namespace ftsh

@@ -1,0 +1,63 @@
+// Host side of idemix owner-signature verification: the
+// wire formats around IBM/idemix NymSignature.Ver, decoded as the reference's
+// Go libraries decode them (paths relative to /root/reference/token/core/):
+//   * RawOwner (identity/owner.go:23-37): Go encoding/asn1 of
+//     struct{Type string; Identity []byte}; interop/htlc/deserializer.go:31-43
+//     dispatches on Type ("si" idemix, "htlc" script -> left to Go);
+//   * msp.SerializedIdentity{Mspid, IdBytes} and msp.SerializedIdemixIdentity
+//     {NymX, NymY, Ou, Role, Proof}, msp.OrganizationUnit, msp.MSPRole
+//     (identity/msp/idemix/common.go:40-117, Deserialize with checkValidity=false);
+//   * idemix NymSignature{ProofC, ProofSSk, ProofSRNym, Nonce} and
+//     IssuerPublicKey{..., HSk, HRand, ..., Hash} protos (IBM/idemix, [EXT]).
+// Protobuf: google.golang.org/protobuf v1.27.1 proto3 rules (go.mod:10,226).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../../include/ftsamd.h"
+
+namespace ftsh {
+
+// One protobuf field as scanned: wire type 0 (value in v) or 2 (bytes p/len).
+struct PbField {
+  uint32_t num;
+  uint8_t wt;
+  uint64_t v;
+  const uint8_t* p;
+  size_t len;
+};
+// Scan a message: every field in order (other wire types are validated and
+// skipped, groups included).  "" or the decoding error.
+std::string pb_scan(const uint8_t* b, size_t n, std::vector<PbField>& out);
+// Go utf8.Valid
+bool utf8_valid(const uint8_t* p, size_t n);
+
+struct IdemixIpk {
+  std::vector<uint8_t> hsk_x, hsk_y, hrand_x, hrand_y;  // ECP coordinates (FromBytes: first 32 bytes)
+  std::vector<uint8_t> hash;                            // IssuerPublicKey.Hash
+};
+// proto IssuerPublicKey: "" or the error
+std::string parse_ipk(const uint8_t* p, size_t n, IdemixIpk& out);
+
+// Result of decoding one (owner, signature) pair on the host.
+struct NymDecoded {
+  int code = 0;           // 0 = go to the device; else FTZ_ERR_OWNER / _SIGNATURE / _UNSUPPORTED
+  std::string why;        // the reference's error text when code != 0
+  uint8_t ints[6][32];    // NymX, NymY, ProofC, ProofSSk, ProofSRNym, Nonce (first 32 bytes each)
+};
+// TransferSignatureValidate's per-input path up to the curve arithmetic:
+// GetOwnerVerifier(owner) then the signature unmarshal of Verify(msg, sigma).
+void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_t* sig, size_t sig_len,
+                            NymDecoded& out);
+
+// Blob of one device pass over the signatures s[idx[0..m)] (all decoded with
+// code 0): the NymJob array at offset 0, then per job the six integers
+// (dev/idemix.h NymJob.sc) and the 176-byte transcript prefix ("sign", zeros
+// for t and Nym, hash_slot at 134), then every distinct message (same pointer
+// and length) once at an offset = 6 mod 16.  blob == nullptr: size only.
+size_t nym_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
+                  const uint8_t hash_slot[32], uint8_t* blob);
+
+}  // namespace ftsh

@@ -5,6 +5,7 @@
 
 #include "dev/jobs.h"
 #include "dev/msm.h"
+#include "dev/idemix.h"
 
 using namespace fts;
 
@@ -96,3 +97,6 @@ __global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JD
                              G1Dev* res, uint8_t* bytes);
 __global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const G1Dev* gtab, G1JDev* jtmp,
                                 uint32_t (*zs)[8], G1Dev* pts);
+
+// idemix owner signatures (k_idemix.hip)
+__global__ void k_nym(const NymJob* jobs, uint32_t n, uint8_t* blob, const QDev* tab, uint8_t* ok);

@@ -22,7 +22,7 @@ from . import _abi
 from ._abi import (FTZ_ERR_MALFORMED, FTZ_ERR_MEMBERSHIP, FTZ_ERR_OPENING, FTZ_ERR_PANIC,  # noqa: F401
                    FTZ_ERR_PARSE, FTZ_ERR_RANGE, FTZ_ERR_WF, FTZ_OK, KERNEL_NAMES, MESSAGES)
 
-__all__ = ["Context", "Batch", "Msm", "Prover", "ZKError", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
+__all__ = ["Context", "Batch", "Msm", "Prover", "ZKError", "Idemix", "OwnerVerifier", "TransferVerifier", "IssueVerifier", "transfer_zkproof_validate",
            "FTZ_OK", "MESSAGES"]
 
 
@@ -454,3 +454,53 @@ def transfer_zkproof_validate(ctx, input_commitments, output_commitments, proof)
     inputs are the commitments of the ledger tokens, not the action's own
     InputCommitments."""
     TransferVerifier(input_commitments, output_commitments, ctx).verify(proof)
+
+
+class Idemix:
+    """Idemix owner-signature verification on FP256BN: the
+    deserializer built from PublicParams.IdemixIssuerPK / IdemixCurveID
+    (zkatdlog/nogh/deserializer.go:45-61, identity/msp/idemix/deserializer.go:33-75)
+    with its Verify path on the GPU."""
+
+    def __init__(self, ctx, ipk, curve_id=_abi.FTZ_CURVE_FP256BN_AMCL):
+        self.ctx = ctx
+        self._lib = ctx._lib
+        h = ctypes.c_void_p()
+        _check(self._lib.ftz_idemix_create(ctx._h, bytes(ipk), len(ipk), curve_id, ctypes.byref(h)), self._lib)
+        self._h = h
+
+    def verify_owner_signatures(self, items):
+        """items: (owner, msg, sig) -> FTZ codes (0 = the signature verifies)"""
+        arr, keep = _abi.pack_owner_sigs(items)
+        codes = (ctypes.c_int32 * max(len(items), 1))()
+        _check(self._lib.ftz_verify_owner_signatures(self._h, len(items), arr, codes), self._lib)
+        return list(codes[:len(items)])
+
+    def owner_verifier(self, owner):
+        """GetOwnerVerifier(tok.Owner) (validator_transfer.go:66)"""
+        return OwnerVerifier(self, owner)
+
+    def close(self):
+        if self._h:
+            self._lib.ftz_idemix_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class OwnerVerifier:
+    """driver.Verifier of an owner identity (identity/msp/idemix/deserializer.go:155-167)."""
+
+    def __init__(self, ix, owner):
+        self.ix = ix
+        self.owner = bytes(owner)
+
+    def verify(self, message, sigma):
+        """Verifier.Verify(message, sigma): raises ZKError on a reject."""
+        code = self.ix.verify_owner_signatures([(self.owner, bytes(message), bytes(sigma))])[0]
+        if code != FTZ_OK:
+            raise ZKError(code)

@@ -32,7 +32,36 @@ MESSAGES = {
     FTZ_ERR_MEMBERSHIP: "invalid membership proof",
     FTZ_ERR_PANIC: "proof would make the reference verifier panic",
     FTZ_ERR_OPENING: "does not match the provided opening",
+    8: "input to spend does not exists",
+    9: "failed deserializing owner",
+    10: "pseudonym signature invalid: zero-knowledge proof is invalid",
+    11: "owner type verified in Go (htlc script)",
 }
+FTZ_ERR_OWNER = 9
+FTZ_ERR_SIGNATURE = 10
+FTZ_ERR_UNSUPPORTED = 11
+FTZ_CURVE_FP256BN_AMCL = 0
+
+
+class OwnerSig(ctypes.Structure):
+    _fields_ = [("owner", ctypes.c_void_p), ("owner_len", ctypes.c_size_t), ("msg", ctypes.c_void_p),
+                ("msg_len", ctypes.c_size_t), ("sig", ctypes.c_void_p), ("sig_len", ctypes.c_size_t)]
+
+
+def pack_owner_sigs(items):
+    """items: (owner, msg, sig) byte strings; identical msg objects share one buffer."""
+    arr = (OwnerSig * max(len(items), 1))()
+    keep = []
+    bufs = {}
+    for i, (o, m, s_) in enumerate(items):
+        def buf(b):
+            k = id(b)
+            if k not in bufs:
+                bufs[k] = ctypes.create_string_buffer(bytes(b), max(len(b), 1))
+                keep.append((b, bufs[k]))
+            return ctypes.cast(bufs[k], ctypes.c_void_p)
+        arr[i] = OwnerSig(buf(o), len(o), buf(m), len(m), buf(s_), len(s_))
+    return arr, keep
 
 
 FTZ_FEXP_EXACT = 0
@@ -191,6 +220,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_token_request_decode", "ftz_verify_token_requests",
+           "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_destroy",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
@@ -246,6 +276,10 @@ def load():
     lib.ftz_msm_destroy.argtypes = [vp]
     lib.ftz_msm_destroy.restype = None
     lib.ftz_g1_sum.argtypes = [vp, sz, ctypes.c_char_p, u8p]
+    lib.ftz_idemix_create.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
+    lib.ftz_verify_owner_signatures.argtypes = [vp, sz, ctypes.POINTER(OwnerSig), ctypes.POINTER(ctypes.c_int32)]
+    lib.ftz_idemix_destroy.argtypes = [vp]
+    lib.ftz_idemix_destroy.restype = None
     lib.ftz_token_request_decode.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(Bytes), sz]
     lib.ftz_verify_token_requests.argtypes = [vp, sz, ctypes.POINTER(Bytes), GET_STATE_FN, vp,
                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]

@@ -230,6 +230,37 @@ typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, con
 int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
                               int32_t* codes, int32_t* failed_action);
 
+/* ---- idemix owner signatures, FP256BN_AMCL.
+ * Replaces, per input token of a transfer, what TransferSignatureValidate
+ * (crypto/validator/validator_transfer.go:42-82) runs after loading the token:
+ * ctx.Deserializer.GetOwnerVerifier(tok.Owner) (nogh/deserializer.go:64-66 ->
+ * interop/htlc/deserializer.go:31-43 -> identity/owner.go:62-68 ->
+ * identity/msp/idemix/deserializer.go:83-95, common.go:40-117) and
+ * verifier.Verify(message, sigma) (common/backend.go:32-41 ->
+ * identity/msp/idemix/deserializer.go:155-167 -> IBM/idemix NymSignature.Ver):
+ * owner = the token's Owner bytes (ASN.1 RawOwner), msg = the signed request
+ * bytes, sig = the NymSignature proto.  ftz_idemix_create takes
+ * PublicParams.IdemixIssuerPK (setup.go:36) -- the IssuerPublicKey proto -- and
+ * IdemixCurveID (only FP256BN_AMCL = 0; the IPK's own proof is checked once by
+ * the Go deserializer, NewDeserializer, and is not re-checked here). */
+#define FTZ_ERR_OWNER 9        /* the owner identity does not deserialize (RawOwner, idemix identity, nym) */
+#define FTZ_ERR_SIGNATURE 10   /* the signature does not unmarshal, or "pseudonym signature invalid"       */
+#define FTZ_ERR_UNSUPPORTED 11 /* owner type verified in Go (an HTLC script owner)                          */
+#define FTZ_CURVE_FP256BN_AMCL 0
+typedef struct ftz_idemix ftz_idemix;
+typedef struct {
+  const uint8_t* owner; /* token.Token.Owner: asn1(RawOwner{Type, Identity})                  */
+  size_t owner_len;
+  const uint8_t* msg;   /* the signed message (request bytes || anchor)                        */
+  size_t msg_len;
+  const uint8_t* sig;   /* proto(NymSignature)                                                 */
+  size_t sig_len;
+} ftz_owner_sig;
+int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curve_id, ftz_idemix** out);
+/* codes[i] = FTZ_OK, FTZ_ERR_OWNER, FTZ_ERR_SIGNATURE or FTZ_ERR_UNSUPPORTED; thread-safe */
+int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_owner_sig* s, int32_t* codes);
+void ftz_idemix_destroy(ftz_idemix* ix);
+
 /* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE configs[2]):
  * out = sum_i k_i P_i as 64-byte gnark RawBytes.  Points: n x 64-byte
  * uncompressed RawBytes (must be canonical and on the curve); scalars: n x 32

@@ -1,0 +1,493 @@
+"""TEST INFRASTRUCTURE ONLY -- oracle restatement of idemix owner-signature
+verification; nothing in the product imports it.
+
+The reference path (paths relative to /root/reference/token/core/):
+* zkatdlog/crypto/validator/validator_transfer.go:42-82 TransferSignatureValidate:
+  for every input token, ctx.Deserializer.GetOwnerVerifier(tok.Owner) and
+  ctx.SignatureProvider.HasBeenSignedBy(tok.Owner, verifier), i.e.
+  verifier.Verify(message, sigma) (common/backend.go:32-41);
+* zkatdlog/nogh/deserializer.go:45-66: the owner deserializer is
+  htlc.NewDeserializer(identity.NewRawOwnerIdentityDeserializer(idemixDes));
+  interop/htlc/deserializer.go:31-43 dispatches on RawOwner.Type ("si" ->
+  identity/owner.go:62-68 -> idemix, "htlc" -> an HTLC script, anything else an
+  error); RawOwner is Go encoding/asn1 of struct{Type string; Identity []byte}
+  (identity/owner.go:23-37);
+* identity/msp/idemix/deserializer.go:83-95 DeserializeVerifier ->
+  common.go:36-117 Deserialize(raw, checkValidity=false): proto
+  msp.SerializedIdentity, then msp.SerializedIdemixIdentity (NymX, NymY must be
+  non-nil), the nym public key imported from NymX||NymY, OU and Role protos;
+* deserializer.go:155-167 Verifier.Verify -> CSP.Verify(NymPK, sigma, msg,
+  IdemixNymSignerOpts{IssuerPK}) -> IBM/idemix NymSignature.Ver.
+
+[EXT] IBM/idemix v0.0.0-20220113150823-80dd4cb2d74e, IBM/mathlib
+v0.0.0-20220112091634-0a7378db6912 (go.mod:6-7) and hyperledger/fabric-amcl
+(go.mod:101) are not vendored; what follows restates their published
+algorithms:
+* NymSignature.Ver: t = HSk^ProofSSk * HRand^ProofSRNym * Nym^-ProofC;
+  c = HashToZr("sign" || t || Nym || ipk.Hash || msg) (G1 as 65 bytes
+  0x04||X||Y, ipk.Hash in a 32-byte slot, proofData of length
+  4 + 2*65 + 32 + len(msg)); accept iff ProofC == HashToZr(c || Nonce)
+  (32-byte big-endian each); error text "pseudonym signature invalid:
+  zero-knowledge proof is invalid".
+* Zr from bytes is amcl FromBytes: the first 32 bytes, big-endian, NOT reduced
+  (a shorter slice panics; the bridge recovers and returns an error);
+  Equals compares the raw integers; G1 Mul by an unreduced scalar = (k mod n) P.
+* The nym public key: raw = NymX || NymY, halves at len(raw)/2, each read by
+  FromBytes; amcl NewECPbigs reduces the coordinates mod q and yields the point
+  at infinity when (x, y) is not on the curve; infinity serialises as
+  0x04 || 0^32 || 1 (amcl's (0, 1, 0) representative) [EXT, unpinned].
+* HashToZr = SHA-256 read big-endian, mod n (pinned: the reference's
+  IssuerPublicKey fixture carries Hash = HashToZr(proto without Hash)).
+* Protobuf (golang/protobuf v1.5.2 over google.golang.org/protobuf v1.27.1,
+  go.mod:10,226): proto3 decoding with unknown fields skipped, last value wins,
+  a known field with the wrong wire type handled as unknown, strings validated
+  as UTF-8, present-but-empty bytes non-nil.
+"""
+import hashlib
+
+from . import request as RQ
+
+# FP256BN (x = -0x6882F5C030B0A801; pinned by tests/test_idemix.py against the
+# reference's idemix fixtures)
+Q = 0xFFFFFFFFFFFCF0CD46E5F25EEE71A49F0CDC65FB12980A82D3292DDBAED33013
+N = 0xFFFFFFFFFFFCF0CD46E5F25EEE71A49E0CDC65FB1299921AF62D536CD10B500D
+B = 3
+G = (1, 2)
+FIELD_BYTES = 32
+SIGN_LABEL = b"sign"
+
+OK = 0
+ERR_OWNER = 9        # the owner identity does not deserialize
+ERR_SIGNATURE = 10   # the signature does not unmarshal / pseudonym signature invalid
+ERR_UNSUPPORTED = 11  # owner type handled in Go (HTLC script)
+ERR_PANIC = 6
+
+
+# ------------------------------------------------------------------ G1 (affine)
+def on_curve(P):
+    return P is None or (P[1] * P[1] - P[0] ** 3 - B) % Q == 0
+
+
+def add(P, R):
+    if P is None:
+        return R
+    if R is None:
+        return P
+    if P[0] == R[0]:
+        if (P[1] + R[1]) % Q == 0:
+            return None
+        lam = 3 * P[0] * P[0] * pow(2 * P[1], -1, Q) % Q
+    else:
+        lam = (R[1] - P[1]) * pow(R[0] - P[0], -1, Q) % Q
+    x = (lam * lam - P[0] - R[0]) % Q
+    return (x, (lam * (P[0] - x) - P[1]) % Q)
+
+
+def neg(P):
+    return None if P is None else (P[0], (-P[1]) % Q)
+
+
+def mul(P, k):
+    k %= N
+    acc, cur = None, P
+    while k:
+        if k & 1:
+            acc = add(acc, cur)
+        cur = add(cur, cur)
+        k >>= 1
+    return acc
+
+
+def g1_bytes(P):
+    """amcl ECP.ToBytes(b, false) as mathlib's G1.Bytes calls it: 65 bytes."""
+    if P is None:
+        return b"\x04" + bytes(32) + (1).to_bytes(32, "big")  # [EXT] infinity
+    return b"\x04" + P[0].to_bytes(32, "big") + P[1].to_bytes(32, "big")
+
+
+def hash_to_zr(data):
+    return int.from_bytes(hashlib.sha256(data).digest(), "big") % N
+
+
+# ------------------------------------------------------------------ protobuf
+class PbError(Exception):
+    pass
+
+
+def _varint(b, i):
+    v = 0
+    for k in range(10):
+        if i >= len(b):
+            raise PbError("unexpected EOF")
+        c = b[i]
+        i += 1
+        if k == 9 and c > 1:
+            raise PbError("variable length integer overflow")
+        v |= (c & 0x7F) << (7 * k)
+        if c < 0x80:
+            return v, i
+    raise PbError("variable length integer overflow")
+
+
+def _skip(b, i, num, wt, depth=0):
+    if wt == 0:
+        return _varint(b, i)[1]
+    if wt == 1:
+        if len(b) - i < 8:
+            raise PbError("unexpected EOF")
+        return i + 8
+    if wt == 5:
+        if len(b) - i < 4:
+            raise PbError("unexpected EOF")
+        return i + 4
+    if wt == 2:
+        n, i = _varint(b, i)
+        if n > len(b) - i:
+            raise PbError("unexpected EOF")
+        return i + n
+    if wt == 3:
+        while True:
+            if i >= len(b):
+                raise PbError("unexpected EOF")
+            tag, i = _varint(b, i)
+            n2, w2 = tag >> 3, tag & 7
+            if n2 < 1 or n2 > (1 << 29) - 1:
+                raise PbError("invalid field number")
+            if w2 == 4:
+                if n2 != num:
+                    raise PbError("mismatching end group marker")
+                return i
+            i = _skip(b, i, n2, w2, depth + 1)
+    raise PbError("cannot parse reserved wire type")
+
+
+def _utf8(v):
+    try:
+        v.decode("utf-8", errors="strict")
+    except UnicodeDecodeError:
+        raise PbError("string field contains invalid UTF-8")
+    return v
+
+
+def pb_decode(b, schema):
+    """schema: {num: kind} with kind in 'bytes', 'string', 'enum', ('msg', schema),
+    and a leading '*' for repeated.  Returns {num: value | [values]}."""
+    out = {}
+    i = 0
+    while i < len(b):
+        tag, i = _varint(b, i)
+        num, wt = tag >> 3, tag & 7
+        if num < 1 or num > (1 << 29) - 1:
+            raise PbError("invalid field number")
+        if wt == 4:
+            raise PbError("unexpected end group")
+        kind = schema.get(num)
+        rep = isinstance(kind, str) and kind.startswith("*") or isinstance(kind, tuple) and kind[0] == "*msg"
+        base = kind[1:] if isinstance(kind, str) and kind.startswith("*") else kind
+        want = None if kind is None else (0 if base == "enum" else 2)
+        if kind is None or wt != want:
+            i = _skip(b, i, num, wt)
+            continue
+        if base == "enum":
+            v, i = _varint(b, i)
+            v &= 0xFFFFFFFF
+            val = v - (1 << 32) if v >= 1 << 31 else v
+        else:
+            n, i = _varint(b, i)
+            if n > len(b) - i:
+                raise PbError("unexpected EOF")
+            raw = bytes(b[i:i + n])
+            i += n
+            if base == "bytes":
+                val = raw
+            elif base == "string":
+                val = _utf8(raw)
+            else:  # message
+                sub = base[1]
+                val = pb_decode(raw, sub)
+                if not rep and num in out:  # singular message seen twice: merge
+                    merged = dict(out[num])
+                    for k2, v2 in val.items():
+                        if isinstance(v2, list):
+                            merged[k2] = merged.get(k2, []) + v2
+                        elif isinstance(v2, dict) and isinstance(merged.get(k2), dict):
+                            m2 = dict(merged[k2])
+                            m2.update(v2)
+                            merged[k2] = m2
+                        else:
+                            merged[k2] = v2
+                    val = merged
+        if rep:
+            out.setdefault(num, []).append(val)
+        else:
+            out[num] = val
+    return out
+
+
+def pb_field(num, wt, payload):
+    """encoder for fixtures: one field"""
+    def vi(v):
+        o = bytearray()
+        while True:
+            c = v & 0x7F
+            v >>= 7
+            if v:
+                o.append(c | 0x80)
+            else:
+                o.append(c)
+                return bytes(o)
+    if wt == 0:
+        return vi(num << 3) + vi(payload)
+    return vi((num << 3) | 2) + vi(len(payload)) + payload
+
+
+ECP_S = {1: "bytes", 2: "bytes"}
+ECP2_S = {1: "bytes", 2: "bytes", 3: "bytes", 4: "bytes"}
+IPK_S = {1: "*string", 2: ("msg", ECP_S), 3: ("msg", ECP_S), 4: ("*msg", ECP_S), 5: ("msg", ECP2_S),
+         6: ("msg", ECP_S), 7: ("msg", ECP_S), 8: "bytes", 9: "bytes", 10: "bytes"}
+SERIALIZED_IDENTITY_S = {1: "string", 2: "bytes"}                          # msp.SerializedIdentity
+SERIALIZED_IDEMIX_S = {1: "bytes", 2: "bytes", 3: "bytes", 4: "bytes", 5: "bytes"}  # NymX NymY Ou Role Proof
+OU_S = {1: "string", 2: "string", 3: "bytes"}                                # msp.OrganizationUnit
+ROLE_S = {1: "string", 2: "enum"}                                            # msp.MSPRole
+NYMSIG_S = {1: "bytes", 2: "bytes", 3: "bytes", 4: "bytes"}                 # ProofC ProofSSk ProofSRNym Nonce
+
+
+def from_bytes32(b):
+    """amcl FromBytes: the first 32 bytes big-endian; a shorter slice panics."""
+    if b is None or len(b) < 32:
+        raise IndexError("index out of range")
+    return int.from_bytes(b[:32], "big")
+
+
+def ecp_from_bytes(x, y):
+    """amcl NewECPbigs(FromBytes(x), FromBytes(y)): coordinates mod q, off-curve -> infinity."""
+    P = (from_bytes32(x) % Q, from_bytes32(y) % Q)
+    return P if on_curve(P) else None
+
+
+class IssuerPK:
+    def __init__(self, raw):
+        m = pb_decode(raw, IPK_S)
+        self.raw = raw
+        self.hsk = ecp_from_bytes(m[2].get(1), m[2].get(2))
+        self.hrand = ecp_from_bytes(m[3].get(1), m[3].get(2))
+        self.hattrs = [ecp_from_bytes(e.get(1), e.get(2)) for e in m.get(4, [])]
+        self.bar_g1 = ecp_from_bytes(m[6].get(1), m[6].get(2))
+        self.bar_g2 = ecp_from_bytes(m[7].get(1), m[7].get(2))
+        self.hash = m.get(10, b"")
+        self.fields = m
+
+
+# ------------------------------------------------------------------ ASN.1 RawOwner
+def _printable(c, amp_star=True):
+    return (ord("a") <= c <= ord("z") or ord("A") <= c <= ord("Z") or ord("0") <= c <= ord("9")
+            or c in b" '()+,-./:=?" or (amp_star and c in b"*&"))
+
+
+def _asn1_string(tag, body):
+    """Go 1.18 encoding/asn1 parseField for a string-typed field."""
+    if tag == 0x13:  # PrintableString
+        if not all(_printable(c) for c in body):
+            raise RQ.Asn1Error("PrintableString contains invalid character")
+        return body.decode("latin-1")
+    if tag == 0x16:  # IA5String
+        if any(c >= 0x80 for c in body):
+            raise RQ.Asn1Error("IA5String contains invalid character")
+        return body.decode("latin-1")
+    if tag in (0x14, 0x1B):  # T61String, GeneralString: bytes as-is
+        return body.decode("latin-1")
+    if tag == 0x0C:  # UTF8String
+        try:
+            return body.decode("utf-8", errors="strict")
+        except UnicodeDecodeError:
+            raise RQ.Asn1Error("invalid UTF-8 string")
+    if tag == 0x12:  # NumericString
+        if not all(ord("0") <= c <= ord("9") or c == 0x20 for c in body):
+            raise RQ.Asn1Error("NumericString contains invalid character")
+        return body.decode("latin-1")
+    if tag == 0x1E:  # BMPString
+        if len(body) % 2:
+            raise RQ.Asn1Error("odd-length BMP string")
+        if len(body) >= 2 and body[-1] == 0 and body[-2] == 0:
+            body = body[:-2]
+        return body.decode("utf-16-be", errors="replace")
+    raise RQ.Asn1Error("tags don't match")
+
+
+def _asn1_len(b, off):
+    if off >= len(b):
+        raise RQ.Asn1Error("truncated tag or length")
+    c = b[off]
+    off += 1
+    if c & 0x80 == 0:
+        n = c
+    else:
+        nb = c & 0x7F
+        if nb == 0:
+            raise RQ.Asn1Error("indefinite length found (not DER)")
+        n = 0
+        for _ in range(nb):
+            if off >= len(b):
+                raise RQ.Asn1Error("truncated tag or length")
+            if n >= 1 << 23:
+                raise RQ.Asn1Error("length too large")
+            n = (n << 8) | b[off]
+            off += 1
+            if n == 0:
+                raise RQ.Asn1Error("superfluous leading zeros in length")
+        if n < 0x80:
+            raise RQ.Asn1Error("non-minimal length")
+    if n > len(b) - off:
+        raise RQ.Asn1Error("data truncated")
+    return n, off
+
+
+def _asn1_tag(b, off):
+    if off >= len(b):
+        raise RQ.Asn1Error("sequence truncated")
+    t = b[off]
+    if t & 0x1F == 0x1F:  # high-tag-number form: no universal string / octet tag fits
+        raise RQ.Asn1Error("tags don't match")
+    return t, off + 1
+
+
+def raw_owner_decode(raw):
+    """identity.UnmarshallRawOwner (identity/owner.go:30-37): (Type, Identity)."""
+    t, off = _asn1_tag(raw, 0)
+    if t != 0x30:
+        raise RQ.Asn1Error("tags don't match")
+    n, off = _asn1_len(raw, off)
+    body = raw[off:off + n]
+    k = 0
+    t, k = _asn1_tag(body, k)
+    n1, k = _asn1_len(body, k)
+    typ = _asn1_string(t, body[k:k + n1])
+    k += n1
+    t, k = _asn1_tag(body, k)
+    if t != 0x04:
+        raise RQ.Asn1Error("tags don't match")
+    n2, k = _asn1_len(body, k)
+    ident = bytes(body[k:k + n2])
+    return typ, ident
+
+
+def _der(tag, body):
+    n = len(body)
+    if n < 0x80:
+        ln = bytes([n])
+    else:
+        nb = (n.bit_length() + 7) // 8
+        ln = bytes([0x80 | nb]) + n.to_bytes(nb, "big")
+    return bytes([tag]) + ln + body
+
+
+def raw_owner_encode(typ, ident, string_tag=0x13):
+    """asn1.Marshal(RawOwner{...}) (PrintableString for printable Type)."""
+    return _der(0x30, _der(string_tag, typ) + _der(0x04, ident))
+
+
+# ------------------------------------------------------------------ idemix
+def make_nym(ipk, sk, r_nym):
+    """Nym = HSk^sk * HRand^RNym (IBM/idemix MakeNym)"""
+    return add(mul(ipk.hsk, sk), mul(ipk.hrand, r_nym))
+
+
+def _proof_data(t, nym, ipk_hash, msg):
+    d = bytearray(len(SIGN_LABEL) + 2 * (2 * FIELD_BYTES + 1) + FIELD_BYTES + len(msg))
+    idx = 0
+    d[idx:idx + 4] = SIGN_LABEL
+    idx += 4
+    d[idx:idx + 65] = g1_bytes(t)
+    idx += 65
+    d[idx:idx + 65] = g1_bytes(nym)
+    idx += 65
+    h = ipk_hash[:len(d) - idx]
+    d[idx:idx + len(h)] = h  # copy(proofData[index:], ipk.Hash)
+    idx += FIELD_BYTES
+    d[idx:] = msg
+    return bytes(d)
+
+
+def nym_sign(ipk, sk, r_nym, nym, msg, r_sk, r_rnym, nonce):
+    """IBM/idemix NewNymSignature with injected randomness (r_sk, r_rnym, nonce):
+    the NymSignature proto bytes."""
+    t = add(mul(ipk.hsk, r_sk), mul(ipk.hrand, r_rnym))
+    c = hash_to_zr(_proof_data(t, nym, ipk.hash, msg))
+    proof_c = hash_to_zr(c.to_bytes(32, "big") + nonce.to_bytes(32, "big"))
+    s_sk = (r_sk + proof_c * sk) % N
+    s_rnym = (r_rnym + proof_c * r_nym) % N
+    return b"".join(pb_field(k + 1, 2, v.to_bytes(32, "big")) for k, v in enumerate((proof_c, s_sk, s_rnym, nonce)))
+
+
+def nym_verify(ipk, nym, sig, msg):
+    """IBM/idemix NymSignature.Ver behind the bridge's recover: (code, text)."""
+    if len(sig) == 0:
+        return ERR_SIGNATURE, "invalid signature, it must not be empty"
+    try:
+        m = pb_decode(sig, NYMSIG_S)
+    except PbError as e:
+        return ERR_SIGNATURE, "error unmarshalling signature: %s" % e
+    try:
+        proof_c, s_sk, s_rnym, nonce = (from_bytes32(m.get(k)) for k in (1, 2, 3, 4))
+    except IndexError as e:
+        return ERR_SIGNATURE, "failure [%s]" % e
+    t = add(add(mul(ipk.hsk, s_sk), mul(ipk.hrand, s_rnym)), neg(mul(nym, proof_c)))
+    c = hash_to_zr(_proof_data(t, nym, ipk.hash, msg))
+    if proof_c != hash_to_zr(c.to_bytes(32, "big") + nonce.to_bytes(32, "big")):
+        return ERR_SIGNATURE, "pseudonym signature invalid: zero-knowledge proof is invalid"
+    return OK, ""
+
+
+def deserialize_idemix_identity(raw):
+    """common.go:40-117 Deserialize(raw, false): the nym point, or (code, text)."""
+    try:
+        si = pb_decode(raw, SERIALIZED_IDENTITY_S)
+    except PbError:
+        return None, (ERR_OWNER, "failed to unmarshal to msp.SerializedIdentity{}")
+    try:
+        ser = pb_decode(si.get(2, b""), SERIALIZED_IDEMIX_S)
+    except PbError:
+        return None, (ERR_OWNER, "could not deserialize a SerializedIdemixIdentity")
+    if ser.get(1) is None or ser.get(2) is None:
+        return None, (ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid")
+    raw_nym = ser[1] + ser[2]
+    half = len(raw_nym) // 2
+    try:
+        nym = ecp_from_bytes(raw_nym[:half], raw_nym[half:])
+    except IndexError:
+        return None, (ERR_OWNER, "failed to import nym public key")
+    try:
+        pb_decode(ser.get(3, b""), OU_S)
+    except PbError:
+        return None, (ERR_OWNER, "cannot deserialize the OU of the identity")
+    try:
+        pb_decode(ser.get(4, b""), ROLE_S)
+    except PbError:
+        return None, (ERR_OWNER, "cannot deserialize the role of the identity")
+    return nym, None
+
+
+def owner_verify(ipk, owner, msg, sig):
+    """One input of TransferSignatureValidate: GetOwnerVerifier(tok.Owner) then
+    verifier.Verify(msg, sigma).  (code, text)."""
+    try:
+        typ, ident = raw_owner_decode(owner)
+    except RQ.Asn1Error:
+        return ERR_OWNER, "failed to unmarshal RawOwner"
+    if typ == "htlc":
+        return ERR_UNSUPPORTED, "htlc script owner: verified in Go"
+    if typ != "si":
+        return ERR_OWNER, "failed to deserialize RawOwner: Unknown owner type %s" % typ
+    nym, err = deserialize_idemix_identity(ident)
+    if err:
+        return err
+    return nym_verify(ipk, nym, sig, msg)
+
+
+def serialize_idemix_identity(nym, mspid="idemix", ou=b"", role=b"", proof=b"", nymx=None, nymy=None):
+    """msp.SerializedIdentity{Mspid, IdBytes: SerializedIdemixIdentity{NymX, NymY, Ou, Role, Proof}}
+    (identity/msp/idemix/id.go Serialize) for fixtures."""
+    x = nym[0].to_bytes(32, "big") if nymx is None else nymx
+    y = nym[1].to_bytes(32, "big") if nymy is None else nymy
+    inner = pb_field(1, 2, x) + pb_field(2, 2, y) + pb_field(3, 2, ou) + pb_field(4, 2, role) + pb_field(5, 2, proof)
+    return pb_field(1, 2, mspid.encode()) + pb_field(2, 2, inner)

@@ -28,7 +28,9 @@ def build_emu():
             os.path.join(ROOT, "tests", "native", "sx_emu.cpp"), os.path.join(ROOT, "tests", "native", "msm_emu.cpp"),
             os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "planner.cpp"), os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "planner_prove.cpp"),
             os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "gojson.cpp"),
-            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "request.cpp")]
+            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "request.cpp"),
+            os.path.join(ROOT, "tests", "native", "idemix_emu.cpp"),
+            os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host", "idemix.cpp")]
     deps = srcs + [os.path.join(d, f) for d in (os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "dev"),
                                               os.path.join(ROOT, "fabric-token-sdk_amd", "csrc", "host"))
                    for f in os.listdir(d) if f.endswith(".h")]
