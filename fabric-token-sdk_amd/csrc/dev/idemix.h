@@ -26,12 +26,17 @@ struct QDev {
 };
 
 struct NymJob {
-  uint32_t sc;       // blob offset (16-aligned): NymX, NymY, ProofC, ProofSSk, ProofSRNym, Nonce (32 bytes BE each)
+  uint32_t sc;       // blob offset (16-aligned) of NYM_SC_BYTES: NymX, NymY, ProofC, ProofSSk, ProofSRNym, Nonce
+                     // (32 bytes BE each), then the GLV split of ProofC (12 u32, host/idemix.h nym_glv_split)
   uint32_t pre;      // blob offset (16-aligned) of the transcript prefix: "sign" | t (65) | Nym (65) | hash (32)
   uint32_t msg;      // blob offset of the message, = 6 mod 16 so that stream byte 192 is 16-aligned
   uint32_t msg_len;
 };
 static constexpr uint32_t NYM_PRE = 4 + 65 + 65 + 32;  // 166
+static constexpr uint32_t NYM_SC_BYTES = 240;
+struct QJDev {
+  uint32_t x[8], y[8], z[8];
+};
 
 FTS_HD q1a q1_load(const QDev& d) {
   q1a a;
@@ -82,26 +87,66 @@ FTS_HD q1j q1_fixed_mul(const QDev* tab, const uint32_t k[8]) {
   return acc;
 }
 
-// one signature: 1 = accept, 0 = "pseudonym signature invalid".  The prefix
-// slot at blob + j.pre receives t and Nym (device-computed bytes).
-FTS_HD uint8_t job_nym(const NymJob& j, uint8_t* blob, const QDev* tab) {
-  uint32_t v[6][8];
-#pragma unroll
-  for (int q = 0; q < 6; q++) be32_to_limbs_g(v[q], blob + j.sc + 32 * q);
-  // the nym: NewECPbigs(x, y) -- coordinates mod q, off-curve -> infinity
+// NewECPbigs(x, y) of the nym: coordinates mod q, off-curve -> infinity
+FTS_HD q1a nym_load(const uint8_t* sc) {
+  uint32_t x[8], y[8];
+  be32_to_limbs_g(x, sc);
+  be32_to_limbs_g(y, sc + 32);
   q1a nym;
-  nym.x = fq_from_int(v[0]);
-  nym.y = fq_from_int(v[1]);
+  nym.x = fq_from_int(x);
+  nym.y = fq_from_int(y);
   nym.inf = false;
   if (!q1_on_curve(nym)) nym.inf = true;
-  // t = s_sk HSk + s_rnym HRand - c Nym
-  q1j acc = q1_fixed_mul(tab, v[3]);
-  acc = jac_add(acc, q1_fixed_mul(tab + NYM_TAB_PER_BASE, v[4]));
-  acc = jac_add(acc, aff_mul(aff_neg(nym), v[2]));
-  q1a t = jac_to_aff(acc);
+  return nym;
+}
+
+// Part `part` (0..3) of t = s_sk HSk + s_rnym HRand - c Nym, four lanes per
+// signature: with -c = k1 + k2 lambda (GLV, split on the host) part 0 computes
+// k1 (-Nym) and part 1 k2 phi(-Nym) (129-bit double-and-add with mixed
+// additions), part 2 s_sk HSk and part 3 s_rnym HRand (32 fixed-base table
+// additions each).
+FTS_HD q1j job_nym_part(const NymJob& j, const uint8_t* blob, const QDev* tab, uint32_t part) {
+  const uint8_t* sc = blob + j.sc;
+  if (part >= 2) {
+    uint32_t s[8];
+    be32_to_limbs_g(s, sc + (part == 3 ? 128 : 96));
+    return q1_fixed_mul(tab + (part - 2) * NYM_TAB_PER_BASE, s);
+  }
+  q1a P = aff_neg(nym_load(sc));
+  const uint32_t* glv = reinterpret_cast<const uint32_t*>(sc + 192);
+  uint32_t k[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) k[i] = glv[5 * part + i];
+  if (part) P.x = P.x * fq_const(Q_GLV_BETA);
+  if ((glv[10] >> part) & 1) P = aff_neg(P);
+  q1j acc = jac_inf<fq>();
+  if (P.inf) return acc;
+  // bits 128..0, consumed from the top by shifting (a dynamically indexed limb
+  // array would live in scratch memory)
+  uint32_t u0 = k[0], u1 = k[1], u2 = k[2], u3 = k[3], u4 = k[4];
+#pragma nounroll
+  for (int i = 128; i >= 0; i--) {
+    acc = jac_dbl(acc);
+    uint32_t bit = u4 & 1;
+    u4 = u3 >> 31;
+    u3 = (u3 << 1) | (u2 >> 31);
+    u2 = (u2 << 1) | (u1 >> 31);
+    u1 = (u1 << 1) | (u0 >> 31);
+    u0 <<= 1;
+    if (bit) acc = jac_add_aff(acc, P);
+  }
+  return acc;
+}
+
+// The rest of NymSignature.Ver for one signature given t in Jacobian form:
+// 1 = accept, 0 = "pseudonym signature invalid".  The prefix slot at
+// blob + j.pre receives t and Nym (device-computed bytes).
+FTS_HD uint8_t job_nym_fin(const NymJob& j, uint8_t* blob, const q1j& tj) {
+  const uint8_t* sc = blob + j.sc;
+  q1a t = jac_to_aff(tj);
   uint8_t* pre = blob + j.pre;
   q1_bytes65(pre + 4, t);
-  q1_bytes65(pre + 69, nym);
+  q1_bytes65(pre + 69, nym_load(sc));
   Sha256 s;
   s.init();
   s.update(pre, NYM_PRE);
@@ -110,20 +155,41 @@ FTS_HD uint8_t job_nym(const NymJob& j, uint8_t* blob, const QDev* tab) {
   s.update(blob + j.msg + head, j.msg_len - head);
   uint8_t d[32];
   s.final(d);
-  uint32_t c[8];
+  uint32_t c[8], v[8];
   digest_mod_n(c, d);
   // ProofC == HashToZr(c || Nonce), Nonce as its raw 32 bytes
   uint8_t cb[64];
   limbs_to_be32(cb, c);
-  limbs_to_be32(cb + 32, v[5]);
+  be32_to_limbs_g(v, sc + 160);
+  limbs_to_be32(cb + 32, v);
   s.init();
   s.update(cb, 64);
   s.final(d);
   digest_mod_n(c, d);
+  be32_to_limbs_g(v, sc + 64);
   uint32_t o = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) o |= c[i] ^ v[2][i];
+  for (int i = 0; i < 8; i++) o |= c[i] ^ v[i];
   return o == 0 ? 1 : 0;
+}
+
+FTS_HD void qj_store(QJDev& d, const q1j& p) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    d.x[i] = p.x.v[i];
+    d.y[i] = p.y.v[i];
+    d.z[i] = p.z.v[i];
+  }
+}
+FTS_HD q1j qj_load(const QJDev& d) {
+  q1j p;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    p.x.v[i] = d.x[i];
+    p.y.v[i] = d.y[i];
+    p.z.v[i] = d.z[i];
+  }
+  return p;
 }
 
 // Host: the fixed-base tables of HSk and HRand (tab[b * NYM_TAB_PER_BASE +

@@ -393,40 +393,132 @@ void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_
     if (!pr[q] || v[q].len < 32) return fail(FTZ_ERR_SIGNATURE, "failure [index out of range]");
     memcpy(out.ints[2 + q], v[q].p, 32);
   }
+  nym_glv_split(out.ints[2], out.glv);
 }
 
-size_t nym_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
-                  const uint8_t hash_slot[32], uint8_t* blob) {
-  constexpr size_t SC_BYTES = 192, PRE_BYTES = 176;
-  size_t off = (m * sizeof(fts::NymJob) + 15) & ~(size_t)15;
-  std::map<std::pair<const uint8_t*, size_t>, size_t> msg_at;
-  size_t jobs_end = off + m * (SC_BYTES + PRE_BYTES);
-  size_t moff = jobs_end;
+namespace {
+// little-endian 32-bit limb arithmetic for the host GLV split
+void mp_mul(const uint32_t* a, int na, const uint32_t* b, int nb, uint32_t* r) {
+  for (int i = 0; i < na + nb; i++) r[i] = 0;
+  for (int i = 0; i < na; i++) {
+    uint64_t c = 0;
+    for (int j = 0; j < nb; j++) {
+      uint64_t t = (uint64_t)a[i] * b[j] + r[i + j] + c;
+      r[i + j] = (uint32_t)t;
+      c = t >> 32;
+    }
+    r[i + nb] = (uint32_t)c;
+  }
+}
+int mp_cmp(const uint32_t* a, const uint32_t* b, int n) {
+  for (int i = n - 1; i >= 0; i--)
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return 0;
+}
+void mp_sub(uint32_t* r, const uint32_t* a, const uint32_t* b, int n) {
+  uint64_t br = 0;
+  for (int i = 0; i < n; i++) {
+    uint64_t t = (uint64_t)a[i] - b[i] - br;
+    r[i] = (uint32_t)t;
+    br = (t >> 63) & 1;
+  }
+}
+void mp_add(uint32_t* r, const uint32_t* a, const uint32_t* b, int n) {
+  uint64_t c = 0;
+  for (int i = 0; i < n; i++) {
+    uint64_t t = (uint64_t)a[i] + b[i] + c;
+    r[i] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+// |x - y| and the sign of x - y (n limbs)
+bool mp_signed_diff(uint32_t* r, const uint32_t* x, const uint32_t* y, int n) {
+  if (mp_cmp(x, y, n) >= 0) {
+    mp_sub(r, x, y, n);
+    return false;
+  }
+  mp_sub(r, y, x, n);
+  return true;
+}
+}  // namespace
+
+void nym_glv_split(const uint8_t kb[32], uint32_t out[12]) {
+  uint32_t k[12] = {0}, t[24];
+  fts::be32_to_limbs(k, kb);
+  if (mp_cmp(k, fts::N_MOD, 8) >= 0) mp_sub(k, k, fts::N_MOD, 8);  // k < 2^256 < 2n
+  uint32_t c1[12] = {0}, c2[12] = {0};
+  mp_mul(k, 8, fts::Q_GLV_G1, 8, t);
+  for (int i = 0; i < 8; i++) c1[i] = t[8 + i];
+  mp_mul(k, 8, fts::Q_GLV_G2, 8, t);
+  for (int i = 0; i < 8; i++) c2[i] = t[8 + i];
+  // k1 = k - c1 a1 - c2 a2, k2 = c1 |b1| - c2 b2 (c_i < 2^130, basis entries < 2^129)
+  uint32_t x[12], y[12], z[12], k1[12], k2[12];
+  mp_mul(c1, 6, fts::Q_GLV_A1, 6, x);
+  mp_mul(c2, 6, fts::Q_GLV_A2, 6, y);
+  mp_add(z, x, y, 12);
+  bool n1 = mp_signed_diff(k1, k, z, 12);
+  mp_mul(c1, 6, fts::Q_GLV_B1ABS, 6, x);
+  mp_mul(c2, 6, fts::Q_GLV_B2, 6, y);
+  bool n2 = mp_signed_diff(k2, x, y, 12);
+  for (int i = 0; i < 5; i++) {
+    out[i] = k1[i];
+    out[5 + i] = k2[i];
+  }
+  out[10] = (n1 ? 1u : 0u) | (n2 ? 2u : 0u);
+  out[11] = 0;
+}
+
+void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymLayout& L) {
+  constexpr size_t PER_JOB = fts::NYM_SC_BYTES + 176;
+  size_t off = ((m * sizeof(fts::NymJob) + 15) & ~(size_t)15) + m * PER_JOB;
+  std::map<std::pair<const uint8_t*, size_t>, uint32_t> at;
+  L.msg_off.resize(m);
+  L.distinct.clear();
   for (size_t k = 0; k < m; k++) {
     const ftz_owner_sig& q = s[idx[k]];
     auto key = std::make_pair(q.msg, q.msg_len);
-    auto it = msg_at.find(key);
-    if (it == msg_at.end()) {
-      moff = ((moff + 15) & ~(size_t)15) + 6;
-      it = msg_at.emplace(key, moff).first;
-      if (blob && q.msg_len) memcpy(blob + moff, q.msg, q.msg_len);
-      moff += q.msg_len;
+    auto it = at.find(key);
+    if (it == at.end()) {
+      off = ((off + 15) & ~(size_t)15) + 6;
+      it = at.emplace(key, (uint32_t)off).first;
+      L.distinct.push_back({(uint32_t)off, (uint32_t)k});
+      off += q.msg_len;
     }
-    if (blob) {
-      fts::NymJob j;
-      j.sc = (uint32_t)(off + k * (SC_BYTES + PRE_BYTES));
-      j.pre = (uint32_t)(j.sc + SC_BYTES);
-      j.msg = (uint32_t)it->second;
-      j.msg_len = (uint32_t)q.msg_len;
-      memcpy(blob + k * sizeof(fts::NymJob), &j, sizeof j);
-      memcpy(blob + j.sc, dec[idx[k]].ints, SC_BYTES);
-      uint8_t* pre = blob + j.pre;
-      memset(pre, 0, PRE_BYTES);
-      memcpy(pre, "sign", 4);
-      memcpy(pre + 134, hash_slot, 32);
-    }
+    L.msg_off[k] = it->second;
   }
-  return moff + 64;  // + slack: the hash reads whole 16-byte words
+  L.total = off + 64;  // + slack: the hash reads whole 16-byte words
+}
+
+void nym_fill(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
+              const uint8_t hash_slot[32], const NymLayout& L, uint8_t* blob,
+              const std::function<void(size_t, const std::function<void(size_t)>&)>& par) {
+  constexpr size_t SC = fts::NYM_SC_BYTES, PRE = 176, PIECE = 256;
+  size_t base = (m * sizeof(fts::NymJob) + 15) & ~(size_t)15;
+  size_t jp = (m + PIECE - 1) / PIECE, mp = (L.distinct.size() + 15) / 16;
+  par(jp + mp, [&](size_t p) {
+    if (p < jp) {
+      for (size_t k = p * PIECE; k < m && k < (p + 1) * PIECE; k++) {
+        fts::NymJob j;
+        j.sc = (uint32_t)(base + k * (SC + PRE));
+        j.pre = (uint32_t)(j.sc + SC);
+        j.msg = L.msg_off[k];
+        j.msg_len = (uint32_t)s[idx[k]].msg_len;
+        memcpy(blob + k * sizeof(fts::NymJob), &j, sizeof j);
+        memcpy(blob + j.sc, dec[idx[k]].ints, 192);
+        memcpy(blob + j.sc + 192, dec[idx[k]].glv, 48);
+        uint8_t* pre = blob + j.pre;
+        memset(pre, 0, PRE);
+        memcpy(pre, "sign", 4);
+        memcpy(pre + 134, hash_slot, 32);
+      }
+    } else {
+      size_t d0 = (p - jp) * 16;
+      for (size_t d = d0; d < L.distinct.size() && d < d0 + 16; d++) {
+        const ftz_owner_sig& q = s[idx[L.distinct[d].second]];
+        if (q.msg_len) memcpy(blob + L.distinct[d].first, q.msg, q.msg_len);
+      }
+    }
+  });
 }
 
 }  // namespace ftsh

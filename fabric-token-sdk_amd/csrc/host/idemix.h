@@ -13,6 +13,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -46,18 +47,30 @@ struct NymDecoded {
   int code = 0;           // 0 = go to the device; else FTZ_ERR_OWNER / _SIGNATURE / _UNSUPPORTED
   std::string why;        // the reference's error text when code != 0
   uint8_t ints[6][32];    // NymX, NymY, ProofC, ProofSSk, ProofSRNym, Nonce (first 32 bytes each)
+  uint32_t glv[12];       // ProofC mod n = k1 + k2 lambda: |k1| (5 limbs), |k2| (5), sign bits, 0
 };
+// k (32 bytes big-endian, any value) mod n split as k1 + k2 lambda with
+// |k1|, |k2| < 2^129: out = |k1| (5 limbs) | |k2| (5 limbs) | (k1 < 0) | (k2 < 0) << 1 | 0
+void nym_glv_split(const uint8_t k[32], uint32_t out[12]);
 // TransferSignatureValidate's per-input path up to the curve arithmetic:
 // GetOwnerVerifier(owner) then the signature unmarshal of Verify(msg, sigma).
 void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_t* sig, size_t sig_len,
                             NymDecoded& out);
 
 // Blob of one device pass over the signatures s[idx[0..m)] (all decoded with
-// code 0): the NymJob array at offset 0, then per job the six integers
-// (dev/idemix.h NymJob.sc) and the 176-byte transcript prefix ("sign", zeros
-// for t and Nym, hash_slot at 134), then every distinct message (same pointer
-// and length) once at an offset = 6 mod 16.  blob == nullptr: size only.
-size_t nym_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
-                  const uint8_t hash_slot[32], uint8_t* blob);
+// code 0): the NymJob array at offset 0, then per job the six integers and
+// the GLV split of ProofC (dev/idemix.h NymJob.sc, 240 bytes) and the 176-byte
+// transcript prefix ("sign", zeros for t and Nym, hash_slot at 134), then every
+// distinct message (same pointer and length) once at an offset = 6 mod 16.
+struct NymLayout {
+  size_t total = 0;                                   // blob bytes (+ slack)
+  std::vector<uint32_t> msg_off;                      // per job
+  std::vector<std::pair<uint32_t, uint32_t>> distinct;  // (blob offset, job whose message is copied there)
+};
+void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymLayout& L);
+// fill the blob; `par` (optional) runs f(0..k) in parallel
+void nym_fill(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
+              const uint8_t hash_slot[32], const NymLayout& L, uint8_t* blob,
+              const std::function<void(size_t, const std::function<void(size_t)>&)>& par);
 
 }  // namespace ftsh

@@ -13,13 +13,30 @@
 #include "launch.h"
 #include "rt_internal.h"
 
+// One pipeline slot: pinned staging, device blob / partials / verdicts, its stream.
+struct NymSlot {
+  PinnedMem h_blob, h_ok;
+  DevMem d_blob, d_ok, d_part;
+  hipStream_t st = nullptr;
+  std::vector<uint32_t> idx;  // call-relative indices of the slot's signatures
+  bool busy = false;
+};
+
 struct ftz_idemix {
   ftz_ctx* ctx = nullptr;
   uint8_t hash_slot[32] = {};  // copy(proofData[index:], ipk.Hash) into the 32-byte slot
   DBuf<QDev> tab;              // HSk and HRand fixed-base tables
   std::mutex mu;               // one call on the device at a time
-  PinnedMem h_blob, h_ok;
-  DevMem d_blob, d_ok;
+  WorkPool* pool = nullptr;    // host decoding / layout threads
+  NymSlot slot[2];             // chunk k+1 is decoded and laid out while chunk k runs
+  ~ftz_idemix() {
+    for (NymSlot& q : slot)
+      if (q.st) {
+        (void)hipStreamSynchronize(q.st);
+        (void)hipStreamDestroy(q.st);
+      }
+    delete pool;
+  }
 };
 
 extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curve_id, ftz_idemix** out) {
@@ -39,6 +56,14 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
   HC(hipSetDevice(ctx->device));
   ftz_idemix* ix = new ftz_idemix();
   ix->ctx = ctx;
+  ix->pool = new WorkPool(ctx->opt.threads ? (int)ctx->opt.threads : 8);
+  for (NymSlot& q : ix->slot) {
+    hipError_t se = hipStreamCreateWithFlags(&q.st, hipStreamNonBlocking);
+    if (se != hipSuccess) {
+      delete ix;
+      return set_err(FTZ_E_DEVICE, std::string("hipStreamCreate failed: ") + hipGetErrorString(se));
+    }
+  }
   memcpy(ix->hash_slot, k.hash.data(), k.hash.size() < 32 ? k.hash.size() : 32);
   hipError_t he = ix->tab.upload(tab, ctx->stream);
   if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
@@ -52,57 +77,86 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
 
 void ftz_idemix_destroy(ftz_idemix* ix) { delete ix; }
 
-// one device pass over the decoded signatures idx[a..b) of a call
 namespace {
 constexpr size_t NYM_CHUNK_BYTES = (size_t)1 << 30;  // keeps every blob offset in 32 bits
+constexpr size_t NYM_CHUNK_SIGS = 4096;              // signatures per pipelined device pass
 
-int nym_pass(ftz_idemix* ix, const ftz_owner_sig* s, const std::vector<uint32_t>& idx,
-             const std::vector<ftsh::NymDecoded>& dec, size_t a, size_t b, int32_t* codes) {
-  size_t m = b - a;
-  size_t total = ftsh::nym_layout(s, idx.data() + a, m, dec.data(), ix->hash_slot, nullptr);
-  HC(ix->h_blob.reserve(total));
-  HC(ix->d_blob.reserve(total));
-  HC(ix->h_ok.reserve(m));
-  HC(ix->d_ok.reserve(m));
-  ftsh::nym_layout(s, idx.data() + a, m, dec.data(), ix->hash_slot, ix->h_blob.p);
-  hipStream_t st = ix->ctx->stream;
-  HC(hipMemcpyAsync(ix->d_blob.p, ix->h_blob.p, total, hipMemcpyHostToDevice, st));
-  k_nym<<<(uint32_t)((m + 63) / 64), 64, 0, st>>>(reinterpret_cast<const NymJob*>(ix->d_blob.p), (uint32_t)m,
-                                                   ix->d_blob.p, ix->tab.p, ix->d_ok.p);
+// collect the verdicts of a slot's pass
+int nym_collect(NymSlot& q, int32_t* codes) {
+  if (!q.busy) return FTZ_SUCCESS;
+  q.busy = false;
+  HC(hipStreamSynchronize(q.st));
+  for (size_t k = 0; k < q.idx.size(); k++) codes[q.idx[k]] = q.h_ok.p[k] ? FTZ_OK : FTZ_ERR_SIGNATURE;
+  return FTZ_SUCCESS;
+}
+
+// decode s[a..b) on the pool; queue the device pass of the ones that reach the curve arithmetic
+int nym_chunk(ftz_idemix* ix, NymSlot& q, const ftz_owner_sig* s, size_t a, size_t b, int32_t* codes) {
+  size_t n = b - a;
+  std::vector<ftsh::NymDecoded> dec(n);
+  ix->pool->run((n + 63) / 64, [&](size_t p) {
+    for (size_t i = p * 64; i < n && i < (p + 1) * 64; i++)
+      ftsh::decode_owner_signature(s[a + i].owner, s[a + i].owner_len, s[a + i].sig, s[a + i].sig_len, dec[i]);
+  });
+  std::vector<uint32_t> idx;  // chunk-relative
+  for (size_t i = 0; i < n; i++) {
+    codes[a + i] = dec[i].code;
+    if (dec[i].code == 0) idx.push_back((uint32_t)i);
+  }
+  if (idx.empty()) return FTZ_SUCCESS;
+  size_t m = idx.size();
+  ftsh::NymLayout L;
+  ftsh::nym_plan_layout(s + a, idx.data(), m, L);
+  HC(q.h_blob.reserve(L.total));
+  HC(q.d_blob.reserve(L.total));
+  HC(q.h_ok.reserve(m));
+  HC(q.d_ok.reserve(m));
+  HC(q.d_part.reserve(4 * m * sizeof(QJDev)));
+  WorkPool* pool = ix->pool;
+  ftsh::nym_fill(s + a, idx.data(), m, dec.data(), ix->hash_slot, L, q.h_blob.p,
+                 [pool](size_t k, const std::function<void(size_t)>& f) { pool->run(k, f); });
+  const NymJob* jobs = reinterpret_cast<const NymJob*>(q.d_blob.p);
+  QJDev* part = reinterpret_cast<QJDev*>(q.d_part.p);
+  HC(hipMemcpyAsync(q.d_blob.p, q.h_blob.p, L.total, hipMemcpyHostToDevice, q.st));
+  k_nym_part<<<(uint32_t)((4 * m + 63) / 64), 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, ix->tab.p, part);
+  k_nym_fin<<<(uint32_t)((m + 63) / 64), 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, part, q.d_ok.p);
   HC(hipGetLastError());
-  HC(hipMemcpyAsync(ix->h_ok.p, ix->d_ok.p, m, hipMemcpyDeviceToHost, st));
-  HC(hipStreamSynchronize(st));
-  for (size_t k = 0; k < m; k++) codes[idx[a + k]] = ix->h_ok.p[k] ? FTZ_OK : FTZ_ERR_SIGNATURE;
+  HC(hipMemcpyAsync(q.h_ok.p, q.d_ok.p, m, hipMemcpyDeviceToHost, q.st));
+  q.idx.resize(m);
+  for (size_t k = 0; k < m; k++) q.idx[k] = (uint32_t)(a + idx[k]);
+  q.busy = true;
   return FTZ_SUCCESS;
 }
 }  // namespace
 
 extern "C" int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_owner_sig* s, int32_t* codes) {
   if (!ix || (n && (!s || !codes))) return set_err(FTZ_E_INVALID, "null argument");
-  std::vector<ftsh::NymDecoded> dec(n);
-  std::vector<uint32_t> idx;
   for (size_t i = 0; i < n; i++) {
     if ((!s[i].owner && s[i].owner_len) || (!s[i].msg && s[i].msg_len) || (!s[i].sig && s[i].sig_len))
       return set_err(FTZ_E_INVALID, "null buffer with non-zero length");
     if (s[i].msg_len > NYM_CHUNK_BYTES / 2) return set_err(FTZ_E_INVALID, "message larger than 512 MiB");
-    ftsh::decode_owner_signature(s[i].owner, s[i].owner_len, s[i].sig, s[i].sig_len, dec[i]);
-    codes[i] = dec[i].code;
-    if (dec[i].code == 0) idx.push_back((uint32_t)i);
   }
-  if (idx.empty()) return FTZ_SUCCESS;
   std::lock_guard<std::mutex> lk(ix->mu);
   HC(hipSetDevice(ix->ctx->device));
-  // cut into device passes whose blob stays below NYM_CHUNK_BYTES
-  size_t a = 0;
-  while (a < idx.size()) {
+  // chunks of <= NYM_CHUNK_SIGS signatures and < NYM_CHUNK_BYTES of blob, alternating
+  // between the two slots: chunk k+1 is decoded and laid out while chunk k runs
+  size_t a = 0, c = 0;
+  int rc = FTZ_SUCCESS;
+  while (a < n && rc == FTZ_SUCCESS) {
     size_t b = a, bytes = 0;
-    while (b < idx.size() && (b == a || bytes + s[idx[b]].msg_len + 512 < NYM_CHUNK_BYTES) && b - a < (1u << 20)) {
-      bytes += s[idx[b]].msg_len + 512;
+    while (b < n && b - a < NYM_CHUNK_SIGS && (b == a || bytes + s[b].msg_len + 512 < NYM_CHUNK_BYTES)) {
+      bytes += s[b].msg_len + 512;
       b++;
     }
-    int rc = nym_pass(ix, s, idx, dec, a, b, codes);
-    if (rc != FTZ_SUCCESS) return rc;
+    NymSlot& q = ix->slot[c & 1];
+    rc = nym_collect(q, codes);
+    if (rc == FTZ_SUCCESS) rc = nym_chunk(ix, q, s, a, b, codes);
     a = b;
+    c++;
   }
-  return FTZ_SUCCESS;
+  for (NymSlot& q : ix->slot) {
+    int r2 = nym_collect(q, codes);
+    if (rc == FTZ_SUCCESS) rc = r2;
+  }
+  return rc;
 }

@@ -1,9 +1,22 @@
-// Idemix owner-signature kernels (dev/idemix.h): one lane per NymSignature.
+// Idemix owner-signature kernels (dev/idemix.h): k_nym_part runs the four
+// parts of t = s_sk HSk + s_rnym HRand - c Nym on four lanes per signature
+// (part-major: lanes [p n, (p+1) n) run part p, so every wave runs one part),
+// k_nym_fin adds them and hashes the transcript, one lane per signature.
 #include "launch.h"
 
-__global__ void __launch_bounds__(64) k_nym(const NymJob* jobs, uint32_t n, uint8_t* blob, const QDev* tab,
-                                            uint8_t* ok) {
+__global__ void __launch_bounds__(64) k_nym_part(const NymJob* jobs, uint32_t n, const uint8_t* blob,
+                                                 const QDev* tab, QJDev* part) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * n) return;
+  uint32_t p = i / n, j = i - p * n;
+  qj_store(part[i], job_nym_part(jobs[j], blob, tab, p));
+}
+
+__global__ void __launch_bounds__(64) k_nym_fin(const NymJob* jobs, uint32_t n, uint8_t* blob, const QJDev* part,
+                                                uint8_t* ok) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  ok[i] = job_nym(jobs[i], blob, tab);
+  q1j t = jac_add(jac_add(qj_load(part[i]), qj_load(part[n + i])),
+                  jac_add(qj_load(part[2 * n + i]), qj_load(part[3 * n + i])));
+  ok[i] = job_nym_fin(jobs[i], blob, t);
 }

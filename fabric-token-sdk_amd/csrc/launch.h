@@ -99,4 +99,5 @@ __global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const 
                                 uint32_t (*zs)[8], G1Dev* pts);
 
 // idemix owner signatures (k_idemix.hip)
-__global__ void k_nym(const NymJob* jobs, uint32_t n, uint8_t* blob, const QDev* tab, uint8_t* ok);
+__global__ void k_nym_part(const NymJob* jobs, uint32_t n, const uint8_t* blob, const QDev* tab, QJDev* part);
+__global__ void k_nym_fin(const NymJob* jobs, uint32_t n, uint8_t* blob, const QJDev* part, uint8_t* ok);

@@ -12,6 +12,7 @@ NewNymSignature from the SignerConfig's secret key, with the oracle's verdicts.
 
     python tests/golden/make_idemix.py
 """
+import hashlib
 import json
 import os
 import random
@@ -22,6 +23,16 @@ sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle", "py"))
 from ftsoracle import idemix as I  # noqa: E402
 
 REF = "/root/reference/token/core/zkatdlog/crypto/validator/testdata/idemix"
+
+
+def expand(seed, n):
+    """message bytes of a bench entry: SHA-256(seed || counter) blocks (bench.py repeats this)"""
+    out = bytearray()
+    k = 0
+    while len(out) < n:
+        out += hashlib.sha256(seed + k.to_bytes(4, "big")).digest()
+        k += 1
+    return bytes(out[:n])
 
 
 def main():
@@ -137,6 +148,19 @@ def main():
     pc = I.hash_to_zr(c.to_bytes(32, "big") + nonce.to_bytes(32, "big"))
     add("off_curve_nym_forgery_accepts", owner(off), msg, sigf([v.to_bytes(32, "big") for v in (pc, ssk, sr, nonce)]))
 
+    # bench workload (bench.py owner_signatures leg): 32 requests of ~9.5 KB (the
+    # size of asn1(TokenRequest) for one 2-in/2-out transfer action), each signed by
+    # two input owners; messages are expanded from a seed so the fixture stays small
+    bench = []
+    for r in range(32):
+        seed = bytes([r]) * 8
+        msg = expand(seed, 9500)
+        for u in range(2):
+            rn, nym = users[(r + u) % 4]
+            sig = I.nym_sign(ipk, sk, rn, nym, msg, rz(), rz(), rz())
+            bench.append({"owner": owner(identity(nym)).hex(), "msg_seed": seed.hex(), "msg_len": len(msg),
+                          "sig": sig.hex()})
+
     out = {
         "comment": "idemix owner signatures on FP256BN (SURVEY 8(f) row 3); made by make_idemix.py",
         "ext_assumptions": {
@@ -157,6 +181,7 @@ def main():
             "attr_strings": {"ou": sc[3].decode(), "enrollment_id": sc[5].decode()},
         },
         "cases": cases,
+        "bench": bench,
     }
     path = os.path.join(HERE, "idemix_golden.json")
     json.dump(out, open(path, "w"), indent=1)

@@ -49,13 +49,20 @@ int emu_verify_owner_signatures(void* p, size_t n, const ftz_owner_sig* s, int32
     if (dec[i].code == 0) idx.push_back((uint32_t)i);
   }
   if (idx.empty()) return 0;
-  size_t total = ftsh::nym_layout(s, idx.data(), idx.size(), dec.data(), ix->hash_slot, nullptr);
-  std::vector<uint8_t> blob(total + 16);
+  ftsh::NymLayout L;
+  ftsh::nym_plan_layout(s, idx.data(), idx.size(), L);
+  std::vector<uint8_t> blob(L.total + 16);
   uint8_t* b = blob.data() + ((16 - ((uintptr_t)blob.data() & 15)) & 15);  // the device blob is 256-aligned
-  ftsh::nym_layout(s, idx.data(), idx.size(), dec.data(), ix->hash_slot, b);
+  ftsh::nym_fill(s, idx.data(), idx.size(), dec.data(), ix->hash_slot, L, b,
+                 [](size_t k, const std::function<void(size_t)>& f) {
+                   for (size_t i = 0; i < k; i++) f(i);
+                 });
   const NymJob* jobs = reinterpret_cast<const NymJob*>(b);
-  for (size_t k = 0; k < idx.size(); k++)
-    codes[idx[k]] = job_nym(jobs[k], b, ix->tab.data()) ? FTZ_OK : FTZ_ERR_SIGNATURE;
+  for (size_t k = 0; k < idx.size(); k++) {
+    q1j t = jac_add(jac_add(job_nym_part(jobs[k], b, ix->tab.data(), 0), job_nym_part(jobs[k], b, ix->tab.data(), 1)),
+                    jac_add(job_nym_part(jobs[k], b, ix->tab.data(), 2), job_nym_part(jobs[k], b, ix->tab.data(), 3)));
+    codes[idx[k]] = job_nym_fin(jobs[k], b, t) ? FTZ_OK : FTZ_ERR_SIGNATURE;
+  }
   return 0;
 }
 
@@ -67,5 +74,8 @@ int emu_decode_owner_signature(const uint8_t* owner, size_t owner_len, const uin
   snprintf(why, cap, "%s", d.why.c_str());
   return d.code;
 }
+
+// host GLV split of a 32-byte scalar (host/idemix.cpp)
+void emu_nym_glv_split(const uint8_t* k, uint32_t* out) { ftsh::nym_glv_split(k, out); }
 
 }  // extern "C"

@@ -142,6 +142,30 @@ def test_emu_random_tamper_matches_oracle(gold, emu_ix):
     assert emu_verify(emu_ix, its) == want
 
 
+def test_emu_glv_split(emu_ix):
+    """host GLV split (host/idemix.cpp nym_glv_split): k = k1 + k2 lambda mod n, |k_i| < 2^129"""
+    lib, _ = emu_ix
+    lib.emu_nym_glv_split.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32)]
+    lam = pow(5, (I.N - 1) // 3, I.N)
+    lams = {lam, lam * lam % I.N}
+    rng = random.Random(3)
+    ks = [0, 1, I.N - 1, I.N, I.N + 5, (1 << 256) - 1, I.N // 2] + [rng.randrange(1 << 256) for _ in range(2000)]
+    out = (ctypes.c_uint32 * 12)()
+    found = set(lams)
+    for k in ks:
+        lib.emu_nym_glv_split(k.to_bytes(32, "big"), out)
+        k1 = sum(out[i] << (32 * i) for i in range(5))
+        k2 = sum(out[5 + i] << (32 * i) for i in range(5))
+        if out[10] & 1:
+            k1 = -k1
+        if out[10] & 2:
+            k2 = -k2
+        assert abs(k1) < 1 << 129 and abs(k2) < 1 << 129
+        found &= {L for L in lams if (k1 + k2 * L - k) % I.N == 0}
+        assert found, k
+    assert len(found) == 1  # one lambda fits every split (the one matching beta)
+
+
 def test_abi_rejects_bad_issuer_key():
     from zkatdlog import _abi as A
     lib = A.load()
