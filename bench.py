@@ -352,6 +352,7 @@ def main():
     ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
     ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
     ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
+    ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -371,7 +372,7 @@ def main():
     from zkatdlog.dist import bitmap_of, verify_shard
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
-    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch, slots=args.slots)
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch, slots=args.slots, threads=args.threads)
     t_setup = time.time()
     valid = W.prove_distinct(ctx, args.distinct, tag=b"bench/%d" % rank)
     bad = W.golden_tampered()

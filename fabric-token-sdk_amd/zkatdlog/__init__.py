@@ -273,6 +273,20 @@ def decode_token_request(raw):
     return out
 
 
+def setup_public_params(base, exponent, seed, idemix_pk=b"idemix-issuer-pk", idemix_curve=0):
+    """crypto.Setup(base, exponent, nymPK, idemixCurveID) (setup.go:214-236) +
+    Serialize, with seed-derived randomness (ftz_pp_setup): the serialized PP bytes."""
+    lib = _abi.load()
+    n = ctypes.c_size_t()
+    seed = bytes(seed)
+    pk = None if idemix_pk is None else bytes(idemix_pk)
+    args = (int(base), int(exponent), pk, 0 if pk is None else len(pk), int(idemix_curve), seed, len(seed))
+    lib.ftz_pp_setup(*args, None, 0, ctypes.byref(n))
+    buf = ctypes.create_string_buffer(n.value)
+    _check(lib.ftz_pp_setup(*args, buf, n.value, ctypes.byref(n)), lib)
+    return buf.raw[:n.value]
+
+
 def validate_public_params(pp_bytes):
     """crypto.PublicParams.Validate (setup.go:238-273): "" or the error text
     (host-side check; no GPU needed)."""

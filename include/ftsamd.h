@@ -125,6 +125,17 @@ int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
  * FTZ_SUCCESS, or FTZ_E_PP with the reference's error text in
  * ftz_last_error().  Point encodings are checked by ftz_ctx_create. */
 int ftz_pp_validate(const uint8_t* pp, size_t pp_len);
+/* crypto.Setup (setup.go:214-236: pssign KeyGen(1), GeneratePedersenParameters
+ * :153-166, GenerateRangeProofParameters :168-184 with the R = generator quirk of
+ * pssign/sign.go:97-98, QuantityPrecision 64) followed by Serialize
+ * (setup.go:119-128): out receives json(driver.SerializedPublicParameters) for
+ * SignedValues of 0..base-1 and the given Exponent / IdemixIssuerPK (NULL: JSON
+ * null) / IdemixCurveID.  The reference draws its scalars from crypto/rand;
+ * here rand(tag) = SHA-256(seed||tag||0) || SHA-256(seed||tag||1) mod r, so a
+ * seed reproduces a parameter set.  Host-side (once per network): no context
+ * or GPU needed.  *out_len = the size; FTZ_E_INVALID if cap is too small. */
+int ftz_pp_setup(uint64_t base, uint32_t exponent, const uint8_t* idemix_pk, size_t idemix_pk_len, int idemix_curve,
+                 const uint8_t* seed, size_t seed_len, uint8_t* out, size_t cap, size_t* out_len);
 /* the context's resolved options (threads, batch, slots, window, fexp) */
 int ftz_ctx_options(const ftz_ctx* ctx, ftz_options* out);
 /* PP properties: base (len(SignedValues)) and exponent */

@@ -62,3 +62,18 @@ def test_pp_validate_matches_oracle():
         else:
             assert got == c["error"], (c["name"], got, c["error"])
     assert sum(1 for c in cases if not c["error"]) == 2
+
+
+def test_pp_setup_reproduces_golden_public_params(golden):
+    """ftz_pp_setup (native crypto.Setup + Serialize, setup.go:119-128,214-236) with
+    the golden fixtures' seeds gives their PP-A / PP-B bytes exactly (the oracle's
+    zkat.setup made those), and the result passes PublicParams.Validate."""
+    import zkatdlog
+    for key, base, exp, seed in (("pp_a", 100, 2, b"golden-pp-A"), ("pp_b", 16, 16, b"golden-pp-B")):
+        got = zkatdlog.setup_public_params(base, exp, seed)
+        assert got == golden[key]["pp"].encode(), key
+        assert not zkatdlog.validate_public_params(got)
+    other = zkatdlog.setup_public_params(10, 3, b"another", idemix_pk=None, idemix_curve=1)
+    from ftsoracle import zkat as Z
+    want = Z.setup(10, 3, Z.Rand(b"another"), idemix_pk=None, idemix_curve=1).to_json()
+    assert other == want
