@@ -1,0 +1,50 @@
+"""Race detection for the product's host code (aux): the
+planner, the shared WorkPool, the flat layout / blob write and the idemix /
+token-request decoders built with ThreadSanitizer and driven by several caller
+threads at once, as the job engine drives them (tests/native/tsan_main.cpp).
+Concurrent plans must equal the single-threaded plan byte for byte and TSAN
+must report no data race."""
+import base64
+import os
+import shutil
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "fabric-token-sdk_amd", "csrc")
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_host_code_is_race_free_under_tsan(golden, tmp_path):
+    exe = tmp_path / "tsan_main"
+    srcs = [os.path.join(ROOT, "tests", "native", "tsan_main.cpp")] + [
+        os.path.join(CSRC, "host", f) for f in ("planner.cpp", "gojson.cpp", "request.cpp", "idemix.cpp")]
+    r = subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=thread", "-Wno-unknown-pragmas", "-pthread"]
+                       + srcs + ["-o", str(exe)], capture_output=True, text=True)
+    if r.returncode != 0 and "tsan" in r.stderr.lower():
+        pytest.skip("ThreadSanitizer runtime not available: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr[-2000:]
+    g = golden["pp_a"]
+    (tmp_path / "pp.json").write_bytes(g["pp"].encode())
+    rec = bytearray()
+    for c in g["cases"]:
+        if c["kind"] != "transfer":
+            continue
+        ins, outs, proof = bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"])
+        rec += struct.pack("<4I", 0, len(ins) // 64, len(outs) // 64, len(proof)) + ins + outs + proof
+    (tmp_path / "tx.bin").write_bytes(bytes(rec) * 8)  # >= 32 items per planning piece on every pool thread
+    import json
+    idm = json.load(open(os.path.join(ROOT, "tests", "golden", "idemix_golden.json")))
+    own = bytearray()
+    for c in idm["cases"]:
+        o, s = bytes.fromhex(c["owner"]), bytes.fromhex(c["sig"])
+        own += struct.pack("<2I", len(o), len(s)) + o + s
+    (tmp_path / "own.bin").write_bytes(bytes(own))
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([str(exe), str(tmp_path / "pp.json"), str(tmp_path / "tx.bin"), str(tmp_path / "own.bin")],
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-2000:])
+    assert "mismatches 0" in r.stdout
