@@ -1,0 +1,296 @@
+// Carry-free BN254 base-field arithmetic for the one-lane G1 loops (variable-
+// and fixed-base scalar multiplication, MSM buckets): signed 9 x 29-bit limbs
+// with 64-bit column accumulators.
+//
+// The 8 x 32-bit Montgomery product of fp.h issues one carry add per MAD
+// (v_mad_u64_u32 + v_addc, ~300 instructions with the column moves); here a
+// limb product is < 2^60 and a column of nine of them plus the reduction terms
+// stays below 2^63, so every MAD accumulates straight into a signed 64-bit
+// column (v_mad_i64_i32, no carries): 162 MADs + ~45 column instructions per
+// product, 126 MADs per squaring.  Additions and subtractions are nine limb
+// adds with no carry chain and no reduction; the cost moves to explicit
+// normalisations (a carry sweep, f29_norm) and value reductions (one quotient
+// estimate + a multiple of p, f29_reduce) placed where the bounds require them.
+//
+// Representation: value = sum l[i] 2^(29 i) with signed limbs, Montgomery radix
+// R = 2^261 (> 169 p).  Bounds the formulas below keep (L = max |limb| in units
+// of 2^29 - 1, B = |value| in units of p):
+//   f29_mul / f29_sqr inputs: L_a L_b <= 2.5 (column |sum| < 9 (L_a L_b + 1) 2^58
+//     < 2^63; f29_sqr needs L <= 1) and B_a B_b < 169 (then |out| < 2p);
+//     output normalised: limbs 0..7 in [0, 2^29), limb 8 small and signed;
+//   f29_add / f29_sub: L and B add (L <= 4 keeps every limb inside int32);
+//   f29_norm: L -> 1, value unchanged;  f29_reduce: L -> 1, |value| <= p/2 + p.
+// Values enter from the 32-bit Montgomery form (R = 2^256) by a shifted limb
+// split (value x 32, B <= 32) and leave through one product by 2^256 mod p, a
+// reduction and a final canonical subtraction (f29_to_fp), so the G1 code around
+// the loops keeps its fp types.  tests/native/emu_exec.cpp checks every
+// formula against the fp.h ones.
+#pragma once
+#include "curve.h"
+#include "fp.h"
+#include "fp29_const.h"
+
+namespace fts {
+
+struct f29 {
+  int32_t l[9];
+};
+static constexpr int32_t F29_MASK = (1 << 29) - 1;
+
+FTS_HD f29 f29_add(const f29& a, const f29& b) {
+  f29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = a.l[i] + b.l[i];
+  return r;
+}
+FTS_HD f29 f29_sub(const f29& a, const f29& b) {
+  f29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = a.l[i] - b.l[i];
+  return r;
+}
+FTS_HD f29 f29_neg(const f29& a) {
+  f29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = -a.l[i];
+  return r;
+}
+
+// carry sweep: limbs 0..7 into [0, 2^29), limb 8 takes the (signed) rest
+FTS_HD f29 f29_norm(const f29& a) {
+  f29 r;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    int32_t t = a.l[i] + c;
+    r.l[i] = t & F29_MASK;
+    c = t >> 29;
+  }
+  r.l[8] = a.l[8] + c;
+  return r;
+}
+
+// Montgomery product a b / 2^261 (product scanning; column k accumulates the
+// a_i b_j and m_i p_j with i + j = k, m_k makes its low 29 bits vanish)
+FTS_HD f29 f29_mul(const f29& a, const f29& b) {
+  FTS_COUNT_MUL();
+  int64_t acc = 0;
+  uint32_t m[9];
+  f29 r;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < 9) acc += (int64_t)a.l[i] * b.l[j];
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (i < k && j >= 0 && j < 9) acc += (int64_t)(int32_t)m[i] * P29[j];
+    }
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * P29_INV) & (uint32_t)F29_MASK;
+      acc += (int64_t)(int32_t)m[k] * P29[0];
+    } else {
+      r.l[k - 9] = (int32_t)(acc & F29_MASK);
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (int32_t)acc;
+  return r;
+}
+
+// a^2 / 2^261: the cross products once with a doubled operand (requires L <= 1)
+FTS_HD f29 f29_sqr(const f29& a) {
+  FTS_COUNT_MUL();
+  int32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a.l[i] + a.l[i];
+  int64_t acc = 0;
+  uint32_t m[9];
+  f29 r;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j > i && j < 9) acc += (int64_t)d[i] * a.l[j];
+    }
+    if ((k & 1) == 0 && k / 2 < 9) acc += (int64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (i < k && j >= 0 && j < 9) acc += (int64_t)(int32_t)m[i] * P29[j];
+    }
+    if (k < 9) {
+      m[k] = ((uint32_t)acc * P29_INV) & (uint32_t)F29_MASK;
+      acc += (int64_t)(int32_t)m[k] * P29[0];
+    } else {
+      r.l[k - 9] = (int32_t)(acc & F29_MASK);
+    }
+    acc >>= 29;
+  }
+  r.l[8] = (int32_t)acc;
+  return r;
+}
+
+// value - q p with q = round(value / p) from the top two limbs (a double
+// estimate: exact when value is a multiple of p), normalised; |result| <= p/2
+// when the estimate is exact, <= 3p/2 otherwise
+FTS_HD f29 f29_reduce(const f29& a) {
+  f29 n = f29_norm(a);
+  double t = (double)n.l[8] * 536870912.0 + (double)n.l[7];
+  int32_t q = (int32_t)__builtin_rint(t / P29_TOP);
+  f29 r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (int64_t)n.l[i] - (int64_t)q * P29[i];
+    if (i < 8) {
+      r.l[i] = (int32_t)(acc & F29_MASK);
+      acc >>= 29;
+    } else {
+      r.l[8] = (int32_t)acc;
+    }
+  }
+  return r;
+}
+
+FTS_HD f29 fe29_p() {
+  f29 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.l[i] = P29[i];
+  return r;
+}
+
+// a == 0 mod p (any bounded input)
+FTS_HD bool f29_is_zero(const f29& a) {
+  f29 r = f29_reduce(a);
+  int32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) o |= r.l[i];
+  return o == 0;
+}
+// a reduced value (f29_reduce output) that is zero
+FTS_HD bool f29_reduced_zero(const f29& r) {
+  int32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) o |= r.l[i];
+  return o == 0;
+}
+
+// 32-bit Montgomery (R = 2^256, any representative < 2^256) -> this form:
+// the limbs of 32 x, i.e. the R = 2^261 Montgomery form of the same element
+// (B <= 32 for x < p, L = 1)
+FTS_HD f29 f29_from_fp(const fp& x) {
+  f29 r;
+  r.l[0] = (int32_t)((x.v[0] << 5) & (uint32_t)F29_MASK);
+#pragma unroll
+  for (int i = 1; i < 9; i++) {
+    const int off = 29 * i - 5, w = off >> 5, s = off & 31;
+    uint64_t lo = x.v[w], hi = w + 1 < 8 ? x.v[w + 1] : 0u;
+    r.l[i] = (int32_t)((uint32_t)(((hi << 32) | lo) >> s) & (uint32_t)F29_MASK);
+  }
+  return r;
+}
+
+// back to the canonical 32-bit Montgomery form (value < p)
+FTS_HD fp f29_to_fp(const f29& a) {
+  f29 p29;
+#pragma unroll
+  for (int i = 0; i < 9; i++) p29.l[i] = P29_R256[i];
+  f29 r = f29_reduce(f29_mul(a, p29));  // a 2^256 / 2^261: the R = 2^256 form, |r| <= 3p/2
+  // into [0, p): add p while negative, subtract p while >= p (normalised limbs
+  // compare lexicographically from the top)
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    f29 s = f29_norm(f29_add(r, fe29_p()));
+    r = r.l[8] < 0 ? s : r;
+  }
+#pragma unroll
+  for (int it = 0; it < 2; it++) {
+    f29 s = f29_norm(f29_sub(r, fe29_p()));
+    r = s.l[8] >= 0 ? s : r;
+  }
+  fp o;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int b = 32 * j, i = b / 29, s = b % 29;
+    uint64_t v = (uint64_t)(uint32_t)r.l[i] | ((uint64_t)(uint32_t)(i + 1 < 9 ? r.l[i + 1] : 0) << 29);
+    if (i + 2 < 9) v |= (uint64_t)(uint32_t)r.l[i + 2] << 58;
+    o.v[j] = (uint32_t)(v >> s);
+  }
+  return o;
+}
+
+// ---------------------------------------------------------------- G1 (a = 0)
+// Jacobian point in this form with an explicit infinity flag.  Coordinates
+// between operations: normalised, |value| <= 3p/2 (f29_reduce outputs or
+// products).  Same formulas (and so the same projective point up to the
+// representation of each coordinate) as curve.h jac_dbl / jac_add_aff.
+struct j29 {
+  f29 x, y, z;
+  bool inf;
+};
+
+// dbl-2009-l: 2M + 5S.  Bounds in comments as (B, L).
+FTS_HD j29 j29_dbl(const j29& p) {
+  f29 A = f29_sqr(p.x);                            // (2, 1)
+  f29 Bq = f29_sqr(p.y);                           // (2, 1)
+  f29 C = f29_sqr(Bq);                             // (2, 1)
+  f29 T2 = f29_sqr(f29_norm(f29_add(p.x, Bq)));    // (1.5 + 2)^2 < 169
+  f29 D1 = f29_norm(f29_sub(f29_sub(T2, A), C));   // (6, 1)
+  f29 D = f29_add(D1, D1);                         // (12, 2)
+  f29 E = f29_norm(f29_add(f29_add(A, A), A));     // (6, 1)
+  f29 F = f29_sqr(E);                              // 36: (2, 1)
+  f29 X3 = f29_reduce(f29_sub(f29_norm(f29_sub(F, D)), D));        // (26, 3) -> (1.5, 1)
+  f29 Y3a = f29_mul(E, f29_norm(f29_sub(D, X3)));  // 6 x 13.5 < 169: (2, 1)
+  f29 C2 = f29_add(C, C);
+  f29 C4 = f29_norm(f29_add(C2, C2));              // (8, 1)
+  f29 Y3 = f29_reduce(f29_sub(Y3a, f29_add(C4, C4)));              // (18, 3) -> (1.5, 1)
+  f29 Z3 = f29_mul(f29_add(p.y, p.y), p.z);        // 3 x 2, L 2 x 1: (2, 1); infinity keeps z = 0
+  return {X3, Y3, Z3, p.inf};
+}
+
+// add-2007-bl mixed addition p + (x2, y2), (x2, y2) affine and not infinity,
+// B <= 32, L <= 1 (f29_from_fp outputs): 7M + 4S.  The exceptional cases are
+// caught after the fact: Z3 = 2 Z1 H vanishes iff H does, and then the sum is
+// infinity (rr != 0) or a doubling (rr == 0, p == (x2, y2)).
+FTS_HD j29 j29_madd(const j29& p, const f29& x2, const f29& y2) {
+  if (p.inf) return {f29_reduce(x2), f29_reduce(y2), f29_reduce(f29_from_fp(fe_one<ModP>())), false};
+  f29 Z1Z1 = f29_sqr(p.z);                         // (2, 1)
+  f29 U2 = f29_mul(x2, Z1Z1);                      // 32 x 2: (2, 1)
+  f29 S2 = f29_mul(y2, f29_mul(p.z, Z1Z1));        // (2, 1)
+  f29 H = f29_norm(f29_sub(U2, p.x));              // (3.5, 1)
+  f29 rr = f29_sub(S2, p.y);                       // (3.5, 2)
+  f29 HH = f29_sqr(H);                             // (2, 1)
+  f29 HH2 = f29_add(HH, HH);
+  f29 I = f29_norm(f29_add(HH2, HH2));             // (8, 1)
+  f29 J = f29_mul(H, I);                           // 28: (2, 1)
+  f29 r2 = f29_norm(f29_add(rr, rr));              // (7, 1)
+  f29 V = f29_mul(p.x, I);                         // 12: (2, 1)
+  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sub(f29_sqr(r2), J), V), V));  // (8, 4) -> (1.5, 1)
+  f29 Y3a = f29_mul(r2, f29_norm(f29_sub(V, X3))); // 7 x 3.5: (2, 1)
+  f29 YJ = f29_mul(p.y, J);                        // (2, 1)
+  f29 Y3 = f29_reduce(f29_sub(f29_sub(Y3a, YJ), YJ));              // (6, 3) -> (1.5, 1)
+  f29 ZH = f29_norm(f29_add(p.z, H));              // (5, 1)
+  f29 Z3 = f29_reduce(f29_sub(f29_sub(f29_sqr(ZH), Z1Z1), HH));    // 25: (6, 3) -> (1.5, 1)
+  if (f29_reduced_zero(Z3)) {
+    if (f29_is_zero(rr)) return j29_dbl(p);  // p == (x2, y2)
+    j29 o = p;
+    o.inf = true;
+    return o;
+  }
+  return {X3, Y3, Z3, false};
+}
+
+FTS_HD j29 j29_from(const g1j& p) {
+  return {f29_reduce(f29_from_fp(p.x)), f29_reduce(f29_from_fp(p.y)), f29_reduce(f29_from_fp(p.z)), is_zero(p.z)};
+}
+FTS_HD g1j j29_to(const j29& p) {
+  if (p.inf) return jac_inf<fp>();
+  return {f29_to_fp(p.x), f29_to_fp(p.y), f29_to_fp(p.z)};
+}
+
+}  // namespace fts

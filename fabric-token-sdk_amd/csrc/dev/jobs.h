@@ -17,6 +17,7 @@
 // issue.Verifier.Verify (issue/issue.go:202), TransferZKProofValidate
 // (validator/validator_transfer.go:84-98).
 #pragma once
+#include "fp29.h"
 #include "fp_wide.h"
 #include "pairing.h"
 #include "sha256.h"
@@ -499,9 +500,41 @@ FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]
   return acc;
 }
 
+#ifndef FTS_G1_F29
+#define FTS_G1_F29 1  // G1 loops in the carry-free 29-bit form (dev/fp29.h); 0: fp.h throughout
+#endif
+
 // sum_w d_w 2^(C w) B over the signed C-bit digits of s (s < r < 2^254, so the
 // top window absorbs the last carry)
+FTS_HD g1j g1_fixed_acc_fp(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]);
 FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]) {
+#if FTS_G1_F29
+  j29 a = j29_from(acc);
+  uint32_t carry = 0;
+  const G1Dev* tb = tab + (size_t)base * G1TAB_WINDOWS * G1TAB_DIGITS;
+#pragma nounroll
+  for (int w = 0; w < G1TAB_WINDOWS; w++) {
+    uint32_t bit = (uint32_t)G1TAB_C * w, limb = bit >> 5, sh = bit & 31;
+    uint64_t lo = limb < 8 ? s[limb] : 0, hi = limb + 1 < 8 ? s[limb + 1] : 0;
+    uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1ull << G1TAB_C) - 1)) + carry;
+    int32_t d = (int32_t)raw;
+    carry = 0;
+    if (raw > (1u << (G1TAB_C - 1))) {
+      d = (int32_t)raw - (int32_t)(1u << G1TAB_C);
+      carry = 1;
+    }
+    if (d) {
+      g1a T = g1_load(tb[(size_t)w * G1TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+      f29 y = f29_from_fp(T.y);
+      a = j29_madd(a, f29_from_fp(T.x), d < 0 ? f29_neg(y) : y);
+    }
+  }
+  return j29_to(a);
+#else
+  return g1_fixed_acc_fp(acc, tab, base, s);
+#endif
+}
+FTS_HD g1j g1_fixed_acc_fp(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]) {
   uint32_t carry = 0;
   const G1Dev* tb = tab + (size_t)base * G1TAB_WINDOWS * G1TAB_DIGITS;
 #pragma nounroll
@@ -707,6 +740,31 @@ FTS_HD g1j g1_mul_glv16(const g1a& p, const uint32_t k[8], G1Dev* tb, size_t st)
     g1dev_put(tb[e * st], X * s2, Y * (s2 * se));
   }
   const bool flip = n1 != n2;  // phi(e P1) = +-phi(e p): sign of the second half
+#if FTS_G1_F29
+  const f29 beta29 = f29_reduce(f29_from_fp(fe_const<ModP>(GLV_BETA)));
+  j29 a = {f29{}, f29{}, f29{}, true};
+#pragma nounroll
+  for (int i = 32; i >= 0; i--) {
+    int d1 = booth16(k1, i), d2 = booth16(k2, i);
+    int m1 = d1 < 0 ? -d1 : d1, m2 = d2 < 0 ? -d2 : d2;
+    fp x1, y1, x2, y2;
+    g1dev_get(tb[(size_t)(m1 ? m1 - 1 : 0) * st], x1, y1);
+    g1dev_get(tb[(size_t)(m2 ? m2 - 1 : 0) * st], x2, y2);
+    if (i != 32) {
+      a = j29_dbl(a);
+      a = j29_dbl(a);
+      a = j29_dbl(a);
+      a = j29_dbl(a);
+    }
+    f29 Y = f29_from_fp(y1);
+    j29 na = j29_madd(a, f29_from_fp(x1), (d1 < 0) ? f29_neg(Y) : Y);
+    if (m1) a = na;
+    Y = f29_from_fp(y2);
+    na = j29_madd(a, f29_mul(f29_from_fp(x2), beta29), ((d2 < 0) != flip) ? f29_neg(Y) : Y);
+    if (m2) a = na;
+  }
+  acc = j29_to(a);
+#else
   const fp beta = fe_const<ModP>(GLV_BETA);
 #pragma nounroll
   for (int i = 32; i >= 0; i--) {
@@ -732,6 +790,7 @@ FTS_HD g1j g1_mul_glv16(const g1a& p, const uint32_t k[8], G1Dev* tb, size_t st)
     nacc = jac_add_aff(acc, A);
     if (m2) acc = nacc;
   }
+#endif
   acc.z = acc.z * Zc;  // back to E (the point at infinity keeps z = 0)
   return acc;
 }

@@ -195,6 +195,10 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   if (lo >= hi) return acc;
   uint32_t v = e[lo];
   G1Dev nxt = pts[v & 0x7FFFFFFFu];
+#if FTS_G1_F29
+  // the additions in the carry-free form (dev/fp29.h), one conversion per slot
+  j29 a = {f29{}, f29{}, f29{}, true};
+#endif
   for (uint32_t q = lo; q < hi; q++) {
     // the next point's load is issued before this point's addition
     G1Dev cur = nxt;
@@ -204,9 +208,19 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
       nxt = pts[v & 0x7FFFFFFFu];
     }
     g1a P = g1_load(cur);
+#if FTS_G1_F29
+    if (!P.inf) {
+      f29 Y = f29_from_fp(P.y);
+      a = j29_madd(a, f29_from_fp(P.x), sign ? f29_neg(Y) : Y);
+    }
+#else
     if (sign) P = aff_neg(P);
     acc = jac_add_aff(acc, P);
+#endif
   }
+#if FTS_G1_F29
+  acc = j29_to(a);
+#endif
   return acc;
 }
 

@@ -352,3 +352,91 @@ int emu_verify_token_requests(void* ctx, size_t n, const ftz_bytes* reqs, ftz_ge
   return ftsh::verify_token_requests(n, reqs, h, codes, failed, err);
 }
 }
+
+// ------------------------------------------------------------------ fp29 check
+// dev/fp29.h (carry-free 29-bit limbs) against the fp.h arithmetic: field
+// products / sums at the bounds the G1 formulas use, and long double-and-add
+// chains of j29_dbl / j29_madd against jac_dbl / jac_add_aff including the
+// exceptional additions (from infinity, P + P, P + (-P)).  Returns the number
+// of mismatches.
+namespace {
+struct Rng64 {
+  uint64_t s;
+  uint64_t next() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return s;
+  }
+};
+fp rand_fp(Rng64& r) {
+  uint32_t v[8];
+  for (int i = 0; i < 8; i++) v[i] = (uint32_t)r.next();
+  v[7] &= 0x1fffffffu;  // < 2^253 < p
+  return fe_from_int<ModP>(v);
+}
+bool aff_same(const g1a& a, const g1a& b) {
+  if (a.inf || b.inf) return a.inf == b.inf;
+  return fe_eq(a.x, b.x) && fe_eq(a.y, b.y);
+}
+}  // namespace
+
+extern "C" int emu_f29_check(uint64_t seed, int iters) {
+  Rng64 r{seed | 1};
+  int bad = 0;
+  fp pm1 = fe_zero<ModP>() - fe_one<ModP>();
+  for (int it = 0; it < iters; it++) {
+    fp a = it == 0 ? pm1 : rand_fp(r), b = it < 2 ? pm1 : rand_fp(r);
+    f29 A = f29_from_fp(a), B = f29_from_fp(b);
+    if (!fe_eq(f29_to_fp(A), a)) bad++;
+    f29 Ar = f29_reduce(A), Br = f29_reduce(B);
+    if (!fe_eq(f29_to_fp(f29_mul(Ar, Br)), a * b)) bad++;
+    if (!fe_eq(f29_to_fp(f29_sqr(Ar)), fe_sqr(a))) bad++;
+    // unreduced entry form (B 32) times a product (B 2), and a 4-term sum
+    f29 Pab = f29_mul(Ar, Br);
+    if (!fe_eq(f29_to_fp(f29_mul(A, Pab)), a * (a * b))) bad++;
+    f29 s = f29_norm(f29_sub(f29_add(f29_add(Pab, Pab), Ar), Br));
+    fp sf = a * b + a * b + a - b;
+    if (!fe_eq(f29_to_fp(s), sf)) bad++;
+    if (!fe_eq(f29_to_fp(f29_neg(Ar)), fe_neg(a))) bad++;
+  }
+  // point chains: a few random affine base points
+  g1a gen = {fe_one<ModP>(), fe_one<ModP>() + fe_one<ModP>(), false};
+  std::vector<g1a> pts;
+  for (int k = 0; k < 8; k++) {
+    uint32_t sc[8];
+    for (int i = 0; i < 8; i++) sc[i] = (uint32_t)r.next();
+    sc[7] &= 0x0fffffffu;
+    pts.push_back(jac_to_aff(aff_mul(gen, sc)));
+  }
+  for (int chain = 0; chain < iters / 8 + 1; chain++) {
+    g1j acc = jac_inf<fp>();
+    j29 a29 = j29_from(acc);
+    for (int step = 0; step < 40; step++) {
+      int kind = (int)(r.next() % 8);
+      if (step > 0 && kind < 3) {
+        int nd = 1 + (int)(r.next() % 4);
+        for (int d = 0; d < nd; d++) {
+          acc = jac_dbl(acc);
+          a29 = j29_dbl(a29);
+        }
+      }
+      g1a q = pts[r.next() % pts.size()];
+      int e = (int)(r.next() % 16);
+      if (e == 0) q = jac_to_aff(acc);                   // P + P
+      if (e == 1) q = aff_neg(jac_to_aff(acc));          // P + (-P)
+      if (q.inf) continue;
+      bool neg = r.next() & 1;
+      f29 Y = f29_from_fp(q.y);
+      a29 = j29_madd(a29, f29_from_fp(q.x), neg ? f29_neg(Y) : Y);
+      acc = jac_add_aff(acc, neg ? aff_neg(q) : q);
+      if (!aff_same(jac_to_aff(j29_to(a29)), jac_to_aff(acc))) {
+        bad++;
+        a29 = j29_from(acc);  // resynchronise
+      }
+    }
+    // round trip through the fp form mid-chain
+    if (!aff_same(jac_to_aff(j29_to(j29_from(acc))), jac_to_aff(acc))) bad++;
+  }
+  return bad;
+}
