@@ -136,12 +136,14 @@ FTS_HD f29 f29_sqr(const f29& a) {
 }
 
 // value - q p with q = round(value / p) from the top two limbs (a double
-// estimate: exact when value is a multiple of p), normalised; |result| <= p/2
-// when the estimate is exact, <= 3p/2 otherwise
+// estimate: exact when value is a multiple of p), normalised in the same carry
+// sweep; |result| <= p/2 + 2^-40 p
 FTS_HD f29 f29_reduce(const f29& a) {
-  f29 n = f29_norm(a);
+  // the estimate needs no normalised input: the limbs below 7 move the value by
+  // at most L 2^203, i.e. q by L / 2^50.6
+  const f29& n = a;
   double t = (double)n.l[8] * 536870912.0 + (double)n.l[7];
-  int32_t q = (int32_t)__builtin_rint(t / P29_TOP);
+  int32_t q = (int32_t)__builtin_rint(t * P29_TOP_INV);  // |error| < 2^-45: exact for multiples of p
   f29 r;
   int64_t acc = 0;
 #pragma unroll
@@ -206,12 +208,16 @@ FTS_HD fp f29_to_fp(const f29& a) {
 #pragma unroll
   for (int it = 0; it < 2; it++) {
     f29 s = f29_norm(f29_add(r, fe29_p()));
-    r = r.l[8] < 0 ? s : r;
+    const bool take = r.l[8] < 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = take ? s.l[i] : r.l[i];
   }
 #pragma unroll
   for (int it = 0; it < 2; it++) {
     f29 s = f29_norm(f29_sub(r, fe29_p()));
-    r = s.l[8] >= 0 ? s : r;
+    const bool take = s.l[8] >= 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.l[i] = take ? s.l[i] : r.l[i];
   }
   fp o;
 #pragma unroll

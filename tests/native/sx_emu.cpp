@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
 
 using namespace fts;
 
@@ -144,6 +145,30 @@ int sxe_fexp(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
     fp2 g = variant == 1 ? sx_final_exp(x, f12_coef(f, x.k)) : sx_final_exp_exact(x, f12_coef(f, x.k));
     sx_gt_bytes(out_sx, x.k, g);
   });
+  return memcmp(out_sx, out_ref, 384) != 0;
+}
+
+// the same with the carry-free sextet final exponentiation (dev/sx29.h): the
+// 32-bit and 29-bit contexts share one slot region, as on the device
+int sxe_fexp29(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
+  uint32_t s = seed | 1;
+  fp12 f = rnd_f12(s);
+  f12_to_bytes(out_ref, final_exp(f, variant));
+  std::vector<uint8_t> raw(SQ_FEXP_BYTES + 64);
+  memset(raw.data(), 0xA5, raw.size());
+  uint8_t* base = raw.data() + (64 - ((uintptr_t)raw.data() & 63)) % 64;
+  pthread_barrier_t b;
+  pthread_barrier_init(&b, nullptr, 6);
+  std::vector<std::thread> th;
+  for (int k = 0; k < 6; k++)
+    th.emplace_back([&, k] {
+      SxH xo{k, (F2Slot*)base, true, {&b}};
+      Sq<SyncHost> x{k, (Q2Slot*)base, true, {&b}};
+      fp2 g = variant == 1 ? sq_final_exp(x, xo, f12_coef(f, k)) : sq_final_exp_exact(x, xo, f12_coef(f, k));
+      sx_gt_bytes(out_sx, k, g);
+    });
+  for (auto& t : th) t.join();
+  pthread_barrier_destroy(&b);
   return memcmp(out_sx, out_ref, 384) != 0;
 }
 

@@ -28,6 +28,15 @@ def test_sextet_final_exp(sx, seed, variant):
     assert bytes(a) == bytes(b)
 
 
+@pytest.mark.parametrize("variant", [0, 1], ids=["exact", "fuentes"])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_sextet_final_exp_carry_free(sx, seed, variant):
+    # dev/sx29.h: the 29-bit balanced-limb accumulation the device kernels run
+    a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
+    assert sx.sxe_fexp29(seed, variant, a, b) == 0
+    assert bytes(a) == bytes(b)
+
+
 @pytest.mark.parametrize("case", ["both", "p2_inf", "p1_inf", "q2_inf"])
 def test_sextet_miller(sx, case):
     rng = random.Random(case)
