@@ -230,6 +230,69 @@ FTS_HD fp f29_to_fp(const f29& a) {
   return o;
 }
 
+// ------------------------------------------------- balanced form, Fp2 (q2)
+// The pairing side (dev/sx29.h) keeps values BALANCED: limbs 0..7 in
+// [-2^28, 2^28), |value| <= p/2 + e, so that a 64-bit column can absorb 117
+// limb products of at most 2^56 each.
+struct q2 {
+  f29 c0, c1;
+};
+
+static constexpr int32_t F29_HALF = 1 << 28;
+
+// balanced low digit of a 64-bit accumulator: lo = acc mod 2^29 in [-2^28, 2^28)
+FTS_HD int32_t f29_bdigit(int64_t acc) {
+  return (int32_t)(((uint32_t)acc + (uint32_t)F29_HALF) & (uint32_t)F29_MASK) - F29_HALF;
+}
+
+// ca a + cb b - q p, balanced (|result| <= p/2 + e).  |ca|, |cb| <= 16 and
+// inputs with |limb| <= 2^29: every term fits the 64-bit sweep.
+FTS_HD f29 f29_lin2(const f29& a, int32_t ca, const f29& b, int32_t cb) {
+  double t = (double)ca * ((double)a.l[8] * 536870912.0 + (double)a.l[7]) +
+             (double)cb * ((double)b.l[8] * 536870912.0 + (double)b.l[7]);
+  const int32_t q = (int32_t)__builtin_rint(t * P29_TOP_INV);
+  f29 r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (int64_t)ca * a.l[i] + (int64_t)cb * b.l[i] - (int64_t)q * P29B[i];
+    if (i < 8) {
+      const int32_t lo = f29_bdigit(acc);
+      r.l[i] = lo;
+      acc = (acc - lo) >> 29;
+    } else {
+      r.l[8] = (int32_t)acc;
+    }
+  }
+  return r;
+}
+
+FTS_HD q2 q2_neg(const q2& a) { return {f29_neg(a.c0), f29_neg(a.c1)}; }
+FTS_HD q2 q2_conj(const q2& a) { return {a.c0, f29_neg(a.c1)}; }
+FTS_HD q2 q2_zero() {
+  q2 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.c0.l[i] = r.c1.l[i] = 0;
+  return r;
+}
+FTS_HD q2 q2_sel(bool c, const q2& a, const q2& b) {
+  q2 r;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    r.c0.l[i] = c ? a.c0.l[i] : b.c0.l[i];
+    r.c1.l[i] = c ? a.c1.l[i] : b.c1.l[i];
+  }
+  return r;
+}
+// xi a = (9 a0 - a1) + (a0 + 9 a1) u, reduced
+FTS_HD q2 q2_mul_xi(const q2& a) { return {f29_lin2(a.c0, 9, a.c1, -1), f29_lin2(a.c0, 1, a.c1, 9)}; }
+
+FTS_HD f29 f29_breduce(const f29& a) { return f29_lin2(a, 1, a, 0); }
+
+// canonical 32-bit Montgomery Fp2 <-> balanced form
+FTS_HD q2 q2_from_fp2(const fp2& a) { return {f29_breduce(f29_from_fp(a.c0)), f29_breduce(f29_from_fp(a.c1))}; }
+FTS_HD fp2 q2_to_fp2(const q2& a) { return {f29_to_fp(a.c0), f29_to_fp(a.c1)}; }
+
 // ---------------------------------------------------------------- G1 (a = 0)
 // Jacobian point in this form with an explicit infinity flag.  Coordinates
 // between operations: normalised, |value| <= 3p/2 (f29_reduce outputs or

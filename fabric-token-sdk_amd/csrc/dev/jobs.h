@@ -1096,7 +1096,8 @@ FTS_HD void job_g2lines(const G2Job& g, const PairJob& j, const uint32_t (*scal)
 //  phase B  the 88 Miller lines of t': each doubling / addition step runs as
 //           layers of one reduced Fp2 product per lane (dbl_step / add_step
 //           formulas), the running point T held identically by every lane;
-//           lanes 0..2 write the three evaluated coefficients of each line.
+//           the six lanes write the six Fp components of each evaluated line
+//           (balanced 29-bit form, EvLineDev).
 template <class X>
 FTS_HD void sx_job_g2lines(const X& x, const G2Job& g, const PairJob& j, const uint32_t (*scal)[8],
                            const G2Dev* tab, G2Dev* g2out, const G1Dev* pts, EvLineDev* lines, uint32_t idx,
@@ -1214,15 +1215,10 @@ FTS_HD void sx_job_g2lines(const X& x, const G2Job& g, const PairJob& j, const u
       TZ = x.get(SX_P + 3);
       x.sync();
     }
-    if (valid && k < 3) {
-      fp2 v = f2_pick(k, use ? l0 : f2_one(), use ? l1 : f2_zero(), use ? l3 : f2_zero(), l0, l0, l0);
-      uint32_t* o = &lines[(size_t)s * njobs + idx].w[16 * k];
-#pragma unroll
-      for (int q = 0; q < 8; q++) {
-        o[q] = v.c0.v[q];
-        o[8 + q] = v.c1.v[q];
-      }
-    }
+    // lane k converts and writes component k & 1 of coefficient k >> 1
+    const int m = k >> 1;
+    fp2 v = m == 0 ? (use ? l0 : f2_one()) : (m == 1 ? (use ? l1 : f2_zero()) : (use ? l3 : f2_zero()));
+    if (valid) evline_put(lines[(size_t)s * njobs + idx], m, k & 1, (k & 1) ? v.c1 : v.c0);
   }
 }
 

@@ -19,6 +19,7 @@
 // code (dev/tower.h, dev/pairing.h): same formulas, same line scaling, so the
 // results are bit-identical (checked on the host by tests/native/sx_emu.cpp).
 #pragma once
+#include "fp29.h"
 #include "fp_wide.h"
 #include "pairing.h"
 
@@ -416,29 +417,37 @@ FTS_HD void sx_gt_bytes(uint8_t* out, int k, const fp2& a) {
   limbs_to_be32(o + 32, t);
 }
 
-// Evaluated line of pair 2: l = c0 + c3 w + c4 w^3 (sx_mul_line_r operands).
+// Evaluated line of pair 2: l = c0 + c3 w + c4 w^3, stored in the balanced
+// 29-bit form of dev/fp29.h (the operand format of the carry-free Miller
+// kernel, dev/sx29.h sq_miller_f): coefficient m at w[18 m], its c0 limbs then
+// its c1 limbs.  Writers: evline_store (one lane) and sx_job_g2lines (lane k
+// writes component k & 1 of coefficient k >> 1); same bytes either way.
 struct EvLineDev {
-  uint32_t w[48];  // c0, c3, c4 as Fp2 (Montgomery, 16 words each)
+  int32_t w[54];
 };
+FTS_HD void evline_put(EvLineDev& d, int m, int part, const fp& v) {
+  f29 b = f29_breduce(f29_from_fp(v));
+#pragma unroll
+  for (int i = 0; i < 9; i++) d.w[18 * m + 9 * part + i] = b.l[i];
+}
 FTS_HD void evline_store(EvLineDev& d, const fp2& c0, const fp2& c3, const fp2& c4) {
   const fp2* v[3] = {&c0, &c3, &c4};
 #pragma unroll
-  for (int m = 0; m < 3; m++)
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      d.w[16 * m + i] = v[m]->c0.v[i];
-      d.w[16 * m + 8 + i] = v[m]->c1.v[i];
-    }
+  for (int m = 0; m < 3; m++) {
+    evline_put(d, m, 0, v[m]->c0);
+    evline_put(d, m, 1, v[m]->c1);
+  }
 }
-FTS_HD fp2 evline_ld(const EvLineDev& d, int m) {
-  fp2 a;
+FTS_HD q2 evline_ld29(const EvLineDev& d, int m) {
+  q2 a;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    a.c0.v[i] = d.w[16 * m + i];
-    a.c1.v[i] = d.w[16 * m + 8 + i];
+  for (int i = 0; i < 9; i++) {
+    a.c0.l[i] = d.w[18 * m + i];
+    a.c1.l[i] = d.w[18 * m + 9 + i];
   }
   return a;
 }
+FTS_HD fp2 evline_ld(const EvLineDev& d, int m) { return q2_to_fp2(evline_ld29(d, m)); }
 
 // ----------------------------------------------------------------- Miller loop
 // State of pair 2 (T, Q, P2) and the evaluated lines live in LDS slots so the

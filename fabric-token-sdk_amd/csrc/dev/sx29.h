@@ -25,65 +25,6 @@
 
 namespace fts {
 
-struct q2 {
-  f29 c0, c1;
-};
-
-static constexpr int32_t F29_HALF = 1 << 28;
-
-// balanced low digit of a 64-bit accumulator: lo = acc mod 2^29 in [-2^28, 2^28)
-FTS_HD int32_t f29_bdigit(int64_t acc) {
-  return (int32_t)(((uint32_t)acc + (uint32_t)F29_HALF) & (uint32_t)F29_MASK) - F29_HALF;
-}
-
-// ca a + cb b - q p, balanced (|result| <= p/2 + e).  |ca|, |cb| <= 16 and
-// inputs with |limb| <= 2^29: every term fits the 64-bit sweep.
-FTS_HD f29 f29_lin2(const f29& a, int32_t ca, const f29& b, int32_t cb) {
-  double t = (double)ca * ((double)a.l[8] * 536870912.0 + (double)a.l[7]) +
-             (double)cb * ((double)b.l[8] * 536870912.0 + (double)b.l[7]);
-  const int32_t q = (int32_t)__builtin_rint(t * P29_TOP_INV);
-  f29 r;
-  int64_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    acc += (int64_t)ca * a.l[i] + (int64_t)cb * b.l[i] - (int64_t)q * P29B[i];
-    if (i < 8) {
-      const int32_t lo = f29_bdigit(acc);
-      r.l[i] = lo;
-      acc = (acc - lo) >> 29;
-    } else {
-      r.l[8] = (int32_t)acc;
-    }
-  }
-  return r;
-}
-
-FTS_HD q2 q2_neg(const q2& a) { return {f29_neg(a.c0), f29_neg(a.c1)}; }
-FTS_HD q2 q2_conj(const q2& a) { return {a.c0, f29_neg(a.c1)}; }
-FTS_HD q2 q2_zero() {
-  q2 r;
-#pragma unroll
-  for (int i = 0; i < 9; i++) r.c0.l[i] = r.c1.l[i] = 0;
-  return r;
-}
-FTS_HD q2 q2_sel(bool c, const q2& a, const q2& b) {
-  q2 r;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    r.c0.l[i] = c ? a.c0.l[i] : b.c0.l[i];
-    r.c1.l[i] = c ? a.c1.l[i] : b.c1.l[i];
-  }
-  return r;
-}
-// xi a = (9 a0 - a1) + (a0 + 9 a1) u, reduced
-FTS_HD q2 q2_mul_xi(const q2& a) { return {f29_lin2(a.c0, 9, a.c1, -1), f29_lin2(a.c0, 1, a.c1, 9)}; }
-
-FTS_HD f29 f29_breduce(const f29& a) { return f29_lin2(a, 1, a, 0); }
-
-// canonical 32-bit Montgomery Fp2 <-> balanced form
-FTS_HD q2 q2_from_fp2(const fp2& a) { return {f29_breduce(f29_from_fp(a.c0)), f29_breduce(f29_from_fp(a.c1))}; }
-FTS_HD fp2 q2_to_fp2(const q2& a) { return {f29_to_fp(a.c0), f29_to_fp(a.c1)}; }
-
 // ----------------------------------------------------------- accumulation
 struct W29 {
   int64_t re[17], im[17];
@@ -255,16 +196,45 @@ FTS_HD q2 sq_expt(X x, q2 a) {
   return r;
 }
 
-// The two final exponentiations (same sequences as sx_final_exp_exact /
-// sx_final_exp).  xo is the 32-bit context on the same LDS region, used for the
-// inversion only; every slot it writes is dead once sx_inv returns.
-template <class X, class XO>
-FTS_HD fp2 sq_final_exp_exact(const X& x, const XO& xo, const fp2& f) {
+// f^-1 (as sx_inv): den = f conj(f) in Fp6 (even lanes), the Fp6 inverse by
+// the f6_inv formula with one Fp2 inversion per lane (32-bit code, converted)
+template <class X>
+FTS_HD q2 sq_inv(X x, q2 f) {
   const int k = x.k;
-  fp2 fi = sx_inv(xo, f);
-  xo.sync();
+  q2 fc = sq_conj(k, f);
+  q2 d = sq_mulv(x, fc, f);  // lanes 0, 2, 4: d0, d1, d2; odd lanes 0
+  sq_pub(x, SX_A, d);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 2; t++) {
+    uint32_t e = term_at(SX_INV_TAB[t], k);
+    q2 u = x.get(e & 63), v = x.get((e >> 6) & 63);
+    v = q2_sel((e & TM_NEG) != 0, q2_neg(v), v);
+    w29_mac(w, q2_sel((e & TM_ZERO) != 0, q2_zero(), u), v);
+  }
+  q2 t = w29_reduce(w);
+  x.put(SX_P + k, t);
+  x.sync();
+  W29 v;
+  w29_init(v);
+#pragma nounroll
+  for (int s = 0; s < 3; s++) w29_mac(v, x.get(s == 0 ? SX_A + 0 : (s == 1 ? SX_AX + 4 : SX_AX + 2)), x.get(SX_P + s));
+  q2 tk = x.get(SX_P + (k >> 1));
+  x.sync();
+  fp2 di = f2_inv(q2_to_fp2(w29_reduce(v)));
+  q2 inv6 = q2_sel((k & 1) == 0, q2_mul(tk, q2_from_fp2(di)), q2_zero());
+  return sq_mulv(x, fc, inv6);
+}
+
+// The two final exponentiations (same sequences as sx_final_exp_exact /
+// sx_final_exp)
+template <class X>
+FTS_HD fp2 sq_final_exp_exact(const X& x, const fp2& f) {
+  const int k = x.k;
   q2 F = q2_from_fp2(f);
-  q2 m = sq_mulv(x, sq_conj(k, F), q2_from_fp2(fi));
+  q2 m = sq_mulv(x, sq_conj(k, F), sq_inv(x, F));
   m = sq_mulv(x, sq_frob2(k, m), m);
   q2 in = m, mx, mx2, mx3;
 #pragma nounroll
@@ -294,12 +264,11 @@ FTS_HD fp2 sq_final_exp_exact(const X& x, const XO& xo, const fp2& f) {
   return q2_to_fp2(sq_mulv(x, sq_cyc_sqr(x, t0), t1));
 }
 
-template <class X, class XO>
-FTS_HD fp2 sq_final_exp(const X& x, const XO& xo, const fp2& f) {
+template <class X>
+FTS_HD fp2 sq_final_exp(const X& x, const fp2& f) {
   const int k = x.k;
-  fp2 fi = sx_inv(xo, f);
-  xo.sync();
-  q2 t = sq_mulv(x, sq_conj(k, q2_from_fp2(f)), q2_from_fp2(fi));
+  q2 F = q2_from_fp2(f);
+  q2 t = sq_mulv(x, sq_conj(k, F), sq_inv(x, F));
   t = sq_mulv(x, sq_frob2(k, t), t);
   q2 in = t, a2, a6, b, c;
 #pragma nounroll
@@ -325,10 +294,106 @@ FTS_HD fp2 sq_final_exp(const X& x, const XO& xo, const fp2& f) {
   return q2_to_fp2(res);
 }
 
-// LDS bytes per sextet for the final exponentiation: the q2 slots, which also
-// hold the 32-bit slots of the inversion (aliased, used one after the other)
-static constexpr uint32_t SQ_FEXP_BYTES =
-    SX_SLOTS_FEXP * sizeof(Q2Slot) > SX_SLOTS_FEXP * sizeof(F2Slot) ? SX_SLOTS_FEXP * sizeof(Q2Slot)
-                                                                   : SX_SLOTS_FEXP * sizeof(F2Slot);
+// ----------------------------------------------------------- Miller f-chain
+// Lines of the fixed Q (precompute_lines order) in the balanced form, built
+// once per context (k_qlines).
+struct LineCoef29 {
+  q2 r0, r1, r2;
+};
+FTS_HD LineCoef29 linecoef29(const LineCoef& l) { return {q2_from_fp2(l.r0), q2_from_fp2(l.r1), q2_from_fp2(l.r2)}; }
+
+// a b / 2^261 balanced (one row of the accumulation)
+FTS_HD f29 f29_mulb(const f29& a, const f29& b) {
+  int64_t c[17];
+#pragma unroll
+  for (int i = 0; i < 17; i++) c[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+#pragma unroll
+    for (int j = 0; j < 9; j++) c[i + j] += (int64_t)a.l[i] * b.l[j];
+  return w29_redc(c);
+}
+
+// c = a^2 (as sx_sqr): a, xi a and 2 a published (2 a unreduced: its limbs
+// are within 2^29 and SX_SQR4_TAB gives every lane at most 6 operand units)
+template <class X>
+FTS_HD q2 sq_sqr(X x, q2 a) {
+  sq_pub(x, SX_A, a);
+  x.put(SX_A2 + x.k, {f29_add(a.c0, a.c0), f29_add(a.c1, a.c1)});
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 4; t++) {
+    uint32_t e = term_at(SX_SQR4_TAB[t], x.k);
+    q2 u = x.get(e & 63);
+    q2 v = x.get((e >> 6) & 63);
+    w29_mac(w, q2_sel((e & TM_ZERO) != 0, q2_zero(), u), v);
+  }
+  x.sync();
+  return w29_reduce(w);
+}
+
+// f * (l0 + l1 w + l3 w^3), the line in registers of every lane (as sx_mul_line_r)
+template <class X>
+FTS_HD q2 sq_mul_line_r(const X& x, const q2& f, const q2& l0, const q2& l1, const q2& l3) {
+  sq_pub(x, SX_A, f);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 3; t++) {
+    int j = x.k - (t == 0 ? 0 : (t == 1 ? 1 : 3));
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w29_mac(w, t == 0 ? l0 : (t == 1 ? l1 : l3), x.get(sb));
+  }
+  x.sync();
+  return w29_reduce(w);
+}
+
+// f * (fixed-Q line at P1) (as sx_fixed_line): lanes 0..3 form r0.c0 yP,
+// r0.c1 yP, r1.c0 xP, r1.c1 xP and exchange them through SX_P
+template <class X>
+FTS_HD q2 sq_fixed_line(const X& x, const q2& f, const LineCoef29& q, const f29& yP, const f29& xP, bool inf) {
+  const int k = x.k;
+  f29 a = (k == 0) ? q.r0.c0 : (k == 1) ? q.r0.c1 : (k == 2) ? q.r1.c0 : q.r1.c1;
+  f29 prod = f29_mulb(a, k < 2 ? yP : xP);
+  x.put(SX_P + k, {prod, prod});
+  x.sync();
+  q2 l0 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
+  q2 l1 = {x.get(SX_P + 2).c0, x.get(SX_P + 3).c0};
+  q2 one = {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1};
+  l0 = q2_sel(inf, one, l0);
+  l1 = q2_sel(inf, q2_zero(), l1);
+  q2 l3 = q2_sel(inf, q2_zero(), q.r2);
+  return sq_mul_line_r(x, f, l0, l1, l3);
+}
+
+// 2-pair Miller loop, pair-2 lines precomputed (as sx_miller_f)
+template <class X>
+FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const EvLineDev* l2, uint32_t njobs) {
+  const f29 yP = f29_breduce(f29_from_fp(P1.y)), xP = f29_breduce(f29_from_fp(P1.x));
+  q2 one = {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1};
+  q2 f = q2_sel(x.k == 0, one, q2_zero());
+#pragma nounroll
+  for (int s = 0; s < MILLER_LINES; s++) {
+    bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
+    if (sq) f = sq_sqr(x, f);
+    f = sq_fixed_line(x, f, qlines[s], yP, xP, P1.inf);
+    const EvLineDev& e = l2[(size_t)s * njobs];
+    f = sq_mul_line_r(x, f, evline_ld29(e, 0), evline_ld29(e, 1), evline_ld29(e, 2));
+  }
+  return f;
+}
+
+// LDS dwords per sextet region: NS slots of 18 dwords, padded so that the
+// regions of a wave's ten sextets start on distinct even banks (stride = 2 x odd
+// mod 64): the b64 reads of the ten sextets, each broadcast to its six lanes,
+// then never share a bank.
+constexpr uint32_t sq_region_dwords(uint32_t ns) {
+  uint32_t s = ns * 18;
+  while ((s % 64) % 4 != 2) s += 2;
+  return s;
+}
 
 }  // namespace fts

@@ -6,6 +6,7 @@
 #include "dev/jobs.h"
 #include "dev/msm.h"
 #include "dev/idemix.h"
+#include "dev/sx29.h"
 
 using namespace fts;
 
@@ -34,6 +35,20 @@ struct SyncWave {
   uint32_t jc = job_ < (n) ? job_ : (n) - 1;                            \
   Sx<SyncWave> x{k_, (SlotT*)(sx_raw_ + sx_ * sx_stride_), !ghost_, {}};
 
+// The same for the carry-free sextet kernels (dev/sx29.h): NS Q2 slots per
+// sextet in a region of sq_region_dwords(NS) dwords.
+#define SQ_KERNEL_PROLOGUE(n, NS)                                                 \
+  static constexpr uint32_t sq_stride_ = sq_region_dwords(NS) / 2;               \
+  __shared__ uint2 sq_raw_[SX_JOBS_PER_WAVE * sq_stride_];                       \
+  uint32_t lane_ = threadIdx.x, sx_ = lane_ / 6;                                 \
+  bool ghost_ = sx_ >= SX_JOBS_PER_WAVE;                                         \
+  int k_ = ghost_ ? (int)(lane_ - 6 * SX_JOBS_PER_WAVE) : (int)(lane_ - 6 * sx_); \
+  if (ghost_) sx_ = SX_JOBS_PER_WAVE - 1;                                        \
+  uint32_t job_ = blockIdx.x * SX_JOBS_PER_WAVE + sx_;                           \
+  bool valid = !ghost_ && job_ < (n);                                            \
+  uint32_t jc = job_ < (n) ? job_ : (n) - 1;                                     \
+  Sq<SyncWave> x{k_, (QSlotT*)(sq_raw_ + sx_ * sq_stride_), !ghost_, {}};
+
 __global__ void k_decode(const DecodeJob* jobs, uint32_t n, const uint8_t* wire, G1Dev* pts, uint8_t* pt_ok,
                          uint8_t* arena);
 __global__ void k_zr(const ZrJob* jobs, uint32_t n, const uint8_t* wire, uint32_t (*scal)[8], uint8_t* canon);
@@ -58,9 +73,9 @@ __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const 
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
 __global__ void k_tab_g2_bw(const G2Dev* bases, G2Dev* bw);
 __global__ void k_tab_g2_fill(const G2Dev* bw, uint32_t chunk, uint32_t (*jt)[48], uint32_t (*zs)[16], G2Dev* tab);
-__global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef* qlines, const EvLineDev* lines2,
+__global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef29* qlines, const EvLineDev* lines2,
                          const G1Dev* g1out, F12Dev* fbuf);
-__global__ void k_qlines(const G2Dev* q, LineCoef* out, int* n);
+__global__ void k_qlines(const G2Dev* q, LineCoef* out, LineCoef29* out29, int* n);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 __global__ void k_fexp_exact(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 

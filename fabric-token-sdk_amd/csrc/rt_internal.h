@@ -16,6 +16,7 @@
 
 #include "../../include/ftsamd.h"
 #include "dev/jobs.h"
+#include "dev/sx29.h"
 #include "host/planner.h"
 
 using namespace fts;
@@ -100,6 +101,7 @@ struct ftz_ctx {
   DBuf<G1Dev> g1tab;
   DBuf<G2Dev> g2tab;
   DBuf<LineCoef> qlines;
+  DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)
   ftz_options opt;                   // resolved options (ftz_ctx_create_ex)
   int serial = 0;                    // profiling: every kernel of a batch on one stream
   WorkPool* pool = nullptr;          // host planning threads

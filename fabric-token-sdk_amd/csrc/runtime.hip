@@ -195,7 +195,7 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     }
     uint32_t t1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, t2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
     if (c->g1tab.alloc(t1) != hipSuccess || c->g2tab.alloc(t2) != hipSuccess ||
-        c->qlines.alloc(MILLER_LINES) != hipSuccess) {
+        c->qlines.alloc(MILLER_LINES) != hipSuccess || c->qlines29.alloc(MILLER_LINES) != hipSuccess) {
       fail(FTZ_E_NOMEM, "table allocation failed");
       break;
     }
@@ -236,7 +236,7 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
       fail(FTZ_E_NOMEM, "alloc");
       break;
     }
-    k_qlines<<<1, 64, 0, c->stream>>>(d_g2.p + 3, c->qlines.p, d_n.p);
+    k_qlines<<<1, 64, 0, c->stream>>>(d_g2.p + 3, c->qlines.p, c->qlines29.p, d_n.p);
     int nl = 0;
     if (hipMemcpyAsync(&nl, d_n.p, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess || nl != MILLER_LINES) {
@@ -277,6 +277,7 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   c->g1tab.alloc(0);
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
+  c->qlines29.alloc(0);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c->pool;
   delete c;
@@ -569,7 +570,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (p.n_pr)
-    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines.p, p.lines2, p.g1out,
+    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
                                                                  p.fbuf);
   HC(hipEventRecord(e[7], s));
   launch_fexp(c, p, s);
@@ -786,7 +787,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (p.n_pr)
-    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines.p, p.lines2, p.g1out,
+    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
                                                                  p.fbuf);
   HC(hipEventRecord(e[7], s));
   launch_fexp(c, p, s);

@@ -39,6 +39,22 @@ void run6(const std::function<void(const SxH&)>& body) {
   pthread_barrier_destroy(&b);
 }
 
+typedef Sq<SyncHost> SqH;
+void run6q(const std::function<void(const SqH&)>& body) {
+  std::vector<Q2Slot> slots(SX_SLOTS_FEXP);
+  memset(slots.data(), 0xA5, slots.size() * sizeof(Q2Slot));
+  pthread_barrier_t b;
+  pthread_barrier_init(&b, nullptr, 6);
+  std::vector<std::thread> th;
+  for (int k = 0; k < 6; k++)
+    th.emplace_back([&, k] {
+      SqH x{k, slots.data(), true, {&b}};
+      body(x);
+    });
+  for (auto& t : th) t.join();
+  pthread_barrier_destroy(&b);
+}
+
 uint32_t xs(uint32_t& s) {
   s ^= s << 13;
   s ^= s >> 17;
@@ -148,27 +164,15 @@ int sxe_fexp(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
   return memcmp(out_sx, out_ref, 384) != 0;
 }
 
-// the same with the carry-free sextet final exponentiation (dev/sx29.h): the
-// 32-bit and 29-bit contexts share one slot region, as on the device
+// the same with the carry-free sextet final exponentiation (dev/sx29.h)
 int sxe_fexp29(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
   uint32_t s = seed | 1;
   fp12 f = rnd_f12(s);
   f12_to_bytes(out_ref, final_exp(f, variant));
-  std::vector<uint8_t> raw(SQ_FEXP_BYTES + 64);
-  memset(raw.data(), 0xA5, raw.size());
-  uint8_t* base = raw.data() + (64 - ((uintptr_t)raw.data() & 63)) % 64;
-  pthread_barrier_t b;
-  pthread_barrier_init(&b, nullptr, 6);
-  std::vector<std::thread> th;
-  for (int k = 0; k < 6; k++)
-    th.emplace_back([&, k] {
-      SxH xo{k, (F2Slot*)base, true, {&b}};
-      Sq<SyncHost> x{k, (Q2Slot*)base, true, {&b}};
-      fp2 g = variant == 1 ? sq_final_exp(x, xo, f12_coef(f, k)) : sq_final_exp_exact(x, xo, f12_coef(f, k));
-      sx_gt_bytes(out_sx, k, g);
-    });
-  for (auto& t : th) t.join();
-  pthread_barrier_destroy(&b);
+  run6q([&](const SqH& x) {
+    fp2 g = variant == 1 ? sq_final_exp(x, f12_coef(f, x.k)) : sq_final_exp_exact(x, f12_coef(f, x.k));
+    sx_gt_bytes(out_sx, x.k, g);
+  });
   return memcmp(out_sx, out_ref, 384) != 0;
 }
 
@@ -192,6 +196,23 @@ int sxe_miller(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2, const ui
   f12_to_bytes(out_ref, want);
   f12_to_bytes(out_sx, from_coefs(got));
   return memcmp(out_sx, out_ref, 384) != 0;
+}
+
+// carry-free Miller f-chain (dev/sx29.h sq_miller_f, the device path) vs the
+// one-lane miller_2: 0 = equal
+int sxe_miller29(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2b, const uint8_t* qfix) {
+  std::vector<LineCoef> ql(MILLER_LINES);
+  precompute_lines(ql.data(), ld_g2(qfix));
+  std::vector<LineCoef29> ql29(MILLER_LINES);
+  for (int i = 0; i < MILLER_LINES; i++) ql29[i] = linecoef29(ql[i]);
+  g1a P1 = ld_g1(p1), P2 = ld_g1(p2);
+  g2a Q2 = ld_g2(q2b);
+  fp12 want = miller_2(ql.data(), P1, P2, Q2);
+  std::vector<EvLineDev> l2(MILLER_LINES);
+  g2lines_emit(Q2, P2, l2.data(), 0, 1);
+  fp2 got[6];
+  run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l2.data(), 1)); });
+  return f12_eq(from_coefs(got), want) ? 0 : 1;
 }
 
 // G2 job + pair-2 lines: sextet (sx_job_g2lines) vs one lane (job_g2lines).

@@ -52,6 +52,7 @@ def test_sextet_miller(sx, case):
         q2 = bytes(128)
     a, b = (ctypes.c_uint8 * 384)(), (ctypes.c_uint8 * 384)()
     assert sx.sxe_miller(p1, p2, q2, qf, a, b) == 0
+    assert sx.sxe_miller29(p1, p2, q2, qf) == 0  # the carry-free f-chain of the device kernel
 
 
 @pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar"])
