@@ -1065,7 +1065,7 @@ FTS_HD void g2lines_emit(const g2a& Q, const g1a& P, EvLineDev* lines, uint32_t 
     fp2 c0 = use ? f2_mul_fp(l.r0, P.y) : f2_one();
     fp2 c3 = use ? f2_mul_fp(l.r1, P.x) : f2_zero();
     fp2 c4 = use ? l.r2 : f2_zero();
-    evline_store(lines[(size_t)n * njobs + idx], c0, c3, c4);
+    evline_store(lines, n, idx, njobs, c0, c3, c4);
     n++;
   };
 #pragma nounroll
@@ -1215,17 +1215,17 @@ FTS_HD void sx_job_g2lines(const X& x, const G2Job& g, const PairJob& j, const u
       TZ = x.get(SX_P + 3);
       x.sync();
     }
-    // lane k converts and writes component k & 1 of coefficient k >> 1
+    // lane k converts and writes component k (part k & 1 of coefficient k >> 1)
     const int m = k >> 1;
     fp2 v = m == 0 ? (use ? l0 : f2_one()) : (m == 1 ? (use ? l1 : f2_zero()) : (use ? l3 : f2_zero()));
-    if (valid) evline_put(lines[(size_t)s * njobs + idx], m, k & 1, (k & 1) ? v.c1 : v.c0);
+    if (valid) evline_put(lines, s, k, idx, njobs, (k & 1) ? v.c1 : v.c0);
   }
 }
 
 template <class X>
 FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, const EvLineDev* lines2,
                           const G1Dev* g1out, F12Dev* fout, uint32_t idx, uint32_t njobs, bool valid) {
-  fp2 f = sx_miller_f(x, qlines, g1_load(g1out[j.p1]), lines2 + idx, njobs);
+  fp2 f = sx_miller_f(x, qlines, g1_load(g1out[j.p1]), lines2, idx, njobs);
   if (valid) {
     uint32_t* o = &fout[idx].w[16 * sx_f12_index(x.k)];
 #pragma unroll

@@ -417,37 +417,52 @@ FTS_HD void sx_gt_bytes(uint8_t* out, int k, const fp2& a) {
   limbs_to_be32(o + 32, t);
 }
 
-// Evaluated line of pair 2: l = c0 + c3 w + c4 w^3, stored in the balanced
-// 29-bit form of dev/fp29.h (the operand format of the carry-free Miller
-// kernel, dev/sx29.h sq_miller_f): coefficient m at w[18 m], its c0 limbs then
-// its c1 limbs.  Writers: evline_store (one lane) and sx_job_g2lines (lane k
-// writes component k & 1 of coefficient k >> 1); same bytes either way.
+// Evaluated lines of pair 2: l = c0 + c3 w + c4 w^3, in the balanced 29-bit
+// form of dev/fp29.h (the operand format of the carry-free Miller kernel,
+// dev/sx29.h sq_miller_f).  Component planes: component c = 2 m + part (part 0:
+// c0 limbs, 1: c1 limbs) of line s of job idx is a 10-word record (9 limbs and
+// a zero pad, 8-byte aligned) at ((s * 6 + c) * njobs + idx) * 10, so that the
+// ten sextets of a wave, which handle consecutive jobs, write and read each
+// plane contiguously.  Writers: evline_store (one lane) and sx_job_g2lines
+// (lane k writes component k); same bytes either way.  EvLineDev is the size
+// of one (line, job).
+static constexpr uint32_t EVL_REC = 10;
 struct EvLineDev {
-  int32_t w[54];
+  int32_t w[6 * EVL_REC];
 };
-FTS_HD void evline_put(EvLineDev& d, int m, int part, const fp& v) {
-  f29 b = f29_breduce(f29_from_fp(v));
-#pragma unroll
-  for (int i = 0; i < 9; i++) d.w[18 * m + 9 * part + i] = b.l[i];
+FTS_HD size_t evl_off(uint32_t s, int c, uint32_t idx, uint32_t njobs) {
+  return (((size_t)s * 6 + c) * njobs + idx) * EVL_REC;
 }
-FTS_HD void evline_store(EvLineDev& d, const fp2& c0, const fp2& c3, const fp2& c4) {
+FTS_HD void evline_put(EvLineDev* base, uint32_t s, int c, uint32_t idx, uint32_t njobs, const fp& v) {
+  f29 b = f29_breduce(f29_from_fp(v));
+  int32_t* o = (int32_t*)base + evl_off(s, c, idx, njobs);
+#pragma unroll
+  for (int i = 0; i < 9; i++) o[i] = b.l[i];
+  o[9] = 0;
+}
+FTS_HD void evline_store(EvLineDev* base, uint32_t s, uint32_t idx, uint32_t njobs, const fp2& c0, const fp2& c3,
+                         const fp2& c4) {
   const fp2* v[3] = {&c0, &c3, &c4};
 #pragma unroll
   for (int m = 0; m < 3; m++) {
-    evline_put(d, m, 0, v[m]->c0);
-    evline_put(d, m, 1, v[m]->c1);
+    evline_put(base, s, 2 * m, idx, njobs, v[m]->c0);
+    evline_put(base, s, 2 * m + 1, idx, njobs, v[m]->c1);
   }
 }
-FTS_HD q2 evline_ld29(const EvLineDev& d, int m) {
+FTS_HD q2 evline_ld29(const EvLineDev* base, uint32_t s, int m, uint32_t idx, uint32_t njobs) {
+  const int32_t* a0 = (const int32_t*)base + evl_off(s, 2 * m, idx, njobs);
+  const int32_t* a1 = (const int32_t*)base + evl_off(s, 2 * m + 1, idx, njobs);
   q2 a;
 #pragma unroll
   for (int i = 0; i < 9; i++) {
-    a.c0.l[i] = d.w[18 * m + i];
-    a.c1.l[i] = d.w[18 * m + 9 + i];
+    a.c0.l[i] = a0[i];
+    a.c1.l[i] = a1[i];
   }
   return a;
 }
-FTS_HD fp2 evline_ld(const EvLineDev& d, int m) { return q2_to_fp2(evline_ld29(d, m)); }
+FTS_HD fp2 evline_ld(const EvLineDev* base, uint32_t s, int m, uint32_t idx, uint32_t njobs) {
+  return q2_to_fp2(evline_ld29(base, s, m, idx, njobs));
+}
 
 // ----------------------------------------------------------------- Miller loop
 // State of pair 2 (T, Q, P2) and the evaluated lines live in LDS slots so the
@@ -645,15 +660,16 @@ static constexpr SqrMask MILLER_SQR = miller_sqr_mask();
 // 2-pair Miller loop with pair 2's lines precomputed per job (job_g2lines,
 // layout [line][job]): same factors, same order as miller_2.
 template <class X>
-FTS_HD fp2 sx_miller_f(const X& x, const LineCoef* qlines, const g1a& P1, const EvLineDev* l2, uint32_t njobs) {
+FTS_HD fp2 sx_miller_f(const X& x, const LineCoef* qlines, const g1a& P1, const EvLineDev* l2, uint32_t idx,
+                       uint32_t njobs) {
   fp2 f = f2_sel(x.k == 0, f2_one(), f2_zero());
 #pragma nounroll
   for (int s = 0; s < MILLER_LINES; s++) {
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sx_sqr(x, f);
     f = sx_fixed_line(x, f, qlines + s, P1);
-    const EvLineDev& e = l2[(size_t)s * njobs];
-    f = sx_mul_line_r(x, f, evline_ld(e, 0), evline_ld(e, 1), evline_ld(e, 2));
+    f = sx_mul_line_r(x, f, evline_ld(l2, s, 0, idx, njobs), evline_ld(l2, s, 1, idx, njobs),
+                      evline_ld(l2, s, 2, idx, njobs));
   }
   return f;
 }

@@ -371,7 +371,8 @@ FTS_HD q2 sq_fixed_line(const X& x, const q2& f, const LineCoef29& q, const f29&
 
 // 2-pair Miller loop, pair-2 lines precomputed (as sx_miller_f)
 template <class X>
-FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const EvLineDev* l2, uint32_t njobs) {
+FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const EvLineDev* l2, uint32_t idx,
+                      uint32_t njobs) {
   const f29 yP = f29_breduce(f29_from_fp(P1.y)), xP = f29_breduce(f29_from_fp(P1.x));
   q2 one = {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1};
   q2 f = q2_sel(x.k == 0, one, q2_zero());
@@ -380,8 +381,8 @@ FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sq_sqr(x, f);
     f = sq_fixed_line(x, f, qlines[s], yP, xP, P1.inf);
-    const EvLineDev& e = l2[(size_t)s * njobs];
-    f = sq_mul_line_r(x, f, evline_ld29(e, 0), evline_ld29(e, 1), evline_ld29(e, 2));
+    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
+                      evline_ld29(l2, s, 2, idx, njobs));
   }
   return f;
 }

@@ -14,7 +14,7 @@ __global__ void __launch_bounds__(64, 2) k_miller(const PairJob* jobs, uint32_t 
                                                   const EvLineDev* lines2, const G1Dev* g1out, F12Dev* fbuf) {
   SQ_KERNEL_PROLOGUE(n, SX_SLOTS_MILLER_F)
   const PairJob& j = jobs[jc];
-  fp2 f = q2_to_fp2(sq_miller_f(x, qlines, g1_load(g1out[j.p1]), lines2 + jc, n));
+  fp2 f = q2_to_fp2(sq_miller_f(x, qlines, g1_load(g1out[j.p1]), lines2, jc, n));
   if (valid) {
     uint32_t* o = &fbuf[jc].w[16 * sx_f12_index(x.k)];
 #pragma unroll

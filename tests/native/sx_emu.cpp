@@ -191,7 +191,7 @@ int sxe_miller(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2, const ui
   std::vector<EvLineDev> l2(MILLER_LINES);
   g2lines_emit(Q2, P2, l2.data(), 0, 1);
   fp2 got2[6];
-  run6([&](const SxH& x) { got2[x.k] = sx_miller_f(x, ql.data(), P1, l2.data(), 1); });
+  run6([&](const SxH& x) { got2[x.k] = sx_miller_f(x, ql.data(), P1, l2.data(), 0, 1); });
   if (!f12_eq(from_coefs(got2), want)) return 2;
   f12_to_bytes(out_ref, want);
   f12_to_bytes(out_sx, from_coefs(got));
@@ -211,7 +211,7 @@ int sxe_miller29(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2b, const
   std::vector<EvLineDev> l2(MILLER_LINES);
   g2lines_emit(Q2, P2, l2.data(), 0, 1);
   fp2 got[6];
-  run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l2.data(), 1)); });
+  run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l2.data(), 0, 1)); });
   return f12_eq(from_coefs(got), want) ? 0 : 1;
 }
 
