@@ -353,6 +353,8 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
     ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
     ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
+    ap.add_argument("--layout", default=os.environ.get("FTZ_LAYOUT", ""),
+                    help="kernel layouts, e.g. 'g2lines=sextet,pairing=one_lane' (ftz_ctx_set_layout)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -373,6 +375,9 @@ def main():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
     ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch, slots=args.slots, threads=args.threads)
+    for kv in filter(None, (args.layout or "").split(",")):  # profiling A/B: stage=layout
+        stage, layout = kv.split("=")
+        ctx.set_layout(stage, layout)
     t_setup = time.time()
     valid = W.prove_distinct(ctx, args.distinct, tag=b"bench/%d" % rank)
     bad = W.golden_tampered()

@@ -26,6 +26,14 @@ __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJo
   sx_job_g2lines(x, g2[jc], pr[jc], scal, tab, g2out, pts, lines, jc, n, valid);
 }
 
+// The same in the one-lane layout (job_g2lines): 64 jobs per wave.
+__global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n,
+                                                 const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out,
+                                                 const G1Dev* pts, EvLineDev* lines) {
+  JOB_KERNEL_PROLOGUE(n);
+  job_g2lines(g2[i], pr[i], scal, tab, g2out, pts, lines, i, n);
+}
+
 // ---- wide-window G2 tables (C > 8), as k_tab_g1_bw / k_tab_g1_fill
 __global__ void __launch_bounds__(64) k_tab_g2_bw(const G2Dev* bases, G2Dev* bw) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

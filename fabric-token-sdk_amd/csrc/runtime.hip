@@ -299,6 +299,14 @@ extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  if (layout != FTZ_LAYOUT_ONE_LANE && layout != FTZ_LAYOUT_SEXTET) return set_err(FTZ_E_INVALID, "unknown layout");
+  if (stage != FTZ_STAGE_G2LINES) return set_err(FTZ_E_INVALID, "unknown stage");
+  c->g2lanes = layout;
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_pp_validate(const uint8_t* pp, size_t pp_len) {
   if (!pp) return set_err(FTZ_E_INVALID, "null argument");
   std::string e = validate_pp(pp, pp_len, "zkatdlog");
@@ -504,6 +512,21 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   return p;
 }
 
+// t' and the pair-2 lines (R read from `pts`): one lane per job (default,
+// k_g2lines1) or the sextet layout (k_g2lines); same bytes either way
+static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s) {
+  if (c->g2lanes == FTZ_LAYOUT_ONE_LANE)
+    k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts, p.lines2);
+  else
+    k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,
+                                                                  p.lines2);
+}
+
+static void launch_miller(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
+  k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
+                                                                 p.fbuf);
+}
+
 static void launch_fexp(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
   if (!p.n_pr) return;
   if (c->opt.fexp == FTZ_FEXP_FUENTES)
@@ -547,8 +570,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   HC(hipStreamWaitEvent(s3, e[4], 0));
   HC(hipEventRecord(e[14], s3));
   if (p.n_g2)
-    k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out,
-                                                                   p.pts, p.lines2);
+    launch_g2lines(c, p, p.pts, s3);
   HC(hipEventRecord(e[15], s3));
   // st[0]: pairing chain
   HC(hipEventRecord(e[16], s));
@@ -570,8 +592,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (p.n_pr)
-    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
-                                                                 p.fbuf);
+    launch_miller(c, p, s);
   HC(hipEventRecord(e[7], s));
   launch_fexp(c, p, s);
   HC(hipEventRecord(e[8], s));
@@ -781,14 +802,12 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   HC(hipStreamWaitEvent(s3, e[5], 0));
   HC(hipEventRecord(e[14], s3));
   if (p.n_g2)
-    k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s3>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out,
-                                                                   p.g1out, p.lines2);
+    launch_g2lines(c, p, p.g1out, s3);
   HC(hipEventRecord(e[15], s3));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
   if (p.n_pr)
-    k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
-                                                                 p.fbuf);
+    launch_miller(c, p, s);
   HC(hipEventRecord(e[7], s));
   launch_fexp(c, p, s);
   HC(hipEventRecord(e[8], s));

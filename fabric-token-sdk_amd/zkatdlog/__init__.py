@@ -148,6 +148,14 @@ class Context:
         """profiling: every kernel of a batch on one stream (ftz_ctx_set_serial)"""
         _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)
 
+    LAYOUTS = {"one_lane": 1, "sextet": 6}
+    STAGES = {"g2lines": 0}
+
+    def set_layout(self, stage, layout):
+        """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines',
+        layout 'one_lane' (default) or 'sextet' -- same results, different speed"""
+        _check(self._lib.ftz_ctx_set_layout(self._h, self.STAGES[stage], self.LAYOUTS[layout]), self._lib)
+
     def verify_issues(self, issues):
         """issues: iterable of (outputs, proof, anonymous)."""
         arr, keep = _abi.pack_issues(issues)

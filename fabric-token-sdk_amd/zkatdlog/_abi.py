@@ -214,7 +214,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
-           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
+           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_set_layout", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
            "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
@@ -242,6 +242,7 @@ def load():
     lib.ftz_ctx_create.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
     lib.ftz_ctx_create_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(vp)]
     lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
+    lib.ftz_ctx_set_layout.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     lib.ftz_ctx_options.argtypes = [vp, ctypes.POINTER(Options)]
     lib.ftz_pp_validate.argtypes = [ctypes.c_char_p, sz]
     lib.ftz_pp_setup.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, sz, ctypes.c_int, ctypes.c_char_p,

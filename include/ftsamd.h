@@ -120,6 +120,14 @@ int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
 /* profiling: 1 = run every kernel of a batch on one stream (per-kernel times
  * without overlap), 0 = the normal three-stream schedule */
 int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
+/* profiling: kernel layout of a pipeline stage (results are identical; only
+ * speed differs).  stage FTZ_STAGE_G2LINES (t' = c PK0 + v PK1 + h PK2 and the
+ * 88 pair-2 Miller lines); layout FTZ_LAYOUT_ONE_LANE (one lane per job, the
+ * default) or FTZ_LAYOUT_SEXTET (six lanes per job, ten jobs per wave). */
+#define FTZ_STAGE_G2LINES 0
+#define FTZ_LAYOUT_ONE_LANE 1
+#define FTZ_LAYOUT_SEXTET 6
+int ftz_ctx_set_layout(ftz_ctx* ctx, int stage, int layout);
 /* crypto.PublicParams.Validate (setup.go:238-273) on serialized public
  * parameters, as the FSC node's loader runs it (nogh/loaders.go:133):
  * FTZ_SUCCESS, or FTZ_E_PP with the reference's error text in

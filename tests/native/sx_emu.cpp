@@ -12,6 +12,7 @@
 
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/g2l29.h"
 
 using namespace fts;
 
@@ -250,6 +251,68 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   for (int s = 0; s < MILLER_LINES; s++)
     if (memcmp(&l1[s], &l2[s], sizeof(EvLineDev))) return 2 + s;
   return 0;
+}
+
+// the literal constants of dev/g2l29.h against their conversions: 0 = equal
+int sxe_g2l29_consts() {
+  const q2 b3 = q2_scale(q2_from_fp2(f2_const(TWIST_B)), 3);
+  const q2 fx = q2_from_fp2(f2_const(TW_FROB_X)), fy = q2_from_fp2(f2_const(TW_FROB_Y));
+  const f29 want[9] = {b3.c0, b3.c1, fx.c0, fx.c1, fy.c0, fy.c1, f29_breduce(f29_from_fp(fe_const<ModP>(TW_FROB2_X))),
+                       f29_breduce(f29_from_fp(fe_const<ModP>(TW_FROB2_Y))), f29_breduce(f29_from_fp(fe_one<ModP>()))};
+  for (int i = 0; i < 9; i++)
+    for (int k = 0; k < 9; k++)
+      if (want[i].l[k] != G2L29_CONST[i][k]) return 1 + i;
+  return 0;
+}
+
+// G2 job + pair-2 lines, one lane on the carry-free form (dev/g2l29.h
+// job_g2lines29) vs the 32-bit one lane (job_g2lines): the same affine t', and
+// lines equal up to Fp factors, so the carry-free Miller f-chain with either
+// set of lines (fixed pair: qfix at p1) gives the same final exponentiation.
+// Returns 0 = equal, 1 = t' differs, 2 = GT differs.
+int sxe_g2lines29(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars, const uint8_t* p1,
+                  const uint8_t* qfix, uint8_t* gt) {
+  std::vector<G2Dev> b(4);
+  for (int i = 0; i < 3; i++) g2_store(b[i], ld_g2(bases + 128 * i));
+  std::vector<uint32_t> sc(8 * 3);
+  for (int i = 0; i < 3; i++) be32_to_limbs(&sc[8 * i], scalars + 32 * i);
+  std::vector<G2Dev> tab((size_t)G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS);
+  for (int f = 0; f < 3; f++)
+    for (int w = 0; w < G2TAB_WINDOWS; w++) {
+      int32_t d = sdigit_at(&sc[8 * f], G2TAB_C, w);
+      if (d)
+        job_tab_g2((uint32_t)((f * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (d < 0 ? -d : d) - 1), b.data(), tab.data());
+    }
+  G2Job g;
+  memset(&g, 0, sizeof(g));
+  g.nfix = 3;
+  for (int f = 0; f < 3; f++) {
+    g.fbase[f] = (uint8_t)f;
+    g.fscal[f] = (uint32_t)f;
+  }
+  G1Dev pt;
+  g1_store(pt, ld_g1(p2));
+  PairJob j = {0, 0, 0, 0};
+  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(sc.data());
+  std::vector<G2Dev> o1(1), o2(1);
+  std::vector<EvLineDev> l1(MILLER_LINES), l2(MILLER_LINES);
+  job_g2lines(g, j, scal, tab.data(), o1.data(), &pt, l1.data(), 0, 1);
+  job_g2lines29<0>(g, j, scal, tab.data(), o2.data(), &pt, l2.data(), 0, 1);
+  if (memcmp(o1.data(), o2.data(), sizeof(G2Dev))) return 1;
+  std::vector<LineCoef> ql(MILLER_LINES);
+  precompute_lines(ql.data(), ld_g2(qfix));
+  std::vector<LineCoef29> ql29(MILLER_LINES);
+  for (int i = 0; i < MILLER_LINES; i++) ql29[i] = linecoef29(ql[i]);
+  g1a P1 = ld_g1(p1);
+  uint8_t out[2][384];
+  for (int v = 0; v < 2; v++) {
+    const EvLineDev* l = v ? l2.data() : l1.data();
+    fp2 got[6];
+    run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l, 0, 1)); });
+    f12_to_bytes(out[v], final_exp(from_coefs(got), 0));
+  }
+  memcpy(gt, out[1], 384);
+  return memcmp(out[0], out[1], 384) ? 2 : 0;
 }
 
 }  // extern "C"

@@ -43,6 +43,18 @@ def test_golden_pp_a_verdicts(ctx_a, golden):
     assert sum(1 for c in cases if c["expect"] == 0) >= 10
 
 
+@pytest.mark.parametrize("g2lines", ["sextet", "one_lane"])
+@pytest.mark.parametrize("pp", ["pp_a", "pp_b"])
+def test_golden_verdicts_every_layout(zk, golden, pp, g2lines):
+    """every kernel layout (ftz_ctx_set_layout) gives the golden verdicts: the
+    t' / pair-2 line stage writes the same bytes whichever layout runs it"""
+    with zk.Context(golden[pp]["pp"].encode(), device=0) as c:
+        c.set_layout("g2lines", g2lines)
+        cases = golden[pp]["cases"]
+        got = _codes(c, cases)
+        assert got == {c_["name"]: c_["expect"] for c_ in cases}
+
+
 def test_golden_pp_b_verdicts(zk, golden):
     if "pp_b" not in golden:
         pytest.skip("no PP-B fixtures")

@@ -66,3 +66,24 @@ def test_sextet_g2_lines(sx, case):
         ks[1] = 0
     scal = b"".join(k.to_bytes(32, "big") for k in ks)
     assert sx.sxe_g2lines(bases, p2, scal) == 0
+
+
+@pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar", "all_zero", "p1_infinity"])
+def test_g2_lines_carry_free(sx, case):
+    """One-lane t' + pair-2 lines on the carry-free form (dev/g2l29.h): same t',
+    and the same GT after the Miller f-chain and the final exponentiation as the
+    32-bit one-lane lines (which test_sextet_g2_lines pins to the sextet ones)."""
+    rng = random.Random("g29" + case)
+    bases = b"".join(C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))) for _ in range(3))
+    p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "r_infinity" else bytes(64)
+    p1 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "p1_infinity" else bytes(64)
+    qf = C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R)))
+    ks = [rng.randrange(C.R) for _ in range(3)]
+    if case == "zero_scalar":
+        ks[1] = 0
+    if case == "all_zero":
+        ks = [0, 0, 0]
+    scal = b"".join(k.to_bytes(32, "big") for k in ks)
+    gt = (ctypes.c_uint8 * 384)()
+    assert sx.sxe_g2lines29(bases, p2, scal, p1, qf, gt) == 0
+    assert sx.sxe_g2l29_consts() == 0
