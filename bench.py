@@ -351,6 +351,8 @@ def main():
     ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
     ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
     ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
+    ap.add_argument("--device-batch", type=int, default=None,
+                    help="proofs per device pass (ftz_options.batch; default: the library's)")
     ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
     ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
     ap.add_argument("--layout", default=os.environ.get("FTZ_LAYOUT", ""),
@@ -374,7 +376,8 @@ def main():
     from zkatdlog.dist import bitmap_of, verify_shard
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
-    ctx = zkatdlog.Context(pp_json, device=local, batch=args.batch, slots=args.slots, threads=args.threads)
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads)
+    db = ctx.options["batch"]  # proofs per device pass: the engine cuts the job into passes of db
     for kv in filter(None, (args.layout or "").split(",")):  # profiling A/B: stage=layout
         stage, layout = kv.split("=")
         ctx.set_layout(stage, layout)
@@ -383,7 +386,10 @@ def main():
     bad = W.golden_tampered()
     n_total = world * args.steps * args.batch
     job = W.mixed_job(valid, bad, n_total, seed=2024)  # the whole N-GPU job (rows are cheap)
-    warm = W.mixed_job(valid, bad, args.warmup * args.batch, seed=7, offset=5)
+    # warm-up: at least one device pass per engine slot (+1), so every slot's
+    # grow-only pinned / device buffers exist before the timed job
+    n_warm = max(args.warmup * args.batch, (ctx.options["slots"] + 1) * db) if args.warmup else 0
+    warm = W.mixed_job(valid, bad, n_warm, seed=7, offset=5)
     t_setup = time.time() - t_setup
     if warm.n:
         wc = ctx.verify_transfers_packed(warm.ptr(), warm.n)
@@ -420,9 +426,9 @@ def main():
         value = n_total / elapsed
         extras = {}
         if not args.no_extras:
-            extras["plan_upload_s_per_batch"] = round(plan_rate(ctx, job, args.batch), 4)
-            extras["device_only"] = device_only(ctx, job, args.batch, args.steps)
-            extras["roofline"] = roofline(ctx, job, args.batch, local, value)
+            extras["plan_upload_s_per_batch"] = round(plan_rate(ctx, job, db), 4)
+            extras["device_only"] = device_only(ctx, job, db, max(4, args.steps * args.batch // db))
+            extras["roofline"] = roofline(ctx, job, db, local, value)
             extras["owner_signatures"] = owner_signatures(ctx)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
@@ -440,7 +446,7 @@ def main():
             "config": {"workload": "batch verify %d zkatdlog transfers per GPU per step (BASELINE configs[1]); "
                                    "%d-GPU job of %d transfers sharded by tx (configs[3])"
                                    % (args.batch, world, n_total),
-                       "batch_per_gpu": args.batch, "pp": "b=100,e=2", "fexp": "exact",
+                       "batch_per_gpu": args.batch, "device_pass": db, "pp": "b=100,e=2", "fexp": "exact",
                        "parallelism": "tx-sharded x%d" % world},
             "verdicts_bit_exact": verdict_ok, "accepted": n_accept, "setup_s": round(t_setup, 2),
             "engine": {"batches": est["batches"], "max_in_flight": est["max_in_flight"],
