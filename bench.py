@@ -343,7 +343,8 @@ def owner_signatures(ctx, n=8192, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=256,
+                    help="steps of --batch transfers per GPU (default: 256 x 4096 = a 1M-transfer job, configs[3])")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=4096, help="transfers per step (per GPU)")
     ap.add_argument("--distinct", type=int, default=16384, help="distinct GPU-made proofs in the workload")

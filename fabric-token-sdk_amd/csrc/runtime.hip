@@ -44,7 +44,7 @@ extern "C" void ftz_options_default(ftz_options* o) {
   if (!o) return;
   memset(o, 0, sizeof(*o));
   o->struct_size = sizeof(ftz_options);
-  o->batch = 4096;
+  o->batch = 8192;
   o->slots = 4;
   o->window_us = 2000;
   o->threads = 0;
@@ -64,7 +64,7 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
   if (opt) {
     if (opt->struct_size != sizeof(ftz_options)) return set_err(FTZ_E_INVALID, "ftz_options.struct_size mismatch");
     o = *opt;
-    if (o.batch == 0) o.batch = 4096;
+    if (o.batch == 0) o.batch = 8192;
     if (o.slots == 0) o.slots = 4;
     if (o.fexp != FTZ_FEXP_EXACT && o.fexp != FTZ_FEXP_FUENTES) return set_err(FTZ_E_INVALID, "unknown fexp variant");
     if (o.batch > (1u << 20) || o.slots > 64) return set_err(FTZ_E_INVALID, "batch / slots out of range");

@@ -94,7 +94,8 @@ typedef struct {
 
 typedef struct {
   uint32_t struct_size; /* sizeof(ftz_options)                                          */
-  uint32_t batch;       /* max proofs per device batch (default 4096)                   */
+  uint32_t batch;       /* max proofs per device batch (default 8192: 4096 leaves the
+                           pairing kernels at 1.6 sextet waves per SIMD, profiles/r02g_*) */
   uint32_t slots;       /* batch slots of the job engine = batches in flight (default 4;
                            measured best of 4/5/6/8, profiles/r02_slots_sweep.txt)      */
   uint32_t window_us;   /* micro-batching: how long a partial batch may wait for more

@@ -105,7 +105,7 @@ def test_fuentes_prover_matches_oracle(zk, golden):
 
 
 def test_engine_chunks_and_mixes(ctx, valid_set, bad_set, golden):
-    """One call of 3 batches + a partial one (batch = 4096): every row's code
+    """One call of 3 x 4096 + 123 proofs (one full 8192 device batch + a partial one): every row's code
     equals its expected code, while another thread's issue verifications share
     the engine (transfers and issues mix in device batches) and get their own
     results."""
@@ -131,7 +131,7 @@ def test_engine_1m_transfer_job_sharded(ctx, valid_set, bad_set):
     """BASELINE configs[3] at N = 1 through the multi-GPU job path: a job of
     2^20 transfers cut with shard_range (world 1, and each half of world 2 run
     back to back on this GPU), each shard verified in ONE call that the engine
-    splits into 4096-proof device batches; codes bit-exact vs expected."""
+    splits into device batches (8192, the default); codes bit-exact vs expected."""
     from zkatdlog import workload as W
     from zkatdlog.dist import bitmap_of, verify_shard
     n = 1 << 20
