@@ -72,6 +72,20 @@ FTS_HD f29 w29_redc(int64_t c[17]) {
   return r;
 }
 FTS_HD q2 w29_reduce(W29& w) { return {w29_redc(w.re), w29_redc(w.im)}; }
+// w += s^2 (s balanced) as (s0 + s1)(s0 - s1) + 2 s0 s1 u: two limb-product rows
+// instead of the four of w29_mac(w, s, s)
+FTS_HD void w29_sqr_acc(W29& w, const q2& s) {
+  FTS_COUNT_MAD(128);
+  FTS_SCHED_FENCE();
+  const f29 p = f29_add(s.c0, s.c1), d = f29_sub(s.c0, s.c1), t = f29_add(s.c0, s.c0);
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      w.re[i + j] += (int64_t)p.l[i] * d.l[j];
+      w.im[i + j] += (int64_t)t.l[i] * s.c1.l[j];
+    }
+}
 
 FTS_HD q2 q2_mul(const q2& a, const q2& b) {
   W29 w;
@@ -141,23 +155,22 @@ FTS_HD q2 sq_mulv(const X& x, const q2& a, const q2& b) {
 }
 
 // Granger-Scott cyclotomic squaring (as sx_cyc_sqr): even lanes 3 r - 2 a,
-// odd lanes 6 r + 2 a, r the lane's one or two products
+// odd lanes 6 r + 2 a, r the lane's one or two products.  Every lane runs one
+// general product (even lanes a_{m+3} (xi a_{m+3}), odd lanes their cross
+// product) and one complex squaring (even lanes a_m^2, odd lanes of zero): six
+// limb-product rows per lane instead of two general products' eight.
 template <class X>
 FTS_HD q2 sq_cyc_sqr(X x, q2 a) {
   const int k = x.k, m = k >> 1;
   sq_pub(x, SX_A, a);
   x.sync();
   bool odd = (k & 1) != 0;
-  int i1 = odd ? (k == 1 ? 5 : (k == 3 ? 3 : 4)) : m;
-  int j1 = odd ? (k == 1 ? SX_AX + 2 : (k == 3 ? SX_A + 0 : SX_A + 1)) : SX_A + m;
+  int i1 = odd ? (k == 1 ? 5 : (k == 3 ? 3 : 4)) : m + 3;
+  int j1 = odd ? (k == 1 ? SX_AX + 2 : (k == 3 ? SX_A + 0 : SX_A + 1)) : SX_AX + m + 3;
   W29 w;
   w29_init(w);
-#pragma nounroll
-  for (int t = 0; t < 2; t++) {
-    q2 u = x.get(t == 0 ? SX_A + i1 : SX_A + m + 3);
-    q2 v = x.get(t == 0 ? j1 : SX_AX + m + 3);
-    w29_mac(w, q2_sel(odd && t == 1, q2_zero(), u), v);
-  }
+  w29_mac(w, x.get(SX_A + i1), x.get(j1));
+  w29_sqr_acc(w, q2_sel(odd, q2_zero(), x.get(SX_A + m)));
   x.sync();
   q2 r = w29_reduce(w);
   const int32_t cr = odd ? 6 : 3, ca = odd ? 2 : -2;

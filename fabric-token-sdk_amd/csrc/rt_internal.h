@@ -104,7 +104,12 @@ struct ftz_ctx {
   DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)
   ftz_options opt;                   // resolved options (ftz_ctx_create_ex)
   int serial = 0;                    // profiling: every kernel of a batch on one stream
-  int g2lanes = FTZ_LAYOUT_ONE_LANE;  // t' + pair-2 lines: k_g2lines1 or the sextet k_g2lines (ftz_ctx_set_layout)
+  // t' + pair-2 lines: k_g2lines1 (one lane per job) or the sextet k_g2lines
+  // (ftz_ctx_set_layout).  The verifier's pipeline is throughput bound (one lane:
+  // fewest instructions); the prover's pass is latency bound (t' waits for R'):
+  // sextet (profiles/r02g_prover_layout.txt)
+  int g2lanes = FTZ_LAYOUT_ONE_LANE;
+  int g2lanes_prover = FTZ_LAYOUT_SEXTET;
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
   // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every

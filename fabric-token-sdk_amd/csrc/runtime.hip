@@ -302,8 +302,12 @@ extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
 extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
   if (!c) return set_err(FTZ_E_INVALID, "null context");
   if (layout != FTZ_LAYOUT_ONE_LANE && layout != FTZ_LAYOUT_SEXTET) return set_err(FTZ_E_INVALID, "unknown layout");
-  if (stage != FTZ_STAGE_G2LINES) return set_err(FTZ_E_INVALID, "unknown stage");
-  c->g2lanes = layout;
+  if (stage == FTZ_STAGE_G2LINES)
+    c->g2lanes = layout;
+  else if (stage == FTZ_STAGE_PROVER_G2LINES)
+    c->g2lanes_prover = layout;
+  else
+    return set_err(FTZ_E_INVALID, "unknown stage");
   return FTZ_SUCCESS;
 }
 
@@ -514,8 +518,8 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
 
 // t' and the pair-2 lines (R read from `pts`): one lane per job (default,
 // k_g2lines1) or the sextet layout (k_g2lines); same bytes either way
-static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s) {
-  if (c->g2lanes == FTZ_LAYOUT_ONE_LANE)
+static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
+  if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE)
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts, p.lines2);
   else
     k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,
@@ -570,7 +574,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   HC(hipStreamWaitEvent(s3, e[4], 0));
   HC(hipEventRecord(e[14], s3));
   if (p.n_g2)
-    launch_g2lines(c, p, p.pts, s3);
+    launch_g2lines(c, p, p.pts, s3, false);
   HC(hipEventRecord(e[15], s3));
   // st[0]: pairing chain
   HC(hipEventRecord(e[16], s));
@@ -802,7 +806,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   HC(hipStreamWaitEvent(s3, e[5], 0));
   HC(hipEventRecord(e[14], s3));
   if (p.n_g2)
-    launch_g2lines(c, p, p.g1out, s3);
+    launch_g2lines(c, p, p.g1out, s3, true);
   HC(hipEventRecord(e[15], s3));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));

@@ -149,11 +149,12 @@ class Context:
         _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)
 
     LAYOUTS = {"one_lane": 1, "sextet": 6}
-    STAGES = {"g2lines": 0}
+    STAGES = {"g2lines": 0, "prover_g2lines": 1}
 
     def set_layout(self, stage, layout):
-        """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines',
-        layout 'one_lane' (default) or 'sextet' -- same results, different speed"""
+        """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines'
+        (verifier, default 'one_lane') or 'prover_g2lines' (default 'sextet'), layout 'one_lane'
+        or 'sextet' -- same results, different speed"""
         _check(self._lib.ftz_ctx_set_layout(self._h, self.STAGES[stage], self.LAYOUTS[layout]), self._lib)
 
     def verify_issues(self, issues):

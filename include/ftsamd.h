@@ -122,10 +122,13 @@ int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
  * without overlap), 0 = the normal three-stream schedule */
 int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
 /* profiling: kernel layout of a pipeline stage (results are identical; only
- * speed differs).  stage FTZ_STAGE_G2LINES (t' = c PK0 + v PK1 + h PK2 and the
- * 88 pair-2 Miller lines); layout FTZ_LAYOUT_ONE_LANE (one lane per job, the
- * default) or FTZ_LAYOUT_SEXTET (six lanes per job, ten jobs per wave). */
+ * speed differs).  stage FTZ_STAGE_G2LINES (the verifier's t' = c PK0 + v PK1
+ * + h PK2 and its 88 pair-2 Miller lines; default one lane) or
+ * FTZ_STAGE_PROVER_G2LINES (the prover's t = rv PK1 + rh PK2 and its lines at
+ * R'; default sextet); layout FTZ_LAYOUT_ONE_LANE (one lane per job) or
+ * FTZ_LAYOUT_SEXTET (six lanes per job, ten jobs per wave). */
 #define FTZ_STAGE_G2LINES 0
+#define FTZ_STAGE_PROVER_G2LINES 1
 #define FTZ_LAYOUT_ONE_LANE 1
 #define FTZ_LAYOUT_SEXTET 6
 int ftz_ctx_set_layout(ftz_ctx* ctx, int stage, int layout);

@@ -143,6 +143,22 @@ def test_gpu_transfer_proofs_match_oracle(gctx, pp_a):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["one_lane", "sextet"])
+def test_gpu_proofs_match_oracle_every_layout(golden, pp_a, layout):
+    """the prover's t / pair-2 line stage in either kernel layout
+    (ftz_ctx_set_layout) gives byte-identical proofs"""
+    import zkatdlog
+    _, pp = pp_a
+    ws = [witness(pp, 320 + i, 2, 2) for i in range(2)]
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0) as c:
+        c.set_layout("prover_g2lines", layout)
+        proofs, codes = c.prove_transfers(ws)
+    assert codes == [0, 0]
+    for w, p in zip(ws, proofs):
+        assert p == oracle_transfer(pp, w)
+
+
+@pytest.mark.gpu
 def test_gpu_issue_proofs_match_oracle(gctx, pp_a):
     _, pp = pp_a
     ws = [issue_witness(pp, 400, 2), issue_witness(pp, 401, 1, ttype="USD", anonymous=True)]
