@@ -266,7 +266,8 @@ def roofline(ctx, job, batch, device, tx_per_s):
     peak = madpeak(device)
     opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["pp_a"]
     names = {"g1": "k_g1_part+k_g1_combine (side stream)", "g1p": "k_g1_part+k_g1_combine (pairing inputs)",
-             "g2": "k_g2lines", "miller": "k_miller", "fexp": "k_fexp_exact", "hash": "k_hash", "decode": "k_decode"}
+             "g2": "k_g2_part+k_g2lines1 (t' + pair-2 lines)", "miller": "k_miller", "fexp": "k_fexp_exact",
+             "hash": "k_hash", "decode": "k_decode"}
     mjob = dict(opc["m_per_job"])
     mjob["g1p"] = mjob["g1"]  # the pairing-input G1 jobs run the same job code
     # device kernel split (tests/native/opcount.py): k_g2lines = t' + pair-2 lines, k_miller = f-chain only

@@ -1089,6 +1089,64 @@ FTS_HD void job_g2lines(const G2Job& g, const PairJob& j, const uint32_t (*scal)
   g2lines_emit(g2_load(g2out[g.out]), g1_load(pts[j.p2]), lines, idx, njobs);
 }
 
+// Split form of job_g2lines for the one-lane kernels: k_g2_part runs four
+// lanes per job, lane q summing the table points of the (base, window)
+// positions q, q + 4, ... into a Jacobian partial; k_g2lines1 adds the four
+// partials, normalises t' and emits its lines.  Same t' (the affine sum does
+// not depend on the order) and the same line bytes as job_g2lines.
+struct G2PartDev {
+  uint32_t w[48];  // Jacobian X, Y, Z (Fp2, Montgomery, c0 then c1)
+};
+FTS_HD void g2part_store(G2PartDev& d, const g2j& a) {
+  const fp2* c[3] = {&a.x, &a.y, &a.z};
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      d.w[16 * m + i] = c[m]->c0.v[i];
+      d.w[16 * m + 8 + i] = c[m]->c1.v[i];
+    }
+}
+FTS_HD g2j g2part_load(const G2PartDev& d) {
+  g2j a;
+  fp2* c[3] = {&a.x, &a.y, &a.z};
+#pragma unroll
+  for (int m = 0; m < 3; m++)
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c[m]->c0.v[i] = d.w[16 * m + i];
+      c[m]->c1.v[i] = d.w[16 * m + 8 + i];
+    }
+  return a;
+}
+FTS_HD void job_g2_part(const G2Job& g, int q, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev& out) {
+  g2j acc = jac_inf<fp2>();
+#pragma nounroll
+  for (int p = q; p < 3 * G2TAB_WINDOWS; p += 4) {
+    int f = p / G2TAB_WINDOWS, w = p % G2TAB_WINDOWS;
+    if (f < g.nfix) {
+      int32_t d = sdigit_at(scal[g.fscal[f]], G2TAB_C, w);
+      if (d) {
+        g2a T = g2_load(tab[((size_t)g.fbase[f] * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+        if (d < 0) T.y = f2_neg(T.y);
+        acc = jac_add_aff(acc, T);
+      }
+    }
+  }
+  g2part_store(out, acc);
+}
+// parts of job idx at part[q * njobs + idx]
+FTS_HD void job_g2lines_parts(const G2Job& g, const PairJob& j, const G2PartDev* part, G2Dev* g2out,
+                              const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+  g2j acc = g2part_load(part[idx]);
+#pragma nounroll
+  for (int q = 1; q < 4; q++) acc = jac_add(acc, g2part_load(part[(size_t)q * njobs + idx]));
+  G2Dev d;
+  g2_store(d, jac_to_aff(acc));
+  g2out[g.out] = d;
+  g2lines_emit(g2_load(d), g1_load(pts[j.p2]), lines, idx, njobs);
+}
+
 // Sextet form of job_g2lines (same values): six lanes per membership digit.
 //  phase A  t' = sum over (base, window) of table points: lane k takes the
 //           pairs k, k+6, ... (16 mixed additions), then a 3-level tree of

@@ -26,12 +26,21 @@ __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJo
   sx_job_g2lines(x, g2[jc], pr[jc], scal, tab, g2out, pts, lines, jc, n, valid);
 }
 
-// The same in the one-lane layout (job_g2lines): 64 jobs per wave.
+// The same in the one-lane layout, split (job_g2_part / job_g2lines_parts):
+// four lanes per job sum the table points (part-major, so every wave runs one
+// part), then one lane per job adds the partials and emits the lines.
+__global__ void __launch_bounds__(64) k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8],
+                                                const G2Dev* tab, G2PartDev* part) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * n) return;
+  uint32_t q = i / n, job = i - q * n;
+  job_g2_part(g2[job], (int)q, scal, tab, part[i]);
+}
 __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n,
-                                                 const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out,
-                                                 const G1Dev* pts, EvLineDev* lines) {
+                                                 const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,
+                                                 EvLineDev* lines) {
   JOB_KERNEL_PROLOGUE(n);
-  job_g2lines(g2[i], pr[i], scal, tab, g2out, pts, lines, i, n);
+  job_g2lines_parts(g2[i], pr[i], part, g2out, pts, lines, i, n);
 }
 
 // ---- wide-window G2 tables (C > 8), as k_tab_g1_bw / k_tab_g1_fill

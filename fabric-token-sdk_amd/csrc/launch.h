@@ -70,8 +70,9 @@ __global__ void k_tab_g1_fill(const G1Dev* bw, uint32_t chunk, G1JDev* jtmp, uin
 __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out);
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
-__global__ void k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
-                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
+__global__ void k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev* part);
+__global__ void k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n, const G2PartDev* part, G2Dev* g2out,
+                           const G1Dev* pts, EvLineDev* lines);
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
 __global__ void k_tab_g2_bw(const G2Dev* bases, G2Dev* bw);
 __global__ void k_tab_g2_fill(const G2Dev* bw, uint32_t chunk, uint32_t (*jt)[48], uint32_t (*zs)[16], G2Dev* tab);

@@ -376,6 +376,7 @@ static void scratch_layout(ftz_batch* b) {
   s.lines2 = take(sizeof(EvLineDev) * n_pr * MILLER_LINES);
   s.part1 = take(sizeof(G1JDev) * 4 * n_g1);
   s.part1p = take(sizeof(G1JDev) * 4 * n_g1p);
+  s.part2 = take(sizeof(G2PartDev) * 4 * n_pr);
   s.vtab1 = take(sizeof(G1Dev) * 16 * n_g1);
   s.vtab1p = take(sizeof(G1Dev) * 16 * n_g1p);
   s.hash_ok = take(f.cnt[PS_HMAIN]);
@@ -448,6 +449,7 @@ struct SlotPtrs {
   F12Dev* fbuf;
   EvLineDev* lines2;
   G1JDev *part1, *part1p;
+  G2PartDev* part2;
   G1Dev *vtab1, *vtab1p;
   int32_t* codes;
   uint32_t* bitmap;
@@ -492,6 +494,7 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   p.lines2 = reinterpret_cast<EvLineDev*>(s + l.lines2);
   p.part1 = reinterpret_cast<G1JDev*>(s + l.part1);
   p.part1p = reinterpret_cast<G1JDev*>(s + l.part1p);
+  p.part2 = reinterpret_cast<G2PartDev*>(s + l.part2);
   p.vtab1 = reinterpret_cast<G1Dev*>(s + l.vtab1);
   p.vtab1p = reinterpret_cast<G1Dev*>(s + l.vtab1p);
   p.hash_ok = s + l.hash_ok;
@@ -516,14 +519,17 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   return p;
 }
 
-// t' and the pair-2 lines (R read from `pts`): one lane per job (default,
-// k_g2lines1) or the sextet layout (k_g2lines); same bytes either way
+// t' and the pair-2 lines (R read from `pts`): one lane per job (default;
+// k_g2_part four lanes per job for the table sums, then k_g2lines1) or the
+// sextet layout (k_g2lines); same bytes either way
 static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
-  if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE)
-    k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts, p.lines2);
-  else
+  if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE) {
+    k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
+    k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);
+  } else {
     k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,
                                                                   p.lines2);
+  }
 }
 
 static void launch_miller(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {

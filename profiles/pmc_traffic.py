@@ -34,10 +34,14 @@ def main(fetch_db, write_db):
     if part and comb:
         out["g1"] = kb(("k_g1_part", part[-1])) + kb(("k_g1_combine", comb[-1]))
         out["g1p"] = kb(("k_g1_part", part[0])) + kb(("k_g1_combine", comb[0]))
-    for key, name in (("miller", "k_miller"), ("fexp", "k_fexp"), ("g2", "k_g2lines"), ("decode", "k_decode")):
-        g = grids(name)
-        if g:
-            out[key] = kb((name, g[-1]))
+    for key, names in (("miller", ("k_miller",)), ("fexp", ("k_fexp_exact", "k_fexp")),
+                       ("g2", ("k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
+        for name in names:
+            parts = name.split("+")
+            gs = [grids(n) for n in parts]
+            if all(gs):  # the largest grid of each kernel (the verification batch)
+                out[key] = sum(kb((n, g[-1])) for n, g in zip(parts, gs))
+                break
     h = grids("k_hash")
     if h:
         out["hash"] = kb(("k_hash", h[-1]))

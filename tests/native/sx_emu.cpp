@@ -250,6 +250,15 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   if (memcmp(o1.data(), o2.data(), sizeof(G2Dev))) return 1;
   for (int s = 0; s < MILLER_LINES; s++)
     if (memcmp(&l1[s], &l2[s], sizeof(EvLineDev))) return 2 + s;
+  // the split one-lane device path (k_g2_part + k_g2lines1)
+  std::vector<G2PartDev> part(4);
+  for (int q = 0; q < 4; q++) job_g2_part(g, q, scal, tab.data(), part[q]);
+  std::vector<G2Dev> o3(1);
+  std::vector<EvLineDev> l3(MILLER_LINES);
+  job_g2lines_parts(g, j, part.data(), o3.data(), &pt, l3.data(), 0, 1);
+  if (memcmp(o1.data(), o3.data(), sizeof(G2Dev))) return 100;
+  for (int s = 0; s < MILLER_LINES; s++)
+    if (memcmp(&l1[s], &l3[s], sizeof(EvLineDev))) return 101 + s;
   return 0;
 }
 
