@@ -965,7 +965,7 @@ extern "C" void ftz_prover_destroy(ftz_prover* b) {
   delete b;
 }
 
-// One-shot proving of any n: batches of opt.batch witnesses pipelined through
+// One-shot proving of any n: passes of min(opt.batch, 4096) witnesses pipelined through
 // the context's reusable prover slots (plan batch k+1 on the host while batch
 // k runs), proofs concatenated into buf in witness order.
 template <class W>
@@ -973,7 +973,11 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
                          int32_t* codes) {
   std::lock_guard<std::mutex> lk(c->prove_mu);
   HC(hipSetDevice(c->device));
-  const size_t K = 3, B = c->opt.batch;
+  // passes of at most 4096 witnesses: the prover's pass is a latency-bound
+  // chain (R' -> t lines -> Miller -> final exponentiation -> challenges ->
+  // responses) planned on the calling thread, and 8192-witness passes fill the
+  // three slots too slowly (65536 proofs: 298k/s vs 426k/s, profiles/r02g_prover_layout.txt)
+  const size_t K = 3, B = std::min<size_t>(c->opt.batch, 4096);
   while (c->pslots.size() < K) {
     ftz_prover* p = new ftz_prover();
     p->ctx = c;
