@@ -240,7 +240,7 @@ def plan_rate(ctx, job, batch, reps=3):
     return best
 
 
-def roofline(ctx, job, batch, device, tx_per_s):
+def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False):
     """Integer-VALU roofline of the dominant kernel.  The timed steps overlap
     three streams, so per-kernel wall times there include shared SIMDs; the
     roofline pass re-runs 3 steps of one batch with every kernel on one stream
@@ -260,7 +260,7 @@ def roofline(ctx, job, batch, device, tx_per_s):
             st = b.stats()
             acc = st if acc is None else {k: (acc[k][0] + st[k][0], st[k][1]) for k in st}
     finally:
-        ctx.set_serial(False)
+        ctx.set_serial(keep_serial)
         b.close()
     kern = {k: (v[0] / 3, v[1]) for k, v in acc.items() if k != "total"}
     peak = madpeak(device)
@@ -357,6 +357,9 @@ def main():
                     help="proofs per device pass (ftz_options.batch; default: the library's)")
     ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
     ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
+    ap.add_argument("--serial", action="store_true",
+                    help="profiling: every kernel on one stream for the whole run (ftz_ctx_set_serial), so that a "
+                         "rocprofv3 kernel trace gives per-kernel durations without overlap")
     ap.add_argument("--layout", default=os.environ.get("FTZ_LAYOUT", ""),
                     help="kernel layouts, e.g. 'g2lines=sextet,pairing=one_lane' (ftz_ctx_set_layout)")
     args = ap.parse_args()
@@ -380,6 +383,8 @@ def main():
     pp_json = g["pp"].encode()
     ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads)
     db = ctx.options["batch"]  # proofs per device pass: the engine cuts the job into passes of db
+    if args.serial:
+        ctx.set_serial(True)
     for kv in filter(None, (args.layout or "").split(",")):  # profiling A/B: stage=layout
         stage, layout = kv.split("=")
         ctx.set_layout(stage, layout)
@@ -429,8 +434,9 @@ def main():
         extras = {}
         if not args.no_extras:
             extras["plan_upload_s_per_batch"] = round(plan_rate(ctx, job, db), 4)
-            extras["device_only"] = device_only(ctx, job, db, max(4, args.steps * args.batch // db))
-            extras["roofline"] = roofline(ctx, job, db, local, value)
+            extras["device_only"] = device_only(ctx, job, db, max(4, args.steps * args.batch // db),
+                                                inflight=1 if args.serial else 4)
+            extras["roofline"] = roofline(ctx, job, db, local, value, keep_serial=args.serial)
             extras["owner_signatures"] = owner_signatures(ctx)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
