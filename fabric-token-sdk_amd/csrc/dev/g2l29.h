@@ -287,4 +287,25 @@ FTS_HD void job_g2lines29(const G2Job& g, const PairJob& j, const uint32_t (*sca
   }
 }
 
+// k_g2_part on the carry-free form: the same Jacobian partial as job_g2_part
+// (j2q_madd runs madd-2007-bl's formulas, so X, Y, Z agree mod p and the
+// canonical 32-bit words written are byte-identical).
+FTS_HD void job_g2_part29(const G2Job& g, int q, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev& out) {
+  j2q acc = {q2_zero(), q2_zero(), q2_zero(), true};
+#pragma nounroll
+  for (int p = q; p < 3 * G2TAB_WINDOWS; p += 4) {
+    int f = p / G2TAB_WINDOWS, w = p % G2TAB_WINDOWS;
+    if (f < g.nfix) {
+      int32_t d = sdigit_at(scal[g.fscal[f]], G2TAB_C, w);
+      if (d) {
+        const G2Dev& T = tab[((size_t)g.fbase[f] * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1];
+        q2 x2 = q2_ld_raw(T.x0, T.x1), y2 = q2_ld_raw(T.y0, T.y1);
+        if (d < 0) y2 = q2_neg(y2);
+        acc = j2q_madd(acc, x2, y2);
+      }
+    }
+  }
+  g2part_store(out, j2q_to32(acc));
+}
+
 }  // namespace fts

@@ -931,6 +931,16 @@ FTS_HD void job_g1_finish(const G1Job& j, const g1j& acc, const fp& zi, G1Dev* g
   g1_emit_bytes(j, r, arena);
 }
 
+// (x/y, 1/y) of the affine point of acc = (X:Y:Z) from inv = 1/(Z Y): x/y = X Z^2 inv,
+// 1/y = Z^4 inv -- the normalised evaluation point of the fixed-Q Miller lines
+// (sx29.h sq_fixed_line_n).  Unused for the point at infinity.
+FTS_HD void g1_pnorm(const g1j& acc, const fp& inv, G1Dev& out) {
+  fp z2 = sqr(acc.z);
+  G1Dev d;
+  g1_store(d, g1a{acc.x * z2 * inv, sqr(z2) * inv, false});
+  out = d;
+}
+
 FTS_HD void job_g1_combine(const G1Job& j, uint32_t jb, uint32_t n, const G1JDev* part, G1Dev* g1out,
                            uint8_t* arena) {
   g1j acc = job_g1_sum_parts(j, jb, n, part);

@@ -382,6 +382,63 @@ FTS_HD q2 sq_fixed_line(const X& x, const q2& f, const LineCoef29& q, const f29&
   return sq_mul_line_r(x, f, l0, l1, l3);
 }
 
+// Fixed-Q line divided by r0 yP (an Fp2 factor, which the final exponentiation
+// sends to 1): 1 + (r1/r0)(xP/yP) w + (r2/r0)(1/yP) w^3.  q holds r1/r0 and
+// r2/r0 in its r1, r2 slots (k_qlines, once per context), xq = xP/yP and
+// yi = 1/yP come from the G1 combine (g1_pnorm).  Lanes 0..3 form the four
+// Fp products; f + f (l1 w + l3 w^3) then costs two limb-product pairs per
+// lane instead of sq_fixed_line's three.
+template <class X>
+FTS_HD q2 sq_fixed_line_n(const X& x, const q2& f, const LineCoef29& q, const f29& xq, const f29& yi, bool inf) {
+  const int k = x.k;
+  f29 a = (k == 0) ? q.r1.c0 : (k == 1) ? q.r1.c1 : (k == 2) ? q.r2.c0 : q.r2.c1;
+  f29 prod = f29_mulb(a, k < 2 ? xq : yi);
+  x.put(SX_P + k, {prod, prod});
+  x.sync();
+  q2 l1 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
+  q2 l3 = {x.get(SX_P + 2).c0, x.get(SX_P + 3).c0};
+  sq_pub(x, SX_A, f);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 2; t++) {
+    int j = k - (t == 0 ? 1 : 3);
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w29_mac(w, t == 0 ? l1 : l3, x.get(sb));
+  }
+  x.sync();
+  q2 r = w29_reduce(w);
+  q2 g = {f29_lin2(f.c0, 1, r.c0, 1), f29_lin2(f.c1, 1, r.c1, 1)};
+  return q2_sel(inf, f, g);
+}
+
+// 2-pair Miller loop with the normalised fixed-Q lines (same GT value after
+// the final exponentiation as sq_miller_f; the Miller value differs by a
+// factor in Fp2*)
+template <class X>
+FTS_HD q2 sq_miller_fn(const X& x, const LineCoef29* qlines_n, const g1a& P1, const G1Dev& pn, const EvLineDev* l2,
+                       uint32_t idx, uint32_t njobs) {
+  fp xqf, yif;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    xqf.v[i] = pn.x[i];
+    yif.v[i] = pn.y[i];
+  }
+  const f29 xq = f29_breduce(f29_from_fp(xqf)), yi = f29_breduce(f29_from_fp(yif));
+  q2 one = {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1};
+  q2 f = q2_sel(x.k == 0, one, q2_zero());
+#pragma nounroll
+  for (int s = 0; s < MILLER_LINES; s++) {
+    bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
+    if (sq) f = sq_sqr(x, f);
+    f = sq_fixed_line_n(x, f, qlines_n[s], xq, yi, P1.inf);
+    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
+                      evline_ld29(l2, s, 2, idx, njobs));
+  }
+  return f;
+}
+
 // 2-pair Miller loop, pair-2 lines precomputed (as sx_miller_f)
 template <class X>
 FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const EvLineDev* l2, uint32_t idx,

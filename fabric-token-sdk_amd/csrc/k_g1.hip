@@ -85,14 +85,20 @@ __device__ fp block_batch_inv(fp x, uint32_t (*pre)[NT], uint32_t (*suf)[NT], ui
 }
 
 static constexpr int COMBINE_NT = 256;
+// One batch inversion of Z Y per block gives both 1/Z (the affine result) and
+// the normalised Miller evaluation point (x/y, 1/y) written to pnorm[out]
+// (g1_pnorm; Y != 0 for every finite point of the prime-order G1).
 __global__ void __launch_bounds__(COMBINE_NT) k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part,
-                                                           G1Dev* g1out, uint8_t* arena) {
+                                                           G1Dev* g1out, uint8_t* arena, G1Dev* pnorm) {
   __shared__ uint32_t pre[8][COMBINE_NT], suf[8][COMBINE_NT], tot[8];
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = i < n;  // every thread of the block takes part in the scans
   g1j acc = valid ? job_g1_sum_parts(jobs[i], i, n, part) : jac_inf<fp>();
-  fp zi = block_batch_inv<COMBINE_NT>(acc.z, pre, suf, tot);
-  if (valid) job_g1_finish(jobs[i], acc, zi, g1out, arena);
+  fp inv = block_batch_inv<COMBINE_NT>(acc.z * acc.y, pre, suf, tot);
+  if (valid) {
+    job_g1_finish(jobs[i], acc, acc.y * inv, g1out, arena);
+    g1_pnorm(acc, inv, pnorm[jobs[i].out]);
+  }
 }
 
 // ---- wide-window G1 tables (C = 16): per (base, window) the point

@@ -63,7 +63,8 @@ __global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev
                      const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
 __global__ void k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
                           const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part, G1Dev* vtab);
-__global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena);
+__global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena,
+                             G1Dev* pnorm);
 __global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
 __global__ void k_tab_g1_bw(const G1Dev* bases, G1Dev* bw);
 __global__ void k_tab_g1_fill(const G1Dev* bw, uint32_t chunk, G1JDev* jtmp, uint32_t (*zs)[8], G1Dev* tab);
@@ -71,6 +72,7 @@ __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], c
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
 __global__ void k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev* part);
+__global__ void k_g2_part29(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev* part);
 __global__ void k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n, const G2PartDev* part, G2Dev* g2out,
                            const G1Dev* pts, EvLineDev* lines);
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);
@@ -78,7 +80,9 @@ __global__ void k_tab_g2_bw(const G2Dev* bases, G2Dev* bw);
 __global__ void k_tab_g2_fill(const G2Dev* bw, uint32_t chunk, uint32_t (*jt)[48], uint32_t (*zs)[16], G2Dev* tab);
 __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef29* qlines, const EvLineDev* lines2,
                          const G1Dev* g1out, F12Dev* fbuf);
-__global__ void k_qlines(const G2Dev* q, LineCoef* out, LineCoef29* out29, int* n);
+__global__ void k_qlines(const G2Dev* q, LineCoef* out, LineCoef29* out29, LineCoef29* out29n, int* n, int* norm);
+__global__ void k_miller_n(const PairJob* jobs, uint32_t n, const LineCoef29* qlines_n, const EvLineDev* lines2,
+                           const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
 __global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 __global__ void k_fexp_exact(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
 

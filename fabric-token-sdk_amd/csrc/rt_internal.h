@@ -102,6 +102,9 @@ struct ftz_ctx {
   DBuf<G2Dev> g2tab;
   DBuf<LineCoef> qlines;
   DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)
+  DBuf<LineCoef29> qlines29n;        // normalised by r0 (k_miller_n); used when qnorm
+  bool qnorm = false;
+  bool qnorm_off = false;  // EXPERIMENT
   ftz_options opt;                   // resolved options (ftz_ctx_create_ex)
   int serial = 0;                    // profiling: every kernel of a batch on one stream
   // t' + pair-2 lines: k_g2lines1 (one lane per job) or the sextet k_g2lines
@@ -110,6 +113,7 @@ struct ftz_ctx {
   // sextet (profiles/r02g_prover_layout.txt)
   int g2lanes = FTZ_LAYOUT_ONE_LANE;
   int g2lanes_prover = FTZ_LAYOUT_SEXTET;
+  bool g2part29 = false;  // EXPERIMENT
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
   // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every
@@ -133,7 +137,7 @@ struct ftz_ctx {
 // Device scratch of a batch (values the kernels produce), sub-allocated from
 // one grow-only buffer.
 struct ScratchLayout {
-  size_t pts, pt_ok, scal, canon, g1out, g2out, fbuf, lines2, part1, part1p, part2, vtab1, vtab1p, hash_ok, hash_ok_pre,
+  size_t pts, pt_ok, scal, canon, g1out, pnorm, g2out, fbuf, lines2, part1, part1p, part2, vtab1, vtab1p, hash_ok, hash_ok_pre,
       codes, bitmap, total;
 };
 

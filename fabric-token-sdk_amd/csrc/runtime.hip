@@ -195,7 +195,8 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     }
     uint32_t t1 = G1B_COUNT * G1TAB_WINDOWS * G1TAB_DIGITS, t2 = G2B_COUNT * G2TAB_WINDOWS * G2TAB_DIGITS;
     if (c->g1tab.alloc(t1) != hipSuccess || c->g2tab.alloc(t2) != hipSuccess ||
-        c->qlines.alloc(MILLER_LINES) != hipSuccess || c->qlines29.alloc(MILLER_LINES) != hipSuccess) {
+        c->qlines.alloc(MILLER_LINES) != hipSuccess || c->qlines29.alloc(MILLER_LINES) != hipSuccess ||
+        c->qlines29n.alloc(MILLER_LINES) != hipSuccess) {
       fail(FTZ_E_NOMEM, "table allocation failed");
       break;
     }
@@ -232,17 +233,18 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
           c->g2tab.p);
     }
     DBuf<int> d_n;
-    if (d_n.alloc(1) != hipSuccess) {
+    if (d_n.alloc(2) != hipSuccess) {
       fail(FTZ_E_NOMEM, "alloc");
       break;
     }
-    k_qlines<<<1, 64, 0, c->stream>>>(d_g2.p + 3, c->qlines.p, c->qlines29.p, d_n.p);
-    int nl = 0;
-    if (hipMemcpyAsync(&nl, d_n.p, sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess || nl != MILLER_LINES) {
+    k_qlines<<<1, 64, 0, c->stream>>>(d_g2.p + 3, c->qlines.p, c->qlines29.p, c->qlines29n.p, d_n.p, d_n.p + 1);
+    int nl[2] = {0, 0};
+    if (hipMemcpyAsync(nl, d_n.p, 2 * sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess || nl[0] != MILLER_LINES) {
       fail(FTZ_E_DEVICE, std::string("context setup kernels failed: ") + hipGetErrorString(hipGetLastError()));
       break;
     }
+    c->qnorm = nl[1] != 0;
   } while (0);
   if (rc != FTZ_SUCCESS) {
     ftz_ctx_destroy(c);
@@ -278,6 +280,7 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   c->g2tab.alloc(0);
   c->qlines.alloc(0);
   c->qlines29.alloc(0);
+  c->qlines29n.alloc(0);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c->pool;
   delete c;
@@ -306,6 +309,10 @@ extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
     c->g2lanes = layout;
   else if (stage == FTZ_STAGE_PROVER_G2LINES)
     c->g2lanes_prover = layout;
+  else if (stage == 2)  // EXPERIMENT: k_g2_part field form (1: 32-bit, 6: carry-free)
+    c->g2part29 = layout == FTZ_LAYOUT_SEXTET;
+  else if (stage == 3)  // EXPERIMENT: fixed-Q lines (1: raw k_miller, 6: normalised k_miller_n if available)
+    c->qnorm_off = layout == FTZ_LAYOUT_ONE_LANE;
   else
     return set_err(FTZ_E_INVALID, "unknown stage");
   return FTZ_SUCCESS;
@@ -371,6 +378,7 @@ static void scratch_layout(ftz_batch* b) {
   s.scal = take(32 * (size_t)f.n_scal);
   s.canon = take(f.n_scal);
   s.g1out = take(sizeof(G1Dev) * (size_t)f.n_g1out);
+  s.pnorm = take(sizeof(G1Dev) * (size_t)f.n_g1out);
   s.g2out = take(sizeof(G2Dev) * (size_t)f.n_g2out);
   s.fbuf = take(sizeof(F12Dev) * n_pr);
   s.lines2 = take(sizeof(EvLineDev) * n_pr * MILLER_LINES);
@@ -445,6 +453,7 @@ struct SlotPtrs {
   uint8_t *pt_ok, *canon, *hash_ok, *hash_ok_pre;
   uint32_t (*scal)[8];
   G1Dev* g1out;
+  G1Dev* pnorm;
   G2Dev* g2out;
   F12Dev* fbuf;
   EvLineDev* lines2;
@@ -489,6 +498,7 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   p.scal = reinterpret_cast<uint32_t (*)[8]>(s + l.scal);
   p.canon = s + l.canon;
   p.g1out = reinterpret_cast<G1Dev*>(s + l.g1out);
+  p.pnorm = reinterpret_cast<G1Dev*>(s + l.pnorm);
   p.g2out = reinterpret_cast<G2Dev*>(s + l.g2out);
   p.fbuf = reinterpret_cast<F12Dev*>(s + l.fbuf);
   p.lines2 = reinterpret_cast<EvLineDev*>(s + l.lines2);
@@ -524,7 +534,10 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
 // sextet layout (k_g2lines); same bytes either way
 static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
   if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE) {
-    k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
+    if (c->g2part29)
+      k_g2_part29<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
+    else
+      k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);
   } else {
     k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,
@@ -533,6 +546,11 @@ static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipS
 }
 
 static void launch_miller(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
+  if (c->qnorm && !c->qnorm_off) {
+    k_miller_n<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29n.p, p.lines2, p.g1out,
+                                                                   p.pnorm, p.fbuf);
+    return;
+  }
   k_miller<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29.p, p.lines2, p.g1out,
                                                                  p.fbuf);
 }
@@ -587,7 +605,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   if (p.n_g1p) {
     k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, c->g1tab.p, p.part1p,
                                                            p.vtab1p);
-    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena);
+    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena, p.pnorm);
   }
   HC(hipEventRecord(e[5], s));
   // st[1]: pairing-independent G1 jobs, started with the jobs the chain waits for
@@ -596,7 +614,7 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   if (p.n_g1) {
     k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, c->g1tab.p, p.part1,
                                                            p.vtab1);
-    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena);
+    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena, p.pnorm);
   }
   HC(hipEventRecord(e[12], s2));
   HC(hipStreamWaitEvent(s, e[15], 0));
@@ -797,7 +815,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   if (p.n_g1) {
     k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, c->g1tab.p, p.part1,
                                                            p.vtab1);
-    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena);
+    k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena, p.pnorm);
   }
   HC(hipEventRecord(e[12], s2));
   // st[0]: R' = rr R and rsbf P (the pairing inputs)
@@ -805,7 +823,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   if (p.n_g1p) {
     k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, c->g1tab.p, p.part1p,
                                                            p.vtab1p);
-    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena);
+    k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena, p.pnorm);
   }
   HC(hipEventRecord(e[5], s));
   // st[2]: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)

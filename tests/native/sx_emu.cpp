@@ -213,7 +213,32 @@ int sxe_miller29(const uint8_t* p1, const uint8_t* p2, const uint8_t* q2b, const
   g2lines_emit(Q2, P2, l2.data(), 0, 1);
   fp2 got[6];
   run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l2.data(), 0, 1)); });
-  return f12_eq(from_coefs(got), want) ? 0 : 1;
+  if (!f12_eq(from_coefs(got), want)) return 1;
+  // normalised fixed lines (k_qlines out29n, k_miller_n): the evaluation point
+  // (x/y, 1/y) from g1_pnorm on a Jacobian representative with Z != 1 (as the
+  // G1 combine sees it); equal to miller_2 after the final exponentiation
+  std::vector<LineCoef29> qn(MILLER_LINES);
+  for (int i = 0; i < MILLER_LINES; i++) {
+    fp2 ri = f2_inv(ql[i].r0);
+    qn[i] = linecoef29(LineCoef{f2_one(), ql[i].r1 * ri, ql[i].r2 * ri});
+  }
+  G1Dev pn;
+  memset(&pn, 0, sizeof(pn));
+  if (!P1.inf) {
+    fp lam = fe_from_int<ModP>(std::vector<uint32_t>{7, 11, 13, 17, 19, 23, 29, 31}.data());
+    fp l2_ = sqr(lam);
+    g1j J = {P1.x * l2_, P1.y * l2_ * lam, lam};
+    g1_pnorm(J, fp_inv(J.z * J.y), pn);
+    fp xq, yi;
+    g1dev_get(pn, xq, yi);
+    if (!fe_eq(yi * P1.y, fe_one<ModP>()) || !fe_eq(xq * P1.y, P1.x)) return 3;
+  }
+  fp2 gotn[6];
+  run6q([&](const SqH& x) { gotn[x.k] = q2_to_fp2(sq_miller_fn(x, qn.data(), P1, pn, l2.data(), 0, 1)); });
+  uint8_t a[384], b[384];
+  f12_to_bytes(a, final_exp(from_coefs(gotn), 0));
+  f12_to_bytes(b, final_exp(want, 0));
+  return memcmp(a, b, 384) ? 2 : 0;
 }
 
 // G2 job + pair-2 lines: sextet (sx_job_g2lines) vs one lane (job_g2lines).
@@ -253,6 +278,11 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   // the split one-lane device path (k_g2_part + k_g2lines1)
   std::vector<G2PartDev> part(4);
   for (int q = 0; q < 4; q++) job_g2_part(g, q, scal, tab.data(), part[q]);
+  for (int q = 0; q < 4; q++) {  // the carry-free part kernel writes the same words
+    G2PartDev p29;
+    job_g2_part29(g, q, scal, tab.data(), p29);
+    if (memcmp(&p29, &part[q], sizeof(G2PartDev))) return 200 + q;
+  }
   std::vector<G2Dev> o3(1);
   std::vector<EvLineDev> l3(MILLER_LINES);
   job_g2lines_parts(g, j, part.data(), o3.data(), &pt, l3.data(), 0, 1);
