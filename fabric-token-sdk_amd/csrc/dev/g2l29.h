@@ -289,7 +289,9 @@ FTS_HD void job_g2lines29(const G2Job& g, const PairJob& j, const uint32_t (*sca
 
 // k_g2_part on the carry-free form: the same Jacobian partial as job_g2_part
 // (j2q_madd runs madd-2007-bl's formulas, so X, Y, Z agree mod p and the
-// canonical 32-bit words written are byte-identical).
+// canonical 32-bit words written are byte-identical).  Measured as a kernel:
+// 256 VGPRs, one wave per SIMD, 3.69 vs 3.57 ms for the t' + lines stage --
+// not launched (profiles/r02g_norm_ab.txt).
 FTS_HD void job_g2_part29(const G2Job& g, int q, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev& out) {
   j2q acc = {q2_zero(), q2_zero(), q2_zero(), true};
 #pragma nounroll

@@ -1,7 +1,6 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
-#include "dev/g2l29.h"
 #include "dev/jobs.h"
 #include "launch.h"
 
@@ -36,14 +35,6 @@ __global__ void __launch_bounds__(64) k_g2_part(const G2Job* g2, uint32_t n, con
   if (i >= 4 * n) return;
   uint32_t q = i / n, job = i - q * n;
   job_g2_part(g2[job], (int)q, scal, tab, part[i]);
-}
-// the same partial sums on the carry-free field form (dev/g2l29.h)
-__global__ void __launch_bounds__(64) k_g2_part29(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8],
-                                                  const G2Dev* tab, G2PartDev* part) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 4 * n) return;
-  uint32_t q = i / n, job = i - q * n;
-  job_g2_part29(g2[job], (int)q, scal, tab, part[i]);
 }
 __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n,
                                                  const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,

@@ -103,8 +103,7 @@ struct ftz_ctx {
   DBuf<LineCoef> qlines;
   DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)
   DBuf<LineCoef29> qlines29n;        // normalised by r0 (k_miller_n); used when qnorm
-  bool qnorm = false;
-  bool qnorm_off = false;  // EXPERIMENT
+  bool qnorm = false;               // every fixed line has r0 != 0: k_miller_n, else k_miller
   ftz_options opt;                   // resolved options (ftz_ctx_create_ex)
   int serial = 0;                    // profiling: every kernel of a batch on one stream
   // t' + pair-2 lines: k_g2lines1 (one lane per job) or the sextet k_g2lines
@@ -113,7 +112,6 @@ struct ftz_ctx {
   // sextet (profiles/r02g_prover_layout.txt)
   int g2lanes = FTZ_LAYOUT_ONE_LANE;
   int g2lanes_prover = FTZ_LAYOUT_SEXTET;
-  bool g2part29 = false;  // EXPERIMENT
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
   // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every

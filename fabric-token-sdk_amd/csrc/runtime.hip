@@ -309,10 +309,6 @@ extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
     c->g2lanes = layout;
   else if (stage == FTZ_STAGE_PROVER_G2LINES)
     c->g2lanes_prover = layout;
-  else if (stage == 2)  // EXPERIMENT: k_g2_part field form (1: 32-bit, 6: carry-free)
-    c->g2part29 = layout == FTZ_LAYOUT_SEXTET;
-  else if (stage == 3)  // EXPERIMENT: fixed-Q lines (1: raw k_miller, 6: normalised k_miller_n if available)
-    c->qnorm_off = layout == FTZ_LAYOUT_ONE_LANE;
   else
     return set_err(FTZ_E_INVALID, "unknown stage");
   return FTZ_SUCCESS;
@@ -534,10 +530,7 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
 // sextet layout (k_g2lines); same bytes either way
 static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
   if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE) {
-    if (c->g2part29)
-      k_g2_part29<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
-    else
-      k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
+    k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);
   } else {
     k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,
@@ -546,7 +539,7 @@ static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipS
 }
 
 static void launch_miller(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
-  if (c->qnorm && !c->qnorm_off) {
+  if (c->qnorm) {
     k_miller_n<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29n.p, p.lines2, p.g1out,
                                                                    p.pnorm, p.fbuf);
     return;

@@ -149,7 +149,7 @@ class Context:
         _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)
 
     LAYOUTS = {"one_lane": 1, "sextet": 6}
-    STAGES = {"g2lines": 0, "prover_g2lines": 1, "g2part": 2, "fixed_lines": 3}
+    STAGES = {"g2lines": 0, "prover_g2lines": 1}
 
     def set_layout(self, stage, layout):
         """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines'
