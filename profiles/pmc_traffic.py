@@ -34,7 +34,7 @@ def main(fetch_db, write_db):
     if part and comb:
         out["g1"] = kb(("k_g1_part", part[-1])) + kb(("k_g1_combine", comb[-1]))
         out["g1p"] = kb(("k_g1_part", part[0])) + kb(("k_g1_combine", comb[0]))
-    for key, names in (("miller", ("k_miller",)), ("fexp", ("k_fexp_exact", "k_fexp")),
+    for key, names in (("miller", ("k_miller_n", "k_miller")), ("fexp", ("k_fexp_exact", "k_fexp")),
                        ("g2", ("k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
         for name in names:
             parts = name.split("+")
