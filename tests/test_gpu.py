@@ -55,6 +55,16 @@ def test_golden_verdicts_every_layout(zk, golden, pp, g2lines):
         assert got == {c_["name"]: c_["expect"] for c_ in cases}
 
 
+def test_set_layout_rejects_unknown_values(zk, ctx_a):
+    """ftz_ctx_set_layout: unknown stage or layout -> FTZ_E_INVALID, the context unchanged"""
+    lib = ctx_a._lib
+    assert lib.ftz_ctx_set_layout(ctx_a._h, 7, 1) != 0
+    assert lib.ftz_ctx_set_layout(ctx_a._h, 0, 2) != 0
+    assert lib.ftz_ctx_set_layout(None, 0, 1) != 0
+    with pytest.raises(KeyError):
+        ctx_a.set_layout("pairing", "one_lane")
+
+
 def test_golden_pp_b_verdicts(zk, golden):
     if "pp_b" not in golden:
         pytest.skip("no PP-B fixtures")
