@@ -2,7 +2,7 @@
 // NymSignature.Ver on FP256BN, one lane per signature.  The reference calls it
 // per input token from TransferSignatureValidate
 // (zkatdlog/crypto/validator/validator_transfer.go:42-82) through
-// identity/msp/idemix/deserializer.go:155-167 Verifier.Verify.  [EXT] IBM/idemix
+// identity/msp/idemix/deserializer.go:153-163 Verifier.Verify.  [EXT] IBM/idemix
 // v0.0.0-20220113150823-80dd4cb2d74e (go.mod:6), restated:
 //   t = HSk^ProofSSk * HRand^ProofSRNym * Nym^-ProofC
 //   c = HashToZr("sign" || t || Nym || ipk.Hash || msg)     (G1 = 0x04||X||Y)

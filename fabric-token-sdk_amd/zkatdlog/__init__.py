@@ -522,7 +522,7 @@ class Idemix:
 
 
 class OwnerVerifier:
-    """driver.Verifier of an owner identity (identity/msp/idemix/deserializer.go:155-167)."""
+    """driver.Verifier of an owner identity (identity/msp/idemix/deserializer.go:153-163)."""
 
     def __init__(self, ix, owner):
         self.ix = ix

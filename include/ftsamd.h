@@ -260,7 +260,7 @@ int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz
  * interop/htlc/deserializer.go:31-43 -> identity/owner.go:62-68 ->
  * identity/msp/idemix/deserializer.go:83-95, common.go:40-117) and
  * verifier.Verify(message, sigma) (common/backend.go:32-41 ->
- * identity/msp/idemix/deserializer.go:155-167 -> IBM/idemix NymSignature.Ver):
+ * identity/msp/idemix/deserializer.go:153-163 -> IBM/idemix NymSignature.Ver):
  * owner = the token's Owner bytes (ASN.1 RawOwner), msg = the signed request
  * bytes, sig = the NymSignature proto.  ftz_idemix_create takes
  * PublicParams.IdemixIssuerPK (setup.go:36) -- the IssuerPublicKey proto -- and

@@ -16,7 +16,7 @@ The reference path (paths relative to /root/reference/token/core/):
   common.go:36-117 Deserialize(raw, checkValidity=false): proto
   msp.SerializedIdentity, then msp.SerializedIdemixIdentity (NymX, NymY must be
   non-nil), the nym public key imported from NymX||NymY, OU and Role protos;
-* deserializer.go:155-167 Verifier.Verify -> CSP.Verify(NymPK, sigma, msg,
+* deserializer.go:153-163 Verifier.Verify -> CSP.Verify(NymPK, sigma, msg,
   IdemixNymSignerOpts{IssuerPK}) -> IBM/idemix NymSignature.Ver.
 
 [EXT] IBM/idemix v0.0.0-20220113150823-80dd4cb2d74e, IBM/mathlib
