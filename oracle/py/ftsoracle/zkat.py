@@ -738,17 +738,19 @@ def issue_prove(pp, rnd, tokens, wit, ttype, anonymous=False, tag="issue"):
 
 def issue_wf_verify(pp, tokens, anonymous, raw):
     """issue/wellformedness.go:206-265."""
+    # wf.Deserialize (json.Unmarshal) covers the syntax and every field's
+    # decoding: any error there is "failed to verify well-formedness proof"
     try:
         v = J.parse(raw if raw is not None else b"")
+        if v[0] == "null":
+            v = ("obj", [])
+        wf = {"Type": dec_zr(J.field(v, "Type")),
+              "Values": J.dec_list(J.field(v, "Values"), dec_zr),
+              "BlindingFactors": J.dec_list(J.field(v, "BlindingFactors"), dec_zr),
+              "TypeInTheClear": J.dec_string(J.field(v, "TypeInTheClear")),
+              "Challenge": dec_zr(J.field(v, "Challenge"))}
     except J.GoJSONError:
         raise VerifyError(ERR_PARSE, "failed to verify well-formedness proof")
-    if v[0] == "null":
-        v = ("obj", [])
-    wf = {"Type": dec_zr(J.field(v, "Type")),
-          "Values": J.dec_list(J.field(v, "Values"), dec_zr),
-          "BlindingFactors": J.dec_list(J.field(v, "BlindingFactors"), dec_zr),
-          "TypeInTheClear": J.dec_string(J.field(v, "TypeInTheClear")),
-          "Challenge": dec_zr(J.field(v, "Challenge"))}
     c = wf["Challenge"]
     if c is None:
         raise VerifyError(ERR_MALFORMED, "failed to verify well-formedness proof: invalid public parameters")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Make tests/golden/fuzz_cases.json: seeded mutations (fuzzmut.mutate) of the
-golden corpus's valid PP-A transfers, each with the verdict of the oracle
-restatement (ftsoracle.zkat.transfer_verify).  Test data only; the cases are
+golden corpus's valid PP-A transfers and issues, each with the verdict of the
+oracle restatement (ftsoracle.zkat.transfer_verify / issue_verify).  Test data only; the cases are
 stored as (base, mode, pos, xor), the proofs are rebuilt by the tests.
 
     python tests/golden/make_fuzz.py [n_per_base]
@@ -20,7 +20,8 @@ sys.path.insert(0, HERE)
 
 from fuzzmut import MODES, mutate  # noqa: E402
 
-BASES = ["valid_2in_2out", "valid_2in_2out_1", "valid_3in_1out", "valid_1in_3out"]
+BASES = ["valid_2in_2out", "valid_2in_2out_1", "valid_3in_1out", "valid_1in_3out", "issue_valid_0",
+         "issue_valid_2_anon"]
 SEED = 20261017
 
 
@@ -38,6 +39,8 @@ def _verdict(job):
     ins = [C.g1_from_bytes(ins_b[64 * i:64 * i + 64]) for i in range(len(ins_b) // 64)]
     outs = [C.g1_from_bytes(outs_b[64 * i:64 * i + 64]) for i in range(len(outs_b) // 64)]
     proof = mutate(base64.b64decode(case["proof"]), mode, pos, xor)
+    if case["kind"] == "issue":
+        return Z.issue_verify(pp, outs, proof, case["anonymous"])[1]
     return Z.transfer_verify(pp, ins, outs, proof)[1]
 
 
@@ -49,14 +52,15 @@ def main():
     for b in BASES:
         for k in range(n):
             mode = MODES[k % len(MODES)]
-            rows.append({"name": "fz_%s_%03d" % (b, k), "base": b, "mode": mode, "pos": rng.randrange(1 << 20),
+            rows.append({"name": "fz_%s_%03d" % (b, k), "base": b, "kind": cases[b]["kind"], "mode": mode,
+                         "pos": rng.randrange(1 << 20),
                          "xor": rng.randrange(1, 256)})
     with Pool(min(8, os.cpu_count() or 1)) as pool:
         codes = pool.map(_verdict, [(pp_json, cases[r["base"]], r["mode"], r["pos"], r["xor"]) for r in rows])
     for r, c in zip(rows, codes):
         r["expect"] = c
     out = {"generator": "tests/golden/make_fuzz.py", "mutations": "tests/golden/fuzzmut.py", "seed": SEED,
-           "oracle": "ftsoracle.zkat.transfer_verify (PP-A)", "cases": rows}
+           "oracle": "ftsoracle.zkat.transfer_verify / issue_verify (PP-A)", "cases": rows}
     with open(os.path.join(HERE, "fuzz_cases.json"), "w") as f:
         json.dump(out, f, indent=0)
     hist = {}

@@ -1,5 +1,5 @@
 """Mutation fuzz corpus (tests/golden/fuzz_cases.json, made by make_fuzz.py with
-the oracle's verdicts): 240 seeded mutations of valid PP-A transfers -- outer
+the oracle's verdicts): 360 seeded mutations of valid PP-A transfers and issues -- outer
 bytes, inner document bytes, and single-bit flips inside well-formed base64
 elements, which reach the curve checks, transcripts and pairings.  The host
 emulation (CPU tier) and the GPU path (gpu tier) must return the oracle's
@@ -22,42 +22,53 @@ def fuzz(golden):
     with open(os.path.join(ROOT, "tests", "golden", "fuzz_cases.json")) as f:
         fz = json.load(f)
     base = {c["name"]: c for c in golden["pp_a"]["cases"]}
-    rows = []
+    tr, iss = [], []
     for r in fz["cases"]:
         c = base[r["base"]]
-        rows.append((bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]),
-                     mutate(base64.b64decode(c["proof"]), r["mode"], r["pos"], r["xor"])))
-    return fz["cases"], rows
+        proof = mutate(base64.b64decode(c["proof"]), r["mode"], r["pos"], r["xor"])
+        if r["kind"] == "issue":
+            iss.append((r, (bytes.fromhex(c["outputs"]), proof, c["anonymous"])))
+        else:
+            tr.append((r, (bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), proof)))
+    return tr, iss
+
+
+def _check(rows, got):
+    bad = {r["name"]: (v, r["expect"]) for (r, _), v in zip(rows, got) if v != r["expect"]}
+    assert not bad, bad
 
 
 def test_fuzz_corpus_shape(fuzz):
-    cases, _ = fuzz
-    assert len(cases) >= 200
-    assert len({c["expect"] for c in cases}) >= 5  # parse, malformed, WF, range, membership, panic classes
+    tr, iss = fuzz
+    assert len(tr) >= 200 and len(iss) >= 100
+    codes = {r["expect"] for r, _ in tr + iss}
+    assert len(codes) >= 5  # parse, malformed, WF, range, membership, panic classes
 
 
 def test_fuzz_emu_matches_oracle(emu, golden, fuzz):
     from zkatdlog import _abi as A
-    cases, rows = fuzz
+    tr, iss = fuzz
     pp = golden["pp_a"]["pp"].encode()
     err = ctypes.create_string_buffer(256)
     ctx = emu.emu_ctx_create(pp, len(pp), err, 256)
     assert ctx, err.value
     try:
-        arr, keep = A.pack_transfers(rows)
-        codes = (ctypes.c_int32 * len(rows))()
-        emu.emu_verify_transfers(ctx, len(rows), arr, codes)
+        arr, keep = A.pack_transfers([t for _, t in tr])
+        codes = (ctypes.c_int32 * len(tr))()
+        emu.emu_verify_transfers(ctx, len(tr), arr, codes)
+        _check(tr, list(codes))
+        arr, keep = A.pack_issues([t for _, t in iss])
+        codes = (ctypes.c_int32 * len(iss))()
+        emu.emu_verify_issues(ctx, len(iss), arr, codes)
+        _check(iss, list(codes))
     finally:
         emu.emu_ctx_destroy(ctx)
-    bad = {c["name"]: (v, c["expect"]) for c, v in zip(cases, codes) if v != c["expect"]}
-    assert not bad, bad
 
 
 @pytest.mark.gpu
 def test_fuzz_gpu_matches_oracle(golden, fuzz):
     import zkatdlog
-    cases, rows = fuzz
+    tr, iss = fuzz
     with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0) as ctx:
-        got = ctx.verify_transfers(rows)
-    bad = {c["name"]: (v, c["expect"]) for c, v in zip(cases, got) if v != c["expect"]}
-    assert not bad, bad
+        _check(tr, ctx.verify_transfers([t for _, t in tr]))
+        _check(iss, ctx.verify_issues([t for _, t in iss]))
