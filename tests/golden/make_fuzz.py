@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Make tests/golden/fuzz_cases.json: seeded mutations (fuzzmut.mutate) of the
-golden corpus's valid PP-A transfers and issues, each with the verdict of the
+golden corpus's valid PP-A / PP-B transfers and issues, each with the verdict of the
 oracle restatement (ftsoracle.zkat.transfer_verify / issue_verify).  Test data only; the cases are
 stored as (base, mode, pos, xor), the proofs are rebuilt by the tests.
 
-    python tests/golden/make_fuzz.py [n_per_base]
+    python tests/golden/make_fuzz.py [scale]
 """
 import base64
 import json
@@ -20,14 +20,16 @@ sys.path.insert(0, HERE)
 
 from fuzzmut import MODES, mutate  # noqa: E402
 
-BASES = ["valid_2in_2out", "valid_2in_2out_1", "valid_3in_1out", "valid_1in_3out", "issue_valid_0",
-         "issue_valid_2_anon"]
+BASES = [("pp_a", b, 60) for b in ["valid_2in_2out", "valid_2in_2out_1", "valid_3in_1out", "valid_1in_3out",
+                                   "issue_valid_0", "issue_valid_2_anon"]]
+BASES += [("pp_b", b, 20) for b in ["ppb_valid_2in_2out_64bit_values", "ppb_issue_valid_2_anon"]]
 SEED = 20261017
 
 
 def _load():
-    g = json.load(open(os.path.join(HERE, "zkatdlog_golden.json")))["pp_a"]
-    return g["pp"], {c["name"]: c for c in g["cases"]}
+    g = json.load(open(os.path.join(HERE, "zkatdlog_golden.json")))
+    return ({k: g[k]["pp"] for k in ("pp_a", "pp_b")},
+            {k: {c["name"]: c for c in g[k]["cases"]} for k in ("pp_a", "pp_b")})
 
 
 def _verdict(job):
@@ -45,22 +47,23 @@ def _verdict(job):
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 60
-    pp_json, cases = _load()
+    scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+    pps, cases = _load()
     rng = random.Random(SEED)
     rows = []
-    for b in BASES:
-        for k in range(n):
+    for pp, b, n in BASES:
+        for k in range(int(n * scale)):
             mode = MODES[k % len(MODES)]
-            rows.append({"name": "fz_%s_%03d" % (b, k), "base": b, "kind": cases[b]["kind"], "mode": mode,
+            rows.append({"name": "fz_%s_%03d" % (b, k), "pp": pp, "base": b, "kind": cases[pp][b]["kind"], "mode": mode,
                          "pos": rng.randrange(1 << 20),
                          "xor": rng.randrange(1, 256)})
     with Pool(min(8, os.cpu_count() or 1)) as pool:
-        codes = pool.map(_verdict, [(pp_json, cases[r["base"]], r["mode"], r["pos"], r["xor"]) for r in rows])
+        codes = pool.map(_verdict, [(pps[r["pp"]], cases[r["pp"]][r["base"]], r["mode"], r["pos"], r["xor"])
+                                    for r in rows])
     for r, c in zip(rows, codes):
         r["expect"] = c
     out = {"generator": "tests/golden/make_fuzz.py", "mutations": "tests/golden/fuzzmut.py", "seed": SEED,
-           "oracle": "ftsoracle.zkat.transfer_verify / issue_verify (PP-A)", "cases": rows}
+           "oracle": "ftsoracle.zkat.transfer_verify / issue_verify (PP-A and PP-B)", "cases": rows}
     with open(os.path.join(HERE, "fuzz_cases.json"), "w") as f:
         json.dump(out, f, indent=0)
     hist = {}
