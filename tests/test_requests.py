@@ -127,3 +127,40 @@ def test_gpu_requests_many(gctx, fx):
     assert codes == [r["expect"] for r in reqs]
     assert failed == [r["failed_action"] for r in reqs]
     print("%d token requests in %.3f s: %.0f requests/s" % (len(reqs), dt, len(reqs) / dt), flush=True)
+
+
+def test_asn1_decoder_mutation_fuzz(fx):
+    """2000 seeded byte / length mutations of the fixture requests: the
+    library's DER TokenRequest decoder (host code) accepts exactly what the
+    oracle restatement of Go encoding/asn1 accepts, with the same fields."""
+    import random
+
+    import zkatdlog
+    rng = random.Random(20261017)
+    raws = [r["raw_b"] for r in fx["requests"] if len(r["raw_b"]) > 4]
+    agree = 0
+    for k in range(2000):
+        b = bytearray(rng.choice(raws))
+        mode = k % 4
+        if mode == 0:  # flip a byte anywhere
+            i = rng.randrange(len(b))
+            b[i] ^= rng.randrange(1, 256)
+        elif mode == 1:  # perturb a header byte near the front (identifiers, lengths)
+            i = rng.randrange(min(len(b), 12))
+            b[i] = rng.randrange(256)
+        elif mode == 2:  # truncate
+            del b[rng.randrange(1, len(b)):]
+        else:  # trailing garbage (FromBytes ignores it)
+            b += bytes(rng.randrange(256) for _ in range(rng.randrange(1, 8)))
+        raw = bytes(b)
+        try:
+            want = R.der_token_request(raw)
+        except R.Asn1Error:
+            want = None
+        try:
+            got = zkatdlog.decode_token_request(raw)
+        except ValueError:
+            got = None
+        assert got == want, (k, mode, raw[:16].hex())
+        agree += 1
+    assert agree == 2000
