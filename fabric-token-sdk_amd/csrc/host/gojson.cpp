@@ -406,6 +406,160 @@ int64_t JDoc::field(uint32_t obj, const char* name) const {
   return found;
 }
 
+namespace {
+
+struct Merger {
+  JDoc& d;
+
+  uint32_t push(JNode n) {
+    d.nodes.push_back(n);
+    return (uint32_t)d.nodes.size() - 1;
+  }
+  uint32_t null_node() { return push({J_NULL, 0, 0, 0}); }
+  uint32_t key_node(const char* name) {
+    uint32_t off = (uint32_t)d.pool.size();
+    d.pool.append(name);
+    d.pool.push_back('\0');
+    return push({J_STR, 0, off, (uint32_t)strlen(name)});
+  }
+  static int schema_len(const JField* s) {
+    int n = 0;
+    while (s && s[n].name) n++;
+    return n;
+  }
+
+  // members of every object in occs (in order) as one object
+  uint32_t merge(const std::vector<uint32_t>& occs, const JField* sch) {
+    int nf = schema_len(sch);
+    std::vector<uint32_t> pairs;
+    std::vector<std::vector<uint32_t>> coll((size_t)nf);
+    for (uint32_t o : occs) {
+      const JNode on = d.nodes[o];
+      for (uint32_t k = 0; k < on.count; k++) {
+        uint32_t key = d.kids[on.first + 2 * k], val = d.kids[on.first + 2 * k + 1];
+        int f = -1;
+        for (int q = 0; q < nf && f < 0; q++)
+          if (go_key_matches(d.str(key), d.nodes[key].count, sch[q].name, strlen(sch[q].name))) f = q;
+        if (f < 0) {
+          pairs.push_back(key);
+          pairs.push_back(val);
+        } else {
+          coll[(size_t)f].push_back(val);
+        }
+      }
+    }
+    bool changed = occs.size() > 1;
+    std::vector<uint32_t> res((size_t)nf, 0);
+    for (int q = 0; q < nf; q++) {
+      if (coll[(size_t)q].empty()) continue;
+      res[(size_t)q] = sch[q].kind == JF_STRUCT ? rstruct(coll[(size_t)q], sch[q].sub)
+                                                 : rslice(coll[(size_t)q], sch[q].sub);
+      changed |= coll[(size_t)q].size() > 1 || res[(size_t)q] != coll[(size_t)q][0];
+    }
+    if (!changed) return occs[0];
+    for (int q = 0; q < nf; q++) {
+      if (coll[(size_t)q].empty()) continue;
+      pairs.push_back(key_node(sch[q].name));
+      pairs.push_back(res[(size_t)q]);
+    }
+    uint32_t first = (uint32_t)d.kids.size();
+    d.kids.insert(d.kids.end(), pairs.begin(), pairs.end());
+    return push({J_OBJ, 0, first, (uint32_t)(pairs.size() / 2)});
+  }
+
+  // *T field: the occurrences since the last null merge
+  uint32_t rstruct(const std::vector<uint32_t>& vals, const JField* sub) {
+    std::vector<uint32_t> cur;
+    bool nil = true;
+    for (uint32_t v : vals) {
+      JType t = d.nodes[v].type;
+      if (t == J_NULL) {
+        cur.clear();
+        nil = true;
+      } else if (t == J_OBJ) {
+        cur.push_back(v);
+        nil = false;
+      } else {
+        return v;  // type error: reported by the typed decoder
+      }
+    }
+    if (nil) return vals.size() == 1 ? vals[0] : null_node();
+    return merge(cur, sub);
+  }
+
+  // []*T field: element slots survive truncation (see gojson.h)
+  uint32_t rslice(const std::vector<uint32_t>& vals, const JField* sub) {
+    struct Slot {
+      bool nil = true;
+      std::vector<uint32_t> occ;
+    };
+    std::vector<Slot> backing;
+    size_t len = 0;
+    bool nil = true;
+    for (uint32_t v : vals) {
+      JType t = d.nodes[v].type;
+      if (t == J_NULL) {
+        backing.clear();
+        len = 0;
+        nil = true;
+        continue;
+      }
+      if (t != J_ARR) return v;
+      nil = false;
+      uint32_t n = d.len(v);
+      size_t i = 0;
+      for (; i < n; i++) {
+        uint32_t e = d.elem(v, (uint32_t)i);
+        if (i >= backing.size()) backing.emplace_back();
+        if (i + 1 > len) len = i + 1;
+        JType te = d.nodes[e].type;
+        if (te == J_NULL) {
+          backing[i] = Slot();
+        } else if (te == J_OBJ) {
+          backing[i].nil = false;
+          backing[i].occ.push_back(e);
+        } else {
+          return e;
+        }
+      }
+      if (i < len) len = i;
+      if (i == 0) {
+        backing.clear();
+        len = 0;
+      }
+    }
+    if (nil) return vals.size() == 1 ? vals[0] : null_node();
+    std::vector<uint32_t> elems(len);
+    bool changed = vals.size() > 1;
+    for (size_t i = 0; i < len; i++) {
+      if (backing[i].nil) {
+        elems[i] = vals.size() == 1 ? d.elem(vals[0], (uint32_t)i) : null_node();
+      } else {
+        elems[i] = merge(backing[i].occ, sub);
+        changed |= backing[i].occ.size() > 1 || elems[i] != backing[i].occ[0];
+      }
+    }
+    if (!changed) return vals[0];
+    uint32_t first = (uint32_t)d.kids.size();
+    d.kids.insert(d.kids.end(), elems.begin(), elems.end());
+    return push({J_ARR, 0, first, (uint32_t)len});
+  }
+};
+
+}  // namespace
+
+void go_merge(JDoc& d, const JField* schema) {
+  if (d.nodes.empty()) return;
+  uint32_t root = d.root();
+  if (d.at(root).type != J_OBJ) return;
+  Merger m{d};
+  uint32_t r = m.merge({root}, schema);
+  if (r != d.root()) {
+    JNode copy = d.nodes[r];
+    d.nodes.push_back(copy);  // root() is the last node
+  }
+}
+
 bool b64_decode_append(const char* s, size_t n, std::vector<uint8_t>& out) {
   size_t base = out.size();
   out.resize(base + n / 4 * 3 + 3);

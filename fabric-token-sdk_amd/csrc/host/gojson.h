@@ -4,7 +4,8 @@
 //   * struct fields match object keys exactly, else by Go's foldFunc for the
 //     field name (encoding/json/fold.go: ASCII case folding, plus U+017F 'ſ'
 //     for s/S and U+212A Kelvin sign for k/K when the name holds those letters);
-//     a later duplicate key overwrites an earlier one; unknown keys are ignored;
+//     a later duplicate key overwrites an earlier leaf value and merges into an
+//     earlier struct / slice-of-struct value (go_merge); unknown keys are ignored;
 //   * strings are unquoted as encoding/json unquoteBytes does: escapes decoded,
 //     unpaired surrogates and invalid UTF-8 bytes become U+FFFD (one per byte);
 //   * JSON null leaves pointers / slices nil;
@@ -52,6 +53,29 @@ struct JDoc {
   uint32_t len(uint32_t i) const { return nodes[i].count; }
   uint32_t elem(uint32_t arr, uint32_t k) const { return kids[nodes[arr].first + k]; }
 };
+
+// Duplicate keys of struct-typed fields (Go 1.18 decode.go): a *T field whose
+// key occurs again is decoded INTO the struct already there (indirect() keeps a
+// non-nil pointer, object() does not zero it), so the occurrences merge key by
+// key, a null in between resetting the pointer; a []*T field decodes element i
+// into the existing element i and then truncates, and the backing array
+// outlives the truncation, so a later, longer array merges into the old
+// elements again (an empty array installs a fresh slice, null a nil one).
+// go_merge rewrites a parsed document so that each such field (named by a
+// schema, recursively) occurs once, holding the merged value -- built from the
+// concatenated members of its occurrences, so field()'s last-match lookup then
+// gives Go's answer for the leaf fields inside as well.  The document is left
+// untouched when nothing needs merging; otherwise the new root is appended
+// last (root() stays valid).  A struct field whose value is neither null nor
+// an object (an array element neither null nor an object) is left to the
+// typed decoder, which reports the type error Unmarshal would return.
+enum JFieldKind : uint8_t { JF_STRUCT = 1, JF_SLICE = 2 };
+struct JField {
+  const char* name;      // nullptr ends a schema
+  JFieldKind kind;
+  const JField* sub;     // schema of the struct / element struct (may be empty)
+};
+void go_merge(JDoc& d, const JField* schema);
 
 // Go encoding/json field matching of an (unescaped) object key against an
 // ASCII struct field name.

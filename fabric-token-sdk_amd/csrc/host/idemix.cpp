@@ -363,7 +363,10 @@ void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_
   static const PbKind k_ser[5] = {PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES};
   if (!pb_simple(idb, idn, 5, k_ser, pr, v).empty())
     return fail(FTZ_ERR_OWNER, "could not deserialize a SerializedIdemixIdentity");
-  if (!pr[0] || !pr[1]) return fail(FTZ_ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid");
+  // proto3 bytes without presence decode through consumeBytesNoZero (append([]byte(nil), v...)):
+  // an empty NymX / NymY is nil even when it is on the wire (common.go:52 nil check)
+  if (!pr[0] || !pr[1] || v[0].len == 0 || v[1].len == 0)
+    return fail(FTZ_ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid");
   // NymPublicKey import: raw = NymX || NymY split in halves, FromBytes reads 32 bytes of each
   size_t tot = v[0].len + v[1].len, half = tot / 2;
   if (half < 32) return fail(FTZ_ERR_OWNER, "failed to import nym public key");

@@ -26,6 +26,20 @@
 
 namespace ftsh {
 
+// struct-pointer / slice-of-struct-pointer fields, whose duplicate keys merge
+// (go_merge): range/proof.go:25-57 RangeProof -> EqualityProofs,
+// MembershipProof -> sigproof/membership.go:19-33 MembershipProof ->
+// pssign.Signature; setup.go:25-54 PublicParams -> RangeProofParams ->
+// SignedValues []*pssign.Signature
+static const JField LEAVES_F[] = {{nullptr, JF_STRUCT, nullptr}};
+static const JField SIGPROOF_F[] = {{"Signature", JF_STRUCT, LEAVES_F}, {nullptr, JF_STRUCT, nullptr}};
+static const JField MP_F[] = {{"SignatureProofs", JF_SLICE, SIGPROOF_F}, {nullptr, JF_STRUCT, nullptr}};
+static const JField RANGE_F[] = {{"EqualityProofs", JF_STRUCT, LEAVES_F},
+                                 {"MembershipProofs", JF_SLICE, MP_F},
+                                 {nullptr, JF_STRUCT, nullptr}};
+static const JField RPP_F[] = {{"SignedValues", JF_SLICE, LEAVES_F}, {nullptr, JF_STRUCT, nullptr}};
+static const JField PP_F[] = {{"RangeProofParams", JF_STRUCT, RPP_F}, {nullptr, JF_STRUCT, nullptr}};
+
 void Plan::clear() {
   rnd.clear();
   sc1.clear();
@@ -76,9 +90,10 @@ struct Doc {
 
   Doc(Plan* p, JDoc& jd) : d(jd), pl(p) {}
 
-  bool parse(const std::vector<uint8_t>& b, bool nil) {
+  bool parse(const std::vector<uint8_t>& b, bool nil, const JField* schema = nullptr) {
     if (nil) return ok = false;  // json.Unmarshal(nil) -> "unexpected end of JSON input"
     ok = d.parse(b.data(), b.size());
+    if (ok && schema) go_merge(d, schema);
     return ok;
   }
 
@@ -598,7 +613,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
     pl.wire.resize(wire_mark);
     r = RangeDoc();
     Doc doc(&pl, jrc);
-    if (!doc.parse(rc, rc_nil)) {
+    if (!doc.parse(rc, rc_nil, RANGE_F)) {
       fail(E_PARSE);
       return;
     }
@@ -1480,6 +1495,7 @@ std::string validate_pp(const uint8_t* p, size_t n, const char* label) {
   if (dec_bytes(outer, outer.field(outer.root(), "Raw"), raw) == D_ERR) return "invalid Raw";
   JDoc d;
   if (!d.parse(raw.data(), raw.size())) return "failed unmarshalling public parameters";
+  go_merge(d, PP_F);
   uint32_t r = d.root();
   if (d.at(r).type == J_NULL) r = NONE;
   else if (d.at(r).type != J_OBJ) return "failed unmarshalling public parameters";
@@ -1540,6 +1556,7 @@ std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out)
   if (dec_bytes(outer, outer.field(root, "Raw"), raw) != D_OK) return "missing Raw";
   JDoc d;
   if (!d.parse(raw.data(), raw.size())) return "failed unmarshalling public parameters";
+  go_merge(d, PP_F);
   uint32_t r = d.root();
   if (d.at(r).type != J_OBJ) return "failed unmarshalling public parameters";
   out.label = ident;

@@ -156,12 +156,14 @@ std::string check_metadata(const JDoc& d, int64_t node) {
 
 // JSON null at the top level leaves the struct untouched (Go Unmarshal into a
 // pointer to a struct); anything else but an object is a type error
-bool top_object(JDoc& d, const uint8_t* p, size_t n, std::string& err, bool& is_null) {
+bool top_object(JDoc& d, const uint8_t* p, size_t n, std::string& err, bool& is_null,
+                const JField* schema = nullptr) {
   is_null = false;
   if (!d.parse(p, n)) {
     err = "invalid JSON";
     return false;
   }
+  if (schema) go_merge(d, schema);
   JType t = d.at(d.root()).type;
   if (t == J_NULL) {
     is_null = true;
@@ -176,6 +178,12 @@ bool top_object(JDoc& d, const uint8_t* p, size_t n, std::string& err, bool& is_
 
 thread_local JDoc tl_doc;
 
+// []*token.Token fields: duplicate keys merge into the tokens already decoded
+// (go_merge; transfer.go / issue.go action structs)
+const JField TOKEN_F[] = {{nullptr, JF_STRUCT, nullptr}};
+const JField TRANSFER_F[] = {{"OutputTokens", JF_SLICE, TOKEN_F}, {nullptr, JF_STRUCT, nullptr}};
+const JField ISSUE_F[] = {{"outputs", JF_SLICE, TOKEN_F}, {nullptr, JF_STRUCT, nullptr}};
+
 }  // namespace
 
 std::string dec_transfer_action(const uint8_t* p, size_t n, TransferAct& a, std::vector<uint8_t>& pool) {
@@ -183,7 +191,7 @@ std::string dec_transfer_action(const uint8_t* p, size_t n, TransferAct& a, std:
   std::string err;
   bool is_null;
   JDoc& d = tl_doc;
-  if (!top_object(d, p, n, err, is_null)) return err;
+  if (!top_object(d, p, n, err, is_null, TRANSFER_F)) return err;
   if (is_null) return "";
   uint32_t root = d.root();
   // Inputs []string
@@ -220,7 +228,7 @@ std::string dec_issue_action(const uint8_t* p, size_t n, IssueAct& a, std::vecto
   std::string err;
   bool is_null;
   JDoc& d = tl_doc;
-  if (!top_object(d, p, n, err, is_null)) return err;
+  if (!top_object(d, p, n, err, is_null, ISSUE_F)) return err;
   if (is_null) return "";
   uint32_t root = d.root();
   std::vector<uint8_t> tmp;

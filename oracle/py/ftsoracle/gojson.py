@@ -9,7 +9,8 @@ Decoding follows ``json.Unmarshal`` of Go 1.18 (reference go.mod:3): object
 keys match struct fields exactly, else by encoding/json fold.go's foldFunc
 for the field name (ASCII case folding; when the name holds k/K/s/S the key
 may also spell them U+212A KELVIN SIGN / U+017F LATIN SMALL LETTER LONG S),
-unknown keys are ignored, a later duplicate overwrites an earlier one,
+unknown keys are ignored, a later duplicate overwrites an earlier leaf value
+and merges into an earlier struct / slice-of-struct value (resolve()),
 ``null`` leaves a nil pointer/slice, strings are unquoted as unquoteBytes does
 (invalid UTF-8 bytes and unpaired surrogates become U+FFFD, one per byte),
 ``[]byte`` is decoded by ``base64.StdEncoding`` (``\\r``/``\\n`` ignored,
@@ -314,6 +315,90 @@ def field(obj, name):
         if key_matches(k, name):
             found = v
     return found
+
+
+# ------------------------------------------------------------------ duplicate keys
+# Go 1.18 decode.go does not REPLACE a struct-pointer or slice-of-struct-pointer
+# field when its key occurs again, it decodes INTO the value already there:
+#   * indirect() keeps a non-nil pointer and object() does not zero the struct,
+#     so two objects for one *T field merge key by key (a null in between resets
+#     the pointer to nil);
+#   * array() decodes element i into the slice's existing element i (a non-nil
+#     *T element again merges), then truncates to the new length; the backing
+#     array survives the truncation, so a later, longer array re-exposes (and
+#     merges into) the old elements -- growth copies every element below the
+#     write index, so nothing reachable is ever dropped; an empty JSON array
+#     installs a fresh empty slice, null a nil one.
+# Leaf fields ([]byte, string, int, mathlib elements with their own
+# UnmarshalJSON) are replaced, which field()'s last-match lookup already gives.
+# resolve() rewrites a parsed value so that every struct-typed field named in
+# `schema` appears once, holding the merged value; schema = {FieldName:
+# (STRUCT | SLICE, sub_schema)}.
+STRUCT, SLICE = "struct", "slice"
+NULL = ("null", None)
+
+
+def resolve(v, schema):
+    """v: a parsed top-level value decoded into a fresh struct."""
+    if v is None or v[0] != "obj" or not schema:
+        return v
+    return _merge([v], schema)
+
+
+def _merge(occs, schema):
+    pairs, coll = [], {}
+    for o in occs:
+        for k, val in o[1]:
+            f = next((n for n in schema if key_matches(k, n)), None)
+            if f is None:
+                pairs.append((k, val))
+            else:
+                coll.setdefault(f, []).append(val)
+    for f, vals in coll.items():
+        kind, sub = schema[f]
+        pairs.append((f, _res_struct(vals, sub) if kind == STRUCT else _res_slice(vals, sub)))
+    return ("obj", pairs)
+
+
+def _res_struct(vals, sub):
+    cur = None
+    for val in vals:
+        if val[0] == "null":
+            cur = None
+        elif val[0] == "obj":
+            cur = (cur or []) + [val]
+        else:
+            return val  # type error: Unmarshal fails whatever follows; the decoder reports it
+    return NULL if cur is None else _merge(cur, sub)
+
+
+def _res_slice(vals, sub):
+    backing, ln, isnil = [], 0, True
+    for val in vals:
+        if val[0] == "null":
+            backing, ln, isnil = [], 0, True
+            continue
+        if val[0] != "arr":
+            return val
+        isnil = False
+        i = 0
+        for e in val[1]:
+            if i >= len(backing):
+                backing.append(None)
+            ln = max(ln, i + 1)
+            if e[0] == "null":
+                backing[i] = None
+            elif e[0] == "obj":
+                backing[i] = (backing[i] or []) + [e]
+            else:
+                return e
+            i += 1
+        ln = i if i < ln else ln
+        if i == 0:
+            backing, ln = [], 0
+    if isnil:
+        return NULL
+    return ("arr", [NULL if s is None else _merge(s, sub) for s in backing[:ln]])
 
 
 def b64_std_decode(s):

@@ -41,7 +41,10 @@ algorithms:
 * Protobuf (golang/protobuf v1.5.2 over google.golang.org/protobuf v1.27.1,
   go.mod:10,226): proto3 decoding with unknown fields skipped, last value wins,
   a known field with the wrong wire type handled as unknown, strings validated
-  as UTF-8, present-but-empty bytes non-nil.
+  as UTF-8.  A proto3 (no-presence) bytes field decodes through
+  consumeBytesNoZero, append([]byte(nil), v...): an EMPTY value, even when it
+  is on the wire, leaves the field nil -- so NymX / NymY of length 0 fail the
+  common.go:52 nil check.
 """
 import hashlib
 
@@ -278,6 +281,116 @@ class IssuerPK:
         self.fields = m
 
 
+# ------------------------------------------------------------------ G2 (issuer key proof)
+# amcl FP256BN: Fp2 = Fp[i]/(i^2 + 1); G2 lives on the M-type sextic twist
+# y^2 = x^3 + 3(1 + i) (every reference IssuerPublicKey W satisfies it).
+B2 = (3, 3)
+H2 = 2 * Q - N  # #E'(Fp2) / n for the BN sextic twist
+# amcl ECP2_generator() (CURVE_Pxa, Pxb, Pya, Pyb).  amcl's ROM is not in the
+# reference; the point is RECOVERED, not assumed: it is H2 * (1, y0) with x = 1
+# the first twist abscissa, and of the two roots y0 exactly one makes
+# issuer_key_check() accept all three reference IssuerPublicKey fixtures -- a
+# SHA-256 match over 579 reference-held bytes, so a wrong generator could not
+# pass (tests/test_idemix.py::test_issuer_key_proof_pins_g2_and_transcript).
+GEN_G2 = ((0xFE0C3350B4C96C2028560F577C28913ACE1C539A12BF843CD22616B689C09EFB,
+           0x4EA66057738AC054DB5AE1C637D813B924DD78E287D03589D269ED34A37E6A2B),
+          (0x702046E7C542A3B376770D75124E3E51EFCB24758D615848E909B481BEDC27FF,
+           0x0554E3BCD388C29042EEA649297EB29F8B4CBE80821A98B3E01281114AAD049B))
+
+
+def _f2m(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % Q, (a[0] * b[1] + a[1] * b[0]) % Q)
+
+
+def _f2a(a, b):
+    return ((a[0] + b[0]) % Q, (a[1] + b[1]) % Q)
+
+
+def _f2s(a, b):
+    return ((a[0] - b[0]) % Q, (a[1] - b[1]) % Q)
+
+
+def _f2i(a):
+    d = pow((a[0] * a[0] + a[1] * a[1]) % Q, -1, Q)
+    return (a[0] * d % Q, -a[1] * d % Q)
+
+
+def g2_on_curve(P):
+    return P is None or _f2s(_f2m(P[1], P[1]), _f2m(P[0], _f2m(P[0], P[0]))) == B2
+
+
+def g2_add(P, R):
+    if P is None:
+        return R
+    if R is None:
+        return P
+    if P[0] == R[0]:
+        if _f2a(P[1], R[1]) == (0, 0):
+            return None
+        lam = _f2m(_f2m((3, 0), _f2m(P[0], P[0])), _f2i(_f2m((2, 0), P[1])))
+    else:
+        lam = _f2m(_f2s(R[1], P[1]), _f2i(_f2s(R[0], P[0])))
+    x = _f2s(_f2s(_f2m(lam, lam), P[0]), R[0])
+    return (x, _f2s(_f2m(lam, _f2s(P[0], x)), P[1]))
+
+
+def g2_mul(P, k):
+    acc = None
+    for bit in bin(k)[2:] if k > 0 else "":
+        acc = g2_add(acc, acc)
+        if bit == "1":
+            acc = g2_add(acc, P)
+    return acc
+
+
+def g2_bytes(P):
+    """amcl ECP2.ToBytes as mathlib's G2.Bytes calls it: 128 bytes Xa||Xb||Ya||Yb
+    (infinity as amcl's affine (0, 0) representative [EXT, unreached])."""
+    (xa, xb), (ya, yb) = P if P is not None else ((0, 0), (0, 0))
+    return b"".join(v.to_bytes(32, "big") for v in (xa, xb, ya, yb))
+
+
+def ecp2_from_proto(e):
+    """amcl NewECP2fp2s(FP2(FromBytes(Xa), FromBytes(Xb)), FP2(FromBytes(Ya), FromBytes(Yb))):
+    off-curve -> infinity (as NewECPbigs in G1)."""
+    P = ((from_bytes32(e.get(1)) % Q, from_bytes32(e.get(2)) % Q),
+         (from_bytes32(e.get(3)) % Q, from_bytes32(e.get(4)) % Q))
+    return P if g2_on_curve(P) else None
+
+
+def issuer_key_check(raw):
+    """IBM/idemix IssuerPublicKey.Check (run when the deserializer imports the
+    issuer key, identity/msp/idemix/deserializer.go:59-75): the key's own
+    Schnorr proof of knowledge of isk with W = g2^isk and BarG2 = BarG1^isk.
+        t1 = g2^ProofS * W^-ProofC,  t2 = BarG1^ProofS * BarG2^-ProofC,
+        ProofC == HashModOrder(t1 || t2 || g2 || BarG1 || W || BarG2)
+    with G2 as 128 bytes, G1 as 65 bytes (0x04||X||Y), proofData of 18*32+3 bytes.
+    Returns (ok, why)."""
+    try:
+        m = pb_decode(raw, IPK_S)
+    except PbError as e:
+        return False, "failed to unmarshal issuer public key: %s" % e
+    if any(m.get(k) is None for k in (2, 3, 5, 6, 7)):
+        return False, "some part of the public key is undefined"
+    try:
+        bar_g1 = ecp_from_bytes(m[6].get(1), m[6].get(2))
+        bar_g2 = ecp_from_bytes(m[7].get(1), m[7].get(2))
+        w = ecp2_from_proto(m[5])
+        proof_c, proof_s = from_bytes32(m.get(8)), from_bytes32(m.get(9))
+    except IndexError as e:
+        return False, "failure [%s]" % e
+    if bar_g1 is None or len(m.get(4, [])) < len(m.get(1, [])):
+        return False, "some part of the public key is undefined"
+    neg_c = (N - proof_c % N) % N
+    t1 = g2_add(g2_mul(GEN_G2, proof_s % N), g2_mul(w, neg_c))
+    t2 = add(mul(bar_g1, proof_s), mul(bar_g2, neg_c))
+    data = (g2_bytes(t1) + g1_bytes(t2) + g2_bytes(GEN_G2) + g1_bytes(bar_g1) + g2_bytes(w) + g1_bytes(bar_g2))
+    assert len(data) == 18 * FIELD_BYTES + 3
+    if proof_c != hash_to_zr(data):
+        return False, "zero knowledge proof in public key invalid"
+    return True, ""
+
+
 # ------------------------------------------------------------------ ASN.1 RawOwner
 def _printable(c, amp_star=True):
     return (ord("a") <= c <= ord("z") or ord("A") <= c <= ord("Z") or ord("0") <= c <= ord("9")
@@ -448,7 +561,7 @@ def deserialize_idemix_identity(raw):
         ser = pb_decode(si.get(2, b""), SERIALIZED_IDEMIX_S)
     except PbError:
         return None, (ERR_OWNER, "could not deserialize a SerializedIdemixIdentity")
-    if ser.get(1) is None or ser.get(2) is None:
+    if not ser.get(1) or not ser.get(2):  # absent OR empty: proto3 bytes decode to nil when empty
         return None, (ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid")
     raw_nym = ser[1] + ser[2]
     half = len(raw_nym) // 2

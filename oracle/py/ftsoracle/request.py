@@ -162,11 +162,17 @@ def _metadata(v):
         J.dec_bytes(x)
 
 
+# []*token.Token fields: duplicate keys merge into the existing tokens (gojson.resolve)
+TRANSFER_SCHEMA = {"OutputTokens": (J.SLICE, {})}
+ISSUE_SCHEMA = {"outputs": (J.SLICE, {})}
+
+
 def decode_transfer_action(raw):
     v = _top(raw)
     a = {"inputs": [], "outputs": [], "proof": None}
     if v is None:
         return a
+    v = J.resolve(v, TRANSFER_SCHEMA)
     ins = J.field(v, "Inputs")
     if ins is not None and ins[0] != "null":
         if ins[0] != "arr":
@@ -189,6 +195,7 @@ def decode_issue_action(raw):
     a = {"outputs": [], "proof": None, "anonymous": False}
     if v is None:
         return a
+    v = J.resolve(v, ISSUE_SCHEMA)
     J.dec_bytes(J.field(v, "Issuer"))
     a["outputs"] = _outputs(J.field(v, "outputs"))
     a["proof"] = J.dec_bytes(J.field(v, "Proof"))

@@ -177,7 +177,7 @@ class PublicParams:
         if ident != label:
             raise ValueError("invalid identifier, expecting [%s], got [%s]" % (label, ident))
         raw = J.dec_bytes(J.field(outer, "Raw"))
-        v = J.parse(raw)
+        v = J.resolve(J.parse(raw), PP_SCHEMA)
         pp = PublicParams()
         pp.label = label
         pp.curve = J.dec_int(J.field(v, "Curve"))
@@ -196,6 +196,14 @@ class PublicParams:
         return pp
 
 
+# struct-pointer / slice-of-struct-pointer fields, whose duplicate keys merge
+# (gojson.resolve): setup.go:25-54 PublicParams / RangeProofParams /
+# pssign.Signature; range/proof.go:25-57 RangeProof / EqualityProofs /
+# MembershipProof -> sigproof/membership.go:19-33 MembershipProof -> Signature
+PP_SCHEMA = {"RangeProofParams": (J.STRUCT, {"SignedValues": (J.SLICE, {})})}
+RANGE_SCHEMA = {"EqualityProofs": (J.STRUCT, {}),
+                "MembershipProofs": (J.SLICE, {"SignatureProofs": (J.SLICE, {"Signature": (J.STRUCT, {})})})}
+
 MATHLIB_CURVES = 3  # [EXT] len(math.Curves) at IBM/mathlib 0a7378db6912: FP256BN_AMCL, BN254, FP256BN_AMCL_MIRACL
 
 
@@ -210,7 +218,7 @@ def validate_json(data, label="zkatdlog"):
         if ident != label:
             return "invalid identifier, expecting [%s], got [%s]" % (label, ident)
         raw = J.dec_bytes(J.field(outer, "Raw"))
-        v = J.parse(raw if raw is not None else b"")
+        v = J.resolve(J.parse(raw if raw is not None else b""), PP_SCHEMA)
         curve = J.dec_int(J.field(v, "Curve"))
         idemix_curve = J.dec_int(J.field(v, "IdemixCurveID"))
         prec = J.dec_int(J.field(v, "QuantityPrecision"))
@@ -505,6 +513,7 @@ def range_verify(pp, tokens, raw):
         raise VerifyError(ERR_PARSE, str(ex))
     if v[0] == "null":
         v = ("obj", [])
+    v = J.resolve(v, RANGE_SCHEMA)
     chal = dec_zr(J.field(v, "Challenge"))
     eqv = J.field(v, "EqualityProofs")
     eq = None

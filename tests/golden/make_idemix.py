@@ -35,6 +35,22 @@ def expand(seed, n):
     return bytes(out[:n])
 
 
+IPK_FILES = ["token/core/zkatdlog/crypto/validator/testdata/idemix/msp/IssuerPublicKey",
+             "token/core/zkatdlog/crypto/testdata/idemix/msp/IssuerPublicKey",
+             "token/core/zkatdlog/crypto/audit/testdata/idemix/msp/IssuerPublicKey",
+             "cmd/tokengen/testdata/idemix/msp/IssuerPublicKey",
+             "cmd/tokengen/testdata/idemix/ca/IssuerPublicKey"]
+
+
+def ipk_fixtures():
+    out = []
+    for rel in IPK_FILES:
+        raw = open(os.path.join("/root/reference", rel), "rb").read()
+        ok, why = I.issuer_key_check(raw)
+        out.append({"path": rel, "raw": raw.hex(), "check_ok": ok, "why": why})
+    return out
+
+
 def main():
     ipk_raw = open(os.path.join(REF, "msp", "IssuerPublicKey"), "rb").read()
     sc = I.pb_decode(open(os.path.join(REF, "user", "SignerConfig"), "rb").read(),
@@ -131,7 +147,10 @@ def main():
     x, y = nym[0].to_bytes(32, "big"), nym[1].to_bytes(32, "big")
     inner_nox = I.pb_field(2, 2, y)
     add("nym_x_missing", owner(I.pb_field(1, 2, b"idemix") + I.pb_field(2, 2, inner_nox)), msg, sig_ok)
-    add("nym_x_empty_y_holds_both", owner(identity(nym, nymx=b"", nymy=x + y)), msg, sig_ok)
+    add("nym_x_empty_is_nil", owner(identity(nym, nymx=b"", nymy=x + y)), msg, sig_ok)
+    inner_twice = I.pb_field(1, 2, x) + I.pb_field(2, 2, y) + I.pb_field(1, 2, b"")
+    add("nym_x_last_value_empty_is_nil", owner(I.pb_field(1, 2, b"idemix") + I.pb_field(2, 2, inner_twice)),
+        msg, sig_ok)
     add("nym_short_halves", owner(identity(nym, nymx=x[:31], nymy=y[:31])), msg, sig_ok)
     add("nym_33_byte_halves", owner(identity(nym, nymx=b"\x00" + x, nymy=b"\x00" + y)), msg, sig_ok)
     add("nym_off_curve", owner(identity(nym, nymy=(nym[1] ^ 1).to_bytes(32, "big"))), msg, sig_ok)
@@ -173,6 +192,10 @@ def main():
                         "wrong wire type = unknown, UTF-8 strings)",
         },
         "ipk": ipk_raw.hex(),
+        # every IssuerPublicKey file the reference holds, with IssuerPublicKey.Check's
+        # verdict (ftsoracle.idemix.issuer_key_check): the proof pins the G2
+        # generator, G1/G2 byte layouts and HashModOrder against reference bytes
+        "ipk_fixtures": ipk_fixtures(),
         "pins": {
             "sk": sc[2].hex(),
             "cred_b": [cred[2][1].hex(), cred[2][2].hex()],

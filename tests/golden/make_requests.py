@@ -191,6 +191,34 @@ def main():
     add("asn1_wrong_element_tag", b"\x30\x0b" + b"\x30\x05\x0c\x03abc" + b"\x30\x00" * 3)
     add("asn1_high_tag_form", b"\x30\x09" + b"\x3f\x10\x00" + b"\x30\x00" * 3)
     add("asn1_element_overruns_sequence", b"\x30\x0b" + b"\x30\x03\x04\x05abc" + b"\x30\x00" * 3 + b"de")
+    # duplicate []*token.Token keys: Go decodes the later array INTO the tokens
+    # already there (gojson.resolve), so fields the later occurrence omits survive
+    own = '{"Owner":"eA=="}'
+
+    def dup(raw, key, before):
+        k = ('"%s":[' % key).encode()
+        assert raw.count(k) == 1
+        return raw.replace(k, before.encode() + k)
+    t_full, _ = tr("valid_2in_2out")
+    # the full array first, then owner-only tokens: Data survives -> accept
+    add("transfer_output_tokens_dup_merges_accepts",
+        enc([[], [t_full.replace(b'"Proof":', ('"OutputTokens":[%s,%s],"Proof":' % (own, own)).encode())], [], []]))
+    add("transfer_output_tokens_dup_null_resets_panics",
+        enc([[], [t_full.replace(b'"Proof":', ('"OutputTokens":null,"OutputTokens":[%s,%s],"Proof":'
+                                               % (own, own)).encode())], [], []]))
+    # [full0, full1] -> [owner] truncates to 1 -> [{}, {}] re-exposes full1
+    add("transfer_output_tokens_truncated_then_reexposed_accepts",
+        enc([[], [t_full.replace(b'"Proof":', ('"OutputTokens":[%s],"outputtokens":[{},{}],"Proof":' % own).encode())],
+             [], []]))
+    add("transfer_output_tokens_empty_array_resets_panics",
+        enc([[], [t_full.replace(b'"Proof":', b'"OutputTokens":[],"OutputTokens":[{},{}],"Proof":')], [], []]))
+    i_dup = iss("issue_valid_1")
+    n_iss = len(split(cases["issue_valid_1"]["outputs"]))
+    add("issue_outputs_dup_merges_accepts",
+        enc([[i_dup.replace(b'"Proof":', ('"OUTPUTS":[%s],"Proof":' % ",".join(["{}"] * n_iss)).encode())],
+             [], [], []]))
+    add("issue_outputs_dup_partial_first_accepts",
+        enc([[dup(i_dup, "outputs", '"outputs":[%s],' % ",".join([own] * n_iss))], [], [], []]))
 
     get = ledger.get
     for r in reqs:

@@ -5,9 +5,11 @@ fixtures (IssuerPublicKey / SignerConfig of the validator tests, recorded in
 tests/golden/idemix_golden.json by make_idemix.py): every IPK point on the
 curve, IPK.Hash = HashToZr(proto without Hash), the credential's
 B = G + sk HSk + S HRand + sum attr_i HAttrs_i with the OU / enrollment-id
-attributes = HashToZr(string).  The NymSignature transcript itself is [EXT]
-(IBM/idemix is not vendored, no reference vector holds a signature): parity
-of that layout is unpinned beyond the restated algorithm.  The oracle, the
+attributes = HashToZr(string); and IBM/idemix IssuerPublicKey.Check accepts
+the key's own proof on all three FP256BN IssuerPublicKey files, which pins the
+G1 point encoding, HashModOrder and Zr equality of the NymSignature transcript
+against reference-held bytes.  The NymSignature field order itself stays [EXT]
+(IBM/idemix is not vendored, no reference vector holds a signature).  The oracle, the
 host emulation (product decoder + device job code on the CPU) and, on the GPU,
 the C ABI must reproduce every golden verdict.
 """
@@ -76,6 +78,70 @@ def test_oracle_pinned_by_reference_fixtures(gold):
     for h, a in zip(ipk.hattrs, attrs):
         b = I.add(b, I.mul(h, a))
     assert b == tuple(int(v, 16) for v in pins["cred_b"])
+
+
+def test_issuer_key_proof_pins_g2_and_transcript(gold):
+    """IBM/idemix IssuerPublicKey.Check (identity/msp/idemix/deserializer.go:59-75)
+    on every IssuerPublicKey the reference holds.  The key's Schnorr proof hashes
+    t1 || t2 || g2 || BarG1 || W || BarG2 with HashModOrder, so its acceptance pins,
+    against reference-held bytes: the 65-byte G1 encoding 0x04||X||Y that the
+    NymSignature transcript also uses, the 128-byte G2 layout Xa||Xb||Ya||Yb,
+    SHA-256-mod-n HashToZr, raw-integer Zr equality and amcl's G2 generator
+    (not in the reference; recovered as H2*(1, y0), see idemix.GEN_G2)."""
+    fx = gold["ipk_fixtures"]
+    ok = [f for f in fx if f["check_ok"]]
+    assert {f["path"].split("/testdata")[0] for f in ok} == {
+        "token/core/zkatdlog/crypto/validator", "token/core/zkatdlog/crypto", "token/core/zkatdlog/crypto/audit"}
+    for f in ok:
+        assert I.issuer_key_check(bytes.fromhex(f["raw"])) == (True, ""), f["path"]
+    # the generator is what the docstring says it is
+    g = I.GEN_G2
+    assert g[0] != (1, 0) and I.g2_on_curve(g) and I.g2_mul(g, I.N) is None
+    base = [P for P in (((1, 0), y) for y in _twist_roots(1)) if I.g2_mul(P, I.H2) == g]
+    assert len(base) == 1
+    # negative controls: each convention, changed, breaks the proof
+    raw = bytes.fromhex(ok[0]["raw"])
+    m = I.pb_decode(raw, I.IPK_S)
+    c = int.from_bytes(m[8], "big")
+    flipped = raw.replace(m[8], (c ^ 1).to_bytes(32, "big"))
+    assert I.issuer_key_check(flipped) == (False, "zero knowledge proof in public key invalid")
+    saved = (I.GEN_G2, I.g2_bytes, I.g1_bytes)
+    try:
+        I.GEN_G2 = (g[0], I._f2s((0, 0), g[1]))  # the other root's multiple
+        assert not I.issuer_key_check(raw)[0]
+        I.GEN_G2 = saved[0]
+        I.g2_bytes = lambda P: b"".join(v.to_bytes(32, "big") for v in (P[0][1], P[0][0], P[1][1], P[1][0]))
+        assert not I.issuer_key_check(raw)[0]
+        I.g2_bytes = saved[1]
+        I.g1_bytes = lambda P: P[0].to_bytes(32, "big") + P[1].to_bytes(32, "big") + b"\x04"
+        assert not I.issuer_key_check(raw)[0]
+    finally:
+        I.GEN_G2, I.g2_bytes, I.g1_bytes = saved
+    assert I.issuer_key_check(raw) == (True, "")
+    # cmd/tokengen's IssuerPublicKey is copied into generated public parameters
+    # without a Check (cmd/tokengen/main_test.go:77); its G1 coordinates are not
+    # FP256BN points, so Check rejects it -- recorded, not a parity case
+    for f in fx:
+        if not f["check_ok"]:
+            assert f["path"].startswith("cmd/tokengen/")
+            tg = I.pb_decode(bytes.fromhex(f["raw"]), I.IPK_S)
+            assert I.ecp_from_bytes(tg[6][1], tg[6][2]) is None
+
+
+def _twist_roots(x0):
+    """both y with y^2 = x0^3 + 3(1+i) in Fp2 (p = 3 mod 4)"""
+    Q = I.Q
+    a = I._f2a(I._f2m((x0, 0), I._f2m((x0, 0), (x0, 0))), I.B2)
+    n = (a[0] * a[0] + a[1] * a[1]) % Q
+    s = pow(n, (Q + 1) // 4, Q)
+    for sg in (s, Q - s):
+        t = (a[0] + sg) * pow(2, -1, Q) % Q
+        r0 = pow(t, (Q + 1) // 4, Q)
+        if r0 and r0 * r0 % Q == t:
+            r = (r0, a[1] * pow(2 * r0, -1, Q) % Q)
+            if I._f2m(r, r) == a:
+                return [r, I._f2s((0, 0), r)]
+    raise AssertionError("no root")
 
 
 def test_oracle_reproduces_golden(gold):
