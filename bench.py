@@ -40,36 +40,67 @@ METRIC = "zkatdlog transfer proofs verified/sec (node) + BN254 G1 MSM 2^20 laten
 MAD_PER_M = 136  # u32 MADs per 254-bit CIOS Montgomery product (8x8 + 8x8 + 8)
 
 
-def cpu_baseline(pp_json, job, sample=2048, reps=5):
-    """The C++ CPU restatement (oracle/cpu/libftscpu.so: the host build of the
-    verifier's planner and job code with 4 x 64-bit Montgomery products) on
-    one thread per core of this process's CPU share, over the first `sample`
-    transfers of the bench job: one warm-up, median of `reps` runs."""
-    import ctypes
+_CPU = {}
 
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
-    import build_cpu
-    lib = ctypes.CDLL(build_cpu.build())
-    from zkatdlog import _abi as A
-    lib.emu_ctx_create.restype = ctypes.c_void_p
-    lib.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
-    lib.emu_ctx_destroy.argtypes = [ctypes.c_void_p]
-    lib.emu_verify_transfers.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Transfer),
-                                         ctypes.POINTER(ctypes.c_int32)]
-    lib.emu_set_threads.argtypes = [ctypes.c_int]
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    cores = min(cores, int(os.environ.get("FTS_CPU_BASELINE_CORES", "16")))  # the box's CPU share per GPU
-    lib.emu_set_threads(cores)
+
+def _cpu_lib():
+    """oracle/cpu/libftscpu.so (the C++ CPU restatement; a labelled baseline,
+    never on the product path)"""
+    if "lib" not in _CPU:
+        import ctypes
+
+        from zkatdlog import _abi as A
+        sys.path.insert(0, os.path.join(ROOT, "oracle", "cpu"))
+        import build_cpu
+        lib = ctypes.CDLL(build_cpu.build())
+        lib.emu_ctx_create.restype = ctypes.c_void_p
+        lib.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        lib.emu_ctx_destroy.argtypes = [ctypes.c_void_p]
+        lib.emu_verify_transfers.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Transfer),
+                                             ctypes.POINTER(ctypes.c_int32)]
+        lib.emu_prove_transfers.restype = ctypes.c_long
+        lib.emu_prove_transfers.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.TransferWitness),
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_char_p, ctypes.c_size_t]
+        lib.emu_set_threads.argtypes = [ctypes.c_int]
+        lib.emu_msm_cpu.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_uint32,
+                                    ctypes.c_char_p]
+        lib.emu_gen_points.argtypes = [ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p]
+        _CPU["lib"] = lib
+    return _CPU["lib"]
+
+
+def host_cores():
+    """(cores this process may run on, the machine's logical CPUs)"""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return aff, os.cpu_count() or aff
+
+
+def _cpu_ctx(pp_json):
+    import ctypes
+    lib = _cpu_lib()
     err = ctypes.create_string_buffer(256)
     c = lib.emu_ctx_create(pp_json, len(pp_json), err, 256)
     if not c:
         raise RuntimeError(err.value.decode())
+    return lib, c
+
+
+def cpu_verify(pp_json, job, cores, sample, reps=3):
+    """The C++ CPU restatement of the verifier (oracle/cpu: host build of the
+    planner + job code, 4 x 64-bit Montgomery) on `cores` threads over the first
+    `sample` transfers of `job`: one warm-up, median of `reps` runs.  Returns
+    (transfers/s, median seconds, sample)."""
+    import ctypes
+
+    import numpy as np
+    lib, c = _cpu_ctx(pp_json)
+    lib.emu_set_threads(cores)
     try:
         n = min(sample, job.n)
         codes = np.zeros(n, dtype=np.int32)
         cp = codes.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
-        lib.emu_verify_transfers(c, min(n, 4 * cores), job.ptr(), cp)  # warm-up
+        lib.emu_verify_transfers(c, min(n, 2 * cores), job.ptr(), cp)  # warm-up
         times = []
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -78,21 +109,107 @@ def cpu_baseline(pp_json, job, sample=2048, reps=5):
         assert np.array_equal(codes, job.expect[:n]), "CPU restatement disagrees with the expected verdicts"
     finally:
         lib.emu_ctx_destroy(c)
-    times.sort()
-    med = times[reps // 2]
-    return {"value": round(n / med, 2), "unit": "transfers/s", "cores": cores, "kind": "port",
-            "impl": "cpp-restatement",
-            "sample": "%d transfers of the bench job (same proofs, same verdicts) verified by the C++ CPU restatement "
-                      "(oracle/cpu: host build of the planner + job code, 4x64-bit Montgomery) on %d threads; "
-                      "median of %d runs after a warm-up: %.2f s" % (n, cores, reps, med)}
+    med = sorted(times)[reps // 2]
+    return n / med, med, n
+
+
+def cpu_prove(pp_json, bases, cores, n, reps=3):
+    """The C++ CPU restatement of the batch prover (planner_prove + job code on
+    the host) on `cores` threads: n 2-in/2-out transfer proofs, median of reps."""
+    import ctypes
+
+    import numpy as np
+
+    from zkatdlog import _abi as A
+    from zkatdlog import workload as W
+    lib, c = _cpu_ctx(pp_json)
+    lib.emu_set_threads(cores)
+    try:
+        sel = np.arange(n) % len(bases)
+        wp, wn, keep = A.pack_transfer_witnesses_tiled(bases, sel, W.seeds(n, b"cpu-prover"))
+        cap = n * 16384
+        buf = np.empty(cap, dtype=np.uint8)
+        offs = np.zeros(n + 1, dtype=np.uint64)
+        codes = np.zeros(n, dtype=np.int32)
+        err = ctypes.create_string_buffer(256)
+        times = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = lib.emu_prove_transfers(c, n, wp, buf.ctypes.data, cap, offs.ctypes.data, codes.ctypes.data, err, 256)
+            times.append(time.perf_counter() - t0)
+            assert r > 0, err.value
+    finally:
+        lib.emu_ctx_destroy(c)
+    med = sorted(times)[reps // 2]
+    return n / med, med
+
+
+def cpu_msm(lg, cores, seed=7):
+    """CPU Pippenger (tests/native/msm_emu.cpp emu_msm_cpu: the device plan's
+    GLV split and signed windows, one point chunk per thread) of the bench's
+    2^lg known-log MSM (P_i = (i+1) G, the same scalars as the GPU leg).
+    Returns (ms of one run, RawBytes result)."""
+    import ctypes
+
+    import numpy as np
+    lib = _cpu_lib()
+    n = 1 << lg
+    scal = np.random.default_rng(seed + lg).bytes(32 * n)
+    pts = ctypes.create_string_buffer(64 * n)
+    lib.emu_gen_points(n, 1, cores, pts)
+    out = ctypes.create_string_buffer(64)
+    t0 = time.perf_counter()
+    rc = lib.emu_msm_cpu(n, pts, scal, cores, 0, out)
+    dt = time.perf_counter() - t0
+    assert rc == 0
+    return dt * 1e3, out.raw
+
+
+def cpu_baselines(pp_a, job_a, pp_b, job_b, bases_a, gpu_msm20):
+    """CPU reference figures: the C++ restatement on ALL
+    cores this process may use (the headline cpu_baseline) and on the 16-core
+    per-GPU share of the box, for PP-A and PP-B verification, PP-A proving and
+    the 2^20 Pippenger.  Samples are sized for a few seconds of CPU work each."""
+    aff, nproc = host_cores()
+    share = min(16, aff)
+    out = {"affinity_cores": aff, "nproc": nproc, "impl": "cpp-restatement (oracle/cpu, 4x64-bit Montgomery)"}
+    head = None
+    for label, cores in (("all", aff), ("share16", share)):
+        r, med, n = cpu_verify(pp_a, job_a, cores, max(2048, 48 * cores))
+        out["verify_pp_a_" + label] = {"value": round(r, 2), "unit": "transfers/s", "cores": cores,
+                                       "sample": "%d transfers, median %.2f s" % (n, med)}
+        if label == "all":
+            head = {"value": round(r, 2), "unit": "transfers/s", "cores": cores, "kind": "port",
+                    "impl": "cpp-restatement", "affinity_cores": aff, "nproc": nproc,
+                    "sample": "%d transfers of the bench job (same proofs, same verdicts) verified by the C++ CPU "
+                              "restatement of the verifier (oracle/cpu: host build of the planner + job code with the "
+                              "GPU path's algorithms -- bilinear membership rewrite, GLV, fixed-base tables -- and "
+                              "4x64-bit Montgomery products) on all %d cores of the process affinity (nproc %d); "
+                              "median of 3 runs after a warm-up: %.2f s" % (n, cores, aff, nproc, med)}
+        if job_b is not None:
+            r, med, n = cpu_verify(pp_b, job_b, cores, max(256, 8 * cores))
+            out["verify_pp_b_" + label] = {"value": round(r, 2), "unit": "transfers/s", "cores": cores,
+                                           "sample": "%d PP-B transfers, median %.2f s" % (n, med)}
+        r, med = cpu_prove(pp_a, bases_a, cores, max(512, 12 * cores))
+        out["prove_pp_a_" + label] = {"value": round(r, 2), "unit": "proofs/s", "cores": cores,
+                                      "sample": "median %.2f s" % med}
+    ms, res = cpu_msm(20, aff)
+    out["msm_2^20_all"] = {"ms": round(ms, 1), "cores": aff, "matches_gpu": gpu_msm20 is None or res == gpu_msm20}
+    return head, out
+
+
+_PEAK = {}
 
 
 def madpeak(device):
+    if device in _PEAK:
+        return _PEAK[device]
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsmadpeak.so"))
     lib.ftz_madpeak.restype = ctypes.c_double
     lib.ftz_madpeak.argtypes = [ctypes.c_int, ctypes.c_uint32]
-    return max(lib.ftz_madpeak(device, 20000) for _ in range(3))
+    _PEAK[device] = max(lib.ftz_madpeak(device, 20000) for _ in range(3))
+    return _PEAK[device]
 
 
 def msm_latency(ctx, lg, reps=5, seed=7):
@@ -120,8 +237,20 @@ def msm_latency(ctx, lg, reps=5, seed=7):
         m.close()
     wall.sort()
     dev.sort()
+    # algorithmic work of a GLV Pippenger with c-bit windows: one mixed addition
+    # (7M + 4S) per (window, virtual point) and 2 Jacobian additions (12M + 4S)
+    # per bucket in the running-sum reduction, in Montgomery products M
+    c = info["window_bits"]
+    windows, nv, buckets = (129 + c - 1) // c, 2 * n, 1 << (c - 1)
+    m_prod = windows * nv * 11 + windows * 2 * buckets * 16
+    peak = madpeak(ctx.device)
+    ach = m_prod * MAD_PER_M / (dev[reps // 2] * 1e-3)
     return {"n": n, "ms": round(wall[reps // 2], 3), "device_ms": round(dev[reps // 2], 3),
-            "window_bits": info["window_bits"]}
+            "window_bits": c, "result": first.hex(),
+            "roofline": {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
+                         "unit": "TMAD/s", "frac": round(ach / peak, 4), "m_products": m_prod,
+                         "note": "W x 2n mixed adds x 11 M + W x 2 x 2^(c-1) Jacobian adds x 16 M, "
+                                 "136 MAD per M, over the device time"}}
 
 
 def msm_split_latency(ctx, lg, rank, world, dist, reps=5, seed=7):
@@ -240,7 +369,7 @@ def plan_rate(ctx, job, batch, reps=3):
     return best
 
 
-def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False):
+def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False, pp_key="pp_a"):
     """Integer-VALU roofline of the dominant kernel.  The timed steps overlap
     three streams, so per-kernel wall times there include shared SIMDs; the
     roofline pass re-runs 3 steps of one batch with every kernel on one stream
@@ -264,9 +393,9 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False):
         b.close()
     kern = {k: (v[0] / 3, v[1]) for k, v in acc.items() if k != "total"}
     peak = madpeak(device)
-    opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))["pp_a"]
+    opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))[pp_key]
     names = {"g1": "k_g1_part+k_g1_combine (side stream)", "g1p": "k_g1_part+k_g1_combine (pairing inputs)",
-             "g2": "k_g2_part+k_g2lines1 (t' + pair-2 lines)", "miller": "k_miller", "fexp": "k_fexp_exact",
+             "g2": "k_g2_part+k_g2lines1 (t' + pair-2 lines)", "miller": "k_miller", "fexp": "k_fexp_easy+k_fexp_expt x3+k_fexp_hard",
              "hash": "k_hash", "decode": "k_decode"}
     mjob = dict(opc["m_per_job"])
     mjob["g1p"] = mjob["g1"]  # the pairing-input G1 jobs run the same job code
@@ -279,7 +408,7 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False):
     achieved = m_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_fetch.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and pp_key == "pp_a":
         traffic = json.load(open(pmc)).get("per_launch_bytes", {}).get(dom)
     step_mad = opc["m_per_tx"] * tx_per_s * MAD_PER_M
     return {"bound": "valu", "kernel": names[dom], "achieved": round(achieved / 1e12, 4),
@@ -294,6 +423,89 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False):
             "note": "integer VALU roofline (v_mad_u64_u32, peak = measured madpeak); per-kernel time from a "
                     "serial pass (ftz_ctx_set_serial) of one batch of the bench job; traffic = HBM bytes per "
                     "launch from rocprofv3 FETCH_SIZE (profiles/pmc_fetch.json)"}
+
+
+def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4096), **opts):
+    """The drop-in seam (BASELINE configs[1] at the Go shim's granularity): the
+    shim calls ftz_verify_transfers with ONE TransferAction per call
+    (validator_transfer.go:84-98).  (a) latency of one call of s transfers with
+    nothing else in flight; (b) closed loop: C native threads each calling
+    ftz_verify_transfers(ctx, 1, ...) back to back for `seconds`
+    (csrc/tools/callers.cpp) -- throughput and per-call p50 / p99 latency.
+    Verdicts are checked against the expected codes."""
+    import ctypes
+
+    import numpy as np
+
+    import zkatdlog
+    from zkatdlog import workload as W
+    lib = ctypes.CDLL(os.path.join(ROOT, "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftscallers.so"))
+    lib.ftz_callers_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                    ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]
+    pool = W.mixed_job(valid, bad, min(valid.n, 16384), seed=11)
+    ctx = zkatdlog.Context(pp_json, device=device, **opts)
+    try:
+        lat = {}
+        for s_ in (1, 16, 64, 256, 1024, 4096):
+            sub = W.Job(pool.rows[:s_], pool.expect[:s_], [pool])
+            ctx.verify_transfers_packed(sub.ptr(), s_)
+            ts = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                codes = ctx.verify_transfers_packed(sub.ptr(), s_)
+                ts.append((time.perf_counter() - t0) * 1e3)
+                assert np.array_equal(codes, sub.expect)
+            lat[str(s_)] = round(sorted(ts)[1], 3)
+        loop = []
+        out = (ctypes.c_double * 6)()
+        exp = np.ascontiguousarray(pool.expect, dtype=np.int32)
+        for c in callers:
+            err = ctypes.create_string_buffer(512)
+            rc = lib.ftz_callers_run(ctx._h, pool.rows.ctypes.data, exp.ctypes.data, pool.n, c, seconds, out, err, 512)
+            if rc != 0:
+                raise RuntimeError("ftz_callers_run failed: %d %s" % (rc, err.value.decode(errors="replace")))
+            loop.append({"callers": c, "transfers_per_s": round(out[0], 1), "p50_ms": round(out[1], 3),
+                         "p99_ms": round(out[2], 3), "max_ms": round(out[5], 3), "calls": int(out[3]),
+                         "verdict_mismatches": int(out[4])})
+        st = ctx.options
+    finally:
+        ctx.close()
+    return {"call_latency_ms_by_size": lat, "closed_loop_n1": loop,
+            "options": {k: st[k] for k in ("batch", "slots", "window_us", "hold_inflight", "small_pass")}}
+
+
+def ppb_leg(device, args, bad_b):
+    """BASELINE configs[0]'s 64-bit range proof (PP-B: base 16, exponent 16) on
+    the GPU: the batch prover and ONE end-to-end ftz_verify_transfers call over
+    the proofs it made (plus tampered PP-B corpus rows), with the verifier's
+    roofline at PP-B (serial pass, profiles/opcounts.json pp_b)."""
+    import numpy as np
+
+    import zkatdlog
+    from zkatdlog import workload as W
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_b"]
+    pp = g["pp"].encode()
+    ctx = zkatdlog.Context(pp, device=device)
+    try:
+        bases = W.random_witness_bases(ctx, 16, seed=16)
+        n_prove = 4096
+        W.prove_distinct(ctx, 512, tag=b"ppb-warm", bases=bases)
+        t0 = time.perf_counter()
+        valid = W.prove_distinct(ctx, n_prove, tag=b"ppb", bases=bases)
+        t_prove = time.perf_counter() - t0
+        job = W.mixed_job(valid, bad_b, 8 * n_prove, seed=5)
+        ctx.verify_transfers_packed(job.ptr(), 2 * ctx.options["batch"])  # warm the engine slots
+        t0 = time.perf_counter()
+        codes = ctx.verify_transfers_packed(job.ptr(), job.n)
+        dt = time.perf_counter() - t0
+        ok = bool(np.array_equal(codes, job.expect))
+        rate = job.n / dt
+        roof = roofline(ctx, job, min(ctx.options["batch"], job.n), device, rate, pp_key="pp_b")
+    finally:
+        ctx.close()
+    return {"verify_transfers_per_s": round(rate, 1), "verify_transfers": job.n, "verdicts_bit_exact": ok,
+            "prove_proofs_per_s": round(n_prove / t_prove, 1), "proofs": n_prove,
+            "pp": "b=16,e=16 (values < 2^64)", "roofline": roof}, (pp, job, bases)
 
 
 def owner_signatures(ctx, n=8192, reps=5):
@@ -352,6 +564,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--msm", default="16,20,24", help="log2 sizes of the standalone G1 MSM (configs[2]); '' = none")
     ap.add_argument("--no-prover", action="store_true", help="skip the batch-prover leg (configs[4])")
+    ap.add_argument("--no-seam", action="store_true", help="skip the n=1 drop-in seam leg (latency curve)")
+    ap.add_argument("--no-ppb", action="store_true", help="skip the PP-B (64-bit range proof) verify / prove leg")
+    ap.add_argument("--seam-seconds", type=float, default=2.0)
     ap.add_argument("--no-extras", action="store_true", help="only the headline (no device-only / roofline legs)")
     ap.add_argument("--device-batch", type=int, default=None,
                     help="proofs per device pass (ftz_options.batch; default: the library's)")
@@ -412,16 +627,18 @@ def main():
     ctx.engine_stats(reset=True)
     t0 = time.perf_counter()
     start, stop, codes = verify_shard(ctx, job.rows, n_total, rank, world)  # ONE call, end to end
+    bits = bitmap_of(codes)
+    if dist is not None:  # configs[3]: the RCCL verdict reduce is part of the timed job
+        from zkatdlog.dist import gather_verdicts, max_elapsed
+        ok_local = bool(np.array_equal(codes, job.expect[start:stop]))
+        _, n_accept, verdict_ok = gather_verdicts(bits, stop - start, ok_local, dist)  # RCCL over xGMI
     barrier()
     elapsed = time.perf_counter() - t0
     est = ctx.engine_stats()
-    ok_local = bool(np.array_equal(codes, job.expect[start:stop]))
-    bits = bitmap_of(codes)
     if dist is not None:
-        from zkatdlog.dist import gather_verdicts, max_elapsed
         elapsed = max_elapsed(elapsed, dist)
-        _, n_accept, verdict_ok = gather_verdicts(bits, stop - start, ok_local, dist)  # RCCL over xGMI
     else:
+        ok_local = bool(np.array_equal(codes, job.expect[start:stop]))
         verdict_ok, n_accept = ok_local, int((codes == 0).sum())
 
     msm_split = None
@@ -440,10 +657,18 @@ def main():
             extras["owner_signatures"] = owner_signatures(ctx)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
+        msm20_bytes = next((bytes.fromhex(r["result"]) for r in msm if r["n"] == 1 << 20), None)
         prover = None if args.no_prover else prover_bench(ctx, args.batch, min(args.steps, 16))
+        ppb, ppb_job = None, None
+        if not args.no_ppb and not args.no_extras:
+            ppb, ppb_job = ppb_leg(local, args, W.golden_tampered("pp_b"))
+        if not args.no_seam and not args.no_extras:
+            extras["seam"] = seam_leg(pp_json, local, valid, bad, seconds=args.seam_seconds)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(pp_json, job)
+            cpu, extras["cpu_baselines"] = cpu_baselines(pp_json, job, ppb_job[0] if ppb_job else None,
+                                                         ppb_job[1] if ppb_job else None, W.witness_bases(),
+                                                         msm20_bytes)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "transfers/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -464,7 +689,7 @@ def main():
                        "parse_rate_transfers_per_s": round(est["proofs"] / max(1e-9, est["plan_ms"] * 1e-3), 1),
                        "planning_threads": ctx.options["threads"]},
             "roofline": extras.pop("roofline", None), "cpu_baseline": cpu,
-            "msm_2^20_latency_ms": msm20, "msm": msm, "msm_split": msm_split, "prover": prover,
+            "msm_2^20_latency_ms": msm20, "msm": msm, "msm_split": msm_split, "prover": prover, "pp_b": ppb,
         }
         line.update(extras)
         print(json.dumps(line), flush=True)

@@ -20,6 +20,7 @@ OBJ = os.path.join(HERE, "build", "obj")
 LIB = os.path.join(HERE, "zkatdlog", "_lib", "libftsamd.so")
 MADPEAK = os.path.join(HERE, "zkatdlog", "_lib", "libftsmadpeak.so")
 FPCHECK = os.path.join(HERE, "zkatdlog", "_lib", "libftsfpcheck.so")
+CALLERS = os.path.join(HERE, "zkatdlog", "_lib", "libftscallers.so")  # bench: closed-loop n=1 callers
 ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # 16-bit signed windows for the G1 fixed-base tables (dev/jobs.h FTS_G1TAB_C)
@@ -75,6 +76,14 @@ def build(jobs=8, force=False, verbose=True):
             r = subprocess.run([HIPCC] + FLAGS + ["-shared", src, "-o", out], capture_output=True, text=True)
             if r.returncode != 0:
                 raise RuntimeError("tool build failed:\n" + r.stderr)
+    src = os.path.join(CSRC, "tools", "callers.cpp")
+    if force or not os.path.exists(CALLERS) or os.path.getmtime(CALLERS) < max(os.path.getmtime(src),
+                                                                               os.path.getmtime(LIB)):
+        r = subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-pthread", src, "-o", CALLERS,
+                            "-L" + os.path.dirname(LIB), "-lftsamd", "-Wl,-rpath,$ORIGIN"],
+                           capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("callers build failed:\n" + r.stderr)
     if verbose:
         print("built", LIB)
     return LIB

@@ -146,7 +146,16 @@ FTS_HDN Jac<F> jac_add(const Jac<F>& p, const Jac<F>& q) {
 }
 
 template <class F>
-FTS_HDN Aff<F> jac_to_aff(const Jac<F>& p) {
+FTS_HD F inv_inl(const F& a) {  // other fields: their own inv()
+  return inv(a);
+}
+FTS_HD fp inv_inl(const fp& a) { return fp_inv_var(a); }
+FTS_HD fp2 inv_inl(const fp2& a) { return f2_inv_inl(a); }
+
+// inline body (callers with the registers for it, e.g. the one-lane line
+// stage); jac_to_aff below is the out-of-line form
+template <class F>
+FTS_HD Aff<F> jac_to_aff_inl(const Jac<F>& p) {
   Aff<F> r;
   if (is_zero(p.z)) {
     r.x = zero_of<F>();
@@ -154,12 +163,16 @@ FTS_HDN Aff<F> jac_to_aff(const Jac<F>& p) {
     r.inf = true;
     return r;
   }
-  F zi = inv(p.z);
+  F zi = inv_inl(p.z);
   F zi2 = sqr(zi);
   r.x = p.x * zi2;
   r.y = p.y * zi2 * zi;
   r.inf = false;
   return r;
+}
+template <class F>
+FTS_HDN Aff<F> jac_to_aff(const Jac<F>& p) {
+  return jac_to_aff_inl(p);
 }
 
 // variable-base scalar multiplication, scalar given as 8 little-endian limbs

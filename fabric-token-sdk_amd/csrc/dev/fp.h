@@ -532,7 +532,10 @@ FTS_HD fp fp_inv_var(const fp& am) {
     }
   }
   // x = (a R)^-1 as a plain integer; the Montgomery form of a^-1 is x R^2
-  fp x = fe_const<ModP>(is_one(u) ? x1 : x2);
+  const bool from_u = is_one(u);  // select values, not arrays: no private-memory copy
+  fp x;
+#pragma unroll
+  for (int i = 0; i < 8; i++) x.v[i] = from_u ? x1[i] : x2[i];
   fp r2 = fe_const<ModP>(P_R2);
   return (x * r2) * r2;
 }

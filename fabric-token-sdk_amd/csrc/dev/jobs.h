@@ -1069,7 +1069,6 @@ FTS_HD int sx_f12_index(int k) { return (k & 1) ? 3 + (k >> 1) : (k >> 1); }
 FTS_HD void g2lines_emit(const g2a& Q, const g1a& P, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
   bool use = !(P.inf || Q.inf);
   g2p T = {Q.x, Q.y, f2_one()};
-  g2a Qn = aff_neg(Q);
   uint32_t n = 0;
   auto emit = [&](const LineCoef& l) {
     fp2 c0 = use ? f2_mul_fp(l.r0, P.y) : f2_one();
@@ -1078,15 +1077,20 @@ FTS_HD void g2lines_emit(const g2a& Q, const g1a& P, EvLineDev* lines, uint32_t 
     evline_store(lines, n, idx, njobs, c0, c3, c4);
     n++;
   };
+  // one inlined doubling and one inlined addition, the step schedule from a
+  // table (uniform per step), so the loop keeps T in registers instead of the
+  // call frames of out-of-line steps
 #pragma nounroll
-  for (int i = 64; i >= 0; i--) {
-    emit(dbl_step(T));
-    int d = naf_digit(i);
-    if (d == 1) emit(add_step(T, Q));
-    if (d == -1) emit(add_step(T, Qn));
+  for (int s = 0; s < MILLER_LINES; s++) {
+    const int t = MILLER_STEPS.t[s];
+    if (t == STEP_DBL) {
+      emit(dbl_step_inl(T));
+    } else {
+      g2a A = t == STEP_FROB1 ? tw_frob(Q) : (t == STEP_FROB2 ? tw_frob2_neg(Q) : Q);
+      if (t == STEP_SUB) A.y = f2_neg(A.y);
+      emit(add_step_inl(T, A));
+    }
   }
-  emit(add_step(T, tw_frob(Q)));
-  emit(add_step(T, tw_frob2_neg(Q)));
 }
 
 // Pair 2 of membership job idx (one lane): t' = c PK0 + v PK1 + h PK2 (the G2
@@ -1150,9 +1154,9 @@ FTS_HD void job_g2lines_parts(const G2Job& g, const PairJob& j, const G2PartDev*
                               const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
   g2j acc = g2part_load(part[idx]);
 #pragma nounroll
-  for (int q = 1; q < 4; q++) acc = jac_add(acc, g2part_load(part[(size_t)q * njobs + idx]));
+  for (int q = 1; q < 4; q++) acc = jac_add_inl(acc, g2part_load(part[(size_t)q * njobs + idx]));
   G2Dev d;
-  g2_store(d, jac_to_aff(acc));
+  g2_store(d, jac_to_aff_inl(acc));  // inline: no call frame in scratch
   g2out[g.out] = d;
   g2lines_emit(g2_load(d), g1_load(pts[j.p2]), lines, idx, njobs);
 }
@@ -1302,20 +1306,6 @@ FTS_HD void sx_job_miller(const X& x, const PairJob& j, const LineCoef* qlines, 
       o[8 + i] = f.c1.v[i];
     }
   }
-}
-
-// EXACT: 0 = Fuentes chain (sx_final_exp), 1 = exact (sx_final_exp_exact)
-template <int EXACT, class X>
-FTS_HD void sx_job_fexp(const X& x, const PairJob& j, const F12Dev* fin, uint32_t idx, uint8_t* arena, bool valid) {
-  const uint32_t* w = &fin[idx].w[16 * sx_f12_index(x.k)];
-  fp2 f;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    f.c0.v[i] = w[i];
-    f.c1.v[i] = w[8 + i];
-  }
-  fp2 g = EXACT ? sx_final_exp_exact(x, f) : sx_final_exp(x, f);
-  if (valid) sx_gt_bytes(arena + j.bytes, x.k, g);
 }
 
 }  // namespace fts

@@ -35,8 +35,10 @@ FTS_HD fp fp_half(const fp& a) {
 }
 FTS_HD fp2 f2_half(const fp2& a) { return {fp_half(a.c0), fp_half(a.c1)}; }
 
-// T <- 2T; returns the tangent line coefficients
-FTS_HDN LineCoef dbl_step(g2p& T) {
+// T <- 2T; returns the tangent line coefficients (inline form: the one-lane
+// line stage, whose loop would otherwise keep T and the coefficients in a call
+// frame in scratch memory)
+FTS_HD LineCoef dbl_step_inl(g2p& T) {
   fp2 A = f2_half(T.x * T.y);
   fp2 B = f2_sqr(T.y);
   fp2 C = f2_sqr(T.z);
@@ -57,9 +59,10 @@ FTS_HDN LineCoef dbl_step(g2p& T) {
   l.r2 = I;
   return l;
 }
+FTS_HDN LineCoef dbl_step(g2p& T) { return dbl_step_inl(T); }
 
 // T <- T + Q (Q affine); returns the chord line coefficients
-FTS_HDN LineCoef add_step(g2p& T, const g2a& Q) {
+FTS_HD LineCoef add_step_inl(g2p& T, const g2a& Q) {
   fp2 O = T.y - Q.y * T.z;
   fp2 L = T.x - Q.x * T.z;
   fp2 C = f2_sqr(O);
@@ -78,6 +81,7 @@ FTS_HDN LineCoef add_step(g2p& T, const g2a& Q) {
   l.r2 = Q.x * O - L * Q.y;
   return l;
 }
+FTS_HDN LineCoef add_step(g2p& T, const g2a& Q) { return add_step_inl(T, Q); }
 
 FTS_HDN fp12 line_mul(const fp12& f, const LineCoef& l, const g1a& P) {
   return f12_mul_034(f, f2_mul_fp(l.r0, P.y), f2_mul_fp(l.r1, P.x), l.r2);
@@ -107,6 +111,28 @@ FTS_HD int naf_digit(int i) {
 }
 
 static constexpr int MILLER_LINES = 65 + 21 + 2;  // doublings + NAF additions + 2 Frobenius lines
+
+// The Miller loop's step sequence (precompute_lines order): for i = 64..0 a
+// doubling, then an addition of Q / -Q where the ate NAF digit is +1 / -1;
+// then the additions of pi(Q) and -pi^2(Q).
+enum : uint8_t { STEP_DBL = 0, STEP_ADD = 1, STEP_SUB = 2, STEP_FROB1 = 3, STEP_FROB2 = 4 };
+struct MillerSteps {
+  uint8_t t[MILLER_LINES];
+};
+constexpr MillerSteps miller_steps() {
+  MillerSteps m{};
+  int n = 0;
+  for (int i = 64; i >= 0; i--) {
+    m.t[n++] = STEP_DBL;
+    bool pos = i < 64 && ((ATE_NAF_POS >> i) & 1), neg = i < 64 && ((ATE_NAF_NEG >> i) & 1);
+    if (pos) m.t[n++] = STEP_ADD;
+    if (neg) m.t[n++] = STEP_SUB;
+  }
+  m.t[n++] = STEP_FROB1;
+  m.t[n++] = STEP_FROB2;
+  return m;
+}
+static constexpr MillerSteps MILLER_STEPS = miller_steps();
 
 // Line coefficients of a fixed G2 point, in consumption order (host precompute
 // at context creation; consumed by miller_2 for the PP generator Q).

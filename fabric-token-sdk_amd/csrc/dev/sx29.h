@@ -100,8 +100,12 @@ struct alignas(8) Q2Slot {
 };
 typedef FTS_LDS Q2Slot QSlotT;
 
-template <class Sync>
+// BOFS: slot of the second operand's group (b_0..b_5, then xi b_0..xi b_5);
+// SX_B in the 30-slot layout, 12 in the 24-slot one of k_fexp_expt (which
+// leaves SX_P unused and so fits two waves per SIMD in LDS).
+template <class Sync, int BOFS = SX_B>
 struct Sq {
+  static constexpr int B = BOFS, BX = BOFS + 6;
   int k;
   QSlotT* s;
   bool wr;
@@ -142,7 +146,7 @@ FTS_HD q2 sq_mul(X x, q2 a) {
 #pragma nounroll
   for (int i = 0; i < 6; i++) {
     int j = x.k - i;
-    int sb = j < 0 ? SX_BX + j + 6 : SX_B + j;
+    int sb = j < 0 ? X::BX + j + 6 : X::B + j;
     w29_mac(w, x.get(SX_A + i), x.get(sb));
   }
   x.sync();
@@ -150,7 +154,7 @@ FTS_HD q2 sq_mul(X x, q2 a) {
 }
 template <class X>
 FTS_HD q2 sq_mulv(const X& x, const q2& a, const q2& b) {
-  sq_pub(x, SX_B, b);
+  sq_pub(x, X::B, b);
   return sq_mul(x, a);
 }
 
@@ -182,13 +186,19 @@ FTS_HD q2 sq_frob1(int k, const q2& a) { return q2_mul(q2_conj(a), q2_from_fp2(f
 FTS_HD q2 sq_frob2(int k, const q2& a) { return q2_mul(a, q2_from_fp2(f2_of_fp(fe_const<ModP>(FROB2[k][0])))); }
 FTS_HD q2 sq_frob3(int k, const q2& a) { return q2_mul(q2_conj(a), q2_from_fp2(f2_const(FROB3[k]))); }
 
-// a^x, as sx_expt (width-4 NAF, a^7 parked in the lane's SX_P slot)
-template <class X>
-FTS_HD q2 sq_expt(X x, q2 a) {
+// a^x, as sx_expt (width-4 NAF).  a, a^3, a^5 and a^7 are parked in pk slots
+// ps .. ps+3 (dev: global dword planes) and republished from there when the
+// digit's magnitude changes, so the loop holds only r and the product's
+// operands and accumulator, and no LDS beyond the operand slots.
+template <class X, class P>
+FTS_HD q2 sq_expt(X x, q2 a, const P& pk, int ps) {
+  pk.put(ps, a);
   q2 a2 = sq_cyc_sqr(x, a);
   q2 a3 = sq_mulv(x, a2, a);
+  pk.put(ps + 1, a3);
   q2 a5 = sq_mulv(x, a3, a2);
-  x.put(SX_P + x.k, sq_mul(x, a5));
+  pk.put(ps + 2, a5);
+  pk.put(ps + 3, sq_mul(x, a5));
   int cur = 0;
   q2 r = a;
 #pragma nounroll
@@ -197,7 +207,7 @@ FTS_HD q2 sq_expt(X x, q2 a) {
     if ((BN_X_W4_NZ >> i) & 1) {
       int m = ((BN_X_W4_M3 >> i) & 1) ? 3 : (((BN_X_W4_M5 >> i) & 1) ? 5 : (((BN_X_W4_M7 >> i) & 1) ? 7 : 1));
       if (m != cur) {
-        sq_pub(x, SX_B, m == 7 ? x.get(SX_P + x.k) : (m == 1 ? a : (m == 3 ? a3 : a5)));
+        sq_pub(x, X::B, pk.get(ps + (m - 1) / 2));
         cur = m;
       }
       bool neg = (BN_X_W4_NEG >> i) & 1;
@@ -236,75 +246,133 @@ FTS_HD q2 sq_inv(X x, q2 f) {
   for (int s = 0; s < 3; s++) w29_mac(v, x.get(s == 0 ? SX_A + 0 : (s == 1 ? SX_AX + 4 : SX_AX + 2)), x.get(SX_P + s));
   q2 tk = x.get(SX_P + (k >> 1));
   x.sync();
-  fp2 di = f2_inv(q2_to_fp2(w29_reduce(v)));
+  fp2 di = f2_inv_inl(q2_to_fp2(w29_reduce(v)));  // inline: the easy-part kernel has the registers
   q2 inv6 = q2_sel((k & 1) == 0, q2_mul(tk, q2_from_fp2(di)), q2_zero());
   return sq_mulv(x, fc, inv6);
 }
 
-// The two final exponentiations (same sequences as sx_final_exp_exact /
-// sx_final_exp)
+// Values handed between the final-exponentiation phases (and parked inside a
+// phase) in global memory.  Plane (s * 18 + d) holds dword d of slot s for
+// every lane of the launch (lane = global thread index), so a wave's put / get
+// is 18 coalesced 256-byte stores / loads.  Ghost lanes neither store nor load
+// (their results are never written).  FEXP_PARK_SLOTS slots per lane.
+static constexpr int FEXP_PARK_SLOTS = 11;
+struct Park {
+  int32_t* base;
+  uint32_t lane, stride;
+  bool on;
+  // plane rows are uniform pointers (scalar registers) and the lane a 32-bit
+  // offset, so the 18 accesses share one address register
+  FTS_HD void put(int slot, const q2& a) const {
+    if (!on) return;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      (base + (size_t)(slot * 18 + i) * stride)[lane] = a.c0.l[i];
+      (base + (size_t)(slot * 18 + 9 + i) * stride)[lane] = a.c1.l[i];
+    }
+  }
+  FTS_HD q2 get(int slot) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::: "memory");  // reload here: the value must not stay in registers since put()
+#endif
+    q2 a = q2_zero();
+    if (!on) return a;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      a.c0.l[i] = (base + (size_t)(slot * 18 + i) * stride)[lane];
+      a.c1.l[i] = (base + (size_t)(slot * 18 + 9 + i) * stride)[lane];
+    }
+    return a;
+  }
+};
+
+// Exact final exponentiation f^((p^12-1)/r) (Scott et al. chain, as
+// final_exp_exact in pairing.h) in three phases that the device runs as
+// separate kernels (k_fexp_easy, k_fexp_expt x 3, k_fexp_hard): composed in
+// one kernel the phases' register needs (171, 236 and ~200 VGPRs alone) did not
+// fit together under the 256 of two waves per SIMD -- the compiler spilled
+// 340 VGPRs (1 KB per lane) and the kernel moved ~26x its algorithmic bytes.
+// Handing m, m^x, m^(x^2), m^(x^3) over in the park planes costs 72 bytes per
+// lane per value.  Park slots: 0 m, 1 m^x, 2 m^(x^2), 3 m^(x^3); 4..7 the
+// odd powers inside sq_expt.
+//
+// easy part: m = f^((p^6-1)(p^2+1))
 template <class X>
-FTS_HD fp2 sq_final_exp_exact(const X& x, const fp2& f) {
+FTS_HD q2 sq_fexp_easy(const X& x, const fp2& f) {
   const int k = x.k;
   q2 F = q2_from_fp2(f);
   q2 m = sq_mulv(x, sq_conj(k, F), sq_inv(x, F));
-  m = sq_mulv(x, sq_frob2(k, m), m);
-  q2 in = m, mx, mx2, mx3;
-#pragma nounroll
-  for (int e = 0; e < 3; e++) {
-    q2 r = sq_expt(x, in);
-    if (e == 0) {
-      mx = r;
-    } else if (e == 1) {
-      mx2 = r;
-    } else {
-      mx3 = r;
-    }
-    in = r;
-  }
-  q2 y3 = sq_conj(k, sq_frob1(k, mx));
-  q2 y4 = sq_conj(k, sq_mulv(x, mx, sq_frob1(k, mx2)));
-  q2 y5 = sq_conj(k, mx2);
-  q2 y2 = sq_frob2(k, mx2);
-  q2 y6 = sq_conj(k, sq_mulv(x, mx3, sq_frob1(k, mx3)));
-  q2 t0 = sq_mulv(x, sq_mulv(x, sq_cyc_sqr(x, y6), y4), y5);
-  q2 t1 = sq_mulv(x, sq_mulv(x, y3, y5), t0);
-  t0 = sq_mulv(x, t0, y2);
+  return sq_mulv(x, sq_frob2(k, m), m);
+}
+// hard part from the four parked powers: y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36 as
+//   t0 = y6^2 y4 y5,  t1 = y3 y5 t0,  t0 <- t0 y2,  t1 <- (t1^2 t0)^2,
+//   result = (t1 y1)^2 (t1 y0)
+// (the products of sx_final_exp_exact, ordered so that at most three Fp12
+// values are live next to a product; inputs reloaded from the park slots)
+template <class X, class P>
+FTS_HD fp2 sq_fexp_hard_exact(const X& x, const P& pk) {
+  const int k = x.k;
+  q2 t0 = pk.get(3);                                                         // m^(x^3)
+  t0 = sq_cyc_sqr(x, sq_conj(k, sq_mulv(x, t0, sq_frob1(k, t0))));         // y6^2
+  q2 u = pk.get(1);                                                          // m^x
+  t0 = sq_mulv(x, t0, sq_conj(k, sq_mulv(x, u, sq_frob1(k, pk.get(2)))));  // y6^2 y4
+  q2 y5 = sq_conj(k, pk.get(2));
+  t0 = sq_mulv(x, t0, y5);                                                   // t0 = y6^2 y4 y5
+  u = sq_mulv(x, sq_conj(k, sq_frob1(k, u)), y5);                            // y3 y5
+  q2 t1 = sq_mulv(x, u, t0);                                                 // t1 = y3 y5 t0
+  t0 = sq_mulv(x, t0, sq_frob2(k, pk.get(2)));                               // t0 y2
   t1 = sq_cyc_sqr(x, sq_mulv(x, sq_cyc_sqr(x, t1), t0));
-  q2 y0 = sq_mulv(x, sq_mulv(x, sq_frob1(k, m), sq_frob2(k, m)), sq_frob3(k, m));
+  q2 m = pk.get(0);
+  u = sq_mulv(x, sq_frob1(k, m), sq_frob2(k, m));
+  u = sq_mulv(x, u, sq_frob3(k, m));                                         // y0
   t0 = sq_mulv(x, t1, sq_conj(k, m));
-  t1 = sq_mulv(x, t1, y0);
+  t1 = sq_mulv(x, t1, u);
   return q2_to_fp2(sq_mulv(x, sq_cyc_sqr(x, t0), t1));
 }
+// the three phases composed (host emulation; the device launches them apart)
+template <class X, class P>
+FTS_HD fp2 sq_final_exp_exact(const X& x, const fp2& f, const P& pk) {
+  pk.put(0, sq_fexp_easy(x, f));
+  for (int e = 0; e < 3; e++) pk.put(e + 1, sq_expt(x, pk.get(e), pk, 4));
+  return sq_fexp_hard_exact(x, pk);
+}
 
-template <class X>
-FTS_HD fp2 sq_final_exp(const X& x, const fp2& f) {
+// Fuentes-Castaneda multiple (the selectable FTZ_FEXP_FUENTES variant), phased
+// like the exact one (k_fexp_easy, k_fexp_expt, k_fexp_fc_mid1, k_fexp_expt,
+// k_fexp_fc_mid2, k_fexp_expt, k_fexp_fc_hard).  Slots: 0 t (easy part), 1 a =
+// t^x, 2 a2, 3 a6, 4 b = a6^x, 5 b^2, 6 c = (b^2)^x; the x-powers' odd powers
+// in FC_EXPT_SLOT ..+3.
+static constexpr int FC_EXPT_SLOT = 7;
+template <class X, class P>
+FTS_HD void sq_fc_mid1(const X& x, const P& pk) {  // a2 = a^2, a6 = a2^3
+  q2 a2 = sq_cyc_sqr(x, pk.get(1));
+  pk.put(2, a2);
+  pk.put(3, sq_mulv(x, sq_cyc_sqr(x, a2), a2));
+}
+template <class X, class P>
+FTS_HD void sq_fc_mid2(const X& x, const P& pk) {  // b^2
+  pk.put(5, sq_cyc_sqr(x, pk.get(4)));
+}
+template <class X, class P>
+FTS_HD fp2 sq_fc_hard(const X& x, const P& pk) {
   const int k = x.k;
-  q2 F = q2_from_fp2(f);
-  q2 t = sq_mulv(x, sq_conj(k, F), sq_inv(x, F));
-  t = sq_mulv(x, sq_frob2(k, t), t);
-  q2 in = t, a2, a6, b, c;
-#pragma nounroll
-  for (int e = 0; e < 3; e++) {
-    q2 r = sq_expt(x, in);
-    if (e == 0) {
-      a2 = sq_cyc_sqr(x, r);
-      a6 = sq_mulv(x, sq_cyc_sqr(x, a2), a2);
-      in = a6;
-    } else if (e == 1) {
-      b = r;
-      in = sq_cyc_sqr(x, b);
-    } else {
-      c = r;
-    }
-  }
-  q2 A = sq_mulv(x, sq_mulv(x, a6, b), c);
-  q2 B = sq_mulv(x, A, sq_conj(k, a2));
-  q2 res = sq_frob2(k, A);
-  res = sq_mulv(x, res, sq_mulv(x, sq_mulv(x, A, b), t));
+  q2 b = pk.get(4);
+  q2 A = sq_mulv(x, sq_mulv(x, pk.get(3), b), pk.get(6));
+  q2 B = sq_mulv(x, A, sq_conj(k, pk.get(2)));
+  q2 res = sq_mulv(x, sq_frob2(k, A), sq_mulv(x, sq_mulv(x, A, b), pk.get(0)));
   res = sq_mulv(x, res, sq_frob1(k, B));
-  res = sq_mulv(x, res, sq_frob3(k, sq_mulv(x, B, sq_conj(k, t))));
+  res = sq_mulv(x, res, sq_frob3(k, sq_mulv(x, B, sq_conj(k, pk.get(0)))));
   return q2_to_fp2(res);
+}
+template <class X, class P>
+FTS_HD fp2 sq_final_exp(const X& x, const fp2& f, const P& pk) {
+  pk.put(0, sq_fexp_easy(x, f));
+  pk.put(1, sq_expt(x, pk.get(0), pk, FC_EXPT_SLOT));
+  sq_fc_mid1(x, pk);
+  pk.put(4, sq_expt(x, pk.get(3), pk, FC_EXPT_SLOT));
+  sq_fc_mid2(x, pk);
+  pk.put(6, sq_expt(x, pk.get(5), pk, FC_EXPT_SLOT));
+  return sq_fc_hard(x, pk);
 }
 
 // ----------------------------------------------------------- Miller f-chain

@@ -53,11 +53,13 @@ FTS_HD fp2 f2_mul_xi(const fp2& a) {
   return {a0_9 - a.c1, a.c0 + a1_9};
 }
 
-FTS_HDN fp2 f2_inv(const fp2& a) {
+FTS_HD fp2 f2_inv_inl(const fp2& a) {
   fp n = fe_sqr(a.c0) + fe_sqr(a.c1);
   fp ni = fp_inv_var(n);  // variable time: every value inverted on this path is public
   return {a.c0 * ni, fe_neg(a.c1 * ni)};
 }
+// out of line where the caller's registers are tight (a call frame instead of spills)
+FTS_HDN fp2 f2_inv(const fp2& a) { return f2_inv_inl(a); }
 
 // ----------------------------------------------------------------- Fp6
 FTS_HD fp6 f6_zero() { return {f2_zero(), f2_zero(), f2_zero()}; }

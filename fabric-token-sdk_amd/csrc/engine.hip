@@ -11,8 +11,10 @@
 //     opt.batch proofs -- which also keeps every 32-bit job index of a batch in
 //     range -- and fills the pipeline by itself;
 //   * small concurrent calls (the Go shim verifies ONE TransferAction per call)
-//     are coalesced: while the GPU has >= 2 batches in flight a partial batch
-//     waits up to opt.window_us for more callers, otherwise it goes at once;
+//     are coalesced: while the GPU has >= opt.hold_inflight batches in flight a
+//     partial batch waits up to opt.window_us for more callers, otherwise it
+//     goes at once; with every slot busy, callers accumulate for the next free
+//     slot anyway;
 //   * transfers and issues share batches (the planner emits the same jobs).
 //
 // Batches cycle through opt.slots reusable slots (pinned staging blob, device
@@ -122,7 +124,7 @@ void Engine::dispatcher() {
     }
     size_t pending = 0;
     for (Request* r : q) pending += r->n - r->next;
-    if (pending < B && inflight.size() >= 2 && !stop) {
+    if (pending < B && inflight.size() >= ctx->opt.hold_inflight && !stop) {
       // the device is busy: let a partial batch wait (a bounded time) for company
       Clock::time_point deadline = q.front()->t0 + window;
       if (Clock::now() < deadline) {

@@ -7,52 +7,69 @@
 
 using namespace fts;
 
-// Final exponentiations, sextet layout (see k_miller): k_fexp_exact computes
-// f^((p^12-1)/r) (FTZ_FEXP_EXACT, the default), k_fexp the Fuentes-Castaneda
-// multiple (FTZ_FEXP_FUENTES); the context's option picks the kernel.
-//
-// FTS_FEXP_F29 = 1 (default): the carry-free 29-bit accumulation of dev/sx29.h;
-// 0: the 32-bit wide accumulation of dev/sextet.h.
-#ifndef FTS_FEXP_F29
-#define FTS_FEXP_F29 1
-#endif
+// Final exponentiations, sextet layout (see k_miller), carry-free 29-bit
+// accumulation (dev/sx29.h).  FTZ_FEXP_EXACT (the default) computes
+// f^((p^12-1)/r) in five launches -- k_fexp_easy, k_fexp_expt x 3, k_fexp_hard
+// -- that hand m, m^x, m^(x^2), m^(x^3) over in the park planes (Park,
+// fexp_park_bytes); FTZ_FEXP_FUENTES (the Fuentes-Castaneda multiple) in
+// seven (the same easy and x-power kernels plus k_fexp_fc_*).  All launches of
+// one pass use the same grid, so a lane's park index is the same in every
+// phase.
 
-#if FTS_FEXP_F29
-template <int EXACT, class X>
-__device__ __forceinline__ void sq_job_fexp(const X& x, const PairJob& j, const F12Dev* fin, uint32_t idx,
-                                            uint8_t* arena, bool valid) {
-  const uint32_t* w = &fin[idx].w[16 * sx_f12_index(x.k)];
+#define FEXP_PARK Park pk{park, blockIdx.x * 64 + threadIdx.x, gridDim.x * 64, !ghost_};
+
+__device__ __forceinline__ fp2 fexp_load(const F12Dev* fin, uint32_t idx, int k) {
+  const uint32_t* w = &fin[idx].w[16 * sx_f12_index(k)];
   fp2 f;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     f.c0.v[i] = w[i];
     f.c1.v[i] = w[8 + i];
   }
-  fp2 g = EXACT ? sq_final_exp_exact(x, f) : sq_final_exp(x, f);
-  if (valid) sx_gt_bytes(arena + j.bytes, x.k, g);
-}
-#endif
-
-__global__ void __launch_bounds__(64, 2) k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf,
-                                             uint8_t* arena) {
-#if FTS_FEXP_F29
-  SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
-  sq_job_fexp<0>(x, jobs[jc], fbuf, jc, arena, valid);
-#else
-  SX_SLOTS_DECL(SX_SLOTS_FEXP)
-  SX_KERNEL_PROLOGUE(n);
-  sx_job_fexp<0>(x, jobs[jc], fbuf, jc, arena, valid);
-#endif
+  return f;
 }
 
-__global__ void __launch_bounds__(64, 2) k_fexp_exact(const PairJob* jobs, uint32_t n, const F12Dev* fbuf,
-                                                   uint8_t* arena) {
-#if FTS_FEXP_F29
+// phase 1: easy part, m -> park slot 0
+__global__ void __launch_bounds__(64, 2) k_fexp_easy(uint32_t n, const F12Dev* fbuf, int32_t* park) {
   SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
-  sq_job_fexp<1>(x, jobs[jc], fbuf, jc, arena, valid);
-#else
-  SX_SLOTS_DECL(SX_SLOTS_FEXP)
-  SX_KERNEL_PROLOGUE(n);
-  sx_job_fexp<1>(x, jobs[jc], fbuf, jc, arena, valid);
-#endif
+  FEXP_PARK
+  pk.put(0, sq_fexp_easy(x, fexp_load(fbuf, jc, x.k)));
+}
+
+// phase 2 (three launches): slot dst = (slot src)^x, odd powers parked from
+// slot ps.  24 LDS slots (A, AX, B, BX): 17.4 KB per workgroup, so LDS admits
+// the two waves per SIMD that the registers allow (the 30-slot region's 21.7 KB
+// admitted 1.75).
+__global__ void __launch_bounds__(64, 2) k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps) {
+  SQ_KERNEL_PROLOGUE_B(n, 24, 12)
+  FEXP_PARK
+  pk.put(dst, sq_expt(x, pk.get(src), pk, ps));
+}
+
+// phase 3: hard part from slots 0..3 -> GT bytes in the membership transcript
+__global__ void __launch_bounds__(64, 1) k_fexp_hard(const PairJob* jobs, uint32_t n, uint8_t* arena,
+                                                  int32_t* park) {
+  SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
+  FEXP_PARK
+  fp2 g = sq_fexp_hard_exact(x, pk);
+  if (valid) sx_gt_bytes(arena + jobs[jc].bytes, x.k, g);
+}
+
+// Fuentes-Castaneda glue and hard part
+__global__ void __launch_bounds__(64, 2) k_fexp_fc_mid1(uint32_t n, int32_t* park) {
+  SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
+  FEXP_PARK
+  sq_fc_mid1(x, pk);
+}
+__global__ void __launch_bounds__(64, 2) k_fexp_fc_mid2(uint32_t n, int32_t* park) {
+  SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
+  FEXP_PARK
+  sq_fc_mid2(x, pk);
+}
+__global__ void __launch_bounds__(64, 1) k_fexp_fc_hard(const PairJob* jobs, uint32_t n, uint8_t* arena,
+                                                     int32_t* park) {
+  SQ_KERNEL_PROLOGUE(n, SX_SLOTS_FEXP)
+  FEXP_PARK
+  fp2 g = sq_fc_hard(x, pk);
+  if (valid) sx_gt_bytes(arena + jobs[jc].bytes, x.k, g);
 }

@@ -37,7 +37,8 @@ struct SyncWave {
 
 // The same for the carry-free sextet kernels (dev/sx29.h): NS Q2 slots per
 // sextet in a region of sq_region_dwords(NS) dwords.
-#define SQ_KERNEL_PROLOGUE(n, NS)                                                 \
+#define SQ_KERNEL_PROLOGUE(n, NS) SQ_KERNEL_PROLOGUE_B(n, NS, SX_B)
+#define SQ_KERNEL_PROLOGUE_B(n, NS, BOFS)                                         \
   static constexpr uint32_t sq_stride_ = sq_region_dwords(NS) / 2;               \
   __shared__ uint2 sq_raw_[SX_JOBS_PER_WAVE * sq_stride_];                       \
   uint32_t lane_ = threadIdx.x, sx_ = lane_ / 6;                                 \
@@ -47,7 +48,7 @@ struct SyncWave {
   uint32_t job_ = blockIdx.x * SX_JOBS_PER_WAVE + sx_;                           \
   bool valid = !ghost_ && job_ < (n);                                            \
   uint32_t jc = job_ < (n) ? job_ : (n) - 1;                                     \
-  Sq<SyncWave> x{k_, (QSlotT*)(sq_raw_ + sx_ * sq_stride_), !ghost_, {}};
+  Sq<SyncWave, BOFS> x{k_, (QSlotT*)(sq_raw_ + sx_ * sq_stride_), !ghost_, {}};
 
 __global__ void k_decode(const DecodeJob* jobs, uint32_t n, const uint8_t* wire, G1Dev* pts, uint8_t* pt_ok,
                          uint8_t* arena);
@@ -82,8 +83,35 @@ __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef29* qlin
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, LineCoef29* out29, LineCoef29* out29n, int* n, int* norm);
 __global__ void k_miller_n(const PairJob* jobs, uint32_t n, const LineCoef29* qlines_n, const EvLineDev* lines2,
                            const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
-__global__ void k_fexp(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
-__global__ void k_fexp_exact(const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena);
+// final exponentiation phases (k_fexp.hip); park: fexp_park_bytes(n) of scratch (dev/sx29.h Park)
+__global__ void k_fexp_easy(uint32_t n, const F12Dev* fbuf, int32_t* park);
+__global__ void k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps);
+__global__ void k_fexp_hard(const PairJob* jobs, uint32_t n, uint8_t* arena, int32_t* park);
+__global__ void k_fexp_fc_mid1(uint32_t n, int32_t* park);
+__global__ void k_fexp_fc_mid2(uint32_t n, int32_t* park);
+__global__ void k_fexp_fc_hard(const PairJob* jobs, uint32_t n, uint8_t* arena, int32_t* park);
+inline size_t fexp_park_bytes(size_t n_pr) {
+  return ((n_pr + SX_JOBS_PER_WAVE - 1) / SX_JOBS_PER_WAVE) * 64 * (size_t)FEXP_PARK_SLOTS * 18 * sizeof(int32_t);
+}
+// exact (FTZ_FEXP_EXACT): easy part, three x-powers, hard part; Fuentes-Castaneda
+// (FTZ_FEXP_FUENTES): easy part and x-powers with its two glue steps
+inline void launch_fexp(bool exact, const PairJob* jobs, uint32_t n, const F12Dev* fbuf, uint8_t* arena,
+                        int32_t* park, hipStream_t s) {
+  if (!n) return;
+  const uint32_t nb = (n + SX_JOBS_PER_WAVE - 1) / SX_JOBS_PER_WAVE;
+  k_fexp_easy<<<nb, 64, 0, s>>>(n, fbuf, park);
+  if (exact) {
+    for (int e = 0; e < 3; e++) k_fexp_expt<<<nb, 64, 0, s>>>(n, park, e, e + 1, 4);
+    k_fexp_hard<<<nb, 64, 0, s>>>(jobs, n, arena, park);
+    return;
+  }
+  k_fexp_expt<<<nb, 64, 0, s>>>(n, park, 0, 1, FC_EXPT_SLOT);
+  k_fexp_fc_mid1<<<nb, 64, 0, s>>>(n, park);
+  k_fexp_expt<<<nb, 64, 0, s>>>(n, park, 3, 4, FC_EXPT_SLOT);
+  k_fexp_fc_mid2<<<nb, 64, 0, s>>>(n, park);
+  k_fexp_expt<<<nb, 64, 0, s>>>(n, park, 5, 6, FC_EXPT_SLOT);
+  k_fexp_fc_hard<<<nb, 64, 0, s>>>(jobs, n, arena, park);
+}
 
 // prover (k_light.hip)
 __global__ void k_rand(const RandJob* jobs, uint32_t n, const uint8_t* arena, uint32_t (*scal)[8]);

@@ -86,12 +86,10 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   HC(hipSetDevice(c->device));
   ftz_msm* m = new ftz_msm();
   m->ctx = c;
-  // tuning overrides (window bits, slot cap, slots per segment); 0 = planner default
-  auto env = [](const char* k) { const char* v = getenv(k); return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u; };
-  uint32_t c_over = env("FTZ_MSM_C");
-  if (c_over > 24) c_over = 0;
-  const char* glv = getenv("FTZ_MSM_GLV");
-  m->p = msm_make_plan(n, c_over, env("FTZ_MSM_T"), env("FTZ_MSM_S"), !(glv && glv[0] == '0'));
+  // planner overrides from the context's options (window bits, slot cap, slots per
+  // segment; 0 = the planner's choice) and the GLV switch
+  const ftz_options& o = c->opt;
+  m->p = msm_make_plan(n, o.msm_window_bits, o.msm_slot_cap, o.msm_seg_slots, o.msm_glv != 0);
   int rc = msm_alloc(m, n);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);

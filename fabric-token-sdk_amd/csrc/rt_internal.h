@@ -135,7 +135,7 @@ struct ftz_ctx {
 // Device scratch of a batch (values the kernels produce), sub-allocated from
 // one grow-only buffer.
 struct ScratchLayout {
-  size_t pts, pt_ok, scal, canon, g1out, pnorm, g2out, fbuf, lines2, part1, part1p, part2, vtab1, vtab1p, hash_ok, hash_ok_pre,
+  size_t pts, pt_ok, scal, canon, g1out, pnorm, g2out, fbuf, fxpark, lines2, part1, part1p, part2, vtab1, vtab1p, hash_ok, hash_ok_pre,
       codes, bitmap, total;
 };
 

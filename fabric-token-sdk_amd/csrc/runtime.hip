@@ -49,6 +49,9 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->window_us = 2000;
   o->threads = 0;
   o->fexp = FTZ_FEXP_EXACT;
+  o->hold_inflight = 2;
+  o->small_pass = 0;
+  o->msm_glv = 1;
 }
 
 extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {
@@ -68,6 +71,8 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     if (o.slots == 0) o.slots = 4;
     if (o.fexp != FTZ_FEXP_EXACT && o.fexp != FTZ_FEXP_FUENTES) return set_err(FTZ_E_INVALID, "unknown fexp variant");
     if (o.batch > (1u << 20) || o.slots > 64) return set_err(FTZ_E_INVALID, "batch / slots out of range");
+    if (o.hold_inflight == 0) o.hold_inflight = 2;
+    if (o.msm_window_bits > 24) return set_err(FTZ_E_INVALID, "msm_window_bits out of range (0..24)");
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -377,6 +382,7 @@ static void scratch_layout(ftz_batch* b) {
   s.pnorm = take(sizeof(G1Dev) * (size_t)f.n_g1out);
   s.g2out = take(sizeof(G2Dev) * (size_t)f.n_g2out);
   s.fbuf = take(sizeof(F12Dev) * n_pr);
+  s.fxpark = take(fexp_park_bytes(n_pr));
   s.lines2 = take(sizeof(EvLineDev) * n_pr * MILLER_LINES);
   s.part1 = take(sizeof(G1JDev) * 4 * n_g1);
   s.part1p = take(sizeof(G1JDev) * 4 * n_g1p);
@@ -452,6 +458,7 @@ struct SlotPtrs {
   G1Dev* pnorm;
   G2Dev* g2out;
   F12Dev* fbuf;
+  int32_t* fxpark;
   EvLineDev* lines2;
   G1JDev *part1, *part1p;
   G2PartDev* part2;
@@ -497,6 +504,7 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   p.pnorm = reinterpret_cast<G1Dev*>(s + l.pnorm);
   p.g2out = reinterpret_cast<G2Dev*>(s + l.g2out);
   p.fbuf = reinterpret_cast<F12Dev*>(s + l.fbuf);
+  p.fxpark = reinterpret_cast<int32_t*>(s + l.fxpark);
   p.lines2 = reinterpret_cast<EvLineDev*>(s + l.lines2);
   p.part1 = reinterpret_cast<G1JDev*>(s + l.part1);
   p.part1p = reinterpret_cast<G1JDev*>(s + l.part1p);
@@ -529,7 +537,11 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
 // k_g2_part four lanes per job for the table sums, then k_g2lines1) or the
 // sextet layout (k_g2lines); same bytes either way
 static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
-  if ((prover ? c->g2lanes_prover : c->g2lanes) == FTZ_LAYOUT_ONE_LANE) {
+  // small passes (few callers waiting) take the low-latency sextet layout: six lanes
+  // per job cut the stage's per-job chain, which bounds a small pass's latency
+  int layout = prover ? c->g2lanes_prover : c->g2lanes;
+  if (!prover && p.n_g2 <= c->opt.small_pass) layout = FTZ_LAYOUT_SEXTET;
+  if (layout == FTZ_LAYOUT_ONE_LANE) {
     k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);
   } else {
@@ -549,11 +561,7 @@ static void launch_miller(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
 }
 
 static void launch_fexp(ftz_ctx* c, const SlotPtrs& p, hipStream_t s) {
-  if (!p.n_pr) return;
-  if (c->opt.fexp == FTZ_FEXP_FUENTES)
-    k_fexp<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, p.fbuf, p.arena);
-  else
-    k_fexp_exact<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, p.fbuf, p.arena);
+  launch_fexp(c->opt.fexp != FTZ_FEXP_FUENTES, p.pr, p.n_pr, p.fbuf, p.arena, p.fxpark, s);
 }
 
 // Verification pipeline.  Three streams after the light decode/scalar kernels:

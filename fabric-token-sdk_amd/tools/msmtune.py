@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """MSM plan sweep: device latency of ftz_msm_run for window bits C, slot cap T
-and slots per segment S (FTZ_MSM_C / _T / _S planner overrides; 0 = default).
+and slots per segment S (ftz_options msm_window_bits / msm_slot_cap / msm_seg_slots;
+0 = the planner's choice).
     python msmtune.py 20 "0,0,0 16,16,0 16,32,0 15,0,0 17,0,0"
 """
 import json
@@ -16,11 +17,10 @@ import zkatdlog  # noqa: E402
 lg = int(sys.argv[1])
 combos = [tuple(int(v) for v in c.split(",")) for c in sys.argv[2].split()]
 pp = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]["pp"].encode()
-ctx = zkatdlog.Context(pp, device=0)
 scal = np.random.default_rng(lg).bytes(32 << lg)
 ref = None
 for c, t, s in combos:
-    os.environ["FTZ_MSM_C"], os.environ["FTZ_MSM_T"], os.environ["FTZ_MSM_S"] = str(c), str(t), str(s)
+    ctx = zkatdlog.Context(pp, device=0, msm_window_bits=c, msm_slot_cap=t, msm_seg_slots=s)
     m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
     out = m.run()
     ms = []
@@ -31,4 +31,4 @@ for c, t, s in combos:
     print("n=2^%d C=%2d T=%3d S=%3d  %8.3f ms  %s" % (lg, m.info()["window_bits"], t, s, min(ms),
                                                      "ok" if out == ref else "MISMATCH"), flush=True)
     m.close()
-ctx.close()
+    ctx.close()

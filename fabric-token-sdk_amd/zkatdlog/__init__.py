@@ -50,16 +50,25 @@ class Context:
     its validator once per process (token/services/network/fabric/tcc/tcc.go:170-182);
     so does this."""
 
-    def __init__(self, pp_bytes, device=0, threads=None, fexp="exact", batch=None, slots=None, window_us=None):
+    def __init__(self, pp_bytes, device=0, threads=None, fexp="exact", batch=None, slots=None, window_us=None,
+                 **options):
         """fexp: "exact" (FTZ_FEXP_EXACT, gnark-crypto v0.6.0) or "fuentes";
-        batch / slots / window_us / threads: job-engine options (ftz_options)."""
+        batch / slots / window_us / threads and any other ftz_options field by name
+        (hold_inflight, small_pass, msm_window_bits, msm_slot_cap, msm_seg_slots,
+        msm_glv): job-engine and MSM options."""
         self._lib = _abi.load()
+        self.device = int(device)
         h = ctypes.c_void_p()
         pp_bytes = bytes(pp_bytes)
         o = _abi.Options()
         self._lib.ftz_options_default(ctypes.byref(o))
         o.fexp = _abi.FEXP[fexp]
-        for k, v in (("batch", batch), ("slots", slots), ("window_us", window_us), ("threads", threads)):
+        names = {k for k, _ in _abi.Options._fields_[1:]} - {"fexp"}
+        unknown = set(options) - names
+        if unknown:
+            raise TypeError("unknown ftz_options field(s): %s" % ", ".join(sorted(unknown)))
+        options.update(batch=batch, slots=slots, window_us=window_us, threads=threads)
+        for k, v in options.items():
             if v is not None:
                 setattr(o, k, int(v))
         _check(self._lib.ftz_ctx_create_ex(pp_bytes, len(pp_bytes), int(device), ctypes.byref(o), ctypes.byref(h)),

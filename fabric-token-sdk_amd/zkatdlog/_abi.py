@@ -71,7 +71,13 @@ FEXP = {"exact": FTZ_FEXP_EXACT, "fuentes": FTZ_FEXP_FUENTES}
 
 class Options(ctypes.Structure):
     _fields_ = [("struct_size", ctypes.c_uint32), ("batch", ctypes.c_uint32), ("slots", ctypes.c_uint32),
-                ("window_us", ctypes.c_uint32), ("threads", ctypes.c_uint32), ("fexp", ctypes.c_uint32)]
+                ("window_us", ctypes.c_uint32), ("threads", ctypes.c_uint32), ("fexp", ctypes.c_uint32),
+                ("hold_inflight", ctypes.c_uint32), ("small_pass", ctypes.c_uint32),
+                ("msm_window_bits", ctypes.c_uint32), ("msm_slot_cap", ctypes.c_uint32),
+                ("msm_seg_slots", ctypes.c_uint32), ("msm_glv", ctypes.c_uint32)]
+
+
+HOLD_NEVER = 0xFFFFFFFF
 
 
 class TokenOpening(ctypes.Structure):

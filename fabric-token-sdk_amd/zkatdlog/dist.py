@@ -49,7 +49,7 @@ def msm_shard(ctx, n_total, rank, world, dist, partial):
     t = torch.frombuffer(bytearray(part), dtype=torch.uint8).to(dev)
     parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t)
-    return start, stop, ctx.g1_sum(b"".join(bytes(p.cpu().tolist()) for p in parts))
+    return start, stop, ctx.g1_sum(b"".join(p.cpu().numpy().tobytes() for p in parts))
 
 
 def bitmap_of(codes):
@@ -82,12 +82,13 @@ def gather_verdicts(bits, n_local, ok_local, dist):
     dist.all_gather(gathered, bt)
     okt = torch.tensor([1 if ok_local else 0], dtype=torch.int64, device=dev)
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    import numpy as np
     out, n_accept = [], 0
     for g, s in zip(gathered, sizes):
-        b = bytes(g.cpu().tolist())[:int(s[0].item())]
+        arr = g.cpu().numpy()[:int(s[0].item())]
         n = int(s[1].item())
-        n_accept += sum(((b[i // 8] >> (i % 8)) & 1) for i in range(n))
-        out.append(b)
+        n_accept += int(np.unpackbits(arr, bitorder="little")[:n].sum())  # vectorised popcount
+        out.append(arr.tobytes())
     return out, n_accept, bool(okt.item())
 
 

@@ -35,6 +35,28 @@ def witness_bases(path=None):
             for t in bs]
 
 
+def random_witness_bases(ctx, n, seed=1, ttype="ABC"):
+    """n 2-in/2-out transfer witnesses for ctx's public parameters (any base
+    and exponent, e.g. PP-B's 64-bit range): input values uniform in
+    [1, max/2], outputs a random re-split of their sum, blinding factors
+    uniform mod r, commitments computed on the device (ftz_commit_tokens =
+    computeTokens, token/token.go:64-76).  Dicts as witness_bases()."""
+    import random
+    R = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+    rng = random.Random(seed)
+    vmax = ctx.base ** ctx.exponent - 1
+    bases = []
+    for _ in range(n):
+        vin = [rng.randint(1, vmax // 2) for _ in range(2)]
+        o1 = rng.randint(0, sum(vin))
+        vout = [o1, sum(vin) - o1]
+        bin_, bout = [rng.randrange(1, R) for _ in range(2)], [rng.randrange(1, R) for _ in range(2)]
+        coms = ctx.commit_tokens([(ttype, v, b) for v, b in zip(vin + vout, bin_ + bout)])
+        bases.append({"inputs": coms[0] + coms[1], "outputs": coms[2] + coms[3], "in_values": vin, "in_bfs": bin_,
+                      "out_values": vout, "out_bfs": bout, "type": ttype})
+    return bases
+
+
 def seeds(n, tag=b"bench"):
     """n distinct 32-byte prover seeds"""
     out = bytearray(32 * n)

@@ -102,7 +102,18 @@ typedef struct {
                            callers while the GPU is busy (default 2000)                 */
   uint32_t threads;     /* host planning threads (0: min(16, hardware threads))         */
   uint32_t fexp;        /* FTZ_FEXP_EXACT (default) or FTZ_FEXP_FUENTES                 */
+  uint32_t hold_inflight; /* a partial batch waits (up to window_us) for more callers
+                           only while at least this many batches are in flight
+                           (default 2; FTZ_HOLD_NEVER: ship at once)                     */
+  uint32_t small_pass;  /* device passes of at most this many proofs run the low-latency
+                           layout of the t' / pair-2 line stage (six lanes per job
+                           instead of one; same bytes); 0 = never                        */
+  uint32_t msm_window_bits; /* MSM planner overrides (ftz_msm_*), 0 = the planner's choice: */
+  uint32_t msm_slot_cap;    /*   window bits c, bucket slot cap T, slots per segment S    */
+  uint32_t msm_seg_slots;
+  uint32_t msm_glv;     /* 1 (default): GLV-split scalars in the MSM; 0: plain 256-bit   */
 } ftz_options;
+#define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
 
 /* pp: json(driver.SerializedPublicParameters{Identifier:"zkatdlog", Raw}) as

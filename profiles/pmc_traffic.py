@@ -34,13 +34,15 @@ def main(fetch_db, write_db):
     if part and comb:
         out["g1"] = kb(("k_g1_part", part[-1])) + kb(("k_g1_combine", comb[-1]))
         out["g1p"] = kb(("k_g1_part", part[0])) + kb(("k_g1_combine", comb[0]))
-    for key, names in (("miller", ("k_miller_n", "k_miller")), ("fexp", ("k_fexp_exact", "k_fexp")),
+    # "3*k" = three launches of k per pass (the final exponentiation's x-powers)
+    for key, names in (("miller", ("k_miller_n", "k_miller")),
+                       ("fexp", ("k_fexp_easy+3*k_fexp_expt+k_fexp_hard", "k_fexp_exact", "k_fexp")),
                        ("g2", ("k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
         for name in names:
-            parts = name.split("+")
-            gs = [grids(n) for n in parts]
+            parts = [(int(p.split("*")[0]), p.split("*")[1]) if "*" in p else (1, p) for p in name.split("+")]
+            gs = [grids(n) for _, n in parts]
             if all(gs):  # the largest grid of each kernel (the verification batch)
-                out[key] = sum(kb((n, g[-1])) for n, g in zip(parts, gs))
+                out[key] = sum(m * kb((n, g[-1])) for (m, n), g in zip(parts, gs))
                 break
     h = grids("k_hash")
     if h:

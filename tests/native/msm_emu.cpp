@@ -70,3 +70,126 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
 extern "C" int emu_g1_sum(size_t n, const uint8_t* points, uint8_t out[64]) {
   return g1_sum_raw((uint32_t)n, points, out) == n ? 0 : -1;
 }
+
+// ---------------------------------------------------------------- CPU baseline
+// bench.py's cpu_msm leg (BASELINE configs[2] on the host): a plain bucket
+// Pippenger with the same GLV split and signed c-bit digits as the device plan,
+// on `threads` host threads -- one contiguous chunk of points per thread, every
+// chunk summed window by window (mixed additions into Jacobian buckets, the
+// running-sum reduction, Horner over the windows), the partials added at the
+// end.  Built with FTS_HOST64 (4 x 64-bit Montgomery) in oracle/cpu.
+#include <thread>
+
+namespace {
+
+g1j msm_chunk(const G1Dev* pts, const G1Dev* phi, const uint32_t (*sc)[8], size_t a, size_t b, uint32_t c) {
+  const uint32_t W = (129 + c - 1) / c, B = 1u << (c - 1);
+  const size_t m = b - a;
+  std::vector<int32_t> dig((size_t)2 * W * m);
+  for (size_t i = 0; i < m; i++) {
+    uint32_t k1[4], k2[4];
+    bool n1, n2;
+    glv_split(sc[a + i], k1, n1, k2, n2);
+    uint32_t x[8] = {k1[0], k1[1], k1[2], k1[3], 0, 0, 0, 0}, y[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
+    uint32_t cx = 0, cy = 0;
+    for (uint32_t w = 0; w < W; w++) {
+      int32_t d1 = msm_digit(x, c, w, cx), d2 = msm_digit(y, c, w, cy);
+      dig[(size_t)w * 2 * m + 2 * i] = n1 ? -d1 : d1;
+      dig[(size_t)w * 2 * m + 2 * i + 1] = n2 ? -d2 : d2;
+    }
+  }
+  std::vector<g1j> bucket(B);
+  g1j acc = jac_inf<fp>();
+  for (int w = (int)W - 1; w >= 0; w--) {
+    for (uint32_t q = 0; q < c; q++) acc = jac_dbl(acc);
+    for (auto& x : bucket) x = jac_inf<fp>();
+    const int32_t* d = &dig[(size_t)w * 2 * m];
+    for (size_t i = 0; i < m; i++)
+      for (int h = 0; h < 2; h++) {
+        int32_t v = d[2 * i + h];
+        if (!v) continue;
+        g1a P = g1_load(h ? phi[a + i] : pts[a + i]);
+        uint32_t u = (uint32_t)(v < 0 ? -v : v);
+        bucket[u - 1] = jac_add_aff(bucket[u - 1], v < 0 ? aff_neg(P) : P);
+      }
+    g1j run = jac_inf<fp>(), sum = jac_inf<fp>();
+    for (int k = (int)B - 1; k >= 0; k--) {
+      run = jac_add(run, bucket[k]);
+      sum = jac_add(sum, run);
+    }
+    acc = jac_add(acc, sum);
+  }
+  return acc;
+}
+
+}  // namespace
+
+// points: n x 64-byte RawBytes, scalars n x 32 bytes big-endian; c = 0: the
+// device planner's window for the chunk size
+extern "C" int emu_msm_cpu(size_t n, const uint8_t* points, const uint8_t* scalars, int threads, uint32_t c,
+                           uint8_t out[64]) {
+  if (threads < 1) threads = 1;
+  std::vector<G1Dev> pts(n), phi(n);
+  std::vector<uint32_t> scal(8 * n);
+  uint32_t(*sc)[8] = reinterpret_cast<uint32_t(*)[8]>(scal.data());
+  auto par = [&](auto&& body) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) th.emplace_back([&, t]() { body((size_t)t); });
+    for (auto& x : th) x.join();
+  };
+  std::vector<int> bad((size_t)threads, 0);
+  par([&](size_t t) {
+    for (size_t i = n * t / threads; i < n * (t + 1) / threads; i++) {
+      uint32_t x[8], y[8], k[8];
+      be32_to_limbs(x, points + 64 * i);
+      be32_to_limbs(y, points + 64 * i + 32);
+      g1a P;
+      P.x = fe_from_int<ModP>(x);
+      P.y = fe_from_int<ModP>(y);
+      P.inf = is_zero(P.x) && is_zero(P.y);
+      if (!g1_on_curve(P)) bad[t] = 1;
+      g1_store(pts[i], P);
+      if (!P.inf) P.x = P.x * fe_const<ModP>(GLV_BETA);
+      g1_store(phi[i], P);
+      be32_to_limbs(k, scalars + 32 * i);
+      fe_to_int(sc[i], fe_from_int<ModR>(k));
+    }
+  });
+  for (int b : bad)
+    if (b) return -1;
+  size_t chunk = (n + threads - 1) / threads;
+  if (!c) c = msm_window_bits(2 * (uint64_t)chunk);
+  std::vector<g1j> part((size_t)threads, jac_inf<fp>());
+  par([&](size_t t) {
+    size_t a = std::min(n, t * chunk), b = std::min(n, a + chunk);
+    if (b > a) part[t] = msm_chunk(pts.data(), phi.data(), sc, a, b, c);
+  });
+  g1j acc = jac_inf<fp>();
+  for (auto& p : part) acc = jac_add(acc, p);
+  g1_to_bytes(out, jac_to_aff(acc));
+  return 0;
+}
+
+// P_i = (offset + i) G for i < n as RawBytes (the bench's known-log points,
+// as ftz_msm_load_gen makes them on the device), on `threads` host threads
+extern "C" int emu_gen_points(size_t n, uint64_t offset, int threads, uint8_t* out) {
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([&, t]() {
+      size_t a = n * t / threads, b = n * (t + 1) / threads;
+      if (b <= a) return;
+      g1a G;
+      G.x = fe_one<ModP>();
+      uint32_t two[8] = {2, 0, 0, 0, 0, 0, 0, 0};
+      G.y = fe_from_int<ModP>(two);
+      G.inf = false;
+      g1j cur = aff_mul_u64(G, offset + a);
+      for (size_t i = a; i < b; i++) {
+        g1_to_bytes(out + 64 * i, jac_to_aff(cur));
+        cur = jac_add_aff(cur, G);
+      }
+    });
+  for (auto& x : th) x.join();
+  return 0;
+}

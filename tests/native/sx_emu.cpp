@@ -170,8 +170,10 @@ int sxe_fexp29(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
   uint32_t s = seed | 1;
   fp12 f = rnd_f12(s);
   f12_to_bytes(out_ref, final_exp(f, variant));
+  std::vector<int32_t> park(6 * FEXP_PARK_SLOTS * 18, (int32_t)0xA5A5A5A5);  // lane planes, stride 6
   run6q([&](const SqH& x) {
-    fp2 g = variant == 1 ? sq_final_exp(x, f12_coef(f, x.k)) : sq_final_exp_exact(x, f12_coef(f, x.k));
+    Park pk{park.data(), (uint32_t)x.k, 6, true};
+    fp2 g = variant == 1 ? sq_final_exp(x, f12_coef(f, x.k), pk) : sq_final_exp_exact(x, f12_coef(f, x.k), pk);
     sx_gt_bytes(out_sx, x.k, g);
   });
   return memcmp(out_sx, out_ref, 384) != 0;

@@ -88,11 +88,12 @@ def test_gpu_msm_explicit(ctx, n):
 
 
 @pytest.mark.gpu
-def test_gpu_msm_without_glv(ctx, monkeypatch):
-    monkeypatch.setenv("FTZ_MSM_GLV", "0")
+def test_gpu_msm_without_glv(golden):
+    import zkatdlog
     pts, ks = rnd_case(300, 901)
     pb, kb = pack(pts, ks)
-    assert ctx.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_glv=0, msm_window_bits=9) as c:
+        assert c.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
 
 
 @pytest.mark.gpu
