@@ -192,11 +192,30 @@ FTS_HD q1j qj_load(const QJDev& d) {
   return p;
 }
 
-// Host: the fixed-base tables of HSk and HRand (tab[b * NYM_TAB_PER_BASE +
+// Auditor owner match (AuditInfo.Match -> IBM/idemix AuditNymEid [EXT]), one
+// lane per token: HAttrs[2]^HashToZr(eid) * HRand^RNymEid == EidNym.Nym.  The
+// job's 128 bytes: SHA-256(eid), RNymEid, EidNym X, EidNym Y (32 bytes BE each,
+// host/idemix.cpp decode_owner_audit).  Returns 1 on a match.
+static constexpr uint32_t EID_JOB_BYTES = 128;
+static constexpr int NYM_TAB_HEID = 2;  // table index of HAttrs[2] (HSk 0, HRand 1)
+FTS_HD uint8_t job_eid(const uint8_t* in, const QDev* tab) {
+  uint32_t h[8], r[8];
+  digest_mod_n(h, in);
+  be32_to_limbs_g(r, in + 32);
+  q1j p = jac_add(q1_fixed_mul(tab + NYM_TAB_HEID * NYM_TAB_PER_BASE, h), q1_fixed_mul(tab + NYM_TAB_PER_BASE, r));
+  q1a e = nym_load(in + 64);  // NewECPbigs: off-curve -> infinity
+  if (is_zero(p.z) || e.inf) return (is_zero(p.z) && e.inf) ? 1 : 0;
+  // X == x Z^2 and Y == y Z^3 (amcl ECP.Equals)
+  fq z2 = sqr(p.z);
+  fq dx = p.x - e.x * z2, dy = p.y - e.y * z2 * p.z;
+  return (is_zero(dx) && is_zero(dy)) ? 1 : 0;
+}
+
+// Host: the fixed-base tables of HSk, HRand and HAttrs[2] (tab[b * NYM_TAB_PER_BASE +
 // w * 255 + d - 1] = d 2^(8w) H_b), built once per issuer key.  Window bases by
 // doublings, entries by mixed additions, one batch inversion per window.
-inline void nym_build_tables(const q1a bases[2], QDev* tab) {
-  for (int b = 0; b < 2; b++) {
+inline void nym_build_tables(const q1a* bases, int nb, QDev* tab) {
+  for (int b = 0; b < nb; b++) {
     q1a bw = bases[b];
     for (int w = 0; w < NYM_WINDOWS; w++) {
       q1j e[255];

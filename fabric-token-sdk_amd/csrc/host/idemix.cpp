@@ -6,6 +6,7 @@
 #include <map>
 
 #include "../dev/idemix.h"
+#include "gojson.h"
 
 namespace ftsh {
 
@@ -326,6 +327,15 @@ std::string parse_ipk(const uint8_t* p, size_t n, IdemixIpk& out) {
       if (pr[1]) y.assign(v[1].p, v[1].p + v[1].len);
       (f.num == 2 ? have_hsk : have_hrand) = true;
     }
+    if (f.num == 4) {  // repeated ECP HAttrs
+      static const PbKind kinds[2] = {PK_BYTES, PK_BYTES};
+      bool pr[2];
+      PbField v[2];
+      e = pb_simple(f.p, f.len, 2, kinds, pr, v);
+      if (!e.empty()) return "issuer public key: " + e;
+      out.hattrs_x.emplace_back(pr[0] ? std::vector<uint8_t>(v[0].p, v[0].p + v[0].len) : std::vector<uint8_t>());
+      out.hattrs_y.emplace_back(pr[1] ? std::vector<uint8_t>(v[1].p, v[1].p + v[1].len) : std::vector<uint8_t>());
+    }
     if (f.num == 10) out.hash.assign(f.p, f.p + f.len);
   }
   if (!have_hsk || !have_hrand) return "issuer public key: some part of the public key is undefined";
@@ -522,6 +532,139 @@ void nym_fill(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDe
       }
     }
   });
+}
+
+}  // namespace ftsh
+
+namespace ftsh {
+
+namespace {
+
+// a singular message field (possibly repeated on the wire: occurrences merge):
+// decode each occurrence's ECP{X = 1, Y = 2}, the last X / Y present wins
+std::string merge_ecp(const PbField& f, std::vector<uint8_t>& x, std::vector<uint8_t>& y, bool& seen) {
+  static const PbKind kinds[2] = {PK_BYTES, PK_BYTES};
+  bool pr[2];
+  PbField v[2];
+  std::string e = pb_simple(f.p, f.len, 2, kinds, pr, v);
+  if (!e.empty()) return e;
+  if (pr[0]) x.assign(v[0].p, v[0].p + v[0].len);
+  if (pr[1]) y.assign(v[1].p, v[1].p + v[1].len);
+  seen = true;
+  return "";
+}
+
+// mathlib Zr UnmarshalJSON on FP256BN_AMCL: D_NIL, D_OK (32 raw bytes, FromBytes
+// reads the first 32), D_ERR (Unmarshal error), D_PANIC (foreign curve / short element)
+DecStatus zr_json(const JDoc& d, int64_t node, uint8_t out[32]) {
+  if (node < 0 || d.at((uint32_t)node).type == J_NULL) return D_NIL;
+  if (d.at((uint32_t)node).type != J_OBJ) return D_ERR;
+  int64_t curve = 0;
+  if (dec_int(d, d.field((uint32_t)node, "curve"), curve) == D_ERR) return D_ERR;
+  std::vector<uint8_t> raw;
+  if (dec_bytes(d, d.field((uint32_t)node, "element"), raw) == D_ERR) return D_ERR;
+  if (curve != FTZ_CURVE_FP256BN_AMCL || raw.size() < 32) return D_PANIC;
+  memcpy(out, raw.data(), 32);
+  return D_OK;
+}
+
+}  // namespace
+
+// crypto/audit/auditor.go:252-274 InspectTokenOwner up to the curve arithmetic
+// of AuditInfo.Match (identity/msp/idemix/audit.go:51-83); see idemix.h
+void decode_owner_audit(const uint8_t* owner, size_t owner_len, const uint8_t* ai, size_t ai_len, size_t n_hattrs,
+                        EidDecoded& out) {
+  out = EidDecoded();
+  auto fail = [&](int code, const std::string& why) {
+    out.code = code;
+    out.why = why;
+  };
+  if (owner_len == 0) return fail(FTZ_ERR_OWNER, "token is a redeem token, cannot inspect ownership");
+  if (ai_len == 0) return fail(FTZ_ERR_OWNER, "failed to inspect owner: owner info is nil");
+  std::string type;
+  const uint8_t* ident;
+  size_t ident_len;
+  if (!raw_owner(owner, owner_len, type, ident, ident_len)) return fail(FTZ_ERR_OWNER, "owner cannot be unwrapped");
+  if (type != "si") return fail(FTZ_ERR_UNSUPPORTED, "script owner: inspected in Go");
+  // GetOwnerMatcher: json.Unmarshal(OwnerInfo, &AuditInfo{}) -- RNymEid and EID of the
+  // embedded *NymEIDAuditData, Attributes [][]byte
+  JDoc d;
+  if (!d.parse(ai, ai_len)) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
+  uint32_t root = d.root();
+  bool nil_ai = d.at(root).type == J_NULL;
+  if (!nil_ai && d.at(root).type != J_OBJ) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
+  DecStatus rs = D_NIL;
+  std::vector<std::vector<uint8_t>> attrs;
+  bool attrs_nil = true;
+  if (!nil_ai) {
+    uint8_t tmp[32];
+    rs = zr_json(d, d.field(root, "RNymEid"), out.rnym);
+    DecStatus es = zr_json(d, d.field(root, "EID"), tmp);
+    if (rs == D_ERR || es == D_ERR) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
+    int64_t an = d.field(root, "Attributes");
+    if (an >= 0 && d.at((uint32_t)an).type != J_NULL) {
+      if (d.at((uint32_t)an).type != J_ARR) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
+      attrs_nil = false;
+      for (uint32_t k = 0; k < d.len((uint32_t)an); k++) {
+        std::vector<uint8_t> b;
+        if (dec_bytes(d, d.elem((uint32_t)an, k), b) == D_ERR) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
+        attrs.push_back(std::move(b));
+      }
+    }
+    if (rs == D_PANIC || es == D_PANIC) return fail(FTZ_ERR_PANIC, "panic: mathlib Zr of another curve");
+  }
+  // Match: the msp protos
+  static const PbKind k_si[2] = {PK_STRING, PK_BYTES};
+  bool pr[5];
+  PbField v[5];
+  if (!pb_simple(ident, ident_len, 2, k_si, pr, v).empty())
+    return fail(FTZ_ERR_AUDIT, "failed to unmarshal to msp.SerializedIdentity{}");
+  const uint8_t* idb = pr[1] ? v[1].p : nullptr;
+  size_t idn = pr[1] ? v[1].len : 0;
+  static const PbKind k_ser[5] = {PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES};
+  if (!pb_simple(idb, idn, 5, k_ser, pr, v).empty())
+    return fail(FTZ_ERR_AUDIT, "could not deserialize a SerializedIdemixIdentity");
+  const uint8_t* proof = pr[4] ? v[4].p : nullptr;
+  size_t proof_len = pr[4] ? v[4].len : 0;
+  // EidNymAuditOpts{EnrollmentID: string(a.Attributes[2])}: index out of range panics
+  if (attrs_nil || attrs.size() <= 2) return fail(FTZ_ERR_PANIC, "panic: index out of range");
+  // AuditNymEid: the idemix Signature proto of the identity's proof
+  std::vector<PbField> fs;
+  std::string pe = pb_scan(proof, proof_len, fs);
+  if (!pe.empty()) return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: " + pe);
+  std::vector<uint8_t> ex, ey;
+  bool eid_nym = false, nym_seen = false;
+  static const PbKind k_nonrev[2] = {PK_ENUM, PK_BYTES};
+  static const PbKind k_ecp2[4] = {PK_BYTES, PK_BYTES, PK_BYTES, PK_BYTES};
+  for (const PbField& f : fs) {
+    if (f.num == 16 || f.wt != 2 || f.num > 18) continue;  // epoch (varint) / unknown / wrong wire type
+    std::vector<uint8_t> dx, dy;
+    bool dummy = false;
+    std::string e;
+    if (f.num == 1 || f.num == 2 || f.num == 3 || f.num == 12) e = merge_ecp(f, dx, dy, dummy);
+    if (f.num == 14) e = pb_simple(f.p, f.len, 4, k_ecp2, pr, v);
+    if (f.num == 17) e = pb_simple(f.p, f.len, 2, k_nonrev, pr, v);
+    if (f.num == 18) {  // EIDNym{Nym = 1 (ECP), ProofSEid = 2}
+      std::vector<PbField> es;
+      e = pb_scan(f.p, f.len, es);
+      for (size_t q = 0; e.empty() && q < es.size(); q++)
+        if (es[q].num == 1 && es[q].wt == 2) e = merge_ecp(es[q], ex, ey, nym_seen);
+      eid_nym = true;
+    }
+    if (!e.empty()) return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: " + e);
+  }
+  if (!eid_nym || !nym_seen) return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: no EidNym provided");
+  if (n_hattrs <= 2)
+    return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: could not access H_a_eid in array");
+  if (nil_ai || rs == D_NIL) return fail(FTZ_ERR_PANIC, "panic: nil RNymEid");
+  if (ex.size() < 32 || ey.size() < 32) return fail(FTZ_ERR_PANIC, "panic: index out of range");
+  memcpy(out.nym_x, ex.data(), 32);
+  memcpy(out.nym_y, ey.data(), 32);
+  // HashToZr(EnrollmentID): SHA-256 read big-endian, reduced mod n on the device
+  fts::Sha256 h;
+  h.init();
+  h.update(attrs[2].data(), attrs[2].size());
+  h.final(out.eid_digest);
 }
 
 }  // namespace ftsh

@@ -37,6 +37,7 @@ bool utf8_valid(const uint8_t* p, size_t n);
 
 struct IdemixIpk {
   std::vector<uint8_t> hsk_x, hsk_y, hrand_x, hrand_y;  // ECP coordinates (FromBytes: first 32 bytes)
+  std::vector<std::vector<uint8_t>> hattrs_x, hattrs_y; // HAttrs[i] (an absent coordinate: empty)
   std::vector<uint8_t> hash;                            // IssuerPublicKey.Hash
 };
 // proto IssuerPublicKey: "" or the error
@@ -56,6 +57,21 @@ void nym_glv_split(const uint8_t k[32], uint32_t out[12]);
 // GetOwnerVerifier(owner) then the signature unmarshal of Verify(msg, sigma).
 void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_t* sig, size_t sig_len,
                             NymDecoded& out);
+
+// Auditor owner match (crypto/audit/auditor.go:252-274 InspectTokenOwner ->
+// idemix DeserializeAuditInfo + AuditInfo.Match, identity/msp/idemix/
+// audit.go:32-83): everything up to the curve arithmetic.  [EXT] IBM/idemix
+// AuditNymEid: Nym_eid = HAttrs[2]^HashToZr(Attributes[2]) * HRand^RNymEid must
+// equal the identity proof's EidNym.Nym (idemix Signature proto field 18).
+struct EidDecoded {
+  int code = 0;             // 0 = go to the device; else FTZ_ERR_OWNER / _AUDIT / _UNSUPPORTED / _PANIC
+  std::string why;
+  uint8_t eid_digest[32];   // SHA-256(EnrollmentID) (HashToZr before the reduction mod n)
+  uint8_t rnym[32];         // RNymEid (FromBytes: raw, unreduced)
+  uint8_t nym_x[32], nym_y[32];  // EidNym.Nym X, Y (first 32 bytes)
+};
+void decode_owner_audit(const uint8_t* owner, size_t owner_len, const uint8_t* audit_info, size_t audit_info_len,
+                        size_t n_hattrs, EidDecoded& out);
 
 // Blob of one device pass over the signatures s[idx[0..m)] (all decoded with
 // code 0): the NymJob array at offset 0, then per job the six integers and

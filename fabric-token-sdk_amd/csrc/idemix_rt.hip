@@ -25,7 +25,11 @@ struct NymSlot {
 struct ftz_idemix {
   ftz_ctx* ctx = nullptr;
   uint8_t hash_slot[32] = {};  // copy(proofData[index:], ipk.Hash) into the 32-byte slot
-  DBuf<QDev> tab;              // HSk and HRand fixed-base tables
+  DBuf<QDev> tab;              // HSk, HRand (and HAttrs[2]) fixed-base tables
+  size_t n_hattrs = 0;         // len(IssuerPublicKey.HAttrs)
+  bool heid_ok = false;        // HAttrs[2] decoded on the curve (its table exists)
+  PinnedMem h_eid, h_eid_ok;   // auditor owner match (ftz_audit_owners)
+  DevMem d_eid, d_eid_ok;
   std::mutex mu;               // one call on the device at a time
   WorkPool* pool = nullptr;    // host decoding / layout threads
   NymSlot slot[2];             // chunk k+1 is decoded and laid out while chunk k runs
@@ -47,12 +51,15 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
   ftsh::IdemixIpk k;
   std::string e = ftsh::parse_ipk(ipk, ipk_len, k);
   if (!e.empty()) return set_err(FTZ_E_PP, e);
-  q1a bases[2];
+  q1a bases[3];
   if (!nym_point_from_be(k.hsk_x.data(), k.hsk_y.data(), bases[0]) ||
       !nym_point_from_be(k.hrand_x.data(), k.hrand_y.data(), bases[1]))
     return set_err(FTZ_E_PP, "issuer public key: HSk / HRand not on FP256BN");
-  std::vector<QDev> tab(2 * NYM_TAB_PER_BASE);
-  nym_build_tables(bases, tab.data());
+  // HAttrs[2] (the enrollment-id base of the auditor's EidNym check)
+  bool heid = k.hattrs_x.size() > 2 && k.hattrs_x[2].size() >= 32 && k.hattrs_y[2].size() >= 32 &&
+              nym_point_from_be(k.hattrs_x[2].data(), k.hattrs_y[2].data(), bases[2]);
+  std::vector<QDev> tab((heid ? 3 : 2) * NYM_TAB_PER_BASE);
+  nym_build_tables(bases, heid ? 3 : 2, tab.data());
   HC(hipSetDevice(ctx->device));
   ftz_idemix* ix = new ftz_idemix();
   ix->ctx = ctx;
@@ -65,6 +72,8 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
     }
   }
   memcpy(ix->hash_slot, k.hash.data(), k.hash.size() < 32 ? k.hash.size() : 32);
+  ix->n_hattrs = k.hattrs_x.size();
+  ix->heid_ok = heid;
   hipError_t he = ix->tab.upload(tab, ctx->stream);
   if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
   if (he != hipSuccess) {
@@ -159,4 +168,50 @@ extern "C" int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_o
     if (rc == FTZ_SUCCESS) rc = r2;
   }
   return rc;
+}
+
+// Auditor owner match: decode on the pool, one device pass over the tokens
+// whose check reaches the curve arithmetic
+extern "C" int ftz_audit_owners(ftz_idemix* ix, size_t n, const ftz_owner_audit* it, int32_t* codes) {
+  if (!ix || (n && (!it || !codes))) return set_err(FTZ_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if ((!it[i].owner && it[i].owner_len) || (!it[i].audit_info && it[i].audit_info_len))
+      return set_err(FTZ_E_INVALID, "null buffer with non-zero length");
+  if (n > (1u << 26)) return set_err(FTZ_E_INVALID, "too many tokens in one call");
+  if (ix->n_hattrs > 2 && !ix->heid_ok) return set_err(FTZ_E_PP, "issuer public key: HAttrs[2] not on FP256BN");
+  std::vector<ftsh::EidDecoded> dec(n);
+  ix->pool->run((n + 63) / 64, [&](size_t p) {
+    for (size_t i = p * 64; i < n && i < (p + 1) * 64; i++)
+      ftsh::decode_owner_audit(it[i].owner, it[i].owner_len, it[i].audit_info, it[i].audit_info_len, ix->n_hattrs,
+                               dec[i]);
+  });
+  std::vector<uint32_t> idx;
+  for (size_t i = 0; i < n; i++) {
+    codes[i] = dec[i].code;
+    if (dec[i].code == 0) idx.push_back((uint32_t)i);
+  }
+  if (idx.empty()) return FTZ_SUCCESS;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  HC(hipSetDevice(ix->ctx->device));
+  size_t m = idx.size();
+  HC(ix->h_eid.reserve(m * EID_JOB_BYTES));
+  HC(ix->d_eid.reserve(m * EID_JOB_BYTES));
+  HC(ix->h_eid_ok.reserve(m));
+  HC(ix->d_eid_ok.reserve(m));
+  for (size_t k = 0; k < m; k++) {
+    const ftsh::EidDecoded& d = dec[idx[k]];
+    uint8_t* o = ix->h_eid.p + k * EID_JOB_BYTES;
+    memcpy(o, d.eid_digest, 32);
+    memcpy(o + 32, d.rnym, 32);
+    memcpy(o + 64, d.nym_x, 32);
+    memcpy(o + 96, d.nym_y, 32);
+  }
+  hipStream_t st = ix->slot[0].st;
+  HC(hipMemcpyAsync(ix->d_eid.p, ix->h_eid.p, m * EID_JOB_BYTES, hipMemcpyHostToDevice, st));
+  k_eid<<<(uint32_t)((m + 63) / 64), 64, 0, st>>>(ix->d_eid.p, (uint32_t)m, ix->tab.p, ix->d_eid_ok.p);
+  HC(hipGetLastError());
+  HC(hipMemcpyAsync(ix->h_eid_ok.p, ix->d_eid_ok.p, m, hipMemcpyDeviceToHost, st));
+  HC(hipStreamSynchronize(st));
+  for (size_t k = 0; k < m; k++) codes[idx[k]] = ix->h_eid_ok.p[k] ? FTZ_OK : FTZ_ERR_AUDIT;
+  return FTZ_SUCCESS;
 }

@@ -20,3 +20,10 @@ __global__ void __launch_bounds__(64) k_nym_fin(const NymJob* jobs, uint32_t n, 
                   jac_add(qj_load(part[2 * n + i]), qj_load(part[3 * n + i])));
   ok[i] = job_nym_fin(jobs[i], blob, t);
 }
+
+// Auditor owner match (dev/idemix.h job_eid): one lane per token
+__global__ void __launch_bounds__(64) k_eid(const uint8_t* in, uint32_t n, const QDev* tab, uint8_t* ok) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  ok[i] = job_eid(in + (size_t)i * EID_JOB_BYTES, tab);
+}

@@ -35,8 +35,9 @@ extern "C" int ftz_callers_run(ftz_ctx* ctx, const ftz_transfer* pool, const int
   std::atomic<bool> err_set{false};
   std::atomic<int> ready{0};
   std::atomic<bool> go{false};
-  const Clock::time_point t_start = Clock::now() + std::chrono::milliseconds(200);
-  const Clock::time_point t_end = t_start + std::chrono::microseconds((int64_t)(seconds * 1e6));
+  // the window opens once every caller thread exists (starting thousands of
+  // threads takes longer than the window itself)
+  Clock::time_point t_start, t_end;
   std::vector<std::thread> th;
   th.reserve((size_t)callers);
   for (int c = 0; c < callers; c++) {
@@ -64,6 +65,8 @@ extern "C" int ftz_callers_run(ftz_ctx* ctx, const ftz_transfer* pool, const int
     });
   }
   while (ready.load() < callers) std::this_thread::yield();
+  t_start = Clock::now() + std::chrono::milliseconds(50);
+  t_end = t_start + std::chrono::microseconds((int64_t)(seconds * 1e6));
   if (getenv("FTZ_CALLERS_DEBUG"))
     fprintf(stderr, "callers: %d ready, %.1f ms to start, window %.1f ms\n", callers,
             std::chrono::duration<double, std::milli>(t_start - Clock::now()).count(),

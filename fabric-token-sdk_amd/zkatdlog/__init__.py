@@ -514,6 +514,16 @@ class Idemix:
         _check(self._lib.ftz_verify_owner_signatures(self._h, n, arr, codes), self._lib)
         return list(codes[:n])
 
+    def audit_owners(self, items):
+        """auditor owner inspection (InspectTokenOwner, crypto/audit/auditor.go:252-274):
+        items (token Owner bytes, OwnerInfo = json(AuditInfo)) -> FTZ codes (0 = the owner
+        matches its audit info; FTZ_ERR_AUDIT = Match failed)"""
+        items = list(items)
+        arr, keep = _abi.pack_owner_audits(items)
+        codes = (ctypes.c_int32 * max(len(items), 1))()
+        _check(self._lib.ftz_audit_owners(self._h, len(items), arr, codes), self._lib)
+        return list(codes[:len(items)])
+
     def owner_verifier(self, owner):
         """GetOwnerVerifier(tok.Owner) (validator_transfer.go:66)"""
         return OwnerVerifier(self, owner)

@@ -123,7 +123,8 @@ def prove_distinct(ctx, n, tag=b"bench", bases=None):
     bases = bases or witness_bases()
     sel = np.arange(n) % len(bases)
     wptr, wn, wkeep = _abi.pack_transfer_witnesses_tiled(bases, sel, seeds(n, tag))
-    blob, offs, codes = ctx.prove_packed("transfer", wptr, wn)
+    # proof size grows with the range proof's digits (2 outputs x exponent membership proofs)
+    blob, offs, codes = ctx.prove_packed("transfer", wptr, wn, bytes_per_proof=4096 + 4096 * ctx.exponent)
     if not (codes == 0).all():
         raise RuntimeError("prover rejected a bench witness")
     ins = np.frombuffer(b"".join(b["inputs"] for b in bases), dtype=np.uint8)

@@ -280,6 +280,7 @@ int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz
 #define FTZ_ERR_OWNER 9        /* the owner identity does not deserialize (RawOwner, idemix identity, nym) */
 #define FTZ_ERR_SIGNATURE 10   /* the signature does not unmarshal, or "pseudonym signature invalid"       */
 #define FTZ_ERR_UNSUPPORTED 11 /* owner type verified in Go (an HTLC script owner)                          */
+#define FTZ_ERR_AUDIT 12       /* the token owner does not match its audit info (AuditInfo.Match failed)    */
 #define FTZ_CURVE_FP256BN_AMCL 0
 typedef struct ftz_idemix ftz_idemix;
 typedef struct {
@@ -294,6 +295,24 @@ int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curv
 /* codes[i] = FTZ_OK, FTZ_ERR_OWNER, FTZ_ERR_SIGNATURE or FTZ_ERR_UNSUPPORTED; thread-safe */
 int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_owner_sig* s, int32_t* codes);
 void ftz_idemix_destroy(ftz_idemix* ix);
+
+/* Auditor owner inspection (the owner half of
+ * crypto/audit/auditor.go:208-274 InspectOutput / InspectInputs ->
+ * InspectTokenOwner): the idemix matcher of the token's OwnerInfo
+ * (identity/msp/idemix/audit.go:32-46 DeserializeAuditInfo, Go encoding/json)
+ * checks the owner identity (audit.go:51-83 AuditInfo.Match ->
+ * CSP.Verify(EidNymAuditOpts) -> IBM/idemix AuditNymEid [EXT]:
+ * HAttrs[2]^HashToZr(Attributes[2]) * HRand^RNymEid == the identity proof's
+ * EidNym).  codes: FTZ_OK, FTZ_ERR_OWNER (redeem token, empty OwnerInfo,
+ * undecodable RawOwner or audit info), FTZ_ERR_AUDIT (Match failed),
+ * FTZ_ERR_UNSUPPORTED (a script owner: inspected in Go), FTZ_ERR_PANIC. */
+typedef struct {
+  const uint8_t* owner;      /* token.Token.Owner: asn1(RawOwner{Type, Identity}) */
+  size_t owner_len;
+  const uint8_t* audit_info; /* the owner's OwnerInfo: json(AuditInfo)           */
+  size_t audit_info_len;
+} ftz_owner_audit;
+int ftz_audit_owners(ftz_idemix* ix, size_t n, const ftz_owner_audit* items, int32_t* codes);
 
 /* ---- standalone BN254 G1 multi-scalar multiplication (BASELINE configs[2]):
  * out = sum_i k_i P_i as 64-byte gnark RawBytes.  Points: n x 64-byte

@@ -604,3 +604,131 @@ def serialize_idemix_identity(nym, mspid="idemix", ou=b"", role=b"", proof=b"", 
     y = nym[1].to_bytes(32, "big") if nymy is None else nymy
     inner = pb_field(1, 2, x) + pb_field(2, 2, y) + pb_field(3, 2, ou) + pb_field(4, 2, role) + pb_field(5, 2, proof)
     return pb_field(1, 2, mspid.encode()) + pb_field(2, 2, inner)
+
+
+# ------------------------------------------------------------------ auditor: owner match
+# crypto/audit/auditor.go:252-274 InspectTokenOwner -> des.GetOwnerMatcher(
+# token.Owner.OwnerInfo) = idemix DeserializeAuditInfo (identity/msp/idemix/
+# audit.go:32-46, Go encoding/json) -> AuditInfo.Match(RawOwner.Identity)
+# (audit.go:51-83): the msp protos, then CSP.Verify(ipk, serialized.Proof, nil,
+# EidNymAuditOpts{EidIndex 2, EnrollmentID string(Attributes[2]), RNymEid}).
+# [EXT] IBM/idemix (not vendored), restated:
+#   AuditNymEid: sig = proto Signature(serialized.Proof); EidNym must be present;
+#   Nym_eid = HAttrs[2]^HashToZr(EnrollmentID) * HRand^RNymEid; match iff
+#   Nym_eid == sig.EidNym.Nym (ECP from its X, Y bytes as NewECPbigs reads them).
+#   Signature proto: 1 a_prime, 2 a_bar, 3 b_prime (ECP), 4..9 proof bytes,
+#   10 repeated proof_s_attrs, 11 nonce, 12 nym (ECP), 13 proof_s_r_nym,
+#   14 revocation_epoch_pk (ECP2), 15 revocation_pk_sig, 16 epoch (int64),
+#   17 non_revocation_proof {1 revocation_alg, 2 non_revocation_proof},
+#   18 eid_nym {1 nym (ECP), 2 proof_s_eid}.
+#   AuditInfo JSON: {"RNymEid": Zr, "EID": Zr (embedded *NymEIDAuditData),
+#   "Attributes": [][]byte}; mathlib Zr as {"curve": FP256BN_AMCL = 0,
+#   "element": base64(>= 32 bytes)}, another curve id panics on use.
+ERR_AUDIT = 12   # Match failed: the owner does not match the audit info
+EID_INDEX = 2
+NONREV_S = {1: "enum", 2: "bytes"}
+EIDNYM_S = {1: ("msg", ECP_S), 2: "bytes"}
+SIGNATURE_S = {1: ("msg", ECP_S), 2: ("msg", ECP_S), 3: ("msg", ECP_S), 4: "bytes", 5: "bytes", 6: "bytes",
+               7: "bytes", 8: "bytes", 9: "bytes", 10: "*bytes", 11: "bytes", 12: ("msg", ECP_S), 13: "bytes",
+               14: ("msg", ECP2_S), 15: "bytes", 16: "enum", 17: ("msg", NONREV_S), 18: ("msg", EIDNYM_S)}
+FP256BN_CURVE_ID = 0
+
+
+class Panic(Exception):
+    pass
+
+
+def _zr_json(v):
+    """mathlib Zr UnmarshalJSON on the FP256BN curve: None for JSON null / absent,
+    "panic" for another curve id or an element shorter than 32 bytes."""
+    from . import gojson as J
+    if v is None or v[0] == "null":
+        return None
+    curve, raw = J.dec_elem(v)
+    if curve != FP256BN_CURVE_ID or raw is None or len(raw) < 32:
+        return "panic"
+    return int.from_bytes(raw[:32], "big")
+
+
+def audit_info_decode(raw):
+    """DeserializeAuditInfo: (rnym_eid, attributes); raises GoJSONError (any
+    decoding error, first) or Panic (a Zr of another curve / too short)."""
+    from . import gojson as J
+    v = J.parse(raw)
+    if v[0] == "null":
+        return None, None
+    if v[0] != "obj":
+        raise J.GoJSONError("cannot unmarshal into AuditInfo")
+    rnym = _zr_json(J.field(v, "RNymEid"))
+    eid = _zr_json(J.field(v, "EID"))
+    attrs = J.dec_list(J.field(v, "Attributes"), J.dec_bytes)
+    if "panic" in (rnym, eid):
+        raise Panic("mathlib Zr of another curve")
+    return rnym, attrs
+
+
+def audit_owner_match(ipk, owner, audit_info):
+    """InspectTokenOwner for one token: (code, text).  owner = token.Owner
+    (ASN.1 RawOwner), audit_info = the owner's OwnerInfo (AuditInfo JSON)."""
+    from . import gojson as J
+    if len(owner) == 0:
+        return ERR_OWNER, "token is a redeem token, cannot inspect ownership"
+    if len(audit_info) == 0:
+        return ERR_OWNER, "failed to inspect owner: owner info is nil"
+    try:
+        typ, ident = raw_owner_decode(owner)
+    except RQ.Asn1Error:
+        return ERR_OWNER, "owner cannot be unwrapped"
+    if typ != "si":
+        return ERR_UNSUPPORTED, "script owner: inspected in Go"
+    try:
+        rnym, attrs = audit_info_decode(audit_info)
+    except J.GoJSONError:
+        return ERR_OWNER, "failed to get owner matcher"
+    except Panic as e:
+        return ERR_PANIC, "panic: %s" % e
+    # Match (audit.go:51-83)
+    try:
+        si = pb_decode(ident, SERIALIZED_IDENTITY_S)
+    except PbError:
+        return ERR_AUDIT, "failed to unmarshal to msp.SerializedIdentity{}"
+    try:
+        ser = pb_decode(si.get(2, b""), SERIALIZED_IDEMIX_S)
+    except PbError:
+        return ERR_AUDIT, "could not deserialize a SerializedIdemixIdentity"
+    if attrs is None or len(attrs) <= EID_INDEX:
+        return ERR_PANIC, "panic: index out of range"
+    eid = attrs[EID_INDEX] or b""
+    try:
+        sig = pb_decode(ser.get(5, b""), SIGNATURE_S)
+    except PbError as e:
+        return ERR_AUDIT, "error while verifying the nym eid: %s" % e
+    en = sig.get(18)
+    if en is None or en.get(1) is None:
+        return ERR_AUDIT, "error while verifying the nym eid: no EidNym provided"
+    if len(ipk.hattrs) <= EID_INDEX:
+        return ERR_AUDIT, "error while verifying the nym eid: could not access H_a_eid in array"
+    if rnym is None:
+        return ERR_PANIC, "panic: nil RNymEid"
+    try:
+        nym_eid = ecp_from_bytes(en[1].get(1), en[1].get(2))
+    except IndexError:
+        return ERR_PANIC, "panic: index out of range"
+    want = add(mul(ipk.hattrs[EID_INDEX], hash_to_zr(eid)), mul(ipk.hrand, rnym))
+    if want != nym_eid:
+        return ERR_AUDIT, "error while verifying the nym eid: eid nym does not match"
+    return OK, ""
+
+
+def audit_info_encode(rnym, eid_zr, attrs, curve=FP256BN_CURVE_ID):
+    """json.Marshal(AuditInfo) for fixtures (Zr as 32-byte big-endian elements)."""
+    from . import gojson as J
+    z = (lambda x: "null" if x is None else J.enc_elem(x.to_bytes(32, "big"), curve))
+    return J.enc_struct([("RNymEid", z(rnym)), ("EID", z(eid_zr)),
+                         ("Attributes", J.enc_list(attrs, J.enc_bytes))]).encode()
+
+
+def signature_with_eid_nym(nym_eid, extra=b""):
+    """an idemix Signature proto carrying eid_nym (and `extra` encoded fields) for fixtures"""
+    ecp = pb_field(1, 2, nym_eid[0].to_bytes(32, "big")) + pb_field(2, 2, nym_eid[1].to_bytes(32, "big"))
+    return extra + pb_field(18, 2, pb_field(1, 2, ecp) + pb_field(2, 2, bytes(32)))

@@ -180,6 +180,58 @@ def main():
             bench.append({"owner": owner(identity(nym)).hex(), "msg_seed": seed.hex(), "msg_len": len(msg),
                           "sig": sig.hex()})
 
+    # auditor owner match (ftz_audit_owners): AuditInfo JSON + owner identities whose
+    # proof carries an EidNym, with the oracle's verdicts (idemix.audit_owner_match)
+    arng = random.Random(0xA0D1)
+    eid = pins_eid = sc[5]
+    audits = []
+
+    def aadd(name, own, ai):
+        code, text = I.audit_owner_match(ipk, own, ai)
+        audits.append({"name": name, "owner": own.hex(), "audit_info": ai.hex(), "expect": code, "text": text})
+    attrs = [sc[3], b"role", eid, b"rh"]
+    for u in range(3):
+        r_eid = arng.randrange(1, I.N)
+        ne = I.add(I.mul(ipk.hattrs[2], I.hash_to_zr(eid)), I.mul(ipk.hrand, r_eid))
+        own = owner(identity(users[u][1], proof=I.signature_with_eid_nym(ne)))
+        aadd("eid_match_%d" % u, own, I.audit_info_encode(r_eid, I.hash_to_zr(eid), attrs))
+    r_eid = arng.randrange(1, I.N)
+    ne = I.add(I.mul(ipk.hattrs[2], I.hash_to_zr(eid)), I.mul(ipk.hrand, r_eid))
+    good_proof = I.signature_with_eid_nym(ne)
+    own = owner(identity(nym, proof=good_proof))
+    ai = I.audit_info_encode(r_eid, I.hash_to_zr(eid), attrs)
+    r_u = arng.randrange(1, (1 << 256) - I.N)
+    ne_u = I.add(I.mul(ipk.hattrs[2], I.hash_to_zr(eid)), I.mul(ipk.hrand, r_u))
+    aadd("eid_match_unreduced_rnym", owner(identity(nym, proof=I.signature_with_eid_nym(ne_u))),
+         I.audit_info_encode(r_u + I.N, 0, attrs))
+    aadd("eid_other_enrollment_id", own, I.audit_info_encode(r_eid, 0, [attrs[0], attrs[1], b"mallory", attrs[3]]))
+    aadd("eid_wrong_rnym", own, I.audit_info_encode(r_eid + 1, 0, attrs))
+    aadd("eid_nym_of_other_identity", owner(identity(nym, proof=I.signature_with_eid_nym(I.mul(ipk.hrand, 5)))), ai)
+    off = (ne[0], (ne[1] + 1) % I.Q)
+    aadd("eid_nym_off_curve", owner(identity(nym, proof=I.signature_with_eid_nym(off))), ai)
+    full = (I.pb_field(1, 2, I.pb_field(1, 2, bytes(32)) + I.pb_field(2, 2, bytes(32))) + I.pb_field(4, 2, bytes(32))
+            + I.pb_field(10, 2, b"a") + I.pb_field(10, 2, b"b") + I.pb_field(16, 0, 7)
+            + I.pb_field(17, 2, I.pb_field(1, 0, 1) + I.pb_field(2, 2, b"x")))
+    aadd("eid_full_signature_proto", owner(identity(nym, proof=I.signature_with_eid_nym(ne, extra=full))), ai)
+    aadd("eid_no_eid_nym", owner(identity(nym, proof=full)), ai)
+    aadd("eid_bad_signature_proto", owner(identity(nym, proof=b"\x0a\x05ab")), ai)
+    aadd("eid_bad_ecp_inside_signature", owner(identity(nym, proof=I.pb_field(1, 2, b"\x0a\x09") + good_proof)), ai)
+    aadd("eid_short_nym_coordinate", owner(identity(nym, proof=I.pb_field(18, 2, I.pb_field(1, 2, I.pb_field(1, 2, b"\x01" * 31) + I.pb_field(2, 2, bytes(32)))))), ai)
+    aadd("eid_attributes_too_short_panics", own, I.audit_info_encode(r_eid, 0, attrs[:2]))
+    aadd("eid_null_audit_info_panics", own, b"null")
+    aadd("eid_nil_rnym_panics", own, I.audit_info_encode(None, 0, attrs))
+    aadd("eid_foreign_curve_panics", own, I.audit_info_encode(r_eid, 0, attrs, curve=1))
+    aadd("audit_info_not_json", own, b"{oops")
+    aadd("audit_info_array", own, b"[]")
+    aadd("audit_info_bad_attribute", own, ai.replace(b'"Attributes":[', b'"Attributes":[1,'))
+    aadd("audit_info_empty", own, b"")
+    aadd("redeem_token", b"", ai)
+    aadd("owner_not_asn1", b"\x30\x05", ai)
+    aadd("htlc_owner_script", owner(b"script", typ=b"htlc"), ai)
+    aadd("identity_not_proto", owner(b"\x0a\xff"), ai)
+    aadd("idemix_identity_not_proto", owner(I.pb_field(1, 2, b"idemix") + I.pb_field(2, 2, b"\x0a\xff")), ai)
+    aadd("audit_info_lowercase_keys", own, ai.replace(b'"RNymEid"', b'"rnymeid"').replace(b'"Attributes"', b'"attributes"'))
+
     out = {
         "comment": "idemix owner signatures on FP256BN (SURVEY 8(f) row 3); made by make_idemix.py",
         "ext_assumptions": {
@@ -204,6 +256,7 @@ def main():
             "attr_strings": {"ou": sc[3].decode(), "enrollment_id": sc[5].decode()},
         },
         "cases": cases,
+        "audit_cases": audits,
         "bench": bench,
     }
     path = os.path.join(HERE, "idemix_golden.json")
