@@ -185,7 +185,7 @@ def cpu_baselines(pp_a, job_a, pp_b, job_b, bases_a, gpu_msm20):
                               "restatement of the verifier (oracle/cpu: host build of the planner + job code with the "
                               "GPU path's algorithms -- bilinear membership rewrite, GLV, fixed-base tables -- and "
                               "4x64-bit Montgomery products) on all %d cores of the process affinity (nproc %d); "
-                              "median of 3 runs after a warm-up: %.2f s" % (n, cores, aff, nproc, med)}
+                              "median of 3 runs after a warm-up: %.2f s" % (n, cores, nproc, med)}
         if job_b is not None:
             r, med, n = cpu_verify(pp_b, job_b, cores, max(256, 8 * cores))
             out["verify_pp_b_" + label] = {"value": round(r, 2), "unit": "transfers/s", "cores": cores,
@@ -216,13 +216,19 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     """BASELINE configs[2]: latency of one BN254 G1 MSM of 2^lg points resident
     in HBM (P_i = (i + 1) G generated on the device, random 256-bit scalars),
     median wall-clock of `reps` synchronous runs after one warm-up; the result
-    must be identical on every run (tests/test_msm.py checks it bit-exactly)."""
+    must be identical on every run (tests/test_msm.py checks it bit-exactly).
+    With ctx.options["msm_precompute"] the resident-point mode (window multiples
+    stored at load, one bucket set, no Horner chain); load_s is the staging
+    time including that precomputation."""
     import numpy as np
 
     import zkatdlog
     n = 1 << lg
+    pre = bool(ctx.options.get("msm_precompute"))
     scal = np.random.default_rng(seed + lg).bytes(32 * n)
+    t_load = time.perf_counter()
     m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
+    t_load = time.perf_counter() - t_load
     try:
         first = m.run()
         wall, dev = [], []
@@ -242,15 +248,16 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     # per bucket in the running-sum reduction, in Montgomery products M
     c = info["window_bits"]
     windows, nv, buckets = (129 + c - 1) // c, 2 * n, 1 << (c - 1)
-    m_prod = windows * nv * 11 + windows * 2 * buckets * 16
+    m_prod = windows * nv * 11 + (1 if pre else windows) * 2 * buckets * 16
     peak = madpeak(ctx.device)
     ach = m_prod * MAD_PER_M / (dev[reps // 2] * 1e-3)
     return {"n": n, "ms": round(wall[reps // 2], 3), "device_ms": round(dev[reps // 2], 3),
-            "window_bits": c, "result": first.hex(),
+            "window_bits": c, "mode": "resident-point" if pre else "variable-base", "load_s": round(t_load, 3),
+            "result": first.hex(),
             "roofline": {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),
                          "unit": "TMAD/s", "frac": round(ach / peak, 4), "m_products": m_prod,
-                         "note": "W x 2n mixed adds x 11 M + W x 2 x 2^(c-1) Jacobian adds x 16 M, "
-                                 "136 MAD per M, over the device time"}}
+                         "note": "W x 2n mixed adds x 11 M + (W, or 1 resident-point) x 2 x 2^(c-1) Jacobian "
+                                 "adds x 16 M, 136 MAD per M, over the device time"}}
 
 
 def msm_split_latency(ctx, lg, rank, world, dist, reps=5, seed=7):
@@ -656,6 +663,14 @@ def main():
             extras["roofline"] = roofline(ctx, job, db, local, value, keep_serial=args.serial)
             extras["owner_signatures"] = owner_signatures(ctx)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
+        msm_res = None
+        if args.msm and not args.no_extras:  # resident-point mode, its own context (ftz_options differ)
+            import zkatdlog
+            with zkatdlog.Context(pp_json, device=local, msm_precompute=1) as cpre:
+                msm_res = [msm_latency(cpre, int(x)) for x in args.msm.split(",") if x]
+                for r in msm_res:  # same points and scalars: the same sum
+                    plain = next((q for q in msm if q["n"] == r["n"]), None)
+                    r["matches_variable_base"] = plain is None or plain["result"] == r["result"]
         msm20 = next((r["ms"] for r in msm if r["n"] == 1 << 20), None)
         msm20_bytes = next((bytes.fromhex(r["result"]) for r in msm if r["n"] == 1 << 20), None)
         prover = None if args.no_prover else prover_bench(ctx, args.batch, min(args.steps, 16))
@@ -689,7 +704,7 @@ def main():
                        "parse_rate_transfers_per_s": round(est["proofs"] / max(1e-9, est["plan_ms"] * 1e-3), 1),
                        "planning_threads": ctx.options["threads"]},
             "roofline": extras.pop("roofline", None), "cpu_baseline": cpu,
-            "msm_2^20_latency_ms": msm20, "msm": msm, "msm_split": msm_split, "prover": prover, "pp_b": ppb,
+            "msm_2^20_latency_ms": msm20, "msm": msm, "msm_resident": msm_res, "msm_split": msm_split, "prover": prover, "pp_b": ppb,
         }
         line.update(extras)
         print(json.dumps(line), flush=True)

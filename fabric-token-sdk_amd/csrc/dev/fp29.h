@@ -354,6 +354,40 @@ FTS_HD j29 j29_madd(const j29& p, const f29& x2, const f29& y2) {
   return {X3, Y3, Z3, false};
 }
 
+// add-2007-bl full Jacobian addition p + q: 11M + 5S, inputs normalised with
+// B <= 2 (products or f29_reduce outputs).  Same exceptional handling as
+// j29_madd: Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H = 2 Z1 Z2 H vanishes iff H does.
+FTS_HD j29 j29_add(const j29& p, const j29& q) {
+  if (p.inf) return q;
+  if (q.inf) return p;
+  f29 Z1Z1 = f29_sqr(p.z);                         // (2, 1)
+  f29 Z2Z2 = f29_sqr(q.z);                         // (2, 1)
+  f29 U1 = f29_mul(p.x, Z2Z2);                     // 2 x 2: (2, 1)
+  f29 U2 = f29_mul(q.x, Z1Z1);                     // (2, 1)
+  f29 S1 = f29_mul(p.y, f29_mul(q.z, Z2Z2));       // (2, 1)
+  f29 S2 = f29_mul(q.y, f29_mul(p.z, Z1Z1));       // (2, 1)
+  f29 H = f29_norm(f29_sub(U2, U1));               // (4, 1)
+  f29 H2 = f29_norm(f29_add(H, H));                // (8, 1)
+  f29 I = f29_sqr(H2);                             // 64: (2, 1)
+  f29 J = f29_mul(H, I);                           // 8: (2, 1)
+  f29 rr = f29_sub(S2, S1);                        // (4, 2)
+  f29 r2 = f29_norm(f29_add(rr, rr));              // (8, 1)
+  f29 V = f29_mul(U1, I);                          // 4: (2, 1)
+  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sub(f29_sqr(r2), J), V), V));  // 64 -> (8, 4) -> (1.5, 1)
+  f29 Y3a = f29_mul(r2, f29_norm(f29_sub(V, X3))); // 8 x 3.5: (2, 1)
+  f29 SJ = f29_mul(S1, J);                         // (2, 1)
+  f29 Y3 = f29_reduce(f29_sub(f29_sub(Y3a, SJ), SJ));              // (6, 3) -> (1.5, 1)
+  f29 ZZ = f29_sqr(f29_norm(f29_add(p.z, q.z)));   // 16: (2, 1)
+  f29 Z3 = f29_reduce(f29_mul(f29_norm(f29_sub(f29_sub(ZZ, Z1Z1), Z2Z2)), H));  // 6 x 4: (2, 1) -> (1.5, 1)
+  if (f29_reduced_zero(Z3)) {
+    if (f29_is_zero(rr)) return j29_dbl(p);  // p == q
+    j29 o = p;
+    o.inf = true;
+    return o;
+  }
+  return {X3, Y3, Z3, false};
+}
+
 FTS_HD j29 j29_from(const g1j& p) {
   return {f29_reduce(f29_from_fp(p.x)), f29_reduce(f29_from_fp(p.y)), f29_reduce(f29_from_fp(p.z)), is_zero(p.z)};
 }

@@ -18,6 +18,16 @@
 //             sums give sum (b+1) S_b restricted to the run
 //   window    tree sum of the segments through LDS
 //   final     Horner over the windows, affine, gnark RawBytes
+//
+// Resident-point mode (MsmPlan.pre, ftz_options.msm_precompute): the points of
+// an ftz_msm handle stay on the device across runs (ftz_msm_set_scalars swaps
+// the scalars), so ftz_msm_load also stores 2^(c w) P_v for every window w
+// (msm_job_precompute).  Window w's digits then select buckets of ONE shared
+// bucket set over those points -- sum_w 2^(c w) sum_b (b+1) S_(w,b) becomes
+// sum_b (b+1) sum_w S'_(w,b) -- so the bucket reduction runs over B buckets
+// instead of W B and the Horner chain of c (W-1) serial doublings disappears;
+// zero digits go to bucket 0 with the identity point (a skipped load), so the
+// sort keys are c - 1 bits.  Memory: W nv 64 bytes of points (1 GiB at 2^20).
 #pragma once
 #include "jobs.h"
 
@@ -34,6 +44,10 @@ struct MsmPlan {
   uint32_t seg_len;    // S: slots per segment
   uint32_t max_slots;  // per window: B + ceil(n / T) bounds sum_b m_b
   uint32_t segs;       // segments per window: ceil(max_slots / S)
+  uint32_t pre;        // 1: resident-point mode (points 2^(c w) P_v precomputed, one bucket set)
+  uint32_t rw;         // reduction windows: W, or 1 with pre
+  uint32_t per;        // sort entries per reduction window: nv, or W nv with pre
+  uint32_t pts;        // resident points: nv, or W nv + 1 with pre (last = the identity)
 };
 
 // window bits for n (virtual) points: floor(log2 n / 2) + 7 clamped to [8, 20]
@@ -48,30 +62,51 @@ FTS_HD uint32_t msm_window_bits(uint64_t n) {
   return c;
 }
 
+// resident-point mode: the bucket reduction runs once (not per window), so
+// wider windows pay: floor(log2 nv / 2) + 10, lowered to the smallest width
+// with the same window count (2^20 points: 19, 7 windows; 2^24: 22, 6 windows)
+FTS_HD uint32_t msm_window_bits_pre(uint64_t nv, bool glv) {
+  uint32_t lg = 0;
+  while ((1ull << (lg + 1)) <= nv) lg++;
+  uint32_t c = lg / 2 + 10, bits = glv ? 129 : 255;
+  if (c < 8) c = 8;
+  if (c > 24) c = 24;
+  uint32_t w = (bits + c - 1) / c;
+  while (c > 8 && (bits + c - 2) / (c - 1) == w) c--;  // same window count, fewer buckets
+  return c;
+}
+
 // plan for n points with c-bit windows (0: msm_window_bits of the virtual point
 // count), slot cap T (0: twice the mean bucket load, at least 4) and S slots per
 // segment (0: sized for >= 64k segment lanes, in [4, 64]).  GLV halves the
 // scalar length, so the Horner chain of c (W-1) doublings and the bucket
 // reduction shrink by half for the same number of bucket additions.
 inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, uint32_t seg_len = 0,
-                             bool glv = true) {
+                             bool glv = true, bool pre = false) {
   MsmPlan p;
   p.n = (uint32_t)n;
   p.glv = glv ? 1 : 0;
   p.nv = glv ? 2 * p.n : p.n;
-  p.c = c ? c : msm_window_bits(p.nv);
+  p.c = c ? c : (pre ? msm_window_bits_pre(p.nv, glv) : msm_window_bits(p.nv));
   uint32_t bits = glv ? 129 : 255;  // magnitude bits + 1 for the signed-digit carry
   p.windows = (bits + p.c - 1) / p.c;
   p.buckets = 1u << (p.c - 1);
+  p.pre = pre ? 1 : 0;
+  p.rw = pre ? 1 : p.windows;
+  p.per = pre ? p.windows * p.nv : p.nv;
+  p.pts = pre ? p.windows * p.nv + 1 : p.nv;
+  // the default cap keeps the per-window mean (about as many bucket lanes per
+  // point as without pre)
   if (!slot_cap) {
     uint64_t mean = (p.nv + p.buckets - 1) / p.buckets;
     slot_cap = (uint32_t)(2 * mean < 4 ? 4 : 2 * mean);
   }
   if (slot_cap > 1023) slot_cap = 1023;  // length bins of the slot ordering (k_msm.hip)
   p.slot_cap = slot_cap;
-  p.max_slots = p.buckets + (uint32_t)((p.nv + slot_cap - 1) / slot_cap);
+  p.max_slots = p.buckets + (uint32_t)((p.per + slot_cap - 1) / slot_cap);
+  if (!seg_len && pre) seg_len = 16;  // measured at 2^20 (2.71 ms against 2.81 with 4)
   if (!seg_len) {
-    uint64_t tot = (uint64_t)p.windows * p.max_slots;
+    uint64_t tot = (uint64_t)p.rw * p.max_slots;
     seg_len = 4;
     while (seg_len < 64 && tot / (2 * seg_len) >= 65536) seg_len *= 2;
   }
@@ -103,24 +138,26 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
 static constexpr uint32_t MSM_KEY_NONE = 0xFFFFFFFFu;
 
 // key bits the sort must look at: g < W B plus one bit so that NONE sorts last
+// (pre: g < B and no NONE keys)
 FTS_HD uint32_t msm_key_bits(const MsmPlan& p) {
-  uint64_t top = (uint64_t)p.windows * p.buckets;
+  uint64_t top = (uint64_t)p.rw * p.buckets;
   uint32_t b = 0;
   while ((1ull << b) < top) b++;
-  return b + 1;
+  return p.pre ? (b ? b : 1) : b + 1;
 }
 
 FTS_HD void msm_put_key(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
                         uint32_t* val) {
   size_t t = (size_t)w * p.nv + vi;
   if (d == 0) {
-    key[t] = MSM_KEY_NONE;
-    val[t] = 0;
+    // pre: bucket 0 with the identity (the last resident point)
+    key[t] = p.pre ? 0u : MSM_KEY_NONE;
+    val[t] = p.pre ? p.pts - 1 : 0u;
     return;
   }
   uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-  key[t] = w * p.buckets + b;
-  val[t] = vi | (((d < 0) != neg) ? 0x80000000u : 0u);
+  key[t] = p.pre ? b : w * p.buckets + b;
+  val[t] = (p.pre ? (uint32_t)t : vi) | (((d < 0) != neg) ? 0x80000000u : 0u);
 }
 
 FTS_HD void msm_job_keys(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val) {
@@ -157,6 +194,27 @@ FTS_HD void msm_job_phi(const MsmPlan& p, uint32_t i, G1Dev* pts) {
   G1Dev d;
   g1_store(d, P);
   pts[p.n + i] = d;
+}
+
+// pre: resident point w nv + v = 2^(c w) P_v for w = 1..W-1 (affine), from
+// P_v (window 0, already holding phi(P) for v >= n); the identity stays zero
+FTS_HD void msm_job_precompute(const MsmPlan& p, uint32_t v, G1Dev* pts) {
+  g1a P = g1_load(pts[v]);
+  g1j acc = {P.x, P.y, fe_one<ModP>()};
+  for (uint32_t w = 1; w < p.windows; w++) {
+    g1a r;
+    r.inf = P.inf;
+    if (!P.inf) {
+      for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
+      // P has order r, so 2^k P is never the identity
+      fp zi = fp_inv_var(acc.z), zi2 = sqr(zi);
+      r.x = acc.x * zi2;
+      r.y = acc.y * zi2 * zi;
+    }
+    G1Dev d;
+    g1_store(d, r);
+    pts[(size_t)w * p.nv + v] = d;
+  }
 }
 
 // bucket g = w B + b: its slot count and, once the counts are scanned into
@@ -224,16 +282,27 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   return acc;
 }
 
-// small-scalar multiple of a Jacobian point (k < 2^32), from the top set bit
-FTS_HD g1j jac_mul_small(const g1j& p, uint32_t k) {
-  g1j acc = jac_inf<fp>();
-  if (!k) return acc;
-  acc = p;
+// The reduction stages (segment, tree, Horner) are latency-bound chains of
+// full additions in few lanes; they run in the carry-free form (dev/fp29.h),
+// whose products accumulate columns without carry chains (shorter dependent
+// chains than the 32-bit CIOS product).  Slot and segment sums are stored in
+// the 32-bit Montgomery Jacobian form (G1JDev).
+FTS_HD j29 j29_inf() {
+  j29 o{};
+  o.inf = true;
+  return o;
+}
+FTS_HD j29 j29_ld(const G1JDev& d) { return j29_from(g1j_load(d)); }
+
+// small-scalar multiple (k < 2^32), from the top set bit
+FTS_HD j29 j29_mul_small(const j29& p, uint32_t k) {
+  if (!k) return j29_inf();
+  j29 acc = p;
   int top = 31;
   while (!((k >> top) & 1)) top--;
   for (int i = top - 1; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k >> i) & 1) acc = jac_add_inl(acc, p);
+    acc = j29_dbl(acc);
+    if ((k >> i) & 1) acc = j29_add(acc, p);
   }
   return acc;
 }
@@ -246,14 +315,14 @@ FTS_HD g1j msm_job_segment(const MsmPlan& p, uint32_t w, uint32_t s, const uint3
                            const uint32_t* owner, const G1JDev* slot_sum) {
   uint32_t lo = wlo[w] + s * p.seg_len, hi = lo + p.seg_len;
   if (hi > whi[w]) hi = whi[w];
-  g1j run = jac_inf<fp>(), acc = jac_inf<fp>();
-  if (lo >= hi) return acc;
+  if (lo >= hi) return jac_inf<fp>();
+  j29 run = j29_inf(), acc = j29_inf();
   for (uint32_t j = hi; j > lo; j--) {
-    run = jac_add_inl(run, g1j_load(slot_sum[j - 1]));
-    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = jac_add_inl(acc, run);
+    run = j29_add(run, j29_ld(slot_sum[j - 1]));
+    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = j29_add(acc, run);
   }
   uint32_t bl = owner[lo] - w * p.buckets;
-  return jac_add_inl(acc, jac_mul_small(run, bl));
+  return j29_to(j29_add(acc, j29_mul_small(run, bl)));
 }
 
 // Decode one 64-byte gnark RawBytes G1 point (uncompressed, big-endian; the

@@ -50,6 +50,7 @@ struct Request {
   std::string err;
   bool done = false;
   Clock::time_point t0;
+  std::condition_variable cv;  // this caller's wake-up (no herd of all waiting callers per batch)
 };
 
 // proof bytes per batch stay well below the 2^31 arena / wire limits
@@ -58,8 +59,9 @@ static constexpr size_t BATCH_PROOF_BYTES = (size_t)256 << 20;
 struct Engine {
   ftz_ctx* ctx = nullptr;
   std::mutex mu;
-  std::condition_variable cv_q, cv_done, cv_free, cv_comp;
+  std::condition_variable cv_q, cv_free, cv_comp;
   std::deque<Request*> q;
+  size_t pending = 0;  // proofs queued and not yet handed to a batch (under mu)
   std::vector<ftz_batch*> slots;
   std::deque<ftz_batch*> free_slots, inflight;
   ftz_engine_stats st{};
@@ -93,6 +95,15 @@ static size_t item_bytes(const Request* r, size_t i) {
                : r->is[i].proof_len + 64 * (size_t)r->is[i].n_out;
 }
 
+// A batch part of request r completed (mu held): wake the caller when it was the last.
+static void finish_part(Request* r, size_t count) {
+  r->outstanding -= count;
+  if (r->outstanding == 0 && r->next == r->n) {
+    r->done = true;
+    r->cv.notify_one();  // under mu: the caller cannot return (and free r) before we unlock
+  }
+}
+
 // Deliver a failed batch's error to its requests (mu held).
 void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err) {
   for (auto& p : b->parts) {
@@ -100,11 +111,9 @@ void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err) {
       p.req->rc = rc;
       p.req->err = err;
     }
-    p.req->outstanding -= p.count;
-    if (p.req->outstanding == 0 && p.req->next == p.req->n) p.req->done = true;
+    finish_part(p.req, p.count);
   }
   b->parts.clear();
-  cv_done.notify_all();
 }
 
 void Engine::dispatcher() {
@@ -122,8 +131,6 @@ void Engine::dispatcher() {
       }
       continue;
     }
-    size_t pending = 0;
-    for (Request* r : q) pending += r->n - r->next;
     if (pending < B && inflight.size() >= ctx->opt.hold_inflight && !stop) {
       // the device is busy: let a partial batch wait (a bounded time) for company
       Clock::time_point deadline = q.front()->t0 + window;
@@ -145,6 +152,7 @@ void Engine::dispatcher() {
         bytes += item_bytes(r, r->next);
         b->items.push_back(item_of(r, r->next));
         r->next++;
+        pending--;
       }
       if (r->next > start) b->parts.push_back({r, start, r->next - start});
       if (r->next == r->n) q.pop_front();
@@ -208,12 +216,8 @@ void Engine::completer() {
     if (rc != FTZ_SUCCESS) {
       fail_parts(b, rc, err);
     } else {
-      for (auto& p : b->parts) {
-        p.req->outstanding -= p.count;
-        if (p.req->outstanding == 0 && p.req->next == p.req->n) p.req->done = true;
-      }
+      for (auto& p : b->parts) finish_part(p.req, p.count);
       b->parts.clear();
-      cv_done.notify_all();
     }
     free_slots.push_back(b);
     cv_free.notify_one();
@@ -263,8 +267,9 @@ int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue*
   std::unique_lock<std::mutex> lk(e->mu);
   if (e->stop) return set_err(FTZ_E_INVALID, "context is being destroyed");
   e->q.push_back(&r);
+  e->pending += n;
   e->cv_q.notify_one();
-  e->cv_done.wait(lk, [&]() { return r.done; });
+  r.cv.wait(lk, [&]() { return r.done; });
   if (r.rc != FTZ_SUCCESS) return set_err(r.rc, r.err);
   return FTZ_SUCCESS;
 }

@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) k_msm_bounds(uint64_t total, const uint32
 // count[g] = end[g] - start[g] and the bucket's slot count
 __global__ void __launch_bounds__(256) k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end,
                                                     uint32_t* count, uint32_t* m) {
-  LANE_PROLOGUE(p.windows * p.buckets);
+  LANE_PROLOGUE(p.rw * p.buckets);
   uint32_t c = end[i] - start[i];
   count[i] = c;
   m[i] = msm_bucket_slots(p, c);
@@ -92,13 +92,19 @@ __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, co
 
 __global__ void __launch_bounds__(256) k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff,
                                                    uint32_t* owner, uint32_t* wlo, uint32_t* whi) {
-  LANE_PROLOGUE(p.windows * p.buckets);
+  LANE_PROLOGUE(p.rw * p.buckets);
   msm_job_owner(p, i, count, soff, owner, wlo, whi);
 }
 
 __global__ void __launch_bounds__(256) k_msm_phi(MsmPlan p, G1Dev* pts) {
   LANE_PROLOGUE(p.n);
   msm_job_phi(p, i, pts);
+}
+
+// resident-point mode: 2^(c w) P_v for every window (dev/msm.h msm_job_precompute)
+__global__ void __launch_bounds__(256) k_msm_precompute(MsmPlan p, G1Dev* pts) {
+  LANE_PROLOGUE(p.nv);
+  msm_job_precompute(p, i, pts);
 }
 
 // ---- bucket slots ordered by length, so that the lanes of a wave add about
@@ -110,7 +116,7 @@ static constexpr uint32_t MSM_LEN_BINS = 1024;  // > slot_cap (checked by the pl
 __global__ void __launch_bounds__(256) k_msm_len_hist(MsmPlan p, const uint32_t* whi, const uint32_t* owner,
                                                       const uint32_t* soff, const uint32_t* count, uint32_t* hist) {
   __shared__ uint32_t h[MSM_LEN_BINS];
-  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.windows - 1];
+  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.rw - 1];
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   if (j < L) atomicAdd(&h[p.slot_cap - msm_slot_len(p, j, owner, soff, count)], 1u);  // longest first
@@ -139,7 +145,7 @@ __global__ void __launch_bounds__(256) k_msm_len_scatter(MsmPlan p, const uint32
                                                          const uint32_t* soff, const uint32_t* count,
                                                          uint32_t* cursor, uint32_t* order) {
   __shared__ uint32_t h[MSM_LEN_BINS];
-  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.windows - 1];
+  uint32_t nb = p.slot_cap + 1, j = blockIdx.x * blockDim.x + threadIdx.x, L = whi[p.rw - 1];
   for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   uint32_t bin = 0, rank = 0;
@@ -160,7 +166,7 @@ __global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* w
                                                     const uint32_t* start, const uint32_t* count,
                                                     const uint32_t* perm, const G1Dev* pts, G1JDev* slot_sum) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= whi[p.windows - 1]) return;
+  if (i >= whi[p.rw - 1]) return;
   uint32_t j = order[i];
   g1j_store(slot_sum[j], msm_job_slot(p, j, owner, soff, start, count, perm, pts));
 }
@@ -175,19 +181,19 @@ __global__ void __launch_bounds__(128) k_msm_segment(MsmPlan p, uint32_t w0, uin
 }
 
 // tree sum of m consecutive parts per window in chunks of 256: out[w][ceil(m/256)]
+// (carry-free form in LDS: one conversion in, one out)
 __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out) {
-  __shared__ G1JDev s[256];
+  __shared__ j29 s[256];
   uint32_t chunks = (m + 255) / 256;
   uint32_t w = blockIdx.x / chunks, ch = blockIdx.x - w * chunks, t = threadIdx.x;
   uint32_t i = ch * 256 + t;
-  g1j v = i < m ? g1j_load(in[(size_t)w * m + i]) : jac_inf<fp>();
-  g1j_store(s[t], v);
+  s[t] = i < m ? j29_ld(in[(size_t)w * m + i]) : j29_inf();
   __syncthreads();
   for (uint32_t o = 128; o > 0; o >>= 1) {
-    if (t < o) g1j_store(s[t], jac_add(g1j_load(s[t]), g1j_load(s[t + o])));
+    if (t < o) s[t] = j29_add(s[t], s[t + o]);
     __syncthreads();
   }
-  if (t == 0) out[(size_t)w * chunks + ch] = s[0];
+  if (t == 0) g1j_store(out[(size_t)w * chunks + ch], j29_to(s[0]));
 }
 
 // ---- 4-lane cooperative point arithmetic for the serial Horner chain.  A
@@ -292,17 +298,20 @@ __device__ g1j coop_add(const Coop& c, const g1j& p, const g1j& q) {
   return {X3, o[0] - o[1] - o[1], Zh + Zh};
 }
 
-// Horner steps for windows w_hi-1 down to w_lo: acc = 2^c acc + W_w, on one
-// wave with the 4-lane cooperative point ops; the last call (w_lo = 0)
-// converts to affine (binary-EEA inverse) and gnark RawBytes.
+// Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
+// on one wave with the 4-lane cooperative point ops (measured: 0.55 ms at 2^20
+// against 1.3 ms for one lane in the carry-free form -- four independent
+// 32-bit products per level beat one carry-free chain); the last call (w_lo = 0)
+// converts to affine (binary-EEA inverse) and gnark RawBytes.  With pre (one
+// reduction window) this is the affine conversion alone.
 __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
                                                    G1JDev* acc_buf, G1Dev* res, uint8_t* bytes) {
   __shared__ uint32_t sh[4][8];
   if (blockIdx.x != 0) return;
   Coop c{(int)threadIdx.x, sh};
-  g1j acc = w_hi == p.windows ? jac_inf<fp>() : g1j_load(*acc_buf);
+  g1j acc = w_hi == p.rw ? jac_inf<fp>() : g1j_load(*acc_buf);
   for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
-    if (w != (int)p.windows - 1)
+    if (w != (int)p.rw - 1)
       for (uint32_t q = 0; q < p.c; q++) acc = coop_dbl(c, acc);
     acc = coop_add(c, acc, g1j_load(wsum[w]));
   }

@@ -131,6 +131,7 @@ __global__ void k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add);
 __global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
                             uint32_t* whi);
 __global__ void k_msm_phi(MsmPlan p, G1Dev* pts);
+__global__ void k_msm_precompute(MsmPlan p, G1Dev* pts);
 __global__ void k_msm_len_hist(MsmPlan p, const uint32_t* whi, const uint32_t* owner, const uint32_t* soff,
                                const uint32_t* count, uint32_t* hist);
 __global__ void k_msm_len_scan(MsmPlan p, uint32_t* hist);

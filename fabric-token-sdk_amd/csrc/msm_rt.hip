@@ -30,8 +30,8 @@ static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
 static int msm_alloc(ftz_msm* m, size_t n) {
   const MsmPlan& p = m->p;
-  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * p.nv, ws = (size_t)p.windows * p.max_slots;
-  HC(m->pts.alloc(p.nv));  // P_i, then phi(P_i) for GLV
+  size_t wb = (size_t)p.rw * p.buckets, wn = (size_t)p.windows * p.nv, ws = (size_t)p.rw * p.max_slots;
+  HC(m->pts.alloc(p.pts));  // P_i, then phi(P_i) for GLV (pre: then 2^(c w) of both, then the identity)
   HC(m->scal.alloc(8 * n));
   HC(m->key.alloc(wn));
   HC(m->skey.alloc(wn));
@@ -48,17 +48,17 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->nsl.alloc(wb));
   HC(m->soff.alloc(wb));
   HC(m->owner.alloc(ws));
-  HC(m->wlo.alloc(p.windows));
-  HC(m->whi.alloc(p.windows));
+  HC(m->wlo.alloc(p.rw));
+  HC(m->whi.alloc(p.rw));
   HC(m->slot_sum.alloc(ws));
   HC(m->order.alloc(ws));
   HC(m->lenhist.alloc(1024));
   HC(m->lencur.alloc(1024));
-  HC(m->part.alloc((size_t)p.windows * p.segs));
-  HC(m->tree.alloc((size_t)p.windows * ((p.segs + 255) / 256) * 2));
+  HC(m->part.alloc((size_t)p.rw * p.segs));
+  HC(m->tree.alloc((size_t)p.rw * ((p.segs + 255) / 256) * 2));
   HC(m->res.alloc(1));
   HC(m->hacc.alloc(1));
-  HC(m->wsum.alloc(p.windows));
+  HC(m->wsum.alloc(p.rw));
   HC(m->bytes.alloc(64));
   HC(m->ok.alloc(n));
   for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
@@ -89,7 +89,12 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   // planner overrides from the context's options (window bits, slot cap, slots per
   // segment; 0 = the planner's choice) and the GLV switch
   const ftz_options& o = c->opt;
-  m->p = msm_make_plan(n, o.msm_window_bits, o.msm_slot_cap, o.msm_seg_slots, o.msm_glv != 0);
+  m->p = msm_make_plan(n, o.msm_window_bits, o.msm_slot_cap, o.msm_seg_slots, o.msm_glv != 0, o.msm_precompute != 0);
+  // sort values carry a point index in 31 bits
+  if (m->p.pre && (uint64_t)m->p.windows * m->p.nv + 1 >= (1ull << 31)) {
+    delete m;
+    return set_err(FTZ_E_INVALID, "msm_precompute: windows x points exceeds 2^31 resident points");
+  }
   int rc = msm_alloc(m, n);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);
@@ -99,11 +104,23 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   return FTZ_SUCCESS;
 }
 
+// resident points from P_i: phi(P_i) = (beta x_i, y_i) next to P_i for the GLV
+// halves; with pre the window multiples 2^(c w) of both and the identity last
+static int prepare_points(ftz_msm* m) {
+  hipStream_t s = m->ctx->stream;
+  const MsmPlan& p = m->p;
+  if (p.glv) k_msm_phi<<<blocks(p.n, 256), 256, 0, s>>>(p, m->pts.p);
+  if (p.pre) {
+    k_msm_precompute<<<blocks(p.nv, 256), 256, 0, s>>>(p, m->pts.p);
+    HC(hipMemsetAsync(m->pts.p + (p.pts - 1), 0, sizeof(G1Dev), s));
+  }
+  HC(hipGetLastError());
+  return FTZ_SUCCESS;
+}
+
 static int upload_scalars(ftz_msm* m, const uint8_t* scalars) {
   hipStream_t s = m->ctx->stream;
   size_t n = m->p.n;
-  // resident points: phi(P_i) = (beta x_i, y_i) next to P_i for the GLV halves
-  if (m->p.glv) k_msm_phi<<<blocks(n, 256), 256, 0, s>>>(m->p, m->pts.p);
   DBuf<uint8_t> raw;
   HC(raw.alloc(32 * n));
   HC(hipMemcpyAsync(raw.p, scalars, 32 * n, hipMemcpyHostToDevice, s));
@@ -140,7 +157,8 @@ extern "C" int ftz_msm_load(ftz_ctx* c, size_t n, const uint8_t* points, const u
         return set_err(FTZ_E_INVALID, "point " + std::to_string(i) + " is not a canonical BN254 G1 point");
       }
   }
-  rc = upload_scalars(m, scalars);
+  rc = prepare_points(m);
+  if (rc == FTZ_SUCCESS) rc = upload_scalars(m, scalars);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);
     return rc;
@@ -173,13 +191,21 @@ extern "C" int ftz_msm_load_gen(ftz_ctx* c, size_t n, uint32_t offset, const uin
       return set_err(FTZ_E_DEVICE, "point generation failed");
     }
   }
-  rc = upload_scalars(m, scalars);
+  rc = prepare_points(m);
+  if (rc == FTZ_SUCCESS) rc = upload_scalars(m, scalars);
   if (rc != FTZ_SUCCESS) {
     ftz_msm_destroy(m);
     return rc;
   }
   *out = m;
   return FTZ_SUCCESS;
+}
+
+extern "C" int ftz_msm_set_scalars(ftz_msm* m, const uint8_t* scalars) {
+  if (!m || !scalars) return set_err(FTZ_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(m->ctx->mu);
+  HC(hipSetDevice(m->ctx->device));
+  return upload_scalars(m, scalars);
 }
 
 extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
@@ -189,7 +215,7 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   HC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const MsmPlan& p = m->p;
-  size_t wb = (size_t)p.windows * p.buckets;
+  size_t wb = (size_t)p.rw * p.buckets;
   HC(hipEventRecord(m->ev[0], s));
   const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
   size_t wn = (size_t)p.windows * p.nv;
@@ -205,7 +231,7 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
   // bucket slots in length order, then one lane per slot
-  size_t sl = (size_t)p.windows * p.max_slots;
+  size_t sl = (size_t)p.rw * p.max_slots;
   HC(hipMemsetAsync(m->lenhist.p, 0, 1024 * sizeof(uint32_t), s));
   k_msm_len_hist<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p, m->lenhist.p);
   k_msm_len_scan<<<1, 1024, 0, s>>>(p, m->lenhist.p);
@@ -213,22 +239,22 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
                                                      m->lenhist.p, m->order.p);
   k_msm_bucket<<<blocks(sl, 128), 128, 0, s>>>(p, m->whi.p, m->order.p, m->owner.p, m->soff.p, m->start.p,
                                                m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
-  k_msm_segment<<<blocks((size_t)p.windows * p.segs, 128), 128, 0, s>>>(p, 0, p.windows, m->wlo.p, m->whi.p,
+  k_msm_segment<<<blocks((size_t)p.rw * p.segs, 128), 128, 0, s>>>(p, 0, p.rw, m->wlo.p, m->whi.p,
                                                                        m->owner.p, m->slot_sum.p, m->part.p);
   // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
-  G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.windows * ((p.segs + 255) / 256)};
+  G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.rw * ((p.segs + 255) / 256)};
   const G1JDev* in = m->part.p;
   uint32_t cnt = p.segs;
   int which = 0;
   do {
     uint32_t chunks = (cnt + 255) / 256;
     G1JDev* out = chunks == 1 ? m->wsum.p : bufs[which];
-    k_msm_tree<<<p.windows * chunks, 256, 0, s>>>(in, cnt, out);
+    k_msm_tree<<<p.rw * chunks, 256, 0, s>>>(in, cnt, out);
     in = out;
     which ^= 1;
     cnt = chunks;
   } while (cnt > 1);
-  k_msm_horner<<<1, 64, 0, s>>>(p, p.windows, 0, m->wsum.p, m->hacc.p, m->res.p, m->bytes.p);
+  k_msm_horner<<<1, 64, 0, s>>>(p, p.rw, 0, m->wsum.p, m->hacc.p, m->res.p, m->bytes.p);
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
   HC(hipMemcpyAsync(out, m->bytes.p, 64, hipMemcpyDeviceToHost, s));

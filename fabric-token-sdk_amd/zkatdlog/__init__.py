@@ -55,7 +55,7 @@ class Context:
         """fexp: "exact" (FTZ_FEXP_EXACT, gnark-crypto v0.6.0) or "fuentes";
         batch / slots / window_us / threads and any other ftz_options field by name
         (hold_inflight, small_pass, msm_window_bits, msm_slot_cap, msm_seg_slots,
-        msm_glv): job-engine and MSM options."""
+        msm_glv, msm_precompute): job-engine and MSM options."""
         self._lib = _abi.load()
         self.device = int(device)
         h = ctypes.c_void_p()
@@ -332,6 +332,13 @@ class Msm:
             self.n = len(points) // 64
             _check(self._lib.ftz_msm_load(ctx._h, self.n, points, scalars, ctypes.byref(h)), self._lib)
         self._h = h
+
+    def set_scalars(self, scalars):
+        """new scalars (n x 32 bytes) for the resident points"""
+        scalars = bytes(scalars)
+        if len(scalars) != 32 * self.n:
+            raise ValueError("scalars must be n x 32 bytes")
+        _check(self._lib.ftz_msm_set_scalars(self._h, scalars), self._lib)
 
     def run(self):
         out = (ctypes.c_uint8 * 64)()

@@ -112,6 +112,10 @@ typedef struct {
   uint32_t msm_slot_cap;    /*   window bits c, bucket slot cap T, slots per segment S    */
   uint32_t msm_seg_slots;
   uint32_t msm_glv;     /* 1 (default): GLV-split scalars in the MSM; 0: plain 256-bit   */
+  uint32_t msm_precompute; /* 1: resident-point MSM -- ftz_msm_load also stores 2^(c w) P
+                           for every window w (W x the point memory) and runs use one shared
+                           bucket set and no Horner chain; for fixed bases (ftz_msm_set_scalars)
+                           0 (default): plain variable-base Pippenger                      */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
@@ -328,6 +332,9 @@ int ftz_msm_load(ftz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* s
 /* test/bench inputs with known discrete logs: P_i = (i + offset) G generated on the device */
 int ftz_msm_load_gen(ftz_ctx* ctx, size_t n, uint32_t offset, const uint8_t* scalars, ftz_msm** out);
 int ftz_msm_run(ftz_msm* m, uint8_t out[64]);
+/* replace the scalars of a loaded MSM (n x 32 bytes big-endian); the points, and
+ * with msm_precompute their window multiples, stay resident */
+int ftz_msm_set_scalars(ftz_msm* m, const uint8_t* scalars);
 /* device time of the last ftz_msm_run in ms (HIP events) and the window size */
 int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits);
 void ftz_msm_destroy(ftz_msm* m);

@@ -438,5 +438,29 @@ extern "C" int emu_f29_check(uint64_t seed, int iters) {
     // round trip through the fp form mid-chain
     if (!aff_same(jac_to_aff(j29_to(j29_from(acc))), jac_to_aff(acc))) bad++;
   }
+  // full Jacobian additions (j29_add vs jac_add): random sums, P + P, P + (-P),
+  // either side infinity, and chained sums of sums
+  for (int it = 0; it < iters / 4 + 4; it++) {
+    uint32_t s1[8], s2[8];
+    for (int i = 0; i < 8; i++) s1[i] = (uint32_t)r.next(), s2[i] = (uint32_t)r.next();
+    s1[7] &= 0x0fffffffu;
+    s2[7] &= 0x0fffffffu;
+    g1j P = aff_mul(pts[it % pts.size()], s1), Q = aff_mul(pts[(it + 3) % pts.size()], s2);
+    int e = it % 6;
+    if (e == 1) Q = jac_dbl(jac_add(P, jac_inf<fp>()));            // Q = 2P (other Z)
+    if (e == 2) Q = P;                                             // P + P, same Z
+    if (e == 3) Q = {P.x, fe_neg(P.y), P.z};                       // P + (-P)
+    if (e == 4) P = jac_inf<fp>();
+    if (e == 5) Q = jac_inf<fp>();
+    j29 A = j29_from(P), B = j29_from(Q);
+    j29 S = j29_add(A, B);
+    g1j want = jac_add(P, Q);
+    if (!aff_same(jac_to_aff(j29_to(S)), jac_to_aff(want))) bad++;
+    // a sum of sums (outputs feed inputs: the B <= 2 bound) and a doubling of a sum
+    j29 S2 = j29_add(S, j29_add(B, S));
+    g1j want2 = jac_add(want, jac_add(Q, want));
+    if (!aff_same(jac_to_aff(j29_to(S2)), jac_to_aff(want2))) bad++;
+    if (!aff_same(jac_to_aff(j29_to(j29_add(S2, S2))), jac_to_aff(jac_dbl(want2)))) bad++;
+  }
   return bad;
 }

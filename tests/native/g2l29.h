@@ -1,3 +1,5 @@
+// TEST-ONLY (host emulation, tests/native/sx_emu.cpp): an experimental carry-free
+// variant of the line stage kept for its parity test; no kernel includes it.
 // k_g2lines in one lane per membership digit, on the carry-free balanced
 // 29-bit field form (dev/fp29.h q2, dev/sx29.h w29 rows):
 //   phase A  t' = c PK0 + v PK1 + h PK2 (pok.go:175-183, folded) from the
@@ -21,8 +23,8 @@
 //   q2_sqr29: (a0 + a1)(a0 - a1) and (2 a0) a1 need balanced a;
 //   q2_lin: |coefficients| <= 16, input limbs <= 2^29; output balanced.
 #pragma once
-#include "jobs.h"
-#include "sx29.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
 
 namespace fts {
 

@@ -11,10 +11,11 @@
 
 using namespace fts;
 
-extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
-                       uint32_t seg_len, uint32_t glv, uint8_t out[64]) {
-  MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len, glv != 0);
-  std::vector<G1Dev> pts(p.nv);
+extern "C" int emu_msm_ex(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
+                          uint32_t seg_len, uint32_t glv, uint32_t pre, uint8_t out[64]) {
+  MsmPlan p = msm_make_plan(n, c, slot_cap, seg_len, glv != 0, pre != 0);
+  std::vector<G1Dev> pts(p.pts);
+  memset(pts.data(), 0, pts.size() * sizeof(G1Dev));
   std::vector<uint32_t> scal(8 * n);
   uint32_t(*sc)[8] = reinterpret_cast<uint32_t(*)[8]>(scal.data());
   for (size_t i = 0; i < n; i++) {
@@ -32,7 +33,9 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   }
   if (p.glv)
     for (uint32_t i = 0; i < n; i++) msm_job_phi(p, i, pts.data());
-  size_t wb = (size_t)p.windows * p.buckets, wn = (size_t)p.windows * p.nv;
+  if (p.pre)
+    for (uint32_t v = 0; v < p.nv; v++) msm_job_precompute(p, v, pts.data());
+  size_t wb = (size_t)p.rw * p.buckets, wn = (size_t)p.windows * p.nv;
   std::vector<uint32_t> key(wn), val(wn), skey(wn), perm(wn), count(wb), start(wb, 0), end(wb, 0);
   for (uint32_t i = 0; i < n; i++) msm_job_keys(p, i, sc, key.data(), val.data());
   // the device's stable radix sort over msm_key_bits(p) bits
@@ -44,18 +47,18 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   for (size_t t = 0; t < wn; t++) skey[t] = key[idx[t]], perm[t] = val[idx[t]];
   for (uint64_t t = 0; t < wn; t++) msm_job_bounds(t, wn, skey.data(), start.data(), end.data());
   for (size_t g = 0; g < wb; g++) count[g] = end[g] - start[g];
-  std::vector<uint32_t> soff(wb), owner((size_t)p.windows * p.max_slots, 0xFFFFFFFFu), wlo(p.windows), whi(p.windows);
+  std::vector<uint32_t> soff(wb), owner((size_t)p.rw * p.max_slots, 0xFFFFFFFFu), wlo(p.rw), whi(p.rw);
   uint32_t run = 0;
   for (size_t b = 0; b < wb; b++) soff[b] = run, run += msm_bucket_slots(p, count[b]);
-  if (run > (size_t)p.windows * p.max_slots) return -2;
+  if (run > (size_t)p.rw * p.max_slots) return -2;
   for (uint32_t g = 0; g < wb; g++) msm_job_owner(p, g, count.data(), soff.data(), owner.data(), wlo.data(), whi.data());
-  if (whi[p.windows - 1] != run) return -3;
+  if (whi[p.rw - 1] != run) return -3;
   std::vector<G1JDev> slot_sum(run);
   for (uint32_t j = 0; j < run; j++)
     g1j_store(slot_sum[j], msm_job_slot(p, j, owner.data(), soff.data(), start.data(), count.data(), perm.data(),
                                         pts.data()));
   g1j acc = jac_inf<fp>();
-  for (int w = (int)p.windows - 1; w >= 0; w--) {
+  for (int w = (int)p.rw - 1; w >= 0; w--) {
     for (uint32_t q = 0; q < p.c; q++) acc = jac_dbl(acc);
     g1j ws = jac_inf<fp>();
     for (uint32_t s = 0; s < p.segs; s++)
@@ -64,6 +67,11 @@ extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, 
   }
   g1_to_bytes(out, jac_to_aff(acc));
   return 0;
+}
+
+extern "C" int emu_msm(size_t n, const uint8_t* points, const uint8_t* scalars, uint32_t c, uint32_t slot_cap,
+                       uint32_t seg_len, uint32_t glv, uint8_t out[64]) {
+  return emu_msm_ex(n, points, scalars, c, slot_cap, seg_len, glv, 0, out);
 }
 
 // host run of the multi-GPU MSM's final add (dev/msm.h g1_sum_raw)

@@ -12,7 +12,7 @@
 
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
-#include "../../fabric-token-sdk_amd/csrc/dev/g2l29.h"
+#include "g2l29.h"
 
 using namespace fts;
 
@@ -294,7 +294,7 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   return 0;
 }
 
-// the literal constants of dev/g2l29.h against their conversions: 0 = equal
+// the literal constants of tests/native/g2l29.h against their conversions: 0 = equal
 int sxe_g2l29_consts() {
   const q2 b3 = q2_scale(q2_from_fp2(f2_const(TWIST_B)), 3);
   const q2 fx = q2_from_fp2(f2_const(TW_FROB_X)), fy = q2_from_fp2(f2_const(TW_FROB_Y));
@@ -306,7 +306,7 @@ int sxe_g2l29_consts() {
   return 0;
 }
 
-// G2 job + pair-2 lines, one lane on the carry-free form (dev/g2l29.h
+// G2 job + pair-2 lines, one lane on the carry-free form (tests/native/g2l29.h
 // job_g2lines29) vs the 32-bit one lane (job_g2lines): the same affine t', and
 // lines equal up to Fp factors, so the carry-free Miller f-chain with either
 // set of lines (fixed pair: qfix at p1) gives the same final exponentiation.

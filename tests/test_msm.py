@@ -32,35 +32,51 @@ def pack(pts, ks):
     return b"".join(C.g1_bytes(p) for p in pts), b"".join(k.to_bytes(32, "big") for k in ks)
 
 
-def emu_msm(emu, pts, ks, c, cap, seg_len, glv=1):
+def emu_msm(emu, pts, ks, c, cap, seg_len, glv=1, pre=0):
     pb, kb = pack(pts, ks)
     out = ctypes.create_string_buffer(64)
-    emu.emu_msm.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
-                            ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
-    assert emu.emu_msm(len(pts), pb, kb, c, cap, seg_len, glv, out) == 0
+    emu.emu_msm_ex.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32,
+                               ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p]
+    assert emu.emu_msm_ex(len(pts), pb, kb, c, cap, seg_len, glv, pre, out) == 0
     return out.raw
 
 
 @pytest.mark.parametrize("n,c,cap,seg", [(1, 4, 1, 1), (7, 2, 1, 1), (33, 5, 2, 3), (40, 8, 0, 0), (64, 3, 3, 2),
                                          (20, 1, 1, 1), (48, 6, 4, 5)])
 @pytest.mark.parametrize("glv", [1, 0])
-def test_emu_pipeline(emu, n, c, cap, seg, glv):
+@pytest.mark.parametrize("pre", [0, 1])
+def test_emu_pipeline(emu, n, c, cap, seg, glv, pre):
+    """pre = 1: resident-point mode (window multiples 2^(c w) P, one bucket set,
+    zero digits on the identity in bucket 0)"""
     pts, ks = rnd_case(n, 100 + n * 7 + c)
-    assert emu_msm(emu, pts, ks, c, cap, seg, glv) == C.g1_bytes(C.g1_msm(pts, ks))
+    assert emu_msm(emu, pts, ks, c, cap, seg, glv, pre) == C.g1_bytes(C.g1_msm(pts, ks))
 
 
-def test_emu_skewed_scalars(emu):
+@pytest.mark.parametrize("pre", [0, 1])
+def test_emu_skewed_scalars(emu, pre):
     # small scalars pile into few buckets: heavy buckets are split over slots
+    # (with pre the zero digits of every upper window land in bucket 0)
     rng = random.Random(77)
     pts, _ = rnd_case(60, 78, special=False)
     ks = [rng.randrange(1, 6) for _ in pts]
-    assert emu_msm(emu, pts, ks, 4, 4, 3) == C.g1_bytes(C.g1_msm(pts, ks))
+    assert emu_msm(emu, pts, ks, 4, 4, 3, 1, pre) == C.g1_bytes(C.g1_msm(pts, ks))
 
 
-def test_emu_cancelling_sum(emu):
+@pytest.mark.parametrize("pre", [0, 1])
+def test_emu_cancelling_sum(emu, pre):
     pts, ks = rnd_case(8, 5, special=False)
     pts2 = pts + [C.g1_neg(p) for p in pts]
-    assert emu_msm(emu, pts2, ks + ks, 4, 3, 2) == C.g1_bytes(None)
+    assert emu_msm(emu, pts2, ks + ks, 4, 3, 2, 1, pre) == C.g1_bytes(None)
+
+
+def test_emu_pre_identity_points(emu):
+    """identity points among the resident points (all their multiples stay the
+    identity) and all-zero scalars (every entry on the identity)"""
+    pts, ks = rnd_case(12, 9, special=False)
+    pts[3] = None
+    pts[7] = None
+    assert emu_msm(emu, pts, ks, 5, 2, 2, 1, 1) == C.g1_bytes(C.g1_msm(pts, ks))
+    assert emu_msm(emu, pts, [0] * len(pts), 5, 2, 2, 1, 1) == C.g1_bytes(None)
 
 
 def test_window_plan():
@@ -94,6 +110,49 @@ def test_gpu_msm_without_glv(golden):
     pb, kb = pack(pts, ks)
     with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_glv=0, msm_window_bits=9) as c:
         assert c.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
+
+
+@pytest.mark.gpu
+def test_gpu_msm_precompute_explicit(golden):
+    """resident-point mode through the C ABI: explicit points (identity and
+    repeated points included), then new scalars on the same resident points"""
+    import zkatdlog
+    pts, ks = rnd_case(500, 902)
+    pts[9] = None
+    pb, kb = pack(pts, ks)
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_precompute=1) as c:
+        assert c.msm_g1(pb, kb) == C.g1_bytes(C.g1_msm(pts, ks))
+        m = zkatdlog.Msm(c, pb, kb)
+        try:
+            assert m.run() == C.g1_bytes(C.g1_msm(pts, ks))
+            ks2 = [random.Random(3).randrange(1 << 256) for _ in pts]
+            m.set_scalars(b"".join(k.to_bytes(32, "big") for k in ks2))
+            assert m.run() == C.g1_bytes(C.g1_msm(pts, ks2))
+            m.set_scalars(bytes(32 * len(pts)))
+            assert m.run() == C.g1_bytes(None)
+        finally:
+            m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lg,bits", [(20, 256), (16, 3)])
+def test_gpu_msm_precompute_known_logs(golden, lg, bits):
+    import zkatdlog
+    n, off = 1 << lg, 999
+    rng = random.Random(lg * 77 + bits)
+    ks = [rng.randrange(1 << bits) for _ in range(n)]
+    kb = b"".join(k.to_bytes(32, "big") for k in ks)
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_precompute=1) as c:
+        m = zkatdlog.Msm(c, scalars=kb, gen_offset=off)
+        try:
+            got = m.run()
+            again = m.run()
+            info = m.info()
+        finally:
+            m.close()
+    assert got == C.g1_bytes(C.g1_mul(C.G1_GEN, _known_log_sum(kb, n, off)))
+    assert again == got
+    print("MSM 2^%d resident-point mode: %.3f ms device, window %d bits" % (lg, info["last_ms"], info["window_bits"]))
 
 
 @pytest.mark.gpu

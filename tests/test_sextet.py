@@ -70,7 +70,7 @@ def test_sextet_g2_lines(sx, case):
 
 @pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar", "all_zero", "p1_infinity"])
 def test_g2_lines_carry_free(sx, case):
-    """One-lane t' + pair-2 lines on the carry-free form (dev/g2l29.h): same t',
+    """One-lane t' + pair-2 lines on the carry-free form (tests/native/g2l29.h): same t',
     and the same GT after the Miller f-chain and the final exponentiation as the
     32-bit one-lane lines (which test_sextet_g2_lines pins to the sextet ones)."""
     rng = random.Random("g29" + case)
