@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r03b}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-SHORT="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-prover --msm 20 --distinct 4096 --serial --slots 1"
+SHORT="bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-prover --no-seam --no-ppb --msm 20 --distinct 4096 --serial --slots 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o k -- python3 $SHORT > $OUT/trace.log 2>&1 || { echo "trace failed"; tail -20 $OUT/trace.log; exit 4; }
 echo "trace ok"
 if [ "${PMC:-1}" = 1 ]; then
