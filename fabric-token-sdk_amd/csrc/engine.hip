@@ -12,9 +12,11 @@
 //     range -- and fills the pipeline by itself;
 //   * small concurrent calls (the Go shim verifies ONE TransferAction per call)
 //     are coalesced: while the GPU has >= opt.hold_inflight batches in flight a
-//     partial batch waits up to opt.window_us for more callers, otherwise it
-//     goes at once; with every slot busy, callers accumulate for the next free
-//     slot anyway;
+//     partial batch waits up to opt.window_us (from its oldest request) for more
+//     callers, otherwise it goes at once (hold_inflight 0: it always waits, so
+//     callers that resubmit together after a batch completes share the next
+//     batch instead of splitting into a lone first request and the rest); with
+//     every slot busy, callers accumulate for the next free slot anyway;
 //   * transfers and issues share batches (the planner emits the same jobs).
 //
 // Batches cycle through opt.slots reusable slots (pinned staging blob, device

@@ -104,7 +104,8 @@ typedef struct {
   uint32_t fexp;        /* FTZ_FEXP_EXACT (default) or FTZ_FEXP_FUENTES                 */
   uint32_t hold_inflight; /* a partial batch waits (up to window_us) for more callers
                            only while at least this many batches are in flight
-                           (default 2; FTZ_HOLD_NEVER: ship at once)                     */
+                           (default 2; 0: always, also with the GPU idle -- closed-loop
+                           callers resubmit together; FTZ_HOLD_NEVER: ship at once)       */
   uint32_t small_pass;  /* device passes of at most this many proofs run the low-latency
                            layout of the t' / pair-2 line stage (six lanes per job
                            instead of one; same bytes); 0 = never                        */

@@ -9,6 +9,6 @@ timeout -k 10 300 python -u fabric-token-sdk_amd/tools/msmtune.py 20 "0,0,0 0,0,
 cat gpurun_out/msmtune20.log
 timeout -k 10 300 python -u fabric-token-sdk_amd/tools/msmtune.py 24 "0,0,0 0,0,0,1 22,0,32,1 21,0,0,1 23,0,0,1" > gpurun_out/msmtune24.log 2>&1 || { echo "msmtune24 failed"; tail -5 gpurun_out/msmtune24.log; exit 7; }
 cat gpurun_out/msmtune24.log
-timeout -k 10 400 python -u fabric-token-sdk_amd/tools/seamsweep.py "" "small_pass=1024" "small_pass=4096,window_us=500" "window_us=500" > gpurun_out/seamsweep.log 2>&1 || { echo "seam sweep failed"; tail -20 gpurun_out/seamsweep.log; exit 3; }
+timeout -k 10 400 python -u fabric-token-sdk_amd/tools/seamsweep.py "" "hold_inflight=0,window_us=300" "hold_inflight=0,window_us=1000" "hold_inflight=0,window_us=300,small_pass=1024" > gpurun_out/seamsweep.log 2>&1 || { echo "seam sweep failed"; tail -20 gpurun_out/seamsweep.log; exit 3; }
 echo "seam sweep ok"
 SKIP_TESTS=1 bash scripts/gpu_check.sh || exit $?
