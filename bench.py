@@ -76,6 +76,24 @@ def host_cores():
     return aff, os.cpu_count() or aff
 
 
+def cpu_quota():
+    """CPUs the cgroup CPU quota grants (cgroup v2 cpu.max or v1 cfs quota /
+    period), or None when unlimited / unknown: on a shared box the affinity
+    mask can list every CPU of the machine while the quota allows a few."""
+    import math
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, math.floor(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // per)
+    except (OSError, ValueError):
+        return None
+
+
 def _cpu_ctx(pp_json):
     import ctypes
     lib = _cpu_lib()
@@ -167,25 +185,37 @@ def cpu_msm(lg, cores, seed=7):
 
 def cpu_baselines(pp_a, job_a, pp_b, job_b, bases_a, gpu_msm20):
     """CPU reference figures: the C++ restatement on ALL
-    cores this process may use (the headline cpu_baseline) and on the 16-core
-    per-GPU share of the box, for PP-A and PP-B verification, PP-A proving and
-    the 2^20 Pippenger.  Samples are sized for a few seconds of CPU work each."""
+    cores this process may use -- threads = the affinity mask's CPUs, capped by
+    the cgroup CPU quota when one is set (the headline cpu_baseline) -- and on
+    the 16-core per-GPU share of the box, for PP-A and PP-B verification, PP-A
+    proving and the 2^20 Pippenger; with a quota below the affinity the
+    oversubscribed all-affinity-threads run is reported too.  Samples are sized
+    for a few seconds of CPU work each."""
     aff, nproc = host_cores()
-    share = min(16, aff)
-    out = {"affinity_cores": aff, "nproc": nproc, "impl": "cpp-restatement (oracle/cpu, 4x64-bit Montgomery)"}
+    quota = cpu_quota()
+    usable = min(aff, quota) if quota else aff
+    share = min(16, usable)
+    out = {"affinity_cores": aff, "nproc": nproc, "cgroup_cpu_quota": quota, "usable_cores": usable,
+           "impl": "cpp-restatement (oracle/cpu, 4x64-bit Montgomery)"}
     head = None
-    for label, cores in (("all", aff), ("share16", share)):
-        r, med, n = cpu_verify(pp_a, job_a, cores, max(2048, 48 * cores))
+    runs = [("all", usable), ("share16", share)]
+    if usable < aff:
+        runs.append(("affinity_threads", aff))
+    for label, cores in runs:
+        r, med, n = cpu_verify(pp_a, job_a, cores, max(2048, 48 * min(cores, usable)))
         out["verify_pp_a_" + label] = {"value": round(r, 2), "unit": "transfers/s", "cores": cores,
                                        "sample": "%d transfers, median %.2f s" % (n, med)}
+        if label == "affinity_threads":
+            continue
         if label == "all":
             head = {"value": round(r, 2), "unit": "transfers/s", "cores": cores, "kind": "port",
-                    "impl": "cpp-restatement", "affinity_cores": aff, "nproc": nproc,
+                    "impl": "cpp-restatement", "affinity_cores": aff, "nproc": nproc, "cgroup_cpu_quota": quota,
                     "sample": "%d transfers of the bench job (same proofs, same verdicts) verified by the C++ CPU "
                               "restatement of the verifier (oracle/cpu: host build of the planner + job code with the "
                               "GPU path's algorithms -- bilinear membership rewrite, GLV, fixed-base tables -- and "
-                              "4x64-bit Montgomery products) on all %d cores of the process affinity (nproc %d); "
-                              "median of 3 runs after a warm-up: %.2f s" % (n, cores, nproc, med)}
+                              "4x64-bit Montgomery products) on %d threads = every CPU this process may use "
+                              "(affinity %d of nproc %d, cgroup CPU quota %s); median of 3 runs after a warm-up: "
+                              "%.2f s" % (n, cores, aff, nproc, quota if quota else "none", med)}
         if job_b is not None:
             r, med, n = cpu_verify(pp_b, job_b, cores, max(256, 8 * cores))
             out["verify_pp_b_" + label] = {"value": round(r, 2), "unit": "transfers/s", "cores": cores,
@@ -193,8 +223,8 @@ def cpu_baselines(pp_a, job_a, pp_b, job_b, bases_a, gpu_msm20):
         r, med = cpu_prove(pp_a, bases_a, cores, max(512, 12 * cores))
         out["prove_pp_a_" + label] = {"value": round(r, 2), "unit": "proofs/s", "cores": cores,
                                       "sample": "median %.2f s" % med}
-    ms, res = cpu_msm(20, aff)
-    out["msm_2^20_all"] = {"ms": round(ms, 1), "cores": aff, "matches_gpu": gpu_msm20 is None or res == gpu_msm20}
+    ms, res = cpu_msm(20, usable)
+    out["msm_2^20_all"] = {"ms": round(ms, 1), "cores": usable, "matches_gpu": gpu_msm20 is None or res == gpu_msm20}
     return head, out
 
 

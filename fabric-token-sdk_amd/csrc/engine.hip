@@ -50,9 +50,13 @@ struct Request {
   size_t outstanding = 0;  // proofs not yet completed (under mu)
   int rc = FTZ_SUCCESS;
   std::string err;
-  bool done = false;
+  bool finished = false;    // all proofs completed (under the engine mu)
   Clock::time_point t0;
-  std::condition_variable cv;  // this caller's wake-up (no herd of all waiting callers per batch)
+  // the caller's own wake-up: it sleeps on m / cv, not on the engine lock, so a
+  // completing pass wakes exactly its callers and they do not queue on one mutex
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;  // under m
 };
 
 // proof bytes per batch stay well below the 2^31 arena / wire limits
@@ -63,7 +67,8 @@ struct Engine {
   std::mutex mu;
   std::condition_variable cv_q, cv_free, cv_comp;
   std::deque<Request*> q;
-  size_t pending = 0;  // proofs queued and not yet handed to a batch (under mu)
+  size_t pending = 0;        // proofs queued and not yet handed to a batch (under mu)
+  bool disp_holding = false;  // the dispatcher is waiting out a window (under mu)
   std::vector<ftz_batch*> slots;
   std::deque<ftz_batch*> free_slots, inflight;
   ftz_engine_stats st{};
@@ -74,7 +79,7 @@ struct Engine {
 
   void dispatcher();
   void completer();
-  void fail_parts(ftz_batch* b, int rc, const std::string& err);
+  void fail_parts(ftz_batch* b, int rc, const std::string& err, std::vector<Request*>& wake);
 };
 
 static PlanItem item_of(const Request* r, size_t i) {
@@ -97,23 +102,35 @@ static size_t item_bytes(const Request* r, size_t i) {
                : r->is[i].proof_len + 64 * (size_t)r->is[i].n_out;
 }
 
-// A batch part of request r completed (mu held): wake the caller when it was the last.
-static void finish_part(Request* r, size_t count) {
+// A batch part of request r completed (mu held): collect the caller when it was the last.
+static void finish_part(Request* r, size_t count, std::vector<Request*>& wake) {
   r->outstanding -= count;
-  if (r->outstanding == 0 && r->next == r->n) {
-    r->done = true;
-    r->cv.notify_one();  // under mu: the caller cannot return (and free r) before we unlock
+  if (r->outstanding == 0 && r->next == r->n && !r->finished) {
+    r->finished = true;
+    wake.push_back(r);
   }
 }
 
+// Wake collected callers (engine mu NOT held).  done is set and notified under
+// the request's own mutex, so the caller cannot return and free r before we
+// let go of it; r is not touched afterwards.
+static void wake_all(std::vector<Request*>& wake) {
+  for (Request* r : wake) {
+    std::lock_guard<std::mutex> g(r->m);
+    r->done = true;
+    r->cv.notify_one();
+  }
+  wake.clear();
+}
+
 // Deliver a failed batch's error to its requests (mu held).
-void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err) {
+void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err, std::vector<Request*>& wake) {
   for (auto& p : b->parts) {
     if (p.req->rc == FTZ_SUCCESS) {
       p.req->rc = rc;
       p.req->err = err;
     }
-    finish_part(p.req, p.count);
+    finish_part(p.req, p.count, wake);
   }
   b->parts.clear();
 }
@@ -137,8 +154,10 @@ void Engine::dispatcher() {
       // the device is busy: let a partial batch wait (a bounded time) for company
       Clock::time_point deadline = q.front()->t0 + window;
       if (Clock::now() < deadline) {
+        disp_holding = true;  // enqueuers now notify only once a full batch is pending
         cv_q.wait_until(lk, deadline);
-        continue;  // re-evaluate: more requests, a completion, or the deadline
+        disp_holding = false;
+        continue;  // re-evaluate: a full batch, a completion, or the deadline
       }
     }
     cv_free.wait(lk, [&]() { return !free_slots.empty(); });
@@ -180,9 +199,13 @@ void Engine::dispatcher() {
         (void)slot_wait(b);
         lk.lock();
       }
-      fail_parts(b, rc, err);
+      std::vector<Request*> wake;
+      fail_parts(b, rc, err, wake);
       free_slots.push_back(b);
       cv_free.notify_one();
+      lk.unlock();
+      wake_all(wake);
+      lk.lock();
       continue;
     }
     inflight.push_back(b);
@@ -193,6 +216,7 @@ void Engine::dispatcher() {
 void Engine::completer() {
   (void)hipSetDevice(ctx->device);
   std::unique_lock<std::mutex> lk(mu);
+  std::vector<Request*> wake;
   while (true) {
     cv_comp.wait(lk, [&]() { return disp_done || !inflight.empty(); });
     if (inflight.empty()) return;  // disp_done: nothing more will arrive
@@ -216,14 +240,17 @@ void Engine::completer() {
     st.wall_ms = std::chrono::duration<double, std::milli>(last - first).count();
     inflight.pop_front();
     if (rc != FTZ_SUCCESS) {
-      fail_parts(b, rc, err);
+      fail_parts(b, rc, err, wake);
     } else {
-      for (auto& p : b->parts) finish_part(p.req, p.count);
+      for (auto& p : b->parts) finish_part(p.req, p.count, wake);
       b->parts.clear();
     }
     free_slots.push_back(b);
     cv_free.notify_one();
     cv_q.notify_one();  // a partial batch may go now that the device has room
+    lk.unlock();
+    wake_all(wake);
+    lk.lock();
   }
 }
 
@@ -266,12 +293,18 @@ int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue*
   r.codes = codes;
   r.outstanding = n;
   r.t0 = Clock::now();
-  std::unique_lock<std::mutex> lk(e->mu);
-  if (e->stop) return set_err(FTZ_E_INVALID, "context is being destroyed");
-  e->q.push_back(&r);
-  e->pending += n;
-  e->cv_q.notify_one();
-  r.cv.wait(lk, [&]() { return r.done; });
+  {
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->stop) return set_err(FTZ_E_INVALID, "context is being destroyed");
+    e->q.push_back(&r);
+    e->pending += n;
+    // a dispatcher waiting out a window only needs waking for a full batch
+    if (!e->disp_holding || e->pending >= e->ctx->opt.batch) e->cv_q.notify_one();
+  }
+  {
+    std::unique_lock<std::mutex> lk(r.m);
+    r.cv.wait(lk, [&]() { return r.done; });
+  }
   if (r.rc != FTZ_SUCCESS) return set_err(r.rc, r.err);
   return FTZ_SUCCESS;
 }

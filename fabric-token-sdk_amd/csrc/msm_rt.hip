@@ -28,21 +28,10 @@ struct ftz_msm {
 
 static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
-// Sort of the (key, value) pairs.  rocPRIM's gfx950 onesweep default takes 8
-// key bits per pass, i.e. three passes for the 17..24-bit keys of 2^16..2^24
-// point MSMs; with 11 bits per pass (2048 digit bins, 256-thread blocks and
-// the match rank algorithm so that the counters fit the LDS) keys of up to 22
-// bits take two.
-using Onesweep11 = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 16>, rocprim::kernel_config<256, 16>,
-                                                       11, rocprim::block_radix_rank_algorithm::match>;
-using SortCfg11 = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Onesweep11>;
-static bool sort_wide(uint32_t key_bits) { return key_bits > 16 && key_bits <= 22; }
-static hipError_t msm_sort(ftz_msm* m, void* tmp, size_t& tmp_bytes, size_t wn, hipStream_t s) {
-  if (sort_wide(m->key_bits))
-    return rocprim::radix_sort_pairs<SortCfg11>(tmp, tmp_bytes, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0,
-                                                m->key_bits, s);
-  return rocprim::radix_sort_pairs(tmp, tmp_bytes, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s);
-}
+// The (key, value) sort uses rocPRIM's gfx950 onesweep default (8 key bits per
+// pass, three passes for 17..24-bit keys).  An 11-bit config (2048 digit bins,
+// 256-thread blocks, match ranking, two passes) measured slower: 2^20 3.29 ->
+// 4.33 ms, 2^24 29.0 -> 44.6 ms.
 
 static int msm_alloc(ftz_msm* m, size_t n) {
   const MsmPlan& p = m->p;
@@ -57,7 +46,8 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->start.alloc(wb));
   HC(m->end.alloc(wb));
   m->key_bits = msm_key_bits(p);
-  HC(msm_sort(m, nullptr, m->sort_tmp_bytes, wn, m->ctx->stream));
+  HC(rocprim::radix_sort_pairs(nullptr, m->sort_tmp_bytes, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0,
+                               m->key_bits, m->ctx->stream));
   HC(m->sort_tmp.alloc(m->sort_tmp_bytes ? m->sort_tmp_bytes : 1));
   HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
   HC(m->nsl.alloc(wb));
@@ -237,7 +227,7 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   // (window, bucket)-sorted point lists: keys, stable radix sort, bucket ranges
   k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
   size_t tb = m->sort_tmp_bytes;
-  HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
+  HC(rocprim::radix_sort_pairs(m->sort_tmp.p, tb, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s));
   HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
   HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
   k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>((uint64_t)wn, m->skey.p, m->start.p, m->end.p);
