@@ -186,19 +186,21 @@ FTS_HD q2 sq_frob1(int k, const q2& a) { return q2_mul(q2_conj(a), q2_from_fp2(f
 FTS_HD q2 sq_frob2(int k, const q2& a) { return q2_mul(a, q2_from_fp2(f2_of_fp(fe_const<ModP>(FROB2[k][0])))); }
 FTS_HD q2 sq_frob3(int k, const q2& a) { return q2_mul(q2_conj(a), q2_from_fp2(f2_const(FROB3[k]))); }
 
-// a^x, as sx_expt (width-4 NAF).  a, a^3, a^5 and a^7 are parked in pk slots
-// ps .. ps+3 (dev: global dword planes) and republished from there when the
-// digit's magnitude changes, so the loop holds only r and the product's
-// operands and accumulator, and no LDS beyond the operand slots.
+// a^x, as sx_expt (width-4 NAF), for a = park slot src.  a^3, a^5 and a^7 are
+// parked in pk slots ps .. ps+2 (dev: global dword planes) and, like a from
+// src, republished from there when the digit's magnitude changes, so the loop
+// holds only r and the product's operands and accumulator, and no LDS beyond
+// the operand slots (in registers the odd powers spill at the 256 VGPRs of two
+// waves per SIMD; in LDS they would halve the waves).
 template <class X, class P>
-FTS_HD q2 sq_expt(X x, q2 a, const P& pk, int ps) {
-  pk.put(ps, a);
+FTS_HD q2 sq_expt(X x, const P& pk, int src, int ps) {
+  q2 a = pk.get(src);
   q2 a2 = sq_cyc_sqr(x, a);
   q2 a3 = sq_mulv(x, a2, a);
-  pk.put(ps + 1, a3);
+  pk.put(ps, a3);
   q2 a5 = sq_mulv(x, a3, a2);
-  pk.put(ps + 2, a5);
-  pk.put(ps + 3, sq_mul(x, a5));
+  pk.put(ps + 1, a5);
+  pk.put(ps + 2, sq_mul(x, a5));
   int cur = 0;
   q2 r = a;
 #pragma nounroll
@@ -207,7 +209,7 @@ FTS_HD q2 sq_expt(X x, q2 a, const P& pk, int ps) {
     if ((BN_X_W4_NZ >> i) & 1) {
       int m = ((BN_X_W4_M3 >> i) & 1) ? 3 : (((BN_X_W4_M5 >> i) & 1) ? 5 : (((BN_X_W4_M7 >> i) & 1) ? 7 : 1));
       if (m != cur) {
-        sq_pub(x, X::B, pk.get(ps + (m - 1) / 2));
+        sq_pub(x, X::B, pk.get(m == 1 ? src : ps + (m - 3) / 2));
         cur = m;
       }
       bool neg = (BN_X_W4_NEG >> i) & 1;
@@ -256,7 +258,7 @@ FTS_HD q2 sq_inv(X x, q2 f) {
 // every lane of the launch (lane = global thread index), so a wave's put / get
 // is 18 coalesced 256-byte stores / loads.  Ghost lanes neither store nor load
 // (their results are never written).  FEXP_PARK_SLOTS slots per lane.
-static constexpr int FEXP_PARK_SLOTS = 11;
+static constexpr int FEXP_PARK_SLOTS = 10;  // the Fuentes variant's 0..6 + 7..9
 struct Park {
   int32_t* base;
   uint32_t lane, stride;
@@ -293,8 +295,8 @@ struct Park {
 // fit together under the 256 of two waves per SIMD -- the compiler spilled
 // 340 VGPRs (1 KB per lane) and the kernel moved ~26x its algorithmic bytes.
 // Handing m, m^x, m^(x^2), m^(x^3) over in the park planes costs 72 bytes per
-// lane per value.  Park slots: 0 m, 1 m^x, 2 m^(x^2), 3 m^(x^3); 4..7 the
-// odd powers inside sq_expt.
+// lane per value.  Park slots: 0 m, 1 m^x, 2 m^(x^2), 3 m^(x^3); 4..6 the
+// odd powers a^3, a^5, a^7 inside sq_expt.
 //
 // easy part: m = f^((p^6-1)(p^2+1))
 template <class X>
@@ -333,7 +335,7 @@ FTS_HD fp2 sq_fexp_hard_exact(const X& x, const P& pk) {
 template <class X, class P>
 FTS_HD fp2 sq_final_exp_exact(const X& x, const fp2& f, const P& pk) {
   pk.put(0, sq_fexp_easy(x, f));
-  for (int e = 0; e < 3; e++) pk.put(e + 1, sq_expt(x, pk.get(e), pk, 4));
+  for (int e = 0; e < 3; e++) pk.put(e + 1, sq_expt(x, pk, e, 4));
   return sq_fexp_hard_exact(x, pk);
 }
 
@@ -341,7 +343,7 @@ FTS_HD fp2 sq_final_exp_exact(const X& x, const fp2& f, const P& pk) {
 // like the exact one (k_fexp_easy, k_fexp_expt, k_fexp_fc_mid1, k_fexp_expt,
 // k_fexp_fc_mid2, k_fexp_expt, k_fexp_fc_hard).  Slots: 0 t (easy part), 1 a =
 // t^x, 2 a2, 3 a6, 4 b = a6^x, 5 b^2, 6 c = (b^2)^x; the x-powers' odd powers
-// in FC_EXPT_SLOT ..+3.
+// in FC_EXPT_SLOT ..+2.
 static constexpr int FC_EXPT_SLOT = 7;
 template <class X, class P>
 FTS_HD void sq_fc_mid1(const X& x, const P& pk) {  // a2 = a^2, a6 = a2^3
@@ -367,11 +369,11 @@ FTS_HD fp2 sq_fc_hard(const X& x, const P& pk) {
 template <class X, class P>
 FTS_HD fp2 sq_final_exp(const X& x, const fp2& f, const P& pk) {
   pk.put(0, sq_fexp_easy(x, f));
-  pk.put(1, sq_expt(x, pk.get(0), pk, FC_EXPT_SLOT));
+  pk.put(1, sq_expt(x, pk, 0, FC_EXPT_SLOT));
   sq_fc_mid1(x, pk);
-  pk.put(4, sq_expt(x, pk.get(3), pk, FC_EXPT_SLOT));
+  pk.put(4, sq_expt(x, pk, 3, FC_EXPT_SLOT));
   sq_fc_mid2(x, pk);
-  pk.put(6, sq_expt(x, pk.get(5), pk, FC_EXPT_SLOT));
+  pk.put(6, sq_expt(x, pk, 5, FC_EXPT_SLOT));
   return sq_fc_hard(x, pk);
 }
 

@@ -36,14 +36,14 @@ __global__ void __launch_bounds__(64, 2) k_fexp_easy(uint32_t n, const F12Dev* f
   pk.put(0, sq_fexp_easy(x, fexp_load(fbuf, jc, x.k)));
 }
 
-// phase 2 (three launches): slot dst = (slot src)^x, odd powers parked from
-// slot ps.  24 LDS slots (A, AX, B, BX): 17.4 KB per workgroup, so LDS admits
-// the two waves per SIMD that the registers allow (the 30-slot region's 21.7 KB
-// admitted 1.75).
+// phase 2 (three launches): slot dst = (slot src)^x, a^3, a^5, a^7 parked
+// from slot ps (a is re-read from src).  24 LDS slots (A, AX, B, BX): 17.4 KB
+// per workgroup, so LDS admits the two waves per SIMD that the registers allow
+// (the 30-slot region's 21.7 KB admitted 1.75).
 __global__ void __launch_bounds__(64, 2) k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps) {
   SQ_KERNEL_PROLOGUE_B(n, 24, 12)
   FEXP_PARK
-  pk.put(dst, sq_expt(x, pk.get(src), pk, ps));
+  pk.put(dst, sq_expt(x, pk, src, ps));
 }
 
 // phase 3: hard part from slots 0..3 -> GT bytes in the membership transcript
