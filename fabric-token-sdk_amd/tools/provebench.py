@@ -25,11 +25,38 @@ def main():
     ap.add_argument("--serial", action="store_true")
     a = ap.parse_args()
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
+    import time
+
+    from zkatdlog import workload as W
     with zkatdlog.Context(g["pp"].encode(), device=0) as ctx:
         if a.serial:
             ctx.set_serial(True)
         bench.prover_bench(ctx, 4096, 1)  # warm-up: slots and tables
         print(json.dumps(bench.prover_bench(ctx, 4096, a.steps)), flush=True)
+        # one staged pass: host planning + upload (ftz_prover_load) apart from the
+        # device run (ftz_prover_run)
+        bases, sd = W.witness_bases(), W.seeds(4096, b"split")
+        ws = [dict(bases[i % len(bases)], seed=sd[32 * i:32 * i + 32]) for i in range(4096)]
+        import ctypes
+
+        from zkatdlog import _abi as A
+        arr, keep = A.pack_transfer_witnesses(ws)
+        lib = ctx._lib
+        for rep in range(3):
+            h = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            assert lib.ftz_prover_load_transfers(ctx._h, len(ws), arr, ctypes.byref(h)) == 0
+            t1 = time.perf_counter()
+            assert lib.ftz_prover_run(h) == 0
+            t2 = time.perf_counter()
+            assert lib.ftz_prover_run(h) == 0
+            t3 = time.perf_counter()
+            st = A.Stats()
+            assert lib.ftz_prover_stats(h, ctypes.byref(st)) == 0
+            lib.ftz_prover_destroy(h)
+            stage_ms = {name: round(st.ms[k], 3) for k, name in enumerate(A.PROVER_STAGE_NAMES)}
+            print(json.dumps({"plan_upload_ms": round((t1 - t0) * 1e3, 3), "run_ms": round((t2 - t1) * 1e3, 3),
+                              "rerun_ms": round((t3 - t2) * 1e3, 3), "stage_ms": stage_ms}), flush=True)
 
 
 if __name__ == "__main__":
