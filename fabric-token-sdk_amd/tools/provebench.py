@@ -23,16 +23,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--serial", action="store_true")
+    ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
+    ap.add_argument("--no-split", action="store_true")
     a = ap.parse_args()
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     import time
 
     from zkatdlog import workload as W
-    with zkatdlog.Context(g["pp"].encode(), device=0) as ctx:
+    with zkatdlog.Context(g["pp"].encode(), device=0, threads=a.threads) as ctx:
         if a.serial:
             ctx.set_serial(True)
         bench.prover_bench(ctx, 4096, 1)  # warm-up: slots and tables
-        print(json.dumps(bench.prover_bench(ctx, 4096, a.steps)), flush=True)
+        r = bench.prover_bench(ctx, 4096, a.steps)
+        r["threads"] = ctx.options["threads"]
+        print(json.dumps(r), flush=True)
+        if a.no_split:
+            return
         # one staged pass: host planning + upload (ftz_prover_load) apart from the
         # device run (ftz_prover_run)
         bases, sd = W.witness_bases(), W.seeds(4096, b"split")

@@ -5,6 +5,8 @@
 // (libftsamd.so) contains no CPU execution path; this file is never part of it.
 #include <string.h>
 
+#include <algorithm>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -272,6 +274,45 @@ long emu_prove_transfers(void* ctx, size_t n, const ftz_transfer_witness* w, uin
     return -1;
   }
   return run_prove_plan(c, p, n, buf, cap, offsets, codes);
+}
+
+// TEST-ONLY diagnostic: host time of one prover pass's planning as the device
+// path runs it (plan_prove_items_transfers on a pool of `threads`, then the
+// flattening into one blob), median of `reps`: out_ms[0] items, [1] layout +
+// write, [2] blob bytes, [3 + s] bytes of blob section s (PlanSec order).
+int emu_plan_prove_ms(void* ctx, size_t n, const ftz_transfer_witness* w, int threads, int reps, double* out_ms) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<TransferWit> t(n);
+  for (size_t i = 0; i < n; i++)
+    t[i] = {w[i].inputs, w[i].n_in, w[i].outputs, w[i].n_out, w[i].in_values, w[i].in_bfs,
+            w[i].out_values, w[i].out_bfs, w[i].type, w[i].type_len, w[i].seed};
+  WorkPool pool(threads);
+  PlanWork work;
+  FlatPlan fp;
+  std::vector<uint8_t> blob;
+  std::vector<double> a, b;
+  using Clk = std::chrono::steady_clock;
+  for (int r = 0; r < reps; r++) {
+    auto t0 = Clk::now();
+    std::string e = plan_prove_items_transfers(c->pp, n, t.data(), work, pool);
+    if (!e.empty()) return -1;
+    auto t1 = Clk::now();
+    e = flat_layout(work, true, fp);
+    if (!e.empty()) return -2;
+    if (blob.size() < fp.bytes) blob.resize(fp.bytes);
+    flat_write(work, fp, blob.data(), c->const_bytes.data(), pool);
+    auto t2 = Clk::now();
+    a.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+    b.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+  }
+  std::sort(a.begin(), a.end());
+  std::sort(b.begin(), b.end());
+  out_ms[0] = a[a.size() / 2];
+  out_ms[1] = b[b.size() / 2];
+  out_ms[2] = (double)fp.bytes;
+  for (int k = 0; k < PS_COUNT; k++)  // per-section bytes
+    out_ms[3 + k] = (double)((k + 1 < PS_COUNT ? fp.off[k + 1] : fp.bytes) - fp.off[k]);
+  return 0;
 }
 
 long emu_prove_issues(void* ctx, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap, size_t* offsets,
