@@ -140,11 +140,12 @@ def get_state_callback(ledger):
         v = lookup(k)
         if v is None:
             return 1
-        buf = hold.get(k)
-        if buf is None:
-            buf = hold[k] = ctypes.create_string_buffer(bytes(v), max(1, len(v)))
-        val[0] = ctypes.addressof(buf)
-        val_len[0] = len(v)
+        v = bytes(v)
+        ent = hold.get(k)
+        if ent is None or ent[0] != v:  # a callable ledger may answer differently later
+            ent = hold[k] = (v, ctypes.create_string_buffer(v, max(1, len(v))))
+        val[0] = ctypes.addressof(ent[1])
+        val_len[0] = len(ent[0])
         return 0
     return GET_STATE_FN(cb)
 

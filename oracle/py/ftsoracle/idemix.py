@@ -391,6 +391,42 @@ def issuer_key_check(raw):
     return True, ""
 
 
+def issuer_key_check_bn254(raw):
+    """The same IssuerPublicKey.Check for an issuer key on BN254 (IBM/idemix
+    with mathlib's BN254 curve and gurvy translator, as cmd/tokengen's testdata
+    key is): points decoded with gnark SetBytes from the proto's coordinates
+    (G1: X||Y; G2: Xa||Xb||Ya||Yb = gnark RawBytes X.A1||X.A0||Y.A1||Y.A0),
+    g2 = gnark's G2 generator, the proof data appended with mathlib's Bytes()
+    (gnark RawBytes: G1 64, G2 128 bytes) into the 18*32+3-byte buffer (576
+    bytes used, 3 zero bytes left) and HashToZr = SHA-256 mod r over all of it.
+    This is the encoding and hash the zkatdlog transcripts use (bn254.g1_bytes,
+    g2_bytes, hash_to_zr), so the key pins them.  Returns (ok, why)."""
+    from . import bn254 as C
+    try:
+        m = pb_decode(raw, IPK_S)
+    except PbError as e:
+        return False, "failed to unmarshal issuer public key: %s" % e
+    if any(m.get(k) is None for k in (2, 3, 5, 6, 7)):
+        return False, "some part of the public key is undefined"
+    try:
+        bar_g1 = C.g1_from_bytes((m[6].get(1) or b"") + (m[6].get(2) or b""))
+        bar_g2 = C.g1_from_bytes((m[7].get(1) or b"") + (m[7].get(2) or b""))
+        w = C.g2_from_bytes(b"".join(m[5].get(k) or b"" for k in (1, 2, 3, 4)))
+    except C.DecodeError as e:
+        return False, "failure [%s]" % e
+    proof_c = int.from_bytes(m.get(8) or b"", "big")
+    proof_s = int.from_bytes(m.get(9) or b"", "big")
+    neg_c = (-proof_c) % C.R
+    t1 = C.g2_add(C.g2_mul(C.G2_GEN, proof_s % C.R), C.g2_mul(w, neg_c))
+    t2 = C.g1_add(C.g1_mul(bar_g1, proof_s), C.g1_mul(bar_g2, neg_c))
+    data = (C.g2_bytes(t1) + C.g1_bytes(t2) + C.g2_bytes(C.G2_GEN) + C.g1_bytes(bar_g1) + C.g2_bytes(w)
+            + C.g1_bytes(bar_g2))
+    data += bytes(18 * 32 + 3 - len(data))
+    if proof_c != C.hash_to_zr(data):
+        return False, "zero knowledge proof in public key invalid"
+    return True, ""
+
+
 # ------------------------------------------------------------------ ASN.1 RawOwner
 def _printable(c, amp_star=True):
     return (ord("a") <= c <= ord("z") or ord("A") <= c <= ord("Z") or ord("0") <= c <= ord("9")

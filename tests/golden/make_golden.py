@@ -94,16 +94,17 @@ EXT_ASSUMPTIONS = {
                             "bn254.FinalExponentiation); the 'pp_a_fuentes' section holds proofs made under the "
                             "Fuentes-Castaneda multiple 2x(6x^2+3x+1)(p^12-1)/r for the FTZ_FEXP_FUENTES option",
     "gt_bytes": "E12.Bytes: C1.B2.A1 first ... C0.B0.A0 last, 32-byte big-endian canonical coefficients",
-    "g1_rawbytes": "X||Y big-endian canonical; infinity = 64 zero bytes (gnark bn254 has no uncompressed-infinity "
-                   "flag)",
+    "g1_rawbytes": "X||Y big-endian canonical (PINNED by cmd/tokengen's BN254 idemix issuer key); infinity = 64 zero "
+                   "bytes (gnark bn254 has no uncompressed-infinity flag; unpinned)",
     "g1_decode": "flags 00 uncompressed (coordinates reduced mod p, must be on the curve; (0,0) = infinity), "
                  "01 infinity, 10/11 compressed (smallest / largest root); anything else rejects",
-    "g2_rawbytes": "X.A1||X.A0||Y.A1||Y.A0",
+    "g2_rawbytes": "X.A1||X.A0||Y.A1||Y.A0 (PINNED: cmd/tokengen's BN254 idemix issuer key, "
+                   "tests/test_idemix.py::test_bn254_issuer_key_pins_zkatdlog_encodings)",
     "zr_equals": "raw big.Int comparison: a challenge c+r is not equal to c (rejects); responses are reduced "
                  "mod r when used",
     "element_json": "{\"curve\":<CurveID>,\"element\":<base64 Bytes()>}, BN254 = 1; a foreign curve id panics "
                     "(reported as FTZ_ERR_PANIC)",
-    "hash_to_zr": "SHA-256(bytes) as a big-endian integer mod r",
+    "hash_to_zr": "SHA-256(bytes) as a big-endian integer mod r (PINNED by the same key)",
     "json_field_matching": "Go 1.18 encoding/json: exact, else foldFunc (ASCII case folding; U+017F for s/S and "
                            "U+212A for k/K in names holding those letters); last duplicate wins",
     "json_strings": "unquoteBytes: invalid UTF-8 bytes / unpaired surrogates become U+FFFD (one per byte)",

@@ -47,7 +47,12 @@ def ipk_fixtures():
     for rel in IPK_FILES:
         raw = open(os.path.join("/root/reference", rel), "rb").read()
         ok, why = I.issuer_key_check(raw)
-        out.append({"path": rel, "raw": raw.hex(), "check_ok": ok, "why": why})
+        ok2, why2 = I.issuer_key_check_bn254(raw)
+        f = {"path": rel, "raw": raw.hex(), "check_ok": ok, "why": why, "check_bn254_ok": ok2, "why_bn254": why2}
+        isk = os.path.join("/root/reference", os.path.dirname(rel), "IssuerSecretKey")
+        if os.path.exists(isk):  # cmd/tokengen/testdata/idemix/ca holds the issuer's secret key too
+            f["isk"] = open(isk, "rb").read().hex()
+        out.append(f)
     return out
 
 

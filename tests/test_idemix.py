@@ -118,14 +118,56 @@ def test_issuer_key_proof_pins_g2_and_transcript(gold):
     finally:
         I.GEN_G2, I.g2_bytes, I.g1_bytes = saved
     assert I.issuer_key_check(raw) == (True, "")
-    # cmd/tokengen's IssuerPublicKey is copied into generated public parameters
-    # without a Check (cmd/tokengen/main_test.go:77); its G1 coordinates are not
-    # FP256BN points, so Check rejects it -- recorded, not a parity case
+    # cmd/tokengen's IssuerPublicKey is a BN254 key (test_bn254_issuer_key_pins_
+    # zkatdlog_encodings): its G1 coordinates are not FP256BN points
     for f in fx:
         if not f["check_ok"]:
             assert f["path"].startswith("cmd/tokengen/")
             tg = I.pb_decode(bytes.fromhex(f["raw"]), I.IPK_S)
             assert I.ecp_from_bytes(tg[6][1], tg[6][2]) is None
+
+
+def test_bn254_issuer_key_pins_zkatdlog_encodings(gold):
+    """cmd/tokengen/testdata/idemix/{ca,msp}/IssuerPublicKey is an idemix issuer
+    key on BN254 (mathlib's curve, gurvy translator), and ca/ holds its
+    IssuerSecretKey.  Its Check proof hashes t1 || t2 || g2 || BarG1 || W || BarG2
+    with mathlib's BN254 Bytes() and HashToZr, so accepting it pins, against
+    reference-held bytes, exactly the conventions the zkatdlog transcripts and
+    public parameters use: gnark G1 RawBytes X||Y (64 bytes), G2 RawBytes
+    X.A1||X.A0||Y.A1||Y.A0 (128 bytes), HashToZr = SHA-256 mod r, gnark's G2
+    generator (W = g2^isk) -- and the IPK Hash field = HashToZr of the proto
+    without it.  Each convention, changed, breaks it."""
+    from ftsoracle import bn254 as C
+    tg = [f for f in gold["ipk_fixtures"] if f["path"].startswith("cmd/tokengen/")]
+    assert len(tg) == 2 and all(f["check_bn254_ok"] for f in tg)
+    ok_fp = [f for f in gold["ipk_fixtures"] if f["check_ok"]]
+    assert ok_fp and not any(f["check_bn254_ok"] for f in ok_fp)  # the FP256BN keys are not BN254 keys
+    f = [f for f in tg if "isk" in f][0]
+    raw = bytes.fromhex(f["raw"])
+    assert I.issuer_key_check_bn254(raw) == (True, "")
+    m = I.pb_decode(raw, I.IPK_S)
+    w = C.g2_from_bytes(b"".join(m[5][k] for k in (1, 2, 3, 4)))
+    assert C.g2_mul(C.G2_GEN, int(f["isk"], 16)) == w
+    # IPK.Hash: HashToZr over the marshalled key without its Hash field (tag 10, 32 bytes)
+    h = m[10]
+    cut = raw.rfind(b"\x52\x20" + h)
+    assert cut > 0 and C.hash_to_zr(raw[:cut] + raw[cut + 34:]) == int.from_bytes(h, "big")
+    # negative controls
+    c = int.from_bytes(m[8], "big")
+    assert not I.issuer_key_check_bn254(raw.replace(m[8], (c ^ 1).to_bytes(32, "big")))[0]
+    saved = (C.g2_bytes, C.g1_bytes, C.hash_to_zr)
+    try:
+        C.g2_bytes = lambda P: b"".join(v.to_bytes(32, "big") for v in (P[0][0], P[0][1], P[1][0], P[1][1]))
+        assert not I.issuer_key_check_bn254(raw)[0]  # A0 before A1
+        C.g2_bytes = saved[0]
+        C.g1_bytes = lambda P: b"\x04" + saved[1](P)  # amcl-style 65-byte G1
+        assert not I.issuer_key_check_bn254(raw)[0]
+        C.g1_bytes = saved[1]
+        C.hash_to_zr = lambda d: saved[2](d.rstrip(b"\x00"))  # hashing only the 576 used bytes
+        assert not I.issuer_key_check_bn254(raw)[0]
+    finally:
+        C.g2_bytes, C.g1_bytes, C.hash_to_zr = saved
+    assert I.issuer_key_check_bn254(raw) == (True, "")
 
 
 def _twist_roots(x0):
