@@ -462,14 +462,17 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False, pp_key="pp_a"
                     "launch from rocprofv3 FETCH_SIZE (profiles/pmc_fetch.json)"}
 
 
-def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4096), **opts):
+def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4096), ctx=None, **opts):
     """The drop-in seam (BASELINE configs[1] at the Go shim's granularity): the
     shim calls ftz_verify_transfers with ONE TransferAction per call
     (validator_transfer.go:84-98).  (a) latency of one call of s transfers with
     nothing else in flight; (b) closed loop: C native threads each calling
     ftz_verify_transfers(ctx, 1, ...) back to back for `seconds`
     (csrc/tools/callers.cpp) -- throughput and per-call p50 / p99 latency.
-    Verdicts are checked against the expected codes."""
+    Verdicts are checked against the expected codes.  ctx: an existing context
+    with the wanted options (the bench's own: a second context's 13 streams
+    next to the first one's would share the 16 hardware queues), else one is
+    made with **opts."""
     import ctypes
 
     import numpy as np
@@ -480,7 +483,9 @@ def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4
     lib.ftz_callers_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.c_double, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]
     pool = W.mixed_job(valid, bad, min(valid.n, 16384), seed=11)
-    ctx = zkatdlog.Context(pp_json, device=device, **opts)
+    own = ctx is None
+    if own:
+        ctx = zkatdlog.Context(pp_json, device=device, **opts)
     try:
         lat = {}
         for s_ in (1, 16, 64, 256, 1024, 4096):
@@ -506,7 +511,8 @@ def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4
                          "verdict_mismatches": int(out[4])})
         st = ctx.options
     finally:
-        ctx.close()
+        if own:
+            ctx.close()
     return {"call_latency_ms_by_size": lat, "closed_loop_n1": loop,
             "options": {k: st[k] for k in ("batch", "slots", "window_us", "hold_inflight", "small_pass")}}
 
@@ -708,7 +714,7 @@ def main():
         if not args.no_ppb and not args.no_extras:
             ppb, ppb_job = ppb_leg(local, args, W.golden_tampered("pp_b"))
         if not args.no_seam and not args.no_extras:
-            extras["seam"] = seam_leg(pp_json, local, valid, bad, seconds=args.seam_seconds)
+            extras["seam"] = seam_leg(pp_json, local, valid, bad, seconds=args.seam_seconds, ctx=ctx)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu, extras["cpu_baselines"] = cpu_baselines(pp_json, job, ppb_job[0] if ppb_job else None,
