@@ -615,7 +615,6 @@ def main():
                     help="proofs per device pass (ftz_options.batch; default: the library's)")
     ap.add_argument("--slots", type=int, default=None, help="job-engine batch slots (ftz_options.slots)")
     ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
-    ap.add_argument("--ramp", type=int, default=None, help="job-engine pass ramp (ftz_options.ramp, default 1)")
     ap.add_argument("--serial", action="store_true",
                     help="profiling: every kernel on one stream for the whole run (ftz_ctx_set_serial), so that a "
                          "rocprofv3 kernel trace gives per-kernel durations without overlap")
@@ -640,8 +639,7 @@ def main():
     from zkatdlog.dist import bitmap_of, verify_shard
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
-    ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads,
-                           ramp=args.ramp)
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads)
     db = ctx.options["batch"]  # proofs per device pass: the engine cuts the job into passes of db
     if args.serial:
         ctx.set_serial(True)

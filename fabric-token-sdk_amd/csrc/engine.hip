@@ -165,25 +165,11 @@ void Engine::dispatcher() {
     free_slots.pop_front();
     b->parts.clear();
     b->items.clear();
-    // ramp (large calls): with the GPU idle or nearly so the first passes are
-    // B/4 and B/2 (planning and the first critical chain start sooner), and the
-    // last B of a call goes as halves down to B/4 (a shorter final chain while
-    // the pipeline drains)
-    size_t cap = B;
-    if (ctx->opt.ramp && q.front()->n >= 2 * B) {
-      if (inflight.size() == 0)
-        cap = B / 4;
-      else if (inflight.size() == 1)
-        cap = B / 2;
-      else if (pending <= B && pending > B / 4)
-        cap = (pending + 1) / 2;
-      cap = std::max<size_t>(cap, 1);
-    }
     size_t bytes = 0;
-    while (!q.empty() && b->items.size() < cap) {
+    while (!q.empty() && b->items.size() < B) {
       Request* r = q.front();
       size_t start = r->next;
-      while (r->next < r->n && b->items.size() < cap && (bytes < BATCH_PROOF_BYTES || b->items.empty())) {
+      while (r->next < r->n && b->items.size() < B && (bytes < BATCH_PROOF_BYTES || b->items.empty())) {
         bytes += item_bytes(r, r->next);
         b->items.push_back(item_of(r, r->next));
         r->next++;

@@ -55,7 +55,7 @@ class Context:
         """fexp: "exact" (FTZ_FEXP_EXACT, gnark-crypto v0.6.0) or "fuentes";
         batch / slots / window_us / threads and any other ftz_options field by name
         (hold_inflight, small_pass, msm_window_bits, msm_slot_cap, msm_seg_slots,
-        msm_glv, msm_precompute, ramp): job-engine and MSM options."""
+        msm_glv, msm_precompute): job-engine and MSM options."""
         self._lib = _abi.load()
         self.device = int(device)
         h = ctypes.c_void_p()

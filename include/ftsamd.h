@@ -113,9 +113,6 @@ typedef struct {
   uint32_t msm_slot_cap;    /*   window bits c, bucket slot cap T, slots per segment S    */
   uint32_t msm_seg_slots;
   uint32_t msm_glv;     /* 1 (default): GLV-split scalars in the MSM; 0: plain 256-bit   */
-  uint32_t ramp;        /* 1 (default): a large call's first passes and last pass are
-                           smaller (1/4, 1/2 of batch; the tail halved) so that the GPU
-                           starts sooner and the last critical chain is shorter; 0: off */
   uint32_t msm_precompute; /* 1: resident-point MSM -- ftz_msm_load also stores 2^(c w) P
                            for every window w (W x the point memory) and runs use one shared
                            bucket set and no Horner chain; for fixed bases (ftz_msm_set_scalars)
