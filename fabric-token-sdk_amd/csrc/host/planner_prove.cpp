@@ -95,11 +95,12 @@ struct PB {
     return (uint32_t)pl.seg.size() - 1;
   }
   uint32_t rnd(const std::string& tag) {
-    std::string t = tagp + tag;
     RandJob j;
     j.seed = seed_off;
-    j.tag = arena_put(t.data(), t.size());
-    j.len = (uint32_t)t.size();
+    j.tag = arena_alloc((uint32_t)(tagp.size() + tag.size()));
+    memcpy(pl.arena.data() + j.tag, tagp.data(), tagp.size());
+    memcpy(pl.arena.data() + j.tag + tagp.size(), tag.data(), tag.size());
+    j.len = (uint32_t)(tagp.size() + tag.size());
     j.out = pl.n_scal++;
     pl.rnd.push_back(j);
     return j.out;

@@ -46,11 +46,11 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->struct_size = sizeof(ftz_options);
   o->batch = 8192;
   o->slots = 4;
-  o->window_us = 2000;
+  o->window_us = 1000;
   o->threads = 0;
   o->fexp = FTZ_FEXP_EXACT;
   o->hold_inflight = 2;
-  o->small_pass = 0;
+  o->small_pass = 4096;
   o->msm_glv = 1;
 }
 

@@ -99,7 +99,8 @@ typedef struct {
   uint32_t slots;       /* batch slots of the job engine = batches in flight (default 4;
                            measured best of 4/5/6/8, profiles/r02_slots_sweep.txt)      */
   uint32_t window_us;   /* micro-batching: how long a partial batch may wait for more
-                           callers while the GPU is busy (default 2000)                 */
+                           callers while the GPU is busy (default 1000; seam sweep,
+                           profiles/r03k/seamsweep.jsonl)                                */
   uint32_t threads;     /* host planning threads (0: min(16, hardware threads))         */
   uint32_t fexp;        /* FTZ_FEXP_EXACT (default) or FTZ_FEXP_FUENTES                 */
   uint32_t hold_inflight; /* a partial batch waits (up to window_us) for more callers
@@ -108,7 +109,7 @@ typedef struct {
                            callers resubmit together; FTZ_HOLD_NEVER: ship at once)       */
   uint32_t small_pass;  /* device passes of at most this many proofs run the low-latency
                            layout of the t' / pair-2 line stage (six lanes per job
-                           instead of one; same bytes); 0 = never                        */
+                           instead of one; same bytes); default 4096, 0 = never          */
   uint32_t msm_window_bits; /* MSM planner overrides (ftz_msm_*), 0 = the planner's choice: */
   uint32_t msm_slot_cap;    /*   window bits c, bucket slot cap T, slots per segment S    */
   uint32_t msm_seg_slots;
