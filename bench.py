@@ -517,6 +517,26 @@ def seam_leg(pp_json, device, valid, bad, seconds=2.0, callers=(64, 256, 1024, 4
             "options": {k: st[k] for k in ("batch", "slots", "window_us", "hold_inflight", "small_pass")}}
 
 
+def seam_subprocess(device, seconds):
+    """The seam leg in a fresh process (tools/seamsweep.py with the default
+    options): measured inside bench.py after the other legs, the same calls ran
+    markedly slower (64 callers: 4.7k/s at p50 15 ms against 11.9k/s at 5.4 ms
+    alone, profiles/r03p), so the latency curve is taken in isolation, as a
+    validator process would run it."""
+    import subprocess
+    assert device == 0, "the seam leg runs on local device 0 (rank 0)"
+    env = dict(os.environ, SEAM_SECONDS=str(seconds))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "fabric-token-sdk_amd", "tools", "seamsweep.py"), ""],
+                       capture_output=True, text=True, env=env, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError("seam leg failed: %s" % r.stderr[-2000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    out.pop("spec", None)
+    out["process"] = "fresh (tools/seamsweep.py)"
+    return out
+
+
 def ppb_leg(device, args, bad_b):
     """BASELINE configs[0]'s 64-bit range proof (PP-B: base 16, exponent 16) on
     the GPU: the batch prover and ONE end-to-end ftz_verify_transfers call over
@@ -714,7 +734,7 @@ def main():
         if not args.no_ppb and not args.no_extras:
             ppb, ppb_job = ppb_leg(local, args, W.golden_tampered("pp_b"))
         if not args.no_seam and not args.no_extras:
-            extras["seam"] = seam_leg(pp_json, local, valid, bad, seconds=args.seam_seconds, ctx=ctx)
+            extras["seam"] = seam_subprocess(local, args.seam_seconds)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu, extras["cpu_baselines"] = cpu_baselines(pp_json, job, ppb_job[0] if ppb_job else None,
