@@ -242,6 +242,21 @@ def madpeak(device):
     return _PEAK[device]
 
 
+def valu_ceiling(device):
+    """Highest measured VALU issue rate (wave-instructions/s, chip-wide) of the
+    hot kernels' static instruction mixes (csrc/tools/madpeak.hip
+    ftz_valu_rate ops 9 and 10) at 2 and 8 waves per SIMD: the issue-rate
+    ceiling a kernel of that mix can reach on this GPU."""
+    key = ("valu", device)
+    if key not in _PEAK:
+        import ctypes
+        lib = ctypes.CDLL(os.path.join(ROOT, "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsmadpeak.so"))
+        lib.ftz_valu_rate.restype = ctypes.c_double
+        lib.ftz_valu_rate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+        _PEAK[key] = max(lib.ftz_valu_rate(device, op, w, 20000) for op in (9, 10) for w in (2, 8))
+    return _PEAK[key]
+
+
 def msm_latency(ctx, lg, reps=5, seed=7):
     """BASELINE configs[2]: latency of one BN254 G1 MSM of 2^lg points resident
     in HBM (P_i = (i + 1) G generated on the device, random 256-bit scalars),
@@ -443,14 +458,26 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False, pp_key="pp_a"
     dom = max((k for k in kern if k in names and mjob.get(k)), key=lambda k: kern[k][0])
     m_job = mjob[dom]
     achieved = m_job * kern[dom][1] * MAD_PER_M / (kern[dom][0] * 1e-3)
-    traffic = None
+    traffic = issue = None
     pmc = os.path.join(ROOT, "profiles", "pmc_fetch.json")
     if os.path.exists(pmc) and pp_key == "pp_a":
-        traffic = json.load(open(pmc)).get("per_launch_bytes", {}).get(dom)
+        pdoc = json.load(open(pmc))
+        traffic = pdoc.get("per_launch_bytes", {}).get(dom)
+        valu = pdoc.get("per_launch_valu", {})
+        if valu:
+            ceil = valu_ceiling(device)
+            rates = {k: valu[k] / (kern[k][0] * 1e-3) for k in valu if k in kern and kern[k][0] > 0}
+            issue = {"unit": "wave-inst/ns", "ceiling": round(ceil / 1e9, 1),
+                     "per_kernel": {k: {"rate": round(r / 1e9, 1), "frac": round(r / ceil, 4)}
+                                    for k, r in rates.items()},
+                     "note": "SQ_INSTS_VALU per launch (profiles/pmc_fetch.json, rocprofv3 --pmc) / serial "
+                             "kernel time, against the highest measured issue rate of the kernels' "
+                             "instruction mixes (ftz_valu_rate, live); counts every issued VALU op, "
+                             "including carries and moves the TMAD figure does not price"}
     step_mad = opc["m_per_tx"] * tx_per_s * MAD_PER_M
     return {"bound": "valu", "kernel": names[dom], "achieved": round(achieved / 1e12, 4),
             "peak": round(peak / 1e12, 4), "unit": "TMAD/s", "frac": round(achieved / peak, 4),
-            "traffic": traffic, "kernel_ms_serial": round(kern[dom][0], 3), "jobs": kern[dom][1],
+            "traffic": traffic, "issue": issue, "kernel_ms_serial": round(kern[dom][0], 3), "jobs": kern[dom][1],
             "m_per_job": round(m_job, 1),
             "serial_ms": {k: round(v[0], 3) for k, v in kern.items()},
             "per_kernel_frac": {k: round(mjob[k] * kern[k][1] * MAD_PER_M / (kern[k][0] * 1e-3) / peak, 4)

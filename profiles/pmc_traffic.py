@@ -4,7 +4,7 @@ passes (FETCH_SIZE and WRITE_SIZE in their own runs, FTZ_SERIAL=1 bench), per
 MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE is in KB and reports half the
 bytes of wide reads on gfx950 (x2 applied), WRITE_SIZE in KB.
     python profiles/pmc_traffic.py gpurun_out/pmc_fetch/p_results.db gpurun_out/pmc_write/p_results.db \\
-        > profiles/pmc_fetch.json
+        [gpurun_out/pmc_sq/p_results.db] > profiles/pmc_fetch.json
 Keys match bench.py's roofline kernel keys."""
 import collections
 import json
@@ -22,8 +22,10 @@ def per_grid(path, counter):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(fetch_db, write_db):
+def main(fetch_db, write_db, valu_db=None):
     f, w = per_grid(fetch_db, "FETCH_SIZE"), per_grid(write_db, "WRITE_SIZE")
+    vv = per_grid(valu_db, "SQ_INSTS_VALU") if valu_db else {}
+    out_valu = {}
     kb = lambda k: f.get(k, 0.0) * 2 * 1024 + w.get(k, 0.0) * 1024
 
     def grids(name):
@@ -43,17 +45,22 @@ def main(fetch_db, write_db):
             gs = [grids(n) for _, n in parts]
             if all(gs):  # the largest grid of each kernel (the verification batch)
                 out[key] = sum(m * kb((n, g[-1])) for (m, n), g in zip(parts, gs))
+                if vv:
+                    out_valu[key] = sum(m * vv.get((n, g[-1]), 0.0) for (m, n), g in zip(parts, gs))
                 break
     h = grids("k_hash")
     if h:
         out["hash"] = kb(("k_hash", h[-1]))
     raw = {"%s[grid=%d]" % k: {"fetch_kb": round(f.get(k, 0), 1), "write_kb": round(w.get(k, 0), 1)}
            for k in sorted(f) if k[0].startswith("k_")}
-    json.dump({"per_launch_bytes": {k: int(v) for k, v in out.items()}, "raw_per_launch": raw,
-               "method": "FETCH_SIZE*1024*2 + WRITE_SIZE*1024 per dispatch, FTZ_SERIAL=1 bench, separate passes"},
-              sys.stdout, indent=1)
+    doc = {"per_launch_bytes": {k: int(v) for k, v in out.items()}, "raw_per_launch": raw,
+           "method": "FETCH_SIZE*1024*2 + WRITE_SIZE*1024 per dispatch, FTZ_SERIAL=1 bench, separate passes"}
+    if out_valu:
+        doc["per_launch_valu"] = {k: int(v) for k, v in out_valu.items()}
+        doc["valu_method"] = "SQ_INSTS_VALU (wave-instructions) per dispatch, summed like the bytes"
+    json.dump(doc, sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
