@@ -51,6 +51,7 @@ struct Request {
   int rc = FTZ_SUCCESS;
   std::string err;
   bool finished = false;    // all proofs completed (under the engine mu)
+  bool solo = false;        // planned in batches of its own (after a shared batch failed to plan; under mu)
   Clock::time_point t0;
   // the caller's own wake-up: it sleeps on m / cv, not on the engine lock, so a
   // completing pass wakes exactly its callers and they do not queue on one mutex
@@ -80,6 +81,7 @@ struct Engine {
   void dispatcher();
   void completer();
   void fail_parts(ftz_batch* b, int rc, const std::string& err, std::vector<Request*>& wake);
+  void requeue_solo(ftz_batch* b);
 };
 
 static PlanItem item_of(const Request* r, size_t i) {
@@ -135,6 +137,23 @@ void Engine::fail_parts(ftz_batch* b, int rc, const std::string& err, std::vecto
   b->parts.clear();
 }
 
+// Undo the hand-out of a batch that failed to plan (mu held): each part goes
+// back to the front of the queue in its old order, its request marked solo.
+// Parts follow queue order and only the last one's request can still be queued.
+void Engine::requeue_solo(ftz_batch* b) {
+  for (size_t k = b->parts.size(); k-- > 0;) {
+    const auto& p = b->parts[k];
+    Request* r = p.req;
+    bool queued = r->next < r->n;  // not popped: it is q.front()
+    r->next = p.start;
+    pending += p.count;
+    r->solo = true;
+    if (!queued) q.push_front(r);
+  }
+  b->parts.clear();
+  b->items.clear();
+}
+
 void Engine::dispatcher() {
   (void)hipSetDevice(ctx->device);
   const size_t B = ctx->opt.batch;
@@ -168,6 +187,7 @@ void Engine::dispatcher() {
     size_t bytes = 0;
     while (!q.empty() && b->items.size() < B) {
       Request* r = q.front();
+      if (r->solo && !b->items.empty()) break;  // a solo request never shares a batch
       size_t start = r->next;
       while (r->next < r->n && b->items.size() < B && (bytes < BATCH_PROOF_BYTES || b->items.empty())) {
         bytes += item_bytes(r, r->next);
@@ -177,12 +197,22 @@ void Engine::dispatcher() {
       }
       if (r->next > start) b->parts.push_back({r, start, r->next - start});
       if (r->next == r->n) q.pop_front();
-      if (bytes >= BATCH_PROOF_BYTES) break;
+      if (bytes >= BATCH_PROOF_BYTES || r->solo) break;
     }
     lk.unlock();
     Clock::time_point t0 = Clock::now();
     int rc = slot_plan_items(b, b->items.size(), b->items.data());
     Clock::time_point t1 = Clock::now();
+    if (rc != FTZ_SUCCESS && b->parts.size() > 1) {
+      // a planning error is one caller's bad input (a limit, a null pointer):
+      // hand every request of the batch back and plan each on its own, so
+      // that the error reaches only the request that caused it
+      lk.lock();
+      requeue_solo(b);
+      free_slots.push_back(b);
+      cv_free.notify_one();
+      continue;
+    }
     if (rc == FTZ_SUCCESS) rc = slot_submit(b, true, true);
     Clock::time_point t2 = Clock::now();
     std::string err = rc == FTZ_SUCCESS ? std::string() : g_err;

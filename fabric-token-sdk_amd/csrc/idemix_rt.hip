@@ -28,6 +28,7 @@ struct ftz_idemix {
   DBuf<QDev> tab;              // HSk, HRand (and HAttrs[2]) fixed-base tables
   size_t n_hattrs = 0;         // len(IssuerPublicKey.HAttrs)
   bool heid_ok = false;        // HAttrs[2] decoded on the curve (its table exists)
+  bool strict_nym = false;     // ftz_idemix_set_strict_nym: reject off-curve nyms on the host
   PinnedMem h_eid, h_eid_ok;   // auditor owner match (ftz_audit_owners)
   DevMem d_eid, d_eid_ok;
   std::mutex mu;               // one call on the device at a time
@@ -86,6 +87,13 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
 
 void ftz_idemix_destroy(ftz_idemix* ix) { delete ix; }
 
+extern "C" int ftz_idemix_set_strict_nym(ftz_idemix* ix, int on) {
+  if (!ix) return set_err(FTZ_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->strict_nym = on != 0;
+  return FTZ_SUCCESS;
+}
+
 namespace {
 constexpr size_t NYM_CHUNK_BYTES = (size_t)1 << 30;  // keeps every blob offset in 32 bits
 constexpr size_t NYM_CHUNK_SIGS = 4096;              // signatures per pipelined device pass
@@ -109,6 +117,13 @@ int nym_chunk(ftz_idemix* ix, NymSlot& q, const ftz_owner_sig* s, size_t a, size
   });
   std::vector<uint32_t> idx;  // chunk-relative
   for (size_t i = 0; i < n; i++) {
+    if (ix->strict_nym && dec[i].code == 0) {
+      q1a nym;
+      if (!nym_point_from_be(dec[i].ints[0], dec[i].ints[1], nym)) {
+        dec[i].code = FTZ_ERR_OWNER;
+        dec[i].why = "pseudonym is not on FP256BN (strict nym import)";
+      }
+    }
     codes[a + i] = dec[i].code;
     if (dec[i].code == 0) idx.push_back((uint32_t)i);
   }

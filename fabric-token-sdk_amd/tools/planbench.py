@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Host planning time of one batch-prover pass, on the CPU (no GPU needed):
+plan_prove_items_transfers on a pool of --threads, then the flattening into one
+blob (tests/native/emu_exec.cpp emu_plan_prove_ms, TEST-ONLY build of the
+product planner).  Prints the median ms of each half and the blob bytes.
+    python fabric-token-sdk_amd/tools/planbench.py --n 4096 --threads 1
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    from conftest import build_emu
+    from zkatdlog import _abi as A
+    from zkatdlog import workload as W
+    lib = ctypes.CDLL(build_emu())
+    lib.emu_ctx_create.restype = ctypes.c_void_p
+    lib.emu_ctx_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+    lib.emu_plan_prove_ms.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.TransferWitness),
+                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
+    pp = g["pp"].encode()
+    err = ctypes.create_string_buffer(256)
+    c = lib.emu_ctx_create(pp, len(pp), err, 256)
+    assert c, err.value
+    bases, sd = W.witness_bases(), W.seeds(a.n, b"plan")
+    ws = [dict(bases[i % len(bases)], seed=sd[32 * i:32 * i + 32]) for i in range(a.n)]
+    arr, keep = A.pack_transfer_witnesses(ws)
+    out = (ctypes.c_double * 64)()
+    assert lib.emu_plan_prove_ms(c, a.n, arr, a.threads, a.reps, out) == 0
+    print(json.dumps({"n": a.n, "threads": a.threads, "items_ms": round(out[0], 2), "layout_write_ms": round(out[1], 2),
+                      "blob_mb": round(out[2] / 1e6, 2),
+                      "sections_mb": [round(out[3 + k] / 1e6, 2) for k in range(24) if out[3 + k] > 0]}))
+
+
+if __name__ == "__main__":
+    main()

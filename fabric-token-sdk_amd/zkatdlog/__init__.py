@@ -515,6 +515,11 @@ class Idemix:
         _check(self._lib.ftz_verify_owner_signatures(self._h, len(items), arr, codes), self._lib)
         return list(codes[:len(items)])
 
+    def set_strict_nym(self, on=True):
+        """opt-in: off-curve nyms are FTZ_ERR_OWNER instead of amcl's point at
+        infinity (ftz_idemix_set_strict_nym; a deliberate deviation, parity unpinned)"""
+        _check(self._lib.ftz_idemix_set_strict_nym(self._h, 1 if on else 0), self._lib)
+
     def verify_owner_signatures_packed(self, arr, n):
         """pre-packed ftz_owner_sig array (bench: the binding's packing stays out of the timed call)"""
         codes = (ctypes.c_int32 * max(n, 1))()

@@ -249,7 +249,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_token_request_decode", "ftz_verify_token_requests",
-           "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_destroy", "ftz_audit_owners",
+           "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
@@ -312,6 +312,7 @@ def load():
     lib.ftz_idemix_create.argtypes = [vp, ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
     lib.ftz_verify_owner_signatures.argtypes = [vp, sz, ctypes.POINTER(OwnerSig), ctypes.POINTER(ctypes.c_int32)]
     lib.ftz_audit_owners.argtypes = [vp, sz, ctypes.POINTER(OwnerAudit), ctypes.POINTER(ctypes.c_int32)]
+    lib.ftz_idemix_set_strict_nym.argtypes = [vp, ctypes.c_int]
     lib.ftz_idemix_destroy.argtypes = [vp]
     lib.ftz_idemix_destroy.restype = None
     lib.ftz_token_request_decode.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(Bytes), sz]

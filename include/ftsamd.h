@@ -300,6 +300,14 @@ typedef struct {
 int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curve_id, ftz_idemix** out);
 /* codes[i] = FTZ_OK, FTZ_ERR_OWNER, FTZ_ERR_SIGNATURE or FTZ_ERR_UNSUPPORTED; thread-safe */
 int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_owner_sig* s, int32_t* codes);
+/* Strict nym import (opt-in, default off).  amcl NewECPbigs turns an off-curve
+ * NymX/NymY into the point at infinity [EXT, unpinned: amcl is not in the
+ * reference], and NymSignature.Ver then accepts a signature made against the
+ * identity without any secret; parity with that reading is the default.  With
+ * on != 0 an off-curve nym is FTZ_ERR_OWNER before any curve arithmetic (a
+ * deliberate deviation from the reference, for deployments that prefer to
+ * reject until the amcl behaviour is confirmed).  Applies to later calls. */
+int ftz_idemix_set_strict_nym(ftz_idemix* ix, int on);
 void ftz_idemix_destroy(ftz_idemix* ix);
 
 /* Auditor owner inspection (the owner half of

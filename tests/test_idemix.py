@@ -380,6 +380,30 @@ def test_gpu_idemix_batch(gold, gpu_ix):
 
 
 @pytest.mark.gpu
+def test_gpu_strict_nym_opt_in(gold):
+    """ftz_idemix_set_strict_nym (opt-in): the off-curve nyms that
+    amcl reads as the identity -- including the forgery the default path accepts
+    [EXT, unpinned] -- become FTZ_ERR_OWNER; every other verdict is unchanged."""
+    import zkatdlog
+    from zkatdlog import _abi
+    g = json.load(open(os.path.join(HERE, "golden", "zkatdlog_golden.json")))["pp_a"]
+    cs = gold["cases"]
+    off = {"nym_off_curve", "off_curve_nym_forgery_accepts"}
+    assert off <= {c["name"] for c in cs}
+    with zkatdlog.Context(g["pp"].encode(), device=0) as ctx:
+        ix = zkatdlog.Idemix(ctx, bytes.fromhex(gold["ipk"]))
+        try:
+            ix.set_strict_nym(True)
+            got = ix.verify_owner_signatures(items(cs))
+            want = [_abi.FTZ_ERR_OWNER if c["name"] in off else c["expect"] for c in cs]
+            assert got == want
+            ix.set_strict_nym(False)
+            assert ix.verify_owner_signatures(items(cs)) == [c["expect"] for c in cs]
+        finally:
+            ix.close()
+
+
+@pytest.mark.gpu
 def test_gpu_owner_verifier_api(gold, gpu_ix):
     import zkatdlog
     ok = [t for c, t in zip(gold["cases"], items(gold["cases"])) if c["name"] == "valid_len_100"][0]
