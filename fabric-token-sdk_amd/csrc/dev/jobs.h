@@ -141,6 +141,14 @@ struct B64Job {
   uint32_t src, len;  // arena range
   uint32_t dst;       // offset in the proof output buffer
 };
+// prover: bytes the host does not write into the arena / proof output (a shape
+// template's image, then the witness bytes patched over it), copied on the
+// device from the wire pool
+struct CopyJob {
+  uint32_t src, len;  // wire range
+  uint32_t dst;       // arena offset, or proof-output offset when to_out
+  uint32_t to_out;
+};
 
 enum CheckKind : uint8_t { CK_STATIC = 0, CK_PTS = 1, CK_HASH = 2 };
 struct Check {
@@ -1006,6 +1014,11 @@ FTS_HD void job_rand(const RandJob& j, const uint8_t* arena, uint32_t (*scal)[8]
   uint32_t out[8];
   fe_to_int(out, v);
   for (int k = 0; k < 8; k++) scal[j.out][k] = out[k];
+}
+
+// prover: byte b of a CopyJob (k_copy: one workgroup per job, lanes stride the bytes)
+FTS_HD void job_copy_byte(const CopyJob& j, uint32_t b, const uint8_t* wire, uint8_t* arena, uint8_t* out) {
+  (j.to_out ? out : arena)[j.dst + b] = wire[j.src + b];
 }
 
 // prover output holes (EmitJob): base64 of a 32-byte big-endian scalar or of

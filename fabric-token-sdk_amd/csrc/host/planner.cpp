@@ -46,9 +46,13 @@ void Plan::clear() {
   sc_post.clear();
   emit.clear();
   b64.clear();
+  cp.clear();
+  cp2.clear();
   out.clear();
   out_off.clear();
   item_off.clear();
+  dev_pools = false;
+  arena_len = out_len = 0;
   wire.clear();
   arena.clear();
   dec.clear();
@@ -1143,6 +1147,7 @@ size_t elem_size(int s) {
     case PS_RND: return sizeof(RandJob);
     case PS_EMIT: return sizeof(EmitJob);
     case PS_B64: return sizeof(B64Job);
+    case PS_CP: case PS_CP2: return sizeof(CopyJob);
   }
   return 1;
 }
@@ -1150,7 +1155,7 @@ size_t elem_size(int s) {
 size_t piece_count(const Plan& p, int s) {
   switch (s) {
     case PS_WIRE: return p.wire.size();
-    case PS_ARENA: return p.arena.size();
+    case PS_ARENA: return p.dev_pools ? p.arena_len : p.arena.size();
     case PS_DEC: return p.dec.size();
     case PS_ZR: return p.zr.size();
     case PS_SC: return p.sc.size();
@@ -1170,23 +1175,27 @@ size_t piece_count(const Plan& p, int s) {
     case PS_SCPOST: return p.sc_post.size();
     case PS_EMIT: return p.emit.size();
     case PS_B64: return p.b64.size();
-    case PS_OUT: return p.out.size();
+    case PS_CP: return p.cp.size();
+    case PS_CP2: return p.cp2.size();
+    case PS_OUT: return p.dev_pools ? p.out_len : p.out.size();
   }
   return 0;
 }
 
-// Piece `b` (indices local to b) written at its place in the flat plan with
-// every index relocated.
-void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8_t* blob) {
+// Piece `b` (indices local to b) written at base `o` of the sections dst[s]
+// (element 0 of each) with every index relocated: the flat plan's blob, or the
+// tail of another Plan (plan_append; const-region segments keep their flag).
+void relocate_into(const Plan& b, const PieceBase& o, bool p2_g1out, bool keep_const, uint8_t* const* dst,
+                   bool copy_pools = true) {
   const uint32_t o_wire = (uint32_t)o.sec[PS_WIRE], o_arena = (uint32_t)o.sec[PS_ARENA];
   const uint32_t o_pts = o.pts, o_scal = o.scal, o_g1 = o.g1out, o_g2 = o.g2out;
   const uint32_t o_list = (uint32_t)o.sec[PS_SCLIST], o_vt = (uint32_t)o.sec[PS_VT], o_seg = (uint32_t)o.sec[PS_SEG];
   const uint32_t o_hmain = (uint32_t)o.sec[PS_HMAIN], o_ck = (uint32_t)o.sec[PS_CK], o_out = (uint32_t)o.sec[PS_OUT];
   auto rel = [](uint32_t v, uint32_t off) { return v == NONE ? NONE : v + off; };
-  if (!b.wire.empty()) memcpy(blob + fp.off[PS_WIRE] + o_wire, b.wire.data(), b.wire.size());
-  if (!b.arena.empty()) memcpy(blob + fp.off[PS_ARENA] + o_arena, b.arena.data(), b.arena.size());
-  if (!b.out.empty()) memcpy(blob + fp.off[PS_OUT] + o_out, b.out.data(), b.out.size());
-  DecodeJob* dec = fp.ptr<DecodeJob>(blob, PS_DEC) + o.sec[PS_DEC];
+  if (!b.wire.empty()) memcpy(dst[PS_WIRE] + o_wire, b.wire.data(), b.wire.size());
+  if (copy_pools && !b.arena.empty()) memcpy(dst[PS_ARENA] + o_arena, b.arena.data(), b.arena.size());
+  if (copy_pools && !b.out.empty()) memcpy(dst[PS_OUT] + o_out, b.out.data(), b.out.size());
+  DecodeJob* dec = reinterpret_cast<DecodeJob*>(dst[PS_DEC]) + o.sec[PS_DEC];
   for (DecodeJob j : b.dec) {
     j.raw += o_wire;
     j.out += o_pts;
@@ -1194,7 +1203,7 @@ void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8
     j.b64 = rel(j.b64, o_arena);
     *dec++ = j;
   }
-  ZrJob* zr = fp.ptr<ZrJob>(blob, PS_ZR) + o.sec[PS_ZR];
+  ZrJob* zr = reinterpret_cast<ZrJob*>(dst[PS_ZR]) + o.sec[PS_ZR];
   for (ZrJob j : b.zr) {
     j.raw += o_wire;
     j.out += o_scal;
@@ -1214,19 +1223,19 @@ void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8
   const int scs[3] = {PS_SC, PS_SC1, PS_SCPOST};
   const std::vector<ScalJob>* scv[3] = {&b.sc, &b.sc1, &b.sc_post};
   for (int k = 0; k < 3; k++) {
-    ScalJob* d = fp.ptr<ScalJob>(blob, (PlanSec)scs[k]) + o.sec[scs[k]];
+    ScalJob* d = reinterpret_cast<ScalJob*>(dst[scs[k]]) + o.sec[scs[k]];
     for (const ScalJob& j : *scv[k]) *d++ = rel_sc(j);
   }
-  uint32_t* sl = fp.ptr<uint32_t>(blob, PS_SCLIST) + o.sec[PS_SCLIST];
+  uint32_t* sl = reinterpret_cast<uint32_t*>(dst[PS_SCLIST]) + o.sec[PS_SCLIST];
   for (uint32_t v : b.sclist) *sl++ = v + o_scal;
-  VTerm* vt = fp.ptr<VTerm>(blob, PS_VT) + o.sec[PS_VT];
+  VTerm* vt = reinterpret_cast<VTerm*>(dst[PS_VT]) + o.sec[PS_VT];
   for (VTerm v : b.vt) {
     v.pt += o_pts;
     *vt++ = v;
   }
   for (int side = 0; side < 2; side++) {
     int sec = side ? PS_G1P : PS_G1;
-    G1Job* d = fp.ptr<G1Job>(blob, (PlanSec)sec) + o.sec[sec];
+    G1Job* d = reinterpret_cast<G1Job*>(dst[sec]) + o.sec[sec];
     for (G1Job j : (side ? b.g1p : b.g1)) {
       for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
       j.vstart += o_vt;
@@ -1237,32 +1246,33 @@ void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8
       *d++ = j;
     }
   }
-  G2Job* g2 = fp.ptr<G2Job>(blob, PS_G2) + o.sec[PS_G2];
+  G2Job* g2 = reinterpret_cast<G2Job*>(dst[PS_G2]) + o.sec[PS_G2];
   for (G2Job j : b.g2) {
     for (int k = 0; k < j.nfix; k++) j.fscal[k] += o_scal;
     j.out += o_g2;
     *g2++ = j;
   }
-  PairJob* pr = fp.ptr<PairJob>(blob, PS_PR) + o.sec[PS_PR];
+  PairJob* pr = reinterpret_cast<PairJob*>(dst[PS_PR]) + o.sec[PS_PR];
   for (PairJob j : b.pr) {
     j.p1 += o_g1;
-    j.p2 += fp.p2_g1out ? o_g1 : o_pts;
+    j.p2 += p2_g1out ? o_g1 : o_pts;
     j.q2 += o_g2;
     j.bytes += o_arena;
     *pr++ = j;
   }
-  Seg* sg = fp.ptr<Seg>(blob, PS_SEG) + o.sec[PS_SEG];
+  Seg* sg = reinterpret_cast<Seg*>(dst[PS_SEG]) + o.sec[PS_SEG];
   for (Seg s : b.seg) {
-    if (s.off & CONST_FLAG)
-      s.off &= ~CONST_FLAG;  // const region sits at absolute offset 0
-    else
+    if (s.off & CONST_FLAG) {
+      if (!keep_const) s.off &= ~CONST_FLAG;  // const region sits at absolute offset 0
+    } else {
       s.off += o_arena;
+    }
     *sg++ = s;
   }
   const int hs[2] = {PS_HPRE, PS_HMAIN};
   const std::vector<HashJob>* hv[2] = {&b.hpre, &b.hmain};
   for (int k = 0; k < 2; k++) {
-    HashJob* d = fp.ptr<HashJob>(blob, (PlanSec)hs[k]) + o.sec[hs[k]];
+    HashJob* d = reinterpret_cast<HashJob*>(dst[hs[k]]) + o.sec[hs[k]];
     for (HashJob h : *hv[k]) {
       h.seg_start += o_seg;
       h.expect = rel(h.expect, o_scal);
@@ -1270,37 +1280,53 @@ void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8
       *d++ = h;
     }
   }
-  Check* ck = fp.ptr<Check>(blob, PS_CK) + o.sec[PS_CK];
+  Check* ck = reinterpret_cast<Check*>(dst[PS_CK]) + o.sec[PS_CK];
   for (Check c : b.ck) {
     if (c.kind == CK_PTS) c.a += o_pts;
     if (c.kind == CK_HASH) c.a += o_hmain;
     *ck++ = c;
   }
-  TxChecks* tx = fp.ptr<TxChecks>(blob, PS_TX) + o.sec[PS_TX];
+  TxChecks* tx = reinterpret_cast<TxChecks*>(dst[PS_TX]) + o.sec[PS_TX];
   for (TxChecks t : b.tx) {
     t.wf_start += o_ck;
     t.rg_start += o_ck;
     *tx++ = t;
   }
-  RandJob* rnd = fp.ptr<RandJob>(blob, PS_RND) + o.sec[PS_RND];
+  RandJob* rnd = reinterpret_cast<RandJob*>(dst[PS_RND]) + o.sec[PS_RND];
   for (RandJob j : b.rnd) {
     j.seed += o_arena;
     j.tag += o_arena;
     j.out += o_scal;
     *rnd++ = j;
   }
-  EmitJob* em = fp.ptr<EmitJob>(blob, PS_EMIT) + o.sec[PS_EMIT];
+  EmitJob* em = reinterpret_cast<EmitJob*>(dst[PS_EMIT]) + o.sec[PS_EMIT];
   for (EmitJob j : b.emit) {
     j.dst += o_arena;
     j.src += j.kind == EM_ZR ? o_scal : o_arena;
     *em++ = j;
   }
-  B64Job* bj = fp.ptr<B64Job>(blob, PS_B64) + o.sec[PS_B64];
+  B64Job* bj = reinterpret_cast<B64Job*>(dst[PS_B64]) + o.sec[PS_B64];
   for (B64Job j : b.b64) {
     j.src += o_arena;
     j.dst += o_out;
     *bj++ = j;
   }
+  const int cps[2] = {PS_CP, PS_CP2};
+  const std::vector<CopyJob>* cpv[2] = {&b.cp, &b.cp2};
+  for (int k = 0; k < 2; k++) {
+    CopyJob* d = reinterpret_cast<CopyJob*>(dst[cps[k]]) + o.sec[cps[k]];
+    for (CopyJob j : *cpv[k]) {
+      j.src += o_wire;
+      j.dst += j.to_out ? o_out : o_arena;
+      *d++ = j;
+    }
+  }
+}
+
+void relocate_piece(const Plan& b, const PieceBase& o, const FlatPlan& fp, uint8_t* blob) {
+  uint8_t* dst[PS_COUNT];
+  for (int s = 0; s < PS_COUNT; s++) dst[s] = blob + fp.off[s];
+  relocate_into(b, o, fp.p2_g1out, false, dst);
 }
 
 }  // namespace
@@ -1344,14 +1370,27 @@ std::string flat_layout(const PlanWork& w, bool p2_g1out, FlatPlan& fp) {
   fp.n_scal = (uint32_t)scal;
   fp.n_g1out = (uint32_t)g1;
   fp.n_g2out = (uint32_t)g2;
+  // device-initialised pools: ARENA and OUT go last, after the uploaded sections
+  fp.dev_pools = w.used > 0;
+  for (size_t k = 0; k < w.used; k++) fp.dev_pools = fp.dev_pools && w.pieces[k].dev_pools;
+  int order[PS_COUNT], no = 0;
+  for (int s = 0; s < PS_COUNT; s++)
+    if (!fp.dev_pools || (s != PS_ARENA && s != PS_OUT)) order[no++] = s;
+  if (fp.dev_pools) {
+    order[no++] = PS_ARENA;
+    order[no++] = PS_OUT;
+  }
   size_t off = 0;
-  for (int s = 0; s < PS_COUNT; s++) {
+  for (int q = 0; q < PS_COUNT; q++) {
+    int s = order[q];
+    if (fp.dev_pools && s == PS_ARENA) fp.upload = off;
     fp.cnt[s] = cur[s];
     fp.off[s] = off;
     size_t bytes = cur[s] * elem_size(s) + (s == PS_WIRE ? WIRE_TAIL : 0);
     off = (off + bytes + SEC_ALIGN - 1) & ~(SEC_ALIGN - 1);
   }
   fp.bytes = std::max<size_t>(off, SEC_ALIGN);
+  if (!fp.dev_pools) fp.upload = fp.bytes;
   return "";
 }
 
@@ -1363,11 +1402,69 @@ void flat_write(const PlanWork& w, const FlatPlan& fp, uint8_t* blob, const uint
     const PieceBase& b = fp.base[k];
     // zero the alignment gap in front of the piece's byte pools
     size_t prev_w = k ? fp.base[k - 1].sec[PS_WIRE] + w.pieces[k - 1].wire.size() : 0;
-    size_t prev_a = k ? fp.base[k - 1].sec[PS_ARENA] + w.pieces[k - 1].arena.size() : C_SIZE;
+    size_t prev_a = k ? fp.base[k - 1].sec[PS_ARENA] + piece_count(w.pieces[k - 1], PS_ARENA) : C_SIZE;
     memset(blob + fp.off[PS_WIRE] + prev_w, 0, b.sec[PS_WIRE] - prev_w);
     memset(blob + fp.off[PS_ARENA] + prev_a, 0, b.sec[PS_ARENA] - prev_a);
     relocate_piece(p, b, fp, blob);
   });
+}
+
+PieceBase plan_append(Plan& d, const Plan& b) {
+  d.wire.resize((d.wire.size() + 15) & ~(size_t)15, 0);  // the pieces' 16-byte alignment
+  if (d.dev_pools)
+    d.arena_len = (d.arena_len + 15) & ~(size_t)15;
+  else
+    d.arena.resize((d.arena.size() + 15) & ~(size_t)15, 0);
+  PieceBase o;
+  for (int s = 0; s < PS_COUNT; s++) o.sec[s] = piece_count(d, s);
+  o.pts = d.n_pts;
+  o.scal = d.n_scal;
+  o.g1out = d.n_g1out;
+  o.g2out = d.n_g2out;
+  d.wire.resize(d.wire.size() + b.wire.size());
+  if (d.dev_pools) {
+    d.arena_len += b.arena.size();
+    d.out_len += b.out.size();
+  } else {
+    d.arena.resize(d.arena.size() + b.arena.size());
+    d.out.resize(d.out.size() + b.out.size());
+  }
+  d.dec.resize(d.dec.size() + b.dec.size());
+  d.zr.resize(d.zr.size() + b.zr.size());
+  d.sc.resize(d.sc.size() + b.sc.size());
+  d.sclist.resize(d.sclist.size() + b.sclist.size());
+  d.vt.resize(d.vt.size() + b.vt.size());
+  d.g1.resize(d.g1.size() + b.g1.size());
+  d.g1p.resize(d.g1p.size() + b.g1p.size());
+  d.g2.resize(d.g2.size() + b.g2.size());
+  d.pr.resize(d.pr.size() + b.pr.size());
+  d.seg.resize(d.seg.size() + b.seg.size());
+  d.hpre.resize(d.hpre.size() + b.hpre.size());
+  d.hmain.resize(d.hmain.size() + b.hmain.size());
+  d.ck.resize(d.ck.size() + b.ck.size());
+  d.tx.resize(d.tx.size() + b.tx.size());
+  d.rnd.resize(d.rnd.size() + b.rnd.size());
+  d.sc1.resize(d.sc1.size() + b.sc1.size());
+  d.sc_post.resize(d.sc_post.size() + b.sc_post.size());
+  d.emit.resize(d.emit.size() + b.emit.size());
+  d.b64.resize(d.b64.size() + b.b64.size());
+  d.cp.resize(d.cp.size() + b.cp.size());
+  d.cp2.resize(d.cp2.size() + b.cp2.size());
+  uint8_t* dst[PS_COUNT] = {
+      d.wire.data(), d.arena.data(), (uint8_t*)d.dec.data(), (uint8_t*)d.zr.data(), (uint8_t*)d.sc.data(),
+      (uint8_t*)d.sclist.data(), (uint8_t*)d.vt.data(), (uint8_t*)d.g1.data(), (uint8_t*)d.g1p.data(),
+      (uint8_t*)d.g2.data(), (uint8_t*)d.pr.data(), (uint8_t*)d.seg.data(), (uint8_t*)d.hpre.data(),
+      (uint8_t*)d.hmain.data(), (uint8_t*)d.ck.data(), (uint8_t*)d.tx.data(), (uint8_t*)d.rnd.data(),
+      (uint8_t*)d.sc1.data(), (uint8_t*)d.sc_post.data(), (uint8_t*)d.emit.data(), (uint8_t*)d.b64.data(),
+      (uint8_t*)d.cp.data(), (uint8_t*)d.cp2.data(), d.out.data()};
+  relocate_into(b, o, b.p2_g1out, true, dst, !d.dev_pools);
+  for (uint32_t v : b.out_off) d.out_off.push_back((uint32_t)(v + o.sec[PS_OUT]));
+  for (uint32_t v : b.item_off) d.item_off.push_back((uint32_t)(v + o.sec[PS_ARENA]));
+  d.n_pts += b.n_pts;
+  d.n_scal += b.n_scal;
+  d.n_g1out += b.n_g1out;
+  d.n_g2out += b.n_g2out;
+  return o;
 }
 
 void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out) {
@@ -1400,6 +1497,8 @@ void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out) {
   take(out.sc_post, PS_SCPOST);
   take(out.emit, PS_EMIT);
   take(out.b64, PS_B64);
+  take(out.cp, PS_CP);
+  take(out.cp2, PS_CP2);
   take(out.out, PS_OUT);
   out.out_off = fp.out_off;
   out.item_off = fp.item_off;

@@ -62,10 +62,16 @@ struct Plan {
   std::vector<ScalJob> sc_post;  // responses, after the transcript hashes
   std::vector<EmitJob> emit;
   std::vector<B64Job> b64;
+  std::vector<CopyJob> cp;        // device-side arena / output initialisation (before every other job)
+  std::vector<CopyJob> cp2;       // then the witness bytes over it
   std::vector<uint8_t> out;       // outer proof JSON templates, concatenated
   std::vector<uint32_t> out_off;  // per proof: start in `out` (plus a final end)
   std::vector<uint32_t> item_off; // openings: arena offset of the 128-byte result (recomputed | decoded)
   bool p2_g1out = false;          // PairJob.p2 indexes g1out (prover) instead of pts
+  // device-initialised pools (prover shape templates): the arena / out bytes are
+  // not held here -- cp / cp2 write them on the device -- only their lengths
+  bool dev_pools = false;
+  size_t arena_len = 0, out_len = 0;
   uint32_t n_pts = 0, n_scal = 0, n_g1out = 0, n_g2out = 0;
   void clear();
 };
@@ -130,7 +136,7 @@ class WorkPool {
 // (from pinned memory) and the device pointers are blob + offset.
 enum PlanSec : int {
   PS_WIRE, PS_ARENA, PS_DEC, PS_ZR, PS_SC, PS_SCLIST, PS_VT, PS_G1, PS_G1P, PS_G2, PS_PR, PS_SEG, PS_HPRE,
-  PS_HMAIN, PS_CK, PS_TX, PS_RND, PS_SC1, PS_SCPOST, PS_EMIT, PS_B64, PS_OUT, PS_COUNT
+  PS_HMAIN, PS_CK, PS_TX, PS_RND, PS_SC1, PS_SCPOST, PS_EMIT, PS_B64, PS_CP, PS_CP2, PS_OUT, PS_COUNT
 };
 static constexpr size_t WIRE_TAIL = 64;  // zero bytes after the wire pool (decode jobs may read past a short element)
 
@@ -144,6 +150,10 @@ struct FlatPlan {
   size_t off[PS_COUNT] = {};  // byte offset of each section in the blob
   size_t cnt[PS_COUNT] = {};  // elements (bytes for WIRE / ARENA / OUT)
   size_t bytes = 0;           // blob size
+  size_t upload = 0;          // host -> device bytes from the blob start: everything, or with
+                              // dev_pools every section before ARENA (ARENA and OUT then come
+                              // last and are written on the device; C_SIZE const bytes aside)
+  bool dev_pools = false;
   size_t n_items = 0;
   uint32_t n_pts = 0, n_scal = 0, n_g1out = 0, n_g2out = 0;
   bool p2_g1out = false;      // prover plans: PairJob.p2 indexes g1out
@@ -180,6 +190,9 @@ void flat_write(const PlanWork& w, const FlatPlan& fp, uint8_t* blob, const uint
 void plan_transfers(const PPInfo& pp, size_t n, const TransferIn* tx, Plan& out, int threads);
 void plan_issues(const PPInfo& pp, size_t n, const IssueIn* is, Plan& out, int threads);
 void plan_unflatten(const FlatPlan& fp, const uint8_t* blob, Plan& out);
+// Append b (indices local to b) to d with every index relocated (wire / arena
+// first padded to 16 bytes); returns where b's sections landed in d.
+PieceBase plan_append(Plan& d, const Plan& b);
 void plan_items_merged(const PPInfo& pp, size_t n, const PlanItem* items, Plan& out, int threads);
 
 // ------------------------------------------------------------------ prover

@@ -19,6 +19,7 @@
 // No arithmetic happens here: the planner writes tag strings, witness bytes and
 // JSON templates into the arena and emits jobs; every scalar, point, GT element,
 // hash and base64 character of the proof is produced on the GPU.
+#include <stdio.h>
 #include <string.h>
 
 #include <string>
@@ -71,13 +72,36 @@ std::string go_json_str(const char* s, size_t n) {
   return o + "\"";
 }
 
+// Witness-dependent bytes of a planned proof (ProofTpl): everything else a
+// proof's plan holds -- jobs, tags, JSON templates, arena layout -- depends only
+// on its shape.  Digit sources index k * e + i (token k, digit i).
+enum SrcKind : uint8_t {
+  SRC_SEED, SRC_IN_PT, SRC_OUT_PT, SRC_IN_VAL, SRC_IN_BF, SRC_OUT_VAL, SRC_OUT_BF, SRC_TYPE,
+  SRC_SIG_R, SRC_SIG_S, SRC_DIGIT, SRC_NONE = 0xFF
+};
+struct Patch {
+  uint8_t arena;  // 1: arena byte offset, 0: wire
+  uint8_t kind;   // SrcKind
+  uint16_t k;
+  uint32_t off, len;
+};
+
 struct PB {
   Plan& pl;
   const PPInfo& pp;
   uint32_t seed_off = 0;
   std::string tagp;  // tag prefix
   std::string err;
+  std::vector<Patch>* rec = nullptr;  // template build: where the witness bytes go
   PB(Plan& p, const PPInfo& q) : pl(p), pp(q) {}
+  void note(bool arena, uint8_t kind, uint32_t k, uint32_t off, uint32_t len) {
+    if (rec && kind != SRC_NONE) rec->push_back({(uint8_t)(arena ? 1 : 0), kind, (uint16_t)k, off, len});
+  }
+  uint32_t arena_data(const void* p, size_t n, uint8_t kind, uint32_t k = 0) {
+    uint32_t off = arena_put(p, n);
+    note(true, kind, k, off, (uint32_t)n);
+    return off;
+  }
 
   // 16-byte aligned allocations (the device SHA-256 streams aligned whole blocks)
   uint32_t arena_alloc(uint32_t n) {
@@ -106,20 +130,21 @@ struct PB {
     return j.out;
   }
   // 32-byte big-endian scalar from the wire (mod r)
-  uint32_t zr32(const uint8_t* b) {
+  uint32_t zr32(const uint8_t* b, uint8_t kind = SRC_NONE, uint32_t k = 0) {
     ZrJob j;
     pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
     j.raw = (uint32_t)pl.wire.size();
+    note(false, kind, k, j.raw, 32);
     pl.wire.insert(pl.wire.end(), b, b + 32);
     j.len = 32;
     j.out = pl.n_scal++;
     pl.zr.push_back(j);
     return j.out;
   }
-  uint32_t zr_u64(uint64_t v) {
+  uint32_t zr_u64(uint64_t v, uint8_t kind = SRC_NONE, uint32_t k = 0) {
     uint8_t b[32] = {0};
-    for (int k = 0; k < 8; k++) b[31 - k] = (uint8_t)(v >> (8 * k));
-    return zr32(b);
+    for (int q = 0; q < 8; q++) b[31 - q] = (uint8_t)(v >> (8 * q));
+    return zr32(b, kind, k);
   }
   // HashToZr of an arena range (before the group work)
   uint32_t hash_pre(uint32_t off, uint32_t len) {
@@ -161,10 +186,11 @@ struct PB {
     pl.sc_post.push_back({SOP_MADD, r, c, o, w});
     return o;
   }
-  uint32_t point(const uint8_t* raw, uint32_t len, uint32_t bytes) {
+  uint32_t point(const uint8_t* raw, uint32_t len, uint32_t bytes, uint8_t kind = SRC_NONE, uint32_t k = 0) {
     DecodeJob j;
     pl.wire.resize((pl.wire.size() + 15) & ~(size_t)15, 0);
     j.raw = (uint32_t)pl.wire.size();
+    note(false, kind, k, j.raw, len);
     pl.wire.insert(pl.wire.end(), raw, raw + len);
     j.len = len;
     j.out = pl.n_pts++;
@@ -267,7 +293,7 @@ struct PB {
                                       uint32_t h_type, const std::string& tag);
   void transfer(const TransferWit& w, size_t idx);
   void issue(const IssueWit& w, size_t idx);
-  void begin(const uint8_t* seed) { seed_off = arena_put(seed, 32); }
+  void begin(const uint8_t* seed) { seed_off = arena_data(seed, 32, SRC_SEED); }
   void checks(uint32_t first_pt) {
     TxChecks t;
     t.wf_start = (uint32_t)pl.ck.size();
@@ -316,14 +342,14 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       x /= base;
       std::string mt = tag + "/mp/" + std::to_string(k) + "/" + std::to_string(i);
       uint32_t dbf = rnd(tag + "/digit/" + std::to_string(k) + "/" + std::to_string(i) + "/bf");
-      uint32_t sd = zr_u64(d);
+      uint32_t sd = zr_u64(d, SRC_DIGIT, k * e + i);
       // Commitments[k][i] = d*Ped0 + dbf*Ped1   (range/proof.go:340-368)
       uint32_t com_off = coms + 64 * (k * e + i);
       g1job({{G1B_PED0, sd}, {G1B_PED1, dbf}}, NONE, NONE, com_off, NONE, false);
       // membership proof of d on the PS signature of d (sigproof/membership.go:112-158)
       uint32_t blinding = rnd(mt + "/sigbf"), rr = rnd(mt + "/randomize");
-      uint32_t Rd = point(pp.sig_r[d].data(), (uint32_t)pp.sig_r[d].size(), NONE);
-      uint32_t Sd = point(pp.sig_s[d].data(), (uint32_t)pp.sig_s[d].size(), NONE);
+      uint32_t Rd = point(pp.sig_r[d].data(), (uint32_t)pp.sig_r[d].size(), NONE, SRC_SIG_R, k * e + i);
+      uint32_t Sd = point(pp.sig_s[d].data(), (uint32_t)pp.sig_s[d].size(), NONE, SRC_SIG_S, k * e + i);
       // slot: [g1c 64 | GT 384 | sig JSON 235 | R' 64 | S'' 64]
       uint32_t slot = arena_alloc(64 + 384 + SIG_JSON_LEN + 128);
       uint8_t* js = &pl.arena[slot + 448];
@@ -340,7 +366,7 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       db[29] = (uint8_t)(d >> 16);
       db[30] = (uint8_t)(d >> 8);
       db[31] = (uint8_t)d;
-      uint32_t h = hash_pre(arena_put(db, 32), 32);
+      uint32_t h = hash_pre(arena_data(db, 32, SRC_DIGIT, k * e + i), 32);
       uint32_t rv = rnd(mt + "/r_value"), rh = rnd(mt + "/r_hash"), rsbf = rnd(mt + "/r_sigbf");
       // GT = FExp(e(R', rv*PK1 + rh*PK2) * e(rsbf*P, Q))   (computeCommitment, :225-257)
       uint32_t p1 = g1job({{G1B_PEDGEN, rsbf}}, NONE, NONE, NONE, NONE, true);
@@ -467,18 +493,18 @@ void PB::transfer(const TransferWit& w, size_t idx) {
   uint32_t first_pt = pl.n_pts;
   // tokens: inputs then outputs, canonical RawBytes (hashed by both transcripts)
   uint32_t tok = arena_alloc(64 * (ni + no));
-  for (uint32_t i = 0; i < ni; i++) point(w.inputs + 64 * i, 64, tok + 64 * i);
-  for (uint32_t k = 0; k < no; k++) point(w.outputs + 64 * k, 64, tok + 64 * (ni + k));
+  for (uint32_t i = 0; i < ni; i++) point(w.inputs + 64 * i, 64, tok + 64 * i, SRC_IN_PT, i);
+  for (uint32_t k = 0; k < no; k++) point(w.outputs + 64 * k, 64, tok + 64 * (ni + k), SRC_OUT_PT, k);
   std::vector<uint32_t> iv(ni), ibf(ni), ovs(no), obf(no);
   for (uint32_t i = 0; i < ni; i++) {
-    iv[i] = zr32(w.in_values + 32 * i);
-    ibf[i] = zr32(w.in_bfs + 32 * i);
+    iv[i] = zr32(w.in_values + 32 * i, SRC_IN_VAL, i);
+    ibf[i] = zr32(w.in_bfs + 32 * i, SRC_IN_BF, i);
   }
   for (uint32_t k = 0; k < no; k++) {
-    ovs[k] = zr32(w.out_values + 32 * k);
-    obf[k] = zr32(w.out_bfs + 32 * k);
+    ovs[k] = zr32(w.out_values + 32 * k, SRC_OUT_VAL, k);
+    obf[k] = zr32(w.out_bfs + 32 * k, SRC_OUT_BF, k);
   }
-  uint32_t h_type = hash_pre(arena_put(w.type, w.type_len), (uint32_t)w.type_len);
+  uint32_t h_type = hash_pre(arena_data(w.type, w.type_len, SRC_TYPE), (uint32_t)w.type_len);
   // range proof first (transfer.go:100-107), then well-formedness
   std::pair<uint32_t, uint32_t> rc(0, 0);
   if (need_range) {
@@ -556,13 +582,13 @@ void PB::issue(const IssueWit& w, size_t idx) {
   begin(w.seed);
   uint32_t first_pt = pl.n_pts;
   uint32_t tok = arena_alloc(64 * n);
-  for (uint32_t k = 0; k < n; k++) point(w.outputs + 64 * k, 64, tok + 64 * k);
+  for (uint32_t k = 0; k < n; k++) point(w.outputs + 64 * k, 64, tok + 64 * k, SRC_OUT_PT, k);
   std::vector<uint32_t> v(n), bf(n);
   for (uint32_t k = 0; k < n; k++) {
-    v[k] = zr32(w.values + 32 * k);
-    bf[k] = zr32(w.bfs + 32 * k);
+    v[k] = zr32(w.values + 32 * k, SRC_OUT_VAL, k);
+    bf[k] = zr32(w.bfs + 32 * k, SRC_OUT_BF, k);
   }
-  uint32_t h_type = hash_pre(arena_put(w.type, w.type_len), (uint32_t)w.type_len);
+  uint32_t h_type = hash_pre(arena_data(w.type, w.type_len, SRC_TYPE), (uint32_t)w.type_len);
   // issue WellFormednessProver (issue/wellformedness.go:74-184)
   const std::string t = "issue/wf";
   uint32_t rt = w.anonymous ? rnd(t + "/r_type") : NONE;
@@ -602,19 +628,165 @@ void PB::issue(const IssueWit& w, size_t idx) {
   checks(first_pt);
 }
 
-template <class W, class Fn>
-std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& work, WorkPool& pool, Fn fn) {
+// ---- shape templates.  A proof's plan depends on its witness only through
+// the bytes PB records as patches (points, scalars, seed, type, the digits'
+// signature points and values): every proof of one shape is the shape's
+// template plan appended with relocated indices (plan_append) plus those
+// bytes.  Planning a 4096-proof pass this way copies jobs instead of rebuilding
+// tag strings, JSON documents and job lists per proof.
+struct ProofTpl {
+  Plan p;
+  std::vector<Patch> patches;
+  uint32_t img_arena = 0, img_out = 0;  // the piece's wire copies of p.arena / p.out
+};
+
+// PB's value checks (transfer.go:100-107 / issue.go via range.Prover): the
+// error text of the first failing proof, and the values its digits come from
+static bool range_values(const PPInfo& pp, const uint8_t* vals, uint32_t n, bool need_range, uint64_t* out) {
+  unsigned __int128 bound = 1;
+  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
+  bool ok = true;
+  for (uint32_t k = 0; k < n; k++)
+    if (!value_u64(vals + 32 * k, out[k]) || (need_range && out[k] >= bound)) {
+      ok = false;
+      out[k] = 0;
+    }
+  return ok;
+}
+
+struct WitView {
+  const uint8_t* seed;
+  const uint8_t *in_pt, *out_pt, *in_val, *in_bf, *out_val, *out_bf;
+  const char* type;
+  const uint64_t* vals;  // output values (digits)
+};
+
+static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& o, const WitView& w, Plan& pl) {
+  const uint32_t e = (uint32_t)pp.exponent;
+  for (const Patch& q : t.patches) {
+    const uint8_t* src = nullptr;
+    uint8_t tmp[32];
+    uint32_t d = 0;
+    if (q.kind >= SRC_SIG_R) d = (uint32_t)((w.vals[q.k / e] / pp.pow[q.k % e]) % pp.base);
+    switch (q.kind) {
+      case SRC_SEED: src = w.seed; break;
+      case SRC_IN_PT: src = w.in_pt + 64 * q.k; break;
+      case SRC_OUT_PT: src = w.out_pt + 64 * q.k; break;
+      case SRC_IN_VAL: src = w.in_val + 32 * q.k; break;
+      case SRC_IN_BF: src = w.in_bf + 32 * q.k; break;
+      case SRC_OUT_VAL: src = w.out_val + 32 * q.k; break;
+      case SRC_OUT_BF: src = w.out_bf + 32 * q.k; break;
+      case SRC_TYPE: src = reinterpret_cast<const uint8_t*>(w.type); break;
+      case SRC_SIG_R: src = pp.sig_r[d].data(); break;
+      case SRC_SIG_S: src = pp.sig_s[d].data(); break;
+      case SRC_DIGIT:  // zr_u64(d) and d.Bytes() of HashToZr: the same 32 big-endian bytes
+        memset(tmp, 0, 32);
+        for (int b = 0; b < 4; b++) tmp[31 - b] = (uint8_t)(d >> (8 * b));
+        src = tmp;
+        break;
+    }
+    if (!q.len) continue;
+    if (!q.arena) {
+      memcpy(pl.wire.data() + o.sec[PS_WIRE] + q.off, src, q.len);
+    } else {  // device-initialised arena: the bytes travel in the wire pool
+      uint32_t at = (uint32_t)pl.wire.size();
+      pl.wire.insert(pl.wire.end(), src, src + q.len);
+      pl.cp2.push_back({at, q.len, (uint32_t)(o.sec[PS_ARENA] + q.off), 0});
+    }
+  }
+}
+
+// templates need every signed value's encodings to have one length
+static bool tpl_ok(const PPInfo& pp) {
+  for (uint32_t d = 0; d < pp.base; d++)
+    if (pp.sig_r[d].size() != pp.sig_r[0].size() || pp.sig_s[d].size() != pp.sig_s[0].size()) return false;
+  return pp.base > 0 && pp.exponent > 0 && pp.exponent <= 64 && pp.pow.size() == (size_t)pp.exponent;
+}
+
+struct TplCache {
+  std::vector<std::pair<std::string, ProofTpl>> v;
+  ProofTpl* find(const std::string& key) {
+    for (auto& e : v)
+      if (e.first == key) return &e.second;
+    return nullptr;
+  }
+};
+
+static std::string key_of(const TransferWit& w) {
+  char b[64];
+  snprintf(b, sizeof b, "t%u/%u/%zu", w.n_in, w.n_out, w.type_len);
+  return b;
+}
+static std::string key_of(const IssueWit& w) {
+  char b[64];
+  snprintf(b, sizeof b, "i%u/%u/%zu/", w.n_out, (unsigned)w.anonymous, w.type_len);
+  // TypeInTheClear is JSON text of the template when the issue is not anonymous
+  return w.anonymous ? std::string(b) : std::string(b) + std::string(w.type, w.type_len);
+}
+
+static void plan_one(PB& b, const TransferWit& x, size_t i) { b.transfer(x, i); }
+static void plan_one(PB& b, const IssueWit& x, size_t i) { b.issue(x, i); }
+
+static bool tpl_values(const PPInfo& pp, const TransferWit& w, uint64_t* v) {
+  return range_values(pp, w.out_values, w.n_out, !(w.n_in == 1 && w.n_out == 1), v);
+}
+static bool tpl_values(const PPInfo& pp, const IssueWit& w, uint64_t* v) {
+  return range_values(pp, w.values, w.n_out, true, v);
+}
+static WitView view_of(const TransferWit& w, const uint64_t* v) {
+  return {w.seed, w.inputs, w.outputs, w.in_values, w.in_bfs, w.out_values, w.out_bfs, w.type, v};
+}
+static WitView view_of(const IssueWit& w, const uint64_t* v) {
+  return {w.seed, nullptr, w.outputs, nullptr, nullptr, w.values, w.bfs, w.type, v};
+}
+
+template <class W>
+std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& work, WorkPool& pool) {
   size_t np = plan_piece_count(n, pool.size());
   if (work.pieces.size() < np) work.pieces.resize(np);
   work.errs.assign(np, std::string());
   work.used = np;
+  const bool tpl = tpl_ok(pp);
   pool.run(np, [&](size_t c) {
     Plan& p = work.pieces[c];
     p.clear();
+    p.p2_g1out = true;
+    p.dev_pools = tpl;
     size_t lo = n * c / np, hi = n * (c + 1) / np;
-    PB b(p, pp);
-    for (size_t i = lo; i < hi; i++) fn(b, w[i], i);
-    work.errs[c] = b.err;
+    if (!tpl) {  // direct planning (ragged signed-value encodings)
+      PB b(p, pp);
+      for (size_t i = lo; i < hi; i++) plan_one(b, w[i], i);
+      work.errs[c] = b.err;
+      return;
+    }
+    TplCache cache;
+    std::vector<uint64_t> vals;
+    for (size_t i = lo; i < hi; i++) {
+      std::string key = key_of(w[i]);
+      ProofTpl* t = cache.find(key);
+      if (!t) {
+        cache.v.emplace_back(key, ProofTpl());
+        t = &cache.v.back().second;
+        t->p.p2_g1out = true;
+        PB b(t->p, pp);
+        b.rec = &t->patches;
+        plan_one(b, w[i], i);
+        // the shape's arena and output images, once per piece (the device copies
+        // them into every proof's block, then the witness bytes over them)
+        p.wire.resize((p.wire.size() + 15) & ~(size_t)15, 0);
+        t->img_arena = (uint32_t)p.wire.size();
+        p.wire.insert(p.wire.end(), t->p.arena.begin(), t->p.arena.end());
+        t->img_out = (uint32_t)p.wire.size();
+        p.wire.insert(p.wire.end(), t->p.out.begin(), t->p.out.end());
+      }
+      vals.assign(w[i].n_out, 0);
+      if (!tpl_values(pp, w[i], vals.data()) && work.errs[c].empty())
+        work.errs[c] = "proof " + std::to_string(i) + ": can't compute range proof: value of token outside authorized range";
+      PieceBase o = plan_append(p, t->p);
+      p.cp.push_back({t->img_arena, (uint32_t)t->p.arena.size(), (uint32_t)o.sec[PS_ARENA], 0});
+      p.cp.push_back({t->img_out, (uint32_t)t->p.out.size(), (uint32_t)o.sec[PS_OUT], 1});
+      apply_patches(pp, *t, o, view_of(w[i], vals.data()), p);
+    }
   });
   for (auto& e : work.errs)
     if (!e.empty()) return e;
@@ -625,7 +797,8 @@ template <class W, class Fn>
 std::string plan_prove(const PPInfo& pp, size_t n, const W* w, Plan& out, int threads, Fn fn) {
   WorkPool pool(threads);
   PlanWork work;
-  std::string e = plan_prove_pieces(pp, n, w, work, pool, fn);
+  (void)fn;
+  std::string e = plan_prove_pieces(pp, n, w, work, pool);
   if (!e.empty()) return e;
   FlatPlan fp;
   e = flat_layout(work, true, fp);
@@ -648,11 +821,11 @@ std::string plan_prove_issues(const PPInfo& pp, size_t n, const IssueWit* w, Pla
 
 std::string plan_prove_items_transfers(const PPInfo& pp, size_t n, const TransferWit* wit, PlanWork& w,
                                        WorkPool& pool) {
-  return plan_prove_pieces(pp, n, wit, w, pool, [](PB& b, const TransferWit& x, size_t i) { b.transfer(x, i); });
+  return plan_prove_pieces(pp, n, wit, w, pool);
 }
 
 std::string plan_prove_items_issues(const PPInfo& pp, size_t n, const IssueWit* wit, PlanWork& w, WorkPool& pool) {
-  return plan_prove_pieces(pp, n, wit, w, pool, [](PB& b, const IssueWit& x, size_t i) { b.issue(x, i); });
+  return plan_prove_pieces(pp, n, wit, w, pool);
 }
 
 }  // namespace ftsh

@@ -58,6 +58,15 @@ __global__ void __launch_bounds__(256) k_emit(const EmitJob* jobs, uint32_t n, c
   job_emit(jobs[i], scal, arena);
 }
 
+// one workgroup per copy job (the prover's device-initialised arena / output
+// pools, dev/jobs.h CopyJob): lanes stride over its bytes
+__global__ void __launch_bounds__(64) k_copy(const CopyJob* jobs, uint32_t n, const uint8_t* wire, uint8_t* arena,
+                                             uint8_t* out) {
+  if (blockIdx.x >= n) return;
+  CopyJob j = jobs[blockIdx.x];
+  for (uint32_t b = threadIdx.x; b < j.len; b += blockDim.x) job_copy_byte(j, b, wire, arena, out);
+}
+
 // one workgroup per inner document: threads stride over its 3-byte groups
 __global__ void __launch_bounds__(256) k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint8_t* out) {
   if (blockIdx.x >= n) return;

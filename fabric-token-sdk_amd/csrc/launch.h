@@ -117,6 +117,7 @@ inline void launch_fexp(bool exact, const PairJob* jobs, uint32_t n, const F12De
 __global__ void k_rand(const RandJob* jobs, uint32_t n, const uint8_t* arena, uint32_t (*scal)[8]);
 __global__ void k_emit(const EmitJob* jobs, uint32_t n, const uint32_t (*scal)[8], uint8_t* arena);
 __global__ void k_b64(const B64Job* jobs, uint32_t n, const uint8_t* arena, uint8_t* out);
+__global__ void k_copy(const CopyJob* jobs, uint32_t n, const uint8_t* wire, uint8_t* arena, uint8_t* out);
 
 // standalone MSM (k_msm.hip)
 __global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, uint8_t* ok);

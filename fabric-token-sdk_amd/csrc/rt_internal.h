@@ -125,6 +125,7 @@ struct ftz_ctx {
   Engine* eng = nullptr;
   // reusable prover slots behind ftz_prove_* (one one-shot prove call at a time)
   std::mutex prove_mu;
+  ftz_prover_host_stats pstats{};  // under prove_mu
   std::vector<ftz_prover*> pslots;
   // slot behind ftz_commit_tokens / ftz_audit_openings
   std::mutex aux_mu;

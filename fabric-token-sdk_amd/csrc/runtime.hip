@@ -10,6 +10,8 @@
 // and executed as a fixed sequence of job kernels on the batch's own three
 // HIP streams (see dev/jobs.h for the job model).
 #include <hip/hip_runtime.h>
+
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -451,6 +453,7 @@ struct SlotPtrs {
   const RandJob* rnd;
   const EmitJob* emit;
   const B64Job* b64;
+  const CopyJob *cp, *cp2;
   G1Dev* pts;
   uint8_t *pt_ok, *canon, *hash_ok, *hash_ok_pre;
   uint32_t (*scal)[8];
@@ -465,7 +468,7 @@ struct SlotPtrs {
   G1Dev *vtab1, *vtab1p;
   int32_t* codes;
   uint32_t* bitmap;
-  uint32_t n_dec, n_zr, n_sc, n_sc1, n_sp, n_rnd, n_em, n_b64, n_g1, n_g1p, n_g2, n_pr, n_hp, n_hm, n_tx;
+  uint32_t n_dec, n_zr, n_sc, n_sc1, n_sp, n_rnd, n_em, n_b64, n_g1, n_g1p, n_g2, n_pr, n_hp, n_hm, n_tx, n_cp, n_cp2;
 };
 
 static SlotPtrs slot_ptrs(ftz_batch* b) {
@@ -495,6 +498,8 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   p.rnd = f.ptr<RandJob>(d, PS_RND);
   p.emit = f.ptr<EmitJob>(d, PS_EMIT);
   p.b64 = f.ptr<B64Job>(d, PS_B64);
+  p.cp = f.ptr<CopyJob>(d, PS_CP);
+  p.cp2 = f.ptr<CopyJob>(d, PS_CP2);
   const ScratchLayout& l = b->sl;
   p.pts = reinterpret_cast<G1Dev*>(s + l.pts);
   p.pt_ok = s + l.pt_ok;
@@ -530,7 +535,20 @@ static SlotPtrs slot_ptrs(ftz_batch* b) {
   p.n_hp = (uint32_t)f.cnt[PS_HPRE];
   p.n_hm = (uint32_t)f.cnt[PS_HMAIN];
   p.n_tx = (uint32_t)f.cnt[PS_TX];
+  p.n_cp = (uint32_t)f.cnt[PS_CP];
+  p.n_cp2 = (uint32_t)f.cnt[PS_CP2];
   return p;
+}
+
+// Host -> device copy of a slot's plan: the blob up to fp.upload, and with
+// device-initialised pools the const region at the start of the arena (the rest
+// of the arena and the proof output are written on the device by k_copy).
+static hipError_t upload_plan(ftz_batch* b, hipStream_t s) {
+  const FlatPlan& f = b->fp;
+  hipError_t e = hipMemcpyAsync(b->d_blob.p, b->h_blob.p, f.upload, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && f.dev_pools)
+    e = hipMemcpyAsync(b->d_blob.p + f.off[PS_ARENA], b->h_blob.p + f.off[PS_ARENA], C_SIZE, hipMemcpyHostToDevice, s);
+  return e;
 }
 
 // t' and the pair-2 lines (R read from `pts`): one lane per job (default;
@@ -582,10 +600,13 @@ int slot_submit(ftz_batch* b, bool upload, bool fetch_codes) {
   for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
   HC(hipEventRecord(e[18], s));
-  if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
+  if (upload) HC(upload_plan(b, s));
   HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
   if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));
   HC(hipEventRecord(e[0], s));
+  // shape images into every proof's arena block and output, then the witness bytes
+  if (p.n_cp) k_copy<<<p.n_cp, 64, 0, s>>>(p.cp, p.n_cp, p.wire, p.arena, p.out);
+  if (p.n_cp2) k_copy<<<p.n_cp2, 64, 0, s>>>(p.cp2, p.n_cp2, p.wire, p.arena, p.out);
   if (p.n_dec) k_decode<<<blocks_for(p.n_dec, 256), 256, 0, s>>>(p.dec, p.n_dec, p.wire, p.pts, p.pt_ok, p.arena);
   HC(hipEventRecord(e[1], s));
   if (p.n_zr) k_zr<<<blocks_for(p.n_zr, 256), 256, 0, s>>>(p.zr, p.n_zr, p.wire, p.scal, p.canon);
@@ -795,10 +816,13 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   for (int k = 0; k < FTZ_NKERNELS; k++) b->jobs_last[k] = jobs[k];
   hipEvent_t* e = b->ev;
   HC(hipEventRecord(e[18], s));
-  if (upload) HC(hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, s));
+  if (upload) HC(upload_plan(b, s));
   HC(hipMemsetAsync(p.bitmap, 0, sizeof(uint32_t) * ((b->n + 31) / 32 + 1), s));
   if (b->fp.n_pts) HC(hipMemsetAsync(p.pt_ok, 1, b->fp.n_pts, s));
   HC(hipEventRecord(e[0], s));
+  // shape images into every proof's arena block and output, then the witness bytes
+  if (p.n_cp) k_copy<<<p.n_cp, 64, 0, s>>>(p.cp, p.n_cp, p.wire, p.arena, p.out);
+  if (p.n_cp2) k_copy<<<p.n_cp2, 64, 0, s>>>(p.cp2, p.n_cp2, p.wire, p.arena, p.out);
   if (p.n_dec) k_decode<<<blocks_for(p.n_dec, 256), 256, 0, s>>>(p.dec, p.n_dec, p.wire, p.pts, p.pt_ok, p.arena);
   HC(hipEventRecord(e[1], s));
   if (p.n_zr) k_zr<<<blocks_for(p.n_zr, 256), 256, 0, s>>>(p.zr, p.n_zr, p.wire, p.scal, p.canon);
@@ -874,7 +898,7 @@ static int prover_load(ftz_ctx* c, size_t n, const W* w, int kind, ftz_prover** 
   int rc = slot_init(b);
   if (rc == FTZ_SUCCESS) rc = prover_plan(b, n, w, kind);
   if (rc == FTZ_SUCCESS) {
-    hipError_t e = hipMemcpyAsync(b->d_blob.p, b->h_blob.p, b->fp.bytes, hipMemcpyHostToDevice, b->st[0]);
+    hipError_t e = upload_plan(b, b->st[0]);
     if (e == hipSuccess) e = hipStreamSynchronize(b->st[0]);
     if (e != hipSuccess) rc = set_err(FTZ_E_DEVICE, std::string("prover upload failed: ") + hipGetErrorString(e));
   }
@@ -992,6 +1016,10 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
                          int32_t* codes) {
   std::lock_guard<std::mutex> lk(c->prove_mu);
   HC(hipSetDevice(c->device));
+  using Clk = std::chrono::steady_clock;
+  auto ms = [](Clk::time_point a, Clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const Clk::time_point t_call = Clk::now();
+  ftz_prover_host_stats& ps = c->pstats;
   // passes of at most 4096 witnesses: the prover's pass is a latency-bound
   // chain (R' -> t lines -> Miller -> final exponentiation -> challenges ->
   // responses) planned on the calling thread, and 8192-witness passes fill the
@@ -1013,7 +1041,10 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
   int rc = FTZ_SUCCESS;
   auto finish = [&](size_t k) {
     ftz_prover* p = c->pslots[k % K];
+    Clk::time_point t0 = Clk::now();
     int r = prover_wait(p);
+    Clk::time_point t1 = Clk::now();
+    ps.wait_ms += ms(t0, t1);
     if (r != FTZ_SUCCESS) return r;
     size_t lo = k * B, nb = p->fp.cnt[PS_OUT];
     if (written + nb > cap) return set_err(FTZ_E_INVALID, "proof buffer too small");
@@ -1033,6 +1064,9 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
       if (codes) codes[lo + i] = slot_codes(p)[i];
     }
     written += nb;
+    ps.copy_ms += ms(t1, Clk::now());
+    ps.passes++;
+    ps.proofs += p->n;
     return FTZ_SUCCESS;
   };
   size_t done = 0;
@@ -1043,8 +1077,12 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
     }
     ftz_prover* p = c->pslots[k % K];
     size_t lo = k * B, cnt = std::min(B, n - lo);
+    Clk::time_point t0 = Clk::now();
     rc = prover_plan(p, cnt, w + lo, kind);
+    Clk::time_point t1 = Clk::now();
     if (rc == FTZ_SUCCESS) rc = prover_submit(p, true, true);
+    ps.plan_ms += ms(t0, t1);
+    ps.submit_ms += ms(t1, Clk::now());
   }
   // drain what is in flight (also after an error, so no slot stays pending)
   int rc2 = FTZ_SUCCESS;
@@ -1057,7 +1095,16 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
   }
   if (rc == FTZ_SUCCESS) rc = rc2;
   if (rc == FTZ_SUCCESS && offsets) offsets[n] = written;
+  ps.wall_ms += ms(t_call, Clk::now());
   return rc;
+}
+
+extern "C" int ftz_ctx_prover_stats(ftz_ctx* c, ftz_prover_host_stats* out, int reset) {
+  if (!c || !out) return set_err(FTZ_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(c->prove_mu);
+  *out = c->pstats;
+  if (reset) c->pstats = ftz_prover_host_stats{};
+  return FTZ_SUCCESS;
 }
 
 extern "C" int ftz_prove_transfers(ftz_ctx* c, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,

@@ -41,8 +41,8 @@ def main():
     out = (ctypes.c_double * 64)()
     assert lib.emu_plan_prove_ms(c, a.n, arr, a.threads, a.reps, out) == 0
     print(json.dumps({"n": a.n, "threads": a.threads, "items_ms": round(out[0], 2), "layout_write_ms": round(out[1], 2),
-                      "blob_mb": round(out[2] / 1e6, 2),
-                      "sections_mb": [round(out[3 + k] / 1e6, 2) for k in range(24) if out[3 + k] > 0]}))
+                      "blob_mb": round(out[2] / 1e6, 2), "upload_mb": round(out[3] / 1e6, 2),
+                      "section_elems": [int(out[4 + k]) for k in range(24)]}))
 
 
 if __name__ == "__main__":

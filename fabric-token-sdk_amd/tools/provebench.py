@@ -34,8 +34,10 @@ def main():
         if a.serial:
             ctx.set_serial(True)
         bench.prover_bench(ctx, 4096, 1)  # warm-up: slots and tables
+        ctx.prover_stats(reset=True)
         r = bench.prover_bench(ctx, 4096, a.steps)
         r["threads"] = ctx.options["threads"]
+        r["host"] = {k: round(v, 2) if isinstance(v, float) else v for k, v in ctx.prover_stats(reset=True).items()}
         print(json.dumps(r), flush=True)
         if a.no_split:
             return

@@ -153,6 +153,12 @@ class Context:
         _check(self._lib.ftz_ctx_engine_stats(self._h, ctypes.byref(st), 1 if reset else 0), self._lib)
         return {k: getattr(st, k) for k, _ in _abi.EngineStats._fields_}
 
+    def prover_stats(self, reset=False):
+        """host-side time of ftz_prove_* (ftz_ctx_prover_stats): wait / copy / plan / submit"""
+        st = _abi.ProverHostStats()
+        _check(self._lib.ftz_ctx_prover_stats(self._h, ctypes.byref(st), 1 if reset else 0), self._lib)
+        return {k: getattr(st, k) for k, _ in _abi.ProverHostStats._fields_}
+
     def set_serial(self, serial):
         """profiling: every kernel of a batch on one stream (ftz_ctx_set_serial)"""
         _check(self._lib.ftz_ctx_set_serial(self._h, 1 if serial else 0), self._lib)

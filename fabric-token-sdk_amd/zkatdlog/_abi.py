@@ -161,6 +161,12 @@ def pack_openings(openings):
     return arr, keep
 
 
+class ProverHostStats(ctypes.Structure):
+    _fields_ = [("passes", ctypes.c_uint64), ("proofs", ctypes.c_uint64), ("wait_ms", ctypes.c_double),
+                ("copy_ms", ctypes.c_double), ("plan_ms", ctypes.c_double), ("submit_ms", ctypes.c_double),
+                ("wall_ms", ctypes.c_double)]
+
+
 class EngineStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("proofs", ctypes.c_uint64), ("plan_ms", ctypes.c_double),
                 ("submit_ms", ctypes.c_double), ("device_ms", ctypes.c_double), ("wall_ms", ctypes.c_double),
@@ -250,7 +256,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_token_request_decode", "ftz_verify_token_requests",
            "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
-           "ftz_prove_transfers", "ftz_prove_issues", "ftz_prover_load_transfers", "ftz_prover_load_issues",
+           "ftz_prove_transfers", "ftz_prove_issues", "ftz_ctx_prover_stats", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
 _lib = None
@@ -280,6 +286,7 @@ def load():
     lib.ftz_audit_openings.argtypes = [vp, sz, ctypes.c_char_p, ctypes.POINTER(TokenOpening),
                                        ctypes.POINTER(ctypes.c_int32)]
     lib.ftz_ctx_engine_stats.argtypes = [vp, ctypes.POINTER(EngineStats), ctypes.c_int]
+    lib.ftz_ctx_prover_stats.argtypes = [vp, ctypes.POINTER(ProverHostStats), ctypes.c_int]
     lib.ftz_ctx_destroy.argtypes = [vp]
     lib.ftz_ctx_destroy.restype = None
     lib.ftz_last_error.restype = ctypes.c_char_p

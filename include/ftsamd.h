@@ -192,6 +192,21 @@ typedef struct {
 } ftz_engine_stats;
 int ftz_ctx_engine_stats(ftz_ctx* ctx, ftz_engine_stats* out, int reset);
 
+/* Host-side time of ftz_prove_transfers / ftz_prove_issues since context
+ * creation (or the last reset), summed over device passes: waiting for a pass
+ * to finish, copying its proofs into the caller's buffer, planning + flattening
+ * the next pass into pinned staging, and enqueueing it (H2D copy + launches). */
+typedef struct {
+  uint64_t passes;
+  uint64_t proofs;
+  double wait_ms;
+  double copy_ms;
+  double plan_ms;
+  double submit_ms;
+  double wall_ms;    /* sum over calls, entry -> return */
+} ftz_prover_host_stats;
+int ftz_ctx_prover_stats(ftz_ctx* ctx, ftz_prover_host_stats* out, int reset);
+
 /* Staged form: plan + upload once, then run the GPU pipeline on resident
  * inputs any number of times (used by bench.py to time the device path).
  * One staged batch is one device pass: n must keep every job pool of the

@@ -214,6 +214,10 @@ static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t ca
   memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
   std::vector<uint8_t> wire = p.wire;
   wire.resize(wire.size() + 64, 0);
+  // device-initialised pools (k_copy): shape images, then the witness bytes
+  for (const auto* cps : {&p.cp, &p.cp2})
+    for (const CopyJob& j : *cps)
+      for (uint32_t b = 0; b < j.len; b++) job_copy_byte(j, b, wire.data(), p.arena.data(), p.out.data());
   std::vector<G1Dev> pts(std::max<uint32_t>(p.n_pts, 1));
   std::vector<uint8_t> pt_ok(std::max<uint32_t>(p.n_pts, 1), 1);
   std::vector<uint32_t> scalv(8 * (size_t)std::max<uint32_t>(p.n_scal, 1));
@@ -279,7 +283,8 @@ long emu_prove_transfers(void* ctx, size_t n, const ftz_transfer_witness* w, uin
 // TEST-ONLY diagnostic: host time of one prover pass's planning as the device
 // path runs it (plan_prove_items_transfers on a pool of `threads`, then the
 // flattening into one blob), median of `reps`: out_ms[0] items, [1] layout +
-// write, [2] blob bytes, [3 + s] bytes of blob section s (PlanSec order).
+// write, [2] blob bytes, [3] bytes uploaded (fp.upload), [4 + s] elements of
+// section s (PlanSec order).
 int emu_plan_prove_ms(void* ctx, size_t n, const ftz_transfer_witness* w, int threads, int reps, double* out_ms) {
   EmuCtx* c = (EmuCtx*)ctx;
   std::vector<TransferWit> t(n);
@@ -310,8 +315,8 @@ int emu_plan_prove_ms(void* ctx, size_t n, const ftz_transfer_witness* w, int th
   out_ms[0] = a[a.size() / 2];
   out_ms[1] = b[b.size() / 2];
   out_ms[2] = (double)fp.bytes;
-  for (int k = 0; k < PS_COUNT; k++)  // per-section bytes
-    out_ms[3 + k] = (double)((k + 1 < PS_COUNT ? fp.off[k + 1] : fp.bytes) - fp.off[k]);
+  out_ms[3] = (double)fp.upload;
+  for (int k = 0; k < PS_COUNT; k++) out_ms[4 + k] = (double)fp.cnt[k];
   return 0;
 }
 

@@ -105,6 +105,35 @@ def test_emu_issue_proofs_match_oracle(emu, pp_a, anonymous):
     assert got[0] == oracle_issue(pp, w)
 
 
+def test_emu_shape_templates_mixed_batch(emu, pp_a):
+    """One planning call over interleaved shapes (the planner plans each shape
+    once and appends the relocated template per proof, patching in the witness
+    bytes): every proof -- different values, hence different digits, signature
+    points and digit hashes per proof -- byte-identical to the oracle's; issues
+    with two TypeInTheClear strings keep their own templates."""
+    js, pp = pp_a
+    shapes = [(2, 2), (1, 1), (2, 2), (1, 2), (2, 2), (1, 1)]
+    ws = []
+    for i, (ni, no) in enumerate(shapes):
+        w = witness(pp, 900 + i, ni, no)
+        if ni != no:
+            v = sum(w["in_values"]) % (pp.base ** pp.exponent)
+            w["out_values"] = [v // 3, v - v // 3]
+            w["_outs"] = [Z.token_commitment(pp, "ABC", a, b) for a, b in zip(w["out_values"], w["out_bfs"])]
+            w["outputs"] = b"".join(C.g1_bytes(p) for p in w["_outs"])
+        ws.append(w)
+    got, codes = emu_prove(emu, js, ws)
+    assert codes == [0] * len(ws)
+    for g, w in zip(got, ws):
+        assert g == oracle_transfer(pp, w)
+    iw = [issue_witness(pp, 950 + i, 2, ttype=t, anonymous=a)
+          for i, (t, a) in enumerate([("ABC", False), ("XY", False), ("ABC", False), ("Q", True)])]
+    got, codes = emu_prove(emu, js, iw, issue=True)
+    assert codes == [0] * len(iw)
+    for g, w in zip(got, iw):
+        assert g == oracle_issue(pp, w)
+
+
 def test_emu_value_out_of_range(emu, pp_a):
     js, pp = pp_a
     w = witness(pp, 5, 2, 2)
