@@ -197,132 +197,167 @@ __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, 
 }
 
 // ---- 4-lane cooperative point arithmetic for the serial Horner chain.  A
-// wave issues a one-lane Montgomery product at the cost of a 64-lane one, so
-// the chain's latency is the number of dependent products: every lane holds
-// the same point, lane k < 4 computes the k-th independent product of each
-// dependency level, and the products are exchanged through LDS.
-struct Coop {
-  int k;
-  uint32_t (*sh)[8];
-  // one level: lane k computes a_k * b_k (k < cnt); returns all cnt products
-  __device__ void level(int cnt, const fp* a, const fp* b, fp* out) const {
-    fp x = a[0], y = b[0];
+// wave issues a one-lane product at the cost of a 64-lane one, so the chain's
+// latency is the number of dependent products times one product's latency:
+// every lane holds the same point, lane k (mod 4) computes the k-th independent
+// product of each dependency level (f29_mul_c: carry-free, column sums, short
+// dependent chains; every quad of lanes does the same) and the lanes read the
+// products of their quad through DPP quad_perm broadcasts (values stay in vector
+// registers: read as uniform values, v_readlane, the compiler moved the point
+// formulas to the scalar unit and spilled).  Same operations as j29_dbl / j29_add (dev/fp29.h) grouped
+// into levels, so the same limbs.
+// out[I..CNT) = the products of lanes I.. of this lane's quad (DPP quad_perm broadcast)
+template <int I, int CNT>
+__device__ __forceinline__ void quad_get(const f29& r, f29 (&out)[CNT]) {
+  if constexpr (I < CNT) {
 #pragma unroll
-    for (int i = 1; i < 4; i++)
-      if (i < cnt && k == i) {
-        x = a[i];
-        y = b[i];
-      }
-    fp r = x * y;
-    if (k < cnt)
-#pragma unroll
-      for (int q = 0; q < 8; q++) sh[k][q] = r.v[q];
-    __syncthreads();
-    for (int i = 0; i < cnt; i++)
-#pragma unroll
-      for (int q = 0; q < 8; q++) out[i].v[q] = sh[i][q];
-    __syncthreads();
+    for (int q = 0; q < 9; q++) out[I].l[q] = __builtin_amdgcn_mov_dpp(r.l[q], 0x55 * I, 0xF, 0xF, false);
+    quad_get<I + 1, CNT>(r, out);
   }
-};
-
-// dbl-2009-l (same values as jac_dbl): 3 product levels instead of 7 products
-__device__ g1j coop_dbl(const Coop& c, const g1j& p) {
-  fp o[4];
-  {
-    fp a[4] = {p.x, p.y, p.y, p.y}, b[4] = {p.x, p.y, p.z, p.z};
-    c.level(3, a, b, o);
-  }
-  fp A = o[0], B = o[1], YZ = o[2];
-  fp E = A + A + A, s = p.x + B;
-  {
-    fp a[4] = {B, s, E, E}, b[4] = {B, s, E, E};
-    c.level(3, a, b, o);
-  }
-  fp C = o[0], D = o[1] - A - C;
-  D = D + D;
-  fp X3 = o[2] - D - D;
-  {
-    fp dx = D - X3;
-    fp a[4] = {E, E, E, E}, b[4] = {dx, dx, dx, dx};
-    c.level(1, a, b, o);
-  }
-  fp C8 = C + C;
-  C8 = C8 + C8;
-  C8 = C8 + C8;
-  return {X3, o[0] - C8, YZ + YZ};
 }
 
-// add-2007-bl (same values as jac_add_inl): 6 product levels instead of 16 products
-__device__ g1j coop_add(const Coop& c, const g1j& p, const g1j& q) {
-  if (is_zero(p.z)) return q;
-  if (is_zero(q.z)) return p;
-  fp o[4];
+template <int CNT>
+__device__ __forceinline__ void coop29_level(const f29 (&a)[CNT], const f29 (&b)[CNT], f29 (&out)[CNT]) {
+  const int k = (int)(threadIdx.x & 3);  // every quad of lanes computes the level
+  f29 x = a[0], y = b[0];
+#pragma unroll
+  for (int i = 1; i < CNT; i++)
+    if (k == i) {
+      x = a[i];
+      y = b[i];
+    }
+  quad_get<0, CNT>(f29_mul_c(x, y), out);
+}
+
+// dbl-2009-l (j29_dbl) in place: 3 product levels instead of 7 products.  The
+// point lives in plain variables (a j29 carried through the loop with its flag
+// was kept in scratch memory)
+__device__ __forceinline__ void coop29_dbl(f29& X, f29& Y, f29& Z) {
+  f29 A, Bq, Z3, C, T2, F, Y3a;
   {
-    fp a[4] = {p.z, q.z, p.z, p.z}, b[4] = {p.z, q.z, q.z, q.z};
-    c.level(3, a, b, o);
+    f29 a[3] = {X, Y, f29_add(Y, Y)}, b[3] = {X, Y, Z}, o[3];
+    coop29_level<3>(a, b, o);
+    A = o[0];
+    Bq = o[1];
+    Z3 = o[2];
   }
-  fp Z1Z1 = o[0], Z2Z2 = o[1], Z1Z2 = o[2];
+  f29 E = f29_norm(f29_add(f29_add(A, A), A));
   {
-    fp a[4] = {p.x, q.x, p.y, q.y}, b[4] = {Z2Z2, Z1Z1, q.z, p.z};
-    c.level(4, a, b, o);
+    f29 t = f29_norm(f29_add(X, Bq));
+    f29 a[3] = {Bq, t, E}, b[3] = {Bq, t, E}, o[3];
+    coop29_level<3>(a, b, o);
+    C = o[0];
+    T2 = o[1];
+    F = o[2];
   }
-  fp U1 = o[0], U2 = o[1];
+  f29 D1 = f29_norm(f29_sub(f29_sub(T2, A), C));
+  f29 D = f29_add(D1, D1);
+  f29 X3 = f29_reduce(f29_sub(f29_norm(f29_sub(F, D)), D));
   {
-    fp a[4] = {o[2], o[3], o[2], o[2]}, b[4] = {Z2Z2, Z1Z1, Z2Z2, Z2Z2};
-    c.level(2, a, b, o);
+    f29 a[1] = {E}, b[1] = {f29_norm(f29_sub(D, X3))}, o[1];
+    coop29_level<1>(a, b, o);
+    Y3a = o[0];
   }
-  fp S1 = o[0];
-  fp H = U2 - U1, rr = o[1] - S1;
-  if (is_zero(H)) {
-    if (is_zero(rr)) return coop_dbl(c, p);
-    return jac_inf<fp>();
+  f29 C2 = f29_add(C, C);
+  f29 C4 = f29_norm(f29_add(C2, C2));
+  X = X3;
+  Y = f29_reduce(f29_sub(Y3a, f29_add(C4, C4)));
+  Z = Z3;
+}
+
+// add-2007-bl (j29_add) in place, (X, Y, Z, inf) += q: 5 product levels
+// instead of 16 products
+__device__ __forceinline__ void coop29_add(f29& X, f29& Y, f29& Z, bool& inf, const j29& q) {
+  if (q.inf) return;
+  if (inf) {
+    X = q.x;
+    Y = q.y;
+    Z = q.z;
+    inf = false;
+    return;
   }
-  fp H2 = H + H;
-  rr = rr + rr;
+  f29 Z1Z1, Z2Z2, ZZ, U1, U2, t1, t2, S1, S2, I, J, V, R2, Z3p, Y3a, SJ;
   {
-    fp a[4] = {H2, rr, Z1Z2, Z1Z2}, b[4] = {H2, rr, H, H};
-    c.level(3, a, b, o);
+    f29 zs = f29_norm(f29_add(Z, q.z));
+    f29 a[3] = {Z, q.z, zs}, b[3] = {Z, q.z, zs}, o[3];
+    coop29_level<3>(a, b, o);
+    Z1Z1 = o[0];
+    Z2Z2 = o[1];
+    ZZ = o[2];
   }
-  fp I = o[0], R2 = o[1], Zh = o[2];
   {
-    fp a[4] = {H, U1, H, H}, b[4] = {I, I, I, I};
-    c.level(2, a, b, o);
+    f29 a[4] = {X, q.x, q.z, Z}, b[4] = {Z2Z2, Z1Z1, Z2Z2, Z1Z1}, o[4];
+    coop29_level<4>(a, b, o);
+    U1 = o[0];
+    U2 = o[1];
+    t1 = o[2];
+    t2 = o[3];
   }
-  fp J = o[0], V = o[1];
-  fp X3 = R2 - J - V - V;
+  f29 H = f29_norm(f29_sub(U2, U1));
+  f29 H2 = f29_norm(f29_add(H, H));
   {
-    fp vx = V - X3;
-    fp a[4] = {rr, S1, rr, rr}, b[4] = {vx, J, vx, vx};
-    c.level(2, a, b, o);
+    f29 a[3] = {Y, q.y, H2}, b[3] = {t1, t2, H2}, o[3];
+    coop29_level<3>(a, b, o);
+    S1 = o[0];
+    S2 = o[1];
+    I = o[2];
   }
-  return {X3, o[0] - o[1] - o[1], Zh + Zh};
+  f29 rr = f29_sub(S2, S1);
+  f29 r2 = f29_norm(f29_add(rr, rr));
+  {
+    f29 zd = f29_norm(f29_sub(f29_sub(ZZ, Z1Z1), Z2Z2));
+    f29 a[4] = {H, U1, r2, zd}, b[4] = {I, I, r2, H}, o[4];
+    coop29_level<4>(a, b, o);
+    J = o[0];
+    V = o[1];
+    R2 = o[2];
+    Z3p = o[3];
+  }
+  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sub(R2, J), V), V));
+  {
+    f29 a[2] = {r2, S1}, b[2] = {f29_norm(f29_sub(V, X3)), J}, o[2];
+    coop29_level<2>(a, b, o);
+    Y3a = o[0];
+    SJ = o[1];
+  }
+  f29 Y3 = f29_reduce(f29_sub(f29_sub(Y3a, SJ), SJ));
+  f29 Z3 = f29_reduce(Z3p);
+  if (f29_reduced_zero(Z3)) {  // H == 0: p == q (a doubling) or p == -q (infinity)
+    if (f29_is_zero(rr))
+      coop29_dbl(X, Y, Z);
+    else
+      inf = true;
+    return;
+  }
+  X = X3;
+  Y = Y3;
+  Z = Z3;
 }
 
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
-// on one wave with the 4-lane cooperative point ops (measured: 0.55 ms at 2^20
-// against 1.3 ms for one lane in the carry-free form -- four independent
-// 32-bit products per level beat one carry-free chain); the last call (w_lo = 0)
-// converts to affine (binary-EEA inverse) and gnark RawBytes.  With pre (one
-// reduction window) this is the affine conversion alone.
+// on one wave with the 4-lane cooperative carry-free point ops; the last call
+// (w_lo = 0) converts to affine (binary-EEA inverse) and gnark RawBytes.  With
+// pre (one reduction window) this is the affine conversion alone.
 __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
                                                    G1JDev* acc_buf, G1Dev* res, uint8_t* bytes) {
-  __shared__ uint32_t sh[4][8];
   if (blockIdx.x != 0) return;
-  Coop c{(int)threadIdx.x, sh};
-  g1j acc = w_hi == p.rw ? jac_inf<fp>() : g1j_load(*acc_buf);
+  j29 a0 = w_hi == p.rw ? j29_inf() : j29_ld(*acc_buf);
+  f29 X = a0.x, Y = a0.y, Z = a0.z;
+  bool inf = a0.inf;
   for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
-    if (w != (int)p.rw - 1)
-      for (uint32_t q = 0; q < p.c; q++) acc = coop_dbl(c, acc);
-    acc = coop_add(c, acc, g1j_load(wsum[w]));
+    if (w != (int)p.rw - 1 && !inf)
+      for (uint32_t q = 0; q < p.c; q++) coop29_dbl(X, Y, Z);
+    coop29_add(X, Y, Z, inf, j29_ld(wsum[w]));
   }
   if (threadIdx.x != 0) return;
-  g1j_store(*acc_buf, acc);
+  g1j a = j29_to({X, Y, Z, inf});
+  g1j_store(*acc_buf, a);
   if (w_lo == 0) {
     g1a r;
-    r.inf = is_zero(acc.z);
-    fp zi = fp_inv_var(acc.z), zi2 = sqr(zi);
-    r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
-    r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
+    r.inf = is_zero(a.z);
+    fp zi = fp_inv_var(a.z), zi2 = sqr(zi);
+    r.x = r.inf ? fe_zero<ModP>() : a.x * zi2;
+    r.y = r.inf ? fe_zero<ModP>() : a.y * zi2 * zi;
     G1Dev d;
     g1_store(d, r);
     *res = d;
