@@ -354,9 +354,11 @@ def prover_bench(ctx, batch, steps):
     n = batch * steps
     sel = np.arange(n) % len(bases)
     wp, wn, keep = A.pack_transfer_witnesses_tiled(bases, sel, W.seeds(n, b"bench-prover"))
+    ctx.prover_stats(reset=True)
     t0 = time.perf_counter()
     blob, offs, codes = ctx.prove_packed("transfer", wp, wn)
     dt = time.perf_counter() - t0
+    host = ctx.prover_stats(reset=True)
     ins = np.frombuffer(b"".join(b["inputs"] for b in bases), dtype=np.uint8)
     outs = np.frombuffer(b"".join(b["outputs"] for b in bases), dtype=np.uint8)
     rows = np.zeros(n, dtype=A.transfer_dtype())
@@ -369,7 +371,11 @@ def prover_bench(ctx, batch, steps):
     v = ctx.verify_transfers_packed(ctypes.cast(rows.ctypes.data, ctypes.POINTER(A.Transfer)), n)
     return {"proofs_per_s": round(n / dt, 1), "ms_per_batch": round(dt / steps * 1e3, 3), "batch": batch,
             "proofs": n, "bytes_per_proof": round(float(offs[-1]) / n, 1),
-            "all_accepted_by_gpu_verifier": bool((codes == 0).all() and (v == 0).all())}
+            "all_accepted_by_gpu_verifier": bool((codes == 0).all() and (v == 0).all()),
+            # host-side time of the call per pass (ftz_ctx_prover_stats): planning +
+            # flattening (shape templates), enqueue, wait for the device, proof copy-out
+            "host_ms_per_pass": {k[:-3]: round(host[k] / max(1, host["passes"]), 3)
+                                 for k in ("plan_ms", "submit_ms", "wait_ms", "copy_ms")}}
 
 
 def device_only(ctx, job, batch, steps, inflight=4):

@@ -133,6 +133,41 @@ FTS_HD f29 f29_mul_c(const f29& a, const f29& b) {
   return r;
 }
 
+// f29_sqr's value by f29_mul_c's scheme: column sums with the cross products
+// once (doubled operand, L <= 1), then the same 9 reduction steps
+FTS_HD f29 f29_sqr_c(const f29& a) {
+  FTS_COUNT_MUL();
+  int32_t d[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a.l[i] + a.l[i];
+  int64_t c[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) c[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    c[2 * i] += (int64_t)a.l[i] * a.l[i];
+#pragma unroll
+    for (int j = i + 1; j < 9; j++) c[i + j] += (int64_t)d[i] * a.l[j];
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const uint32_t m = ((uint32_t)c[k] * P29_INV) & (uint32_t)F29_MASK;
+    const int64_t t = c[k] + (int64_t)(int32_t)m * P29[0];
+#pragma unroll
+    for (int j = 1; j < 9; j++) c[k + j] += (int64_t)(int32_t)m * P29[j];
+    c[k + 1] += t >> 29;
+  }
+  f29 r;
+#pragma unroll
+  for (int k = 9; k < 16; k++) {
+    r.l[k - 9] = (int32_t)(c[k] & F29_MASK);
+    c[k + 1] += c[k] >> 29;
+  }
+  r.l[7] = (int32_t)(c[16] & F29_MASK);
+  r.l[8] = (int32_t)(c[16] >> 29);
+  return r;
+}
+
 // a^2 / 2^261: the cross products once with a doubled operand (requires L <= 1)
 FTS_HD f29 f29_sqr(const f29& a) {
   FTS_COUNT_MUL();

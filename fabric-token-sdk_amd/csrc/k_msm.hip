@@ -216,36 +216,59 @@ __device__ __forceinline__ void quad_get(const f29& r, f29 (&out)[CNT]) {
   }
 }
 
+// the operand of lane k (mod 4): a per-limb select chain on values pinned in
+// vector registers (an empty asm per limb: otherwise the compiler turned the
+// selects into loads from a dynamically indexed stack copy of the operands)
+__device__ __forceinline__ f29 lane_sel(int k, const f29& v0, const f29& v1, const f29& v2, const f29& v3) {
+  f29 r;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    int32_t x0 = v0.l[q], x1 = v1.l[q], x2 = v2.l[q], x3 = v3.l[q];
+    asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+    int32_t t = k == 1 ? x1 : x0;
+    t = k == 2 ? x2 : t;
+    r.l[q] = k == 3 ? x3 : t;
+  }
+  return r;
+}
+
+// a level of squarings only (f29_sqr_c: 45 limb products instead of 81)
+template <int CNT>
+__device__ __forceinline__ void coop29_sqr_level(const f29 (&a)[CNT], f29 (&out)[CNT]) {
+  const int k = (int)(threadIdx.x & 3);
+  quad_get<0, CNT>(f29_sqr_c(lane_sel(k, a[0], a[CNT > 1 ? 1 : 0], a[CNT > 2 ? 2 : 0], a[CNT > 3 ? 3 : 0])), out);
+}
+
 template <int CNT>
 __device__ __forceinline__ void coop29_level(const f29 (&a)[CNT], const f29 (&b)[CNT], f29 (&out)[CNT]) {
   const int k = (int)(threadIdx.x & 3);  // every quad of lanes computes the level
-  f29 x = a[0], y = b[0];
-#pragma unroll
-  for (int i = 1; i < CNT; i++)
-    if (k == i) {
-      x = a[i];
-      y = b[i];
-    }
-  quad_get<0, CNT>(f29_mul_c(x, y), out);
+  const f29& a1 = a[CNT > 1 ? 1 : 0];
+  const f29& a2 = a[CNT > 2 ? 2 : 0];
+  const f29& a3 = a[CNT > 3 ? 3 : 0];
+  const f29& b1 = b[CNT > 1 ? 1 : 0];
+  const f29& b2 = b[CNT > 2 ? 2 : 0];
+  const f29& b3 = b[CNT > 3 ? 3 : 0];
+  quad_get<0, CNT>(f29_mul_c(lane_sel(k, a[0], a1, a2, a3), lane_sel(k, b[0], b1, b2, b3)), out);
 }
 
-// dbl-2009-l (j29_dbl) in place: 3 product levels instead of 7 products.  The
-// point lives in plain variables (a j29 carried through the loop with its flag
-// was kept in scratch memory)
+// dbl-2009-l (j29_dbl's formulas) in place: 3 product levels instead of 7
+// products, the first two squarings only (Z3 = 2 Y Z as (Y + Z)^2 - Y^2 - Z^2:
+// the same value, another representative).  The point lives in plain variables
+// (a j29 carried through the loop with its flag was kept in scratch memory)
 __device__ __forceinline__ void coop29_dbl(f29& X, f29& Y, f29& Z) {
   f29 A, Bq, Z3, C, T2, F, Y3a;
   {
-    f29 a[3] = {X, Y, f29_add(Y, Y)}, b[3] = {X, Y, Z}, o[3];
-    coop29_level<3>(a, b, o);
+    f29 a[4] = {X, Y, f29_norm(f29_add(Y, Z)), Z}, o[4];  // (Y + Z): B <= 3.5, L 1
+    coop29_sqr_level<4>(a, o);
     A = o[0];
     Bq = o[1];
-    Z3 = o[2];
+    Z3 = f29_reduce(f29_sub(f29_sub(o[2], o[1]), o[3]));  // (6, 3) -> (1.5, 1)
   }
   f29 E = f29_norm(f29_add(f29_add(A, A), A));
   {
     f29 t = f29_norm(f29_add(X, Bq));
-    f29 a[3] = {Bq, t, E}, b[3] = {Bq, t, E}, o[3];
-    coop29_level<3>(a, b, o);
+    f29 a[3] = {Bq, t, E}, o[3];
+    coop29_sqr_level<3>(a, o);
     C = o[0];
     T2 = o[1];
     F = o[2];
