@@ -37,6 +37,13 @@ struct F12Dev {
 };
 
 enum G1Base : uint8_t { G1B_PED0 = 0, G1B_PED1, G1B_PED2, G1B_PEDGEN, G1B_GEN, G1B_COUNT };
+// The prover's table set appends the public parameters' PS signatures of the
+// range digits (setup.go SignedValues): base G1B_SIG0 + 2 d is R_d, + 2 d + 1
+// is S_d, so that R' = rr R_d and rr S_d are fixed-base products (16 table
+// additions instead of a GLV variable-base chain).  fbase is 8 bits: digits
+// base <= G1B_SIG_MAX_DIGITS.
+static constexpr uint32_t G1B_SIG0 = G1B_COUNT;
+static constexpr uint32_t G1B_SIG_MAX_DIGITS = (255 - G1B_SIG0) / 2;
 enum G2Base : uint8_t { G2B_PK0 = 0, G2B_PK1, G2B_PK2, G2B_Q, G2B_COUNT };
 // G2 fixed-base tables: signed FTS_G2TAB_C-bit windows, same layout as G1
 // below (product library: C = 13, 20 windows, 4 x 20 x 4096 x 128 B = 42 MB;

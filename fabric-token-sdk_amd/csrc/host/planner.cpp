@@ -1643,6 +1643,19 @@ std::string validate_pp(const uint8_t* p, size_t n, const char* label) {
 
 // crypto.PublicParams.Deserialize (setup.go:134-151) + the structural subset
 // of Validate (setup.go:238-273) the verifier relies on.
+bool pp_sig_tables(const PPInfo& pp) {
+  if (pp.base == 0 || pp.base > G1B_SIG_MAX_DIGITS || pp.sig_r.size() != pp.base || pp.sig_s.size() != pp.base)
+    return false;
+  auto zero = [](const std::vector<uint8_t>& v) {
+    for (uint8_t b : v)
+      if (b) return false;
+    return true;
+  };
+  for (uint32_t d = 0; d < pp.base; d++)
+    if (zero(pp.sig_r[d]) || zero(pp.sig_s[d])) return false;
+  return true;
+}
+
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out) {
   JDoc outer;
   if (!outer.parse(p, n)) return "invalid public parameters json";

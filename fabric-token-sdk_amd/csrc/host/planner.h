@@ -35,6 +35,11 @@ struct PPInfo {
   std::string label;
   std::vector<uint64_t> pow;                      // base^i, i < exponent
 };
+// The prover multiplies by the PS signature points of the digits through fixed-
+// base tables (G1B_SIG0 ..) when every digit fits the 8-bit base index and no
+// signature point is the identity (64 zero bytes); else through the variable-
+// base path.  The runtime / host emulation build those tables on first use.
+bool pp_sig_tables(const PPInfo& pp);
 // Returns empty string on success, else an error message.
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out);
 // PublicParams.Validate (setup.go:238-273) on serialized PP: "" or the error text

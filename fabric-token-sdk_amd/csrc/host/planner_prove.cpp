@@ -85,6 +85,15 @@ struct Patch {
   uint16_t k;
   uint32_t off, len;
 };
+// ... and the digit-dependent fixed base of a G1 job (the signature point
+// table of digit k: R_d for s == 0, S_d for s == 1)
+struct BasePatch {
+  uint8_t g1p;   // 1: pl.g1p, 0: pl.g1
+  uint8_t slot;  // fbase slot
+  uint8_t s;
+  uint16_t k;
+  uint32_t job;  // template-local job index
+};
 
 struct PB {
   Plan& pl;
@@ -93,7 +102,12 @@ struct PB {
   std::string tagp;  // tag prefix
   std::string err;
   std::vector<Patch>* rec = nullptr;  // template build: where the witness bytes go
-  PB(Plan& p, const PPInfo& q) : pl(p), pp(q) {}
+  std::vector<BasePatch>* brec = nullptr;
+  const bool sigtab;                   // digit signature points through fixed-base tables
+  PB(Plan& p, const PPInfo& q) : pl(p), pp(q), sigtab(pp_sig_tables(q)) {}
+  void note_base(bool g1p, uint8_t slot, uint8_t s, uint32_t k) {
+    if (brec) brec->push_back({(uint8_t)(g1p ? 1 : 0), slot, s, (uint16_t)k, (uint32_t)((g1p ? pl.g1p : pl.g1).size() - 1)});
+  }
   void note(bool arena, uint8_t kind, uint32_t k, uint32_t off, uint32_t len) {
     if (rec && kind != SRC_NONE) rec->push_back({(uint8_t)(arena ? 1 : 0), kind, (uint16_t)k, off, len});
   }
@@ -348,8 +362,6 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       g1job({{G1B_PED0, sd}, {G1B_PED1, dbf}}, NONE, NONE, com_off, NONE, false);
       // membership proof of d on the PS signature of d (sigproof/membership.go:112-158)
       uint32_t blinding = rnd(mt + "/sigbf"), rr = rnd(mt + "/randomize");
-      uint32_t Rd = point(pp.sig_r[d].data(), (uint32_t)pp.sig_r[d].size(), NONE, SRC_SIG_R, k * e + i);
-      uint32_t Sd = point(pp.sig_s[d].data(), (uint32_t)pp.sig_s[d].size(), NONE, SRC_SIG_S, k * e + i);
       // slot: [g1c 64 | GT 384 | sig JSON 235 | R' 64 | S'' 64]
       uint32_t slot = arena_alloc(64 + 384 + SIG_JSON_LEN + 128);
       uint8_t* js = &pl.arena[slot + 448];
@@ -358,8 +370,19 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       memcpy(js + 27 + 88 + 29 + 88, SIG_JSON_E, 3);
       uint32_t rp_bytes = slot + 448 + SIG_JSON_LEN, obfs_bytes = rp_bytes + 64;
       // R' = rr*R, S'' = rr*S + blinding*P  (obfuscateSignature, :196-222)
-      uint32_t Rp = g1job({}, Rd, rr, rp_bytes, slot + 448 + 27, true);
-      g1job({{G1B_PEDGEN, blinding}}, Sd, rr, obfs_bytes, slot + 448 + 27 + 88 + 29, false);
+      uint32_t Rp;
+      if (sigtab) {  // (R, S) = SignedValues[d]: fixed bases of the prover's table set
+        Rp = g1job({{(uint8_t)(G1B_SIG0 + 2 * d), rr}}, NONE, NONE, rp_bytes, slot + 448 + 27, true);
+        note_base(true, 0, 0, k * e + i);
+        g1job({{G1B_PEDGEN, blinding}, {(uint8_t)(G1B_SIG0 + 2 * d + 1), rr}}, NONE, NONE, obfs_bytes,
+              slot + 448 + 27 + 88 + 29, false);
+        note_base(false, 1, 1, k * e + i);
+      } else {
+        uint32_t Rd = point(pp.sig_r[d].data(), (uint32_t)pp.sig_r[d].size(), NONE, SRC_SIG_R, k * e + i);
+        uint32_t Sd = point(pp.sig_s[d].data(), (uint32_t)pp.sig_s[d].size(), NONE, SRC_SIG_S, k * e + i);
+        Rp = g1job({}, Rd, rr, rp_bytes, slot + 448 + 27, true);
+        g1job({{G1B_PEDGEN, blinding}}, Sd, rr, obfs_bytes, slot + 448 + 27 + 88 + 29, false);
+      }
       // h = HashToZr(d.Bytes())
       uint8_t db[32] = {0};
       db[28] = (uint8_t)(d >> 24);
@@ -637,6 +660,7 @@ void PB::issue(const IssueWit& w, size_t idx) {
 struct ProofTpl {
   Plan p;
   std::vector<Patch> patches;
+  std::vector<BasePatch> bpatches;
   uint32_t img_arena = 0, img_out = 0;  // the piece's wire copies of p.arena / p.out
 };
 
@@ -663,6 +687,11 @@ struct WitView {
 
 static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& o, const WitView& w, Plan& pl) {
   const uint32_t e = (uint32_t)pp.exponent;
+  for (const BasePatch& q : t.bpatches) {
+    uint32_t d = (uint32_t)((w.vals[q.k / e] / pp.pow[q.k % e]) % pp.base);
+    G1Job& j = q.g1p ? pl.g1p[o.sec[PS_G1P] + q.job] : pl.g1[o.sec[PS_G1] + q.job];
+    j.fbase[q.slot] = (uint8_t)(G1B_SIG0 + 2 * d + q.s);
+  }
   for (const Patch& q : t.patches) {
     const uint8_t* src = nullptr;
     uint8_t tmp[32];
@@ -770,6 +799,7 @@ std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& 
         t->p.p2_g1out = true;
         PB b(t->p, pp);
         b.rec = &t->patches;
+        b.brec = &t->bpatches;
         plan_one(b, w[i], i);
         // the shape's arena and output images, once per piece (the device copies
         // them into every proof's block, then the witness bytes over them)

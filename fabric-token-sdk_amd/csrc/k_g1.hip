@@ -105,9 +105,9 @@ __global__ void __launch_bounds__(COMBINE_NT) k_g1_combine(const G1Job* jobs, ui
 // B_w = 2^(C w) B, then every lane fills a chunk of consecutive digits by
 // repeated mixed additions of B_w, made affine together (Montgomery batch
 // inversion; jtmp / zs hold chunk * lanes Jacobian points / prefix products).
-__global__ void __launch_bounds__(64) k_tab_g1_bw(const G1Dev* bases, G1Dev* bw) {
+__global__ void __launch_bounds__(64) k_tab_g1_bw(const G1Dev* bases, uint32_t nb, G1Dev* bw) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (uint32_t)(G1B_COUNT * G1TAB_WINDOWS)) return;
+  if (i >= nb * (uint32_t)G1TAB_WINDOWS) return;
   uint32_t b = i / G1TAB_WINDOWS, w = i - b * G1TAB_WINDOWS;
   g1j acc = jac_from_aff(g1_load(bases[b]));
   for (uint32_t q = 0; q < (uint32_t)G1TAB_C * w; q++) acc = jac_dbl(acc);
@@ -116,10 +116,10 @@ __global__ void __launch_bounds__(64) k_tab_g1_bw(const G1Dev* bases, G1Dev* bw)
   bw[i] = d;
 }
 
-__global__ void __launch_bounds__(128) k_tab_g1_fill(const G1Dev* bw, uint32_t chunk, G1JDev* jtmp,
+__global__ void __launch_bounds__(128) k_tab_g1_fill(const G1Dev* bw, uint32_t nb, uint32_t chunk, G1JDev* jtmp,
                                                      uint32_t (*zs)[8], G1Dev* tab) {
   uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x, per = G1TAB_DIGITS / chunk;
-  if (lane >= (uint32_t)(G1B_COUNT * G1TAB_WINDOWS) * per) return;
+  if (lane >= nb * (uint32_t)G1TAB_WINDOWS * per) return;
   uint32_t t = lane / per, c = lane - t * per;
   size_t base = (size_t)t * G1TAB_DIGITS + (size_t)c * chunk;  // entry of |d| = c chunk + 1
   g1a B = g1_load(bw[t]);

@@ -67,8 +67,8 @@ __global__ void k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const 
 __global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena,
                              G1Dev* pnorm);
 __global__ void k_tab_g1(const G1Dev* bases, uint32_t n, G1Dev* tab);
-__global__ void k_tab_g1_bw(const G1Dev* bases, G1Dev* bw);
-__global__ void k_tab_g1_fill(const G1Dev* bw, uint32_t chunk, G1JDev* jtmp, uint32_t (*zs)[8], G1Dev* tab);
+__global__ void k_tab_g1_bw(const G1Dev* bases, uint32_t nb, G1Dev* bw);
+__global__ void k_tab_g1_fill(const G1Dev* bw, uint32_t nb, uint32_t chunk, G1JDev* jtmp, uint32_t (*zs)[8], G1Dev* tab);
 __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2Dev* g2out);
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);

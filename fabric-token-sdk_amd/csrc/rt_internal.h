@@ -99,6 +99,12 @@ struct ftz_ctx {
   PPInfo pp;
   std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
   DBuf<G1Dev> g1tab;
+  // the prover's table set: g1tab's bases, then the PS signature points of the
+  // range digits (G1B_SIG0 ..), built on the first proving call
+  std::vector<G1Dev> pp_g1;          // decoded PP G1 points: PedGen, Ped0..2, G, then R_d, S_d per digit
+  std::mutex ptab_mu;
+  DBuf<G1Dev> g1tab_p;
+  bool ptab_ready = false;
   DBuf<G2Dev> g2tab;
   DBuf<LineCoef> qlines;
   DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)
@@ -108,10 +114,12 @@ struct ftz_ctx {
   int serial = 0;                    // profiling: every kernel of a batch on one stream
   // t' + pair-2 lines: k_g2lines1 (one lane per job) or the sextet k_g2lines
   // (ftz_ctx_set_layout).  The verifier's pipeline is throughput bound (one lane:
-  // fewest instructions); the prover's pass is latency bound (t' waits for R'):
-  // sextet (profiles/r02g_prover_layout.txt)
+  // fewest instructions).  The prover's pass was latency bound (t' waits for R')
+  // and took the sextet (profiles/r02g_prover_layout.txt); with R' and S'' on
+  // fixed-base tables (round 3) its passes fill the device and one lane is ahead
+  // (profiles/r03s_prover_layout.txt)
   int g2lanes = FTZ_LAYOUT_ONE_LANE;
-  int g2lanes_prover = FTZ_LAYOUT_SEXTET;
+  int g2lanes_prover = FTZ_LAYOUT_ONE_LANE;
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
   // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every

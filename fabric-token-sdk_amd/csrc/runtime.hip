@@ -185,8 +185,9 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     memcpy(&c->const_bytes[C_PK_Q + 384], &g2b[384], 128);  // Q again (PK0..2 shared)
     // fixed-base tables: G1 base order must follow G1Base: PED0, PED1, PED2, PEDGEN, GEN
     std::vector<G1Dev> hb(5);
-    std::vector<G1Dev> got(5);
-    if (hipMemcpy(got.data(), d_g1.p, 5 * sizeof(G1Dev), hipMemcpyDeviceToHost) != hipSuccess) {
+    std::vector<G1Dev>& got = c->pp_g1;  // kept: the prover's signature-point tables (g1tab_p)
+    got.resize(n1);
+    if (hipMemcpy(got.data(), d_g1.p, n1 * sizeof(G1Dev), hipMemcpyDeviceToHost) != hipSuccess) {
       fail(FTZ_E_DEVICE, "copy failed");
       break;
     }
@@ -219,9 +220,9 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
         fail(FTZ_E_NOMEM, "table scratch allocation failed");
         break;
       }
-      k_tab_g1_bw<<<blocks_for(G1B_COUNT * G1TAB_WINDOWS, 64), 64, 0, c->stream>>>(d_b1.p, d_bw.p);
+      k_tab_g1_bw<<<blocks_for(G1B_COUNT * G1TAB_WINDOWS, 64), 64, 0, c->stream>>>(d_b1.p, G1B_COUNT, d_bw.p);
       k_tab_g1_fill<<<blocks_for(lanes, 128), 128, 0, c->stream>>>(
-          d_bw.p, chunk, d_jt.p, reinterpret_cast<uint32_t (*)[8]>(d_zs.p), c->g1tab.p);
+          d_bw.p, G1B_COUNT, chunk, d_jt.p, reinterpret_cast<uint32_t (*)[8]>(d_zs.p), c->g1tab.p);
     }
     DBuf<G2Dev> d_bw2;
     DBuf<uint32_t> d_jt2, d_zs2;
@@ -426,8 +427,57 @@ int slot_plan_items(ftz_batch* b, size_t n, const PlanItem* items) {
   return slot_finish_plan(b, n, false);
 }
 
+// The prover's G1 table set (ftz_ctx.g1tab_p): g1tab's bases, then R_d, S_d of
+// every digit (PP SignedValues), 32 MB per base with 16-bit windows (6.4 GB
+// for b = 100), built once -- in groups of 16 bases, the same kernels as g1tab
+// -- on the first proving call of a context whose PP qualify (pp_sig_tables).
+static int ensure_prover_tables(ftz_ctx* c) {
+  std::lock_guard<std::mutex> lk(c->ptab_mu);
+  if (c->ptab_ready || !pp_sig_tables(c->pp)) return FTZ_SUCCESS;
+  HC(hipSetDevice(c->device));
+  const uint32_t nsig = 2 * c->pp.base, nb = G1B_SIG0 + nsig;
+  const size_t per = (size_t)G1TAB_WINDOWS * G1TAB_DIGITS;
+  if (c->pp_g1.size() != G1B_COUNT + (size_t)nsig) return set_err(FTZ_E_PP, "signature points not decoded");
+  if (c->g1tab_p.alloc(nb * per) != hipSuccess) return set_err(FTZ_E_NOMEM, "prover table allocation failed");
+  hipStream_t s = c->stream;
+  HC(hipMemcpyAsync(c->g1tab_p.p, c->g1tab.p, G1B_COUNT * per * sizeof(G1Dev), hipMemcpyDeviceToDevice, s));
+  std::vector<G1Dev> sig(c->pp_g1.begin() + G1B_COUNT, c->pp_g1.end());  // R_0, S_0, R_1, S_1, ...
+  DBuf<G1Dev> d_b;
+  HC(d_b.upload(sig, s));
+  if (G1TAB_C <= 8) {
+    const uint32_t t = (uint32_t)(nsig * per);
+    k_tab_g1<<<blocks_for(t, 64), 64, 0, s>>>(d_b.p, t, c->g1tab_p.p + G1B_COUNT * per);
+  } else {
+    const uint32_t group = 16, chunk = 128;
+    DBuf<G1Dev> d_bw;
+    DBuf<G1JDev> d_jt;
+    DBuf<uint32_t> d_zs;
+    if (d_bw.alloc(group * G1TAB_WINDOWS) != hipSuccess || d_jt.alloc(group * per) != hipSuccess ||
+        d_zs.alloc(8 * group * per) != hipSuccess)
+      return set_err(FTZ_E_NOMEM, "prover table scratch allocation failed");
+    for (uint32_t g = 0; g < nsig; g += group) {
+      const uint32_t m = std::min(group, nsig - g), lanes = m * G1TAB_WINDOWS * (G1TAB_DIGITS / chunk);
+      k_tab_g1_bw<<<blocks_for(m * G1TAB_WINDOWS, 64), 64, 0, s>>>(d_b.p + g, m, d_bw.p);
+      k_tab_g1_fill<<<blocks_for(lanes, 128), 128, 0, s>>>(d_bw.p, m, chunk, d_jt.p,
+                                                           reinterpret_cast<uint32_t (*)[8]>(d_zs.p),
+                                                           c->g1tab_p.p + (G1B_COUNT + g) * per);
+    }
+    HC(hipGetLastError());
+    HC(hipStreamSynchronize(s));  // the scratch buffers go out of scope
+  }
+  HC(hipGetLastError());
+  HC(hipStreamSynchronize(s));
+  c->ptab_ready = true;
+  return FTZ_SUCCESS;
+}
+
+// fixed-base tables the prover's G1 jobs index (G1B_SIG0 .. only with g1tab_p)
+static const G1Dev* prover_g1tab(ftz_ctx* c) { return c->ptab_ready ? c->g1tab_p.p : c->g1tab.p; }
+
 int prover_plan(ftz_batch* b, size_t n, const void* wit, int kind) {
   ftz_ctx* c = b->ctx;
+  int trc = ensure_prover_tables(c);
+  if (trc != FTZ_SUCCESS) return trc;
   std::string e = kind == 0
                       ? plan_prove_items_transfers(c->pp, n, static_cast<const TransferWit*>(wit), b->work, *c->pool)
                       : plan_prove_items_issues(c->pp, n, static_cast<const IssueWit*>(wit), b->work, *c->pool);
@@ -838,7 +888,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   HC(hipStreamWaitEvent(s2, e[4], 0));
   HC(hipEventRecord(e[11], s2));
   if (p.n_g1) {
-    k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, c->g1tab.p, p.part1,
+    k_g1_part<<<blocks_for(4 * p.n_g1, 128), 128, 0, s2>>>(p.g1, p.n_g1, p.vt, p.pts, p.scal, prover_g1tab(c), p.part1,
                                                            p.vtab1);
     k_g1_combine<<<blocks_for(p.n_g1, 256), 256, 0, s2>>>(p.g1, p.n_g1, p.part1, p.g1out, p.arena, p.pnorm);
   }
@@ -846,7 +896,7 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   // st[0]: R' = rr R and rsbf P (the pairing inputs)
   HC(hipEventRecord(e[16], s));
   if (p.n_g1p) {
-    k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, c->g1tab.p, p.part1p,
+    k_g1_part<<<blocks_for(4 * p.n_g1p, 128), 128, 0, s>>>(p.g1p, p.n_g1p, p.vt, p.pts, p.scal, prover_g1tab(c), p.part1p,
                                                            p.vtab1p);
     k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena, p.pnorm);
   }
@@ -1023,8 +1073,9 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
   // passes of at most 4096 witnesses: the prover's pass is a latency-bound
   // chain (R' -> t lines -> Miller -> final exponentiation -> challenges ->
   // responses) planned on the calling thread, and 8192-witness passes fill the
-  // three slots too slowly (65536 proofs: 298k/s vs 426k/s, profiles/r02g_prover_layout.txt)
-  const size_t K = 3, B = std::min<size_t>(c->opt.batch, 4096);
+  // slots too slowly (65536 proofs: 298k/s vs 426k/s, profiles/r02g_prover_layout.txt);
+  // opt.slots of them in flight (clamped to [2, 8])
+  const size_t K = std::max<size_t>(2, std::min<size_t>(c->opt.slots, 8)), B = std::min<size_t>(c->opt.batch, 4096);
   while (c->pslots.size() < K) {
     ftz_prover* p = new ftz_prover();
     p->ctx = c;

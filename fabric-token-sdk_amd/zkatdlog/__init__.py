@@ -168,7 +168,7 @@ class Context:
 
     def set_layout(self, stage, layout):
         """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines'
-        (verifier, default 'one_lane') or 'prover_g2lines' (default 'sextet'), layout 'one_lane'
+        (verifier, default 'one_lane') or 'prover_g2lines' (default 'one_lane'), layout 'one_lane'
         or 'sextet' -- same results, different speed"""
         _check(self._lib.ftz_ctx_set_layout(self._h, self.STAGES[stage], self.LAYOUTS[layout]), self._lib)
 

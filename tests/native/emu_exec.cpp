@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -25,7 +26,9 @@ thread_local unsigned long long fts_mont_count = 0;
 struct EmuCtx {
   PPInfo pp;
   std::vector<uint8_t> const_bytes;
-  std::vector<G1Dev> g1tab;
+  std::vector<G1Dev> g1tab;  // + the prover's signature-point bases once built (G1B_SIG0 ..)
+  std::mutex sig_mu;
+  bool sig_ready = false;
   std::vector<G2Dev> g2tab;
   std::vector<LineCoef> qlines;
   int fexp = 0;  // 0: exact (FTZ_FEXP_EXACT), 1: Fuentes
@@ -111,6 +114,51 @@ void* emu_ctx_create(const uint8_t* pp, size_t len, char* err, size_t errlen) {
 }
 
 void emu_ctx_destroy(void* c) { delete (EmuCtx*)c; }
+
+// The prover's fixed-base tables of the PP signature points (runtime.hip
+// ensure_prover_tables): the same entries |d| 2^(C w) B, built per (base,
+// window) by successive additions and one batch inversion (the per-entry
+// scalar multiplication of job_tab_g1 is too slow for 2 b bases on the host)
+static void emu_ensure_sig_tables(EmuCtx* c) {
+  std::lock_guard<std::mutex> lk(c->sig_mu);
+  if (c->sig_ready || !pp_sig_tables(c->pp)) return;
+  const uint32_t nsig = 2 * c->pp.base;
+  const size_t per = (size_t)G1TAB_WINDOWS * G1TAB_DIGITS, old = (size_t)G1B_COUNT * per;
+  std::vector<G1Dev> sig(nsig);
+  for (uint32_t k = 0; k < nsig; k++) {
+    std::vector<uint8_t> raw = (k & 1) ? c->pp.sig_s[k / 2] : c->pp.sig_r[k / 2];
+    raw.resize(std::max<size_t>(raw.size(), 64) + 64, 0);
+    DecodeJob j{0, 64, k, NONE, NONE};
+    (void)job_decode(j, raw.data(), sig.data(), nullptr);
+  }
+  c->g1tab.resize(old + nsig * per);
+  par_for(nsig * G1TAB_WINDOWS, [&](uint32_t t) {
+    const uint32_t b = t / G1TAB_WINDOWS, w = t % G1TAB_WINDOWS;
+    g1j acc = jac_from_aff(g1_load(sig[b]));
+    for (uint32_t q = 0; q < (uint32_t)G1TAB_C * w; q++) acc = jac_dbl(acc);
+    const g1a Bw = jac_to_aff(acc);
+    std::vector<g1j> e(G1TAB_DIGITS);
+    std::vector<fp> pre(G1TAB_DIGITS);
+    e[0] = jac_from_aff(Bw);
+    for (int d = 1; d < G1TAB_DIGITS; d++) e[d] = jac_add_aff(e[d - 1], Bw);
+    pre[0] = e[0].z;
+    for (int d = 1; d < G1TAB_DIGITS; d++) pre[d] = pre[d - 1] * e[d].z;
+    fp inv = fp_inv(pre[G1TAB_DIGITS - 1]);
+    for (int d = G1TAB_DIGITS - 1; d >= 0; d--) {
+      fp zi = d ? inv * pre[d - 1] : inv;
+      if (d) inv = inv * e[d].z;
+      fp zi2 = sqr(zi);
+      g1a a;
+      a.x = e[d].x * zi2;
+      a.y = e[d].y * zi2 * zi;
+      a.inf = false;
+      G1Dev o;
+      g1_store(o, a);
+      c->g1tab[old + (size_t)b * per + (size_t)w * G1TAB_DIGITS + d] = o;
+    }
+  });
+  c->sig_ready = true;
+}
 void emu_ctx_set_fexp(void* c, int variant) { ((EmuCtx*)c)->fexp = variant; }
 void emu_set_threads(int t) { g_threads = t > 0 ? (unsigned)t : 0; }
 
@@ -267,6 +315,7 @@ static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t ca
 long emu_prove_transfers(void* ctx, size_t n, const ftz_transfer_witness* w, uint8_t* buf, size_t cap,
                          size_t* offsets, int32_t* codes, char* err, size_t errlen) {
   EmuCtx* c = (EmuCtx*)ctx;
+  emu_ensure_sig_tables(c);
   std::vector<TransferWit> t(n);
   for (size_t i = 0; i < n; i++)
     t[i] = {w[i].inputs, w[i].n_in, w[i].outputs, w[i].n_out, w[i].in_values, w[i].in_bfs,
@@ -323,6 +372,7 @@ int emu_plan_prove_ms(void* ctx, size_t n, const ftz_transfer_witness* w, int th
 long emu_prove_issues(void* ctx, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap, size_t* offsets,
                       int32_t* codes, char* err, size_t errlen) {
   EmuCtx* c = (EmuCtx*)ctx;
+  emu_ensure_sig_tables(c);
   std::vector<IssueWit> t(n);
   for (size_t i = 0; i < n; i++)
     t[i] = {w[i].outputs, w[i].n_out, w[i].values, w[i].bfs, w[i].type, w[i].type_len, w[i].anonymous, w[i].seed};
