@@ -524,7 +524,14 @@ FTS_HD g2j g2_fixed_acc(g2j acc, const G2Dev* tab, int base, const uint32_t s[8]
 FTS_HD g1j g1_fixed_acc_fp(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]);
 FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]) {
 #if FTS_G1_F29
-  j29 a = j29_from(acc);
+  // runs of mixed additions: the XYZZ accumulator (fp29.h x29_madd)
+  x29 a{};
+  a.inf = is_zero(acc.z);
+  if (!a.inf) {
+    j29 aj = j29_from(acc);
+    f29 zz = f29_sqr(aj.z);
+    a = {aj.x, aj.y, zz, f29_mul(zz, aj.z), false};
+  }
   uint32_t carry = 0;
   const G1Dev* tb = tab + (size_t)base * G1TAB_WINDOWS * G1TAB_DIGITS;
 #pragma nounroll
@@ -541,10 +548,10 @@ FTS_HD g1j g1_fixed_acc(g1j acc, const G1Dev* tab, int base, const uint32_t s[8]
     if (d) {
       g1a T = g1_load(tb[(size_t)w * G1TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
       f29 y = f29_from_fp(T.y);
-      a = j29_madd(a, f29_from_fp(T.x), d < 0 ? f29_neg(y) : y);
+      a = x29_madd(a, f29_from_fp(T.x), d < 0 ? f29_neg(y) : y);
     }
   }
-  return j29_to(a);
+  return j29_to(x29_to_j29(a));
 #else
   return g1_fixed_acc_fp(acc, tab, base, s);
 #endif

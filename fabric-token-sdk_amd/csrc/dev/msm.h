@@ -251,8 +251,9 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   uint32_t v = e[lo];
   G1Dev nxt = pts[v & 0x7FFFFFFFu];
 #if FTS_G1_F29
-  // the additions in the carry-free form (dev/fp29.h), one conversion per slot
-  j29 a = {f29{}, f29{}, f29{}, true};
+  // the additions in the carry-free XYZZ form (dev/fp29.h), one conversion per slot
+  x29 a{};
+  a.inf = true;
 #endif
   for (uint32_t q = lo; q < hi; q++) {
     // the next point's load is issued before this point's addition
@@ -266,7 +267,7 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
 #if FTS_G1_F29
     if (!P.inf) {
       f29 Y = f29_from_fp(P.y);
-      a = j29_madd(a, f29_from_fp(P.x), sign ? f29_neg(Y) : Y);
+      a = x29_madd(a, f29_from_fp(P.x), sign ? f29_neg(Y) : Y);
     }
 #else
     if (sign) P = aff_neg(P);
@@ -274,7 +275,7 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
 #endif
   }
 #if FTS_G1_F29
-  acc = j29_to(a);
+  acc = j29_to(x29_to_j29(a));
 #endif
   return acc;
 }
