@@ -114,9 +114,10 @@ struct G2Job {
 
 struct PairJob {
   uint32_t p1;     // g1out index, paired with the PP generator Q (precomputed lines)
-  uint32_t p2;     // pts index (signature R)
-  uint32_t q2;     // g2out index
+  uint32_t p2;     // pts index (signature R); fixed pairs: g1out index paired with PK1
+  uint32_t q2;     // g2out index (NONE with fixed pairs)
   uint32_t bytes;  // arena offset for the 384 GT bytes
+  uint32_t p3;     // fixed pairs (prover): g1out index paired with PK2; else NONE
 };
 
 struct Seg {
@@ -980,6 +981,15 @@ FTS_HD void job_g2(const G2Job& j, const uint32_t (*scal)[8], const G2Dev* tab, 
 FTS_HD void job_miller(const PairJob& j, const LineCoef* qlines, const G1Dev* g1out, const G1Dev* pts,
                        const G2Dev* g2out, F12Dev* fout, uint32_t idx) {
   fp12 f = miller_2(qlines, g1_load(g1out[j.p1]), g1_load(pts[j.p2]), g2_load(g2out[j.q2]));
+  f12_store(fout[idx], f);
+}
+
+// the prover's fixed-pair product f(C, Q) f(A, PK1) f(B, PK2) (host emulation;
+// the device runs k_miller_f3 on precomputed normalised lines of all three)
+FTS_HD void job_miller3(const PairJob& j, const LineCoef* qlines, const G1Dev* g1out, const G2Dev* g2pp,
+                        F12Dev* fout, uint32_t idx) {
+  fp12 f = miller_2(qlines, g1_load(g1out[j.p1]), g1_load(g1out[j.p2]), g2_load(g2pp[G2B_PK1]));
+  f = f * miller_1(g1_load(g1out[j.p3]), g2_load(g2pp[G2B_PK2]));
   f12_store(fout[idx], f);
 }
 

@@ -504,6 +504,67 @@ FTS_HD q2 sq_fixed_line_n(const X& x, const q2& f, const LineCoef29& q, const f2
   return q2_sel(inf, f, g);
 }
 
+// sq_fixed_line_n with the lane's multiplicand v already selected (lanes 0, 1:
+// xP/yP, lanes 2, 3: 1/yP; lanes 4, 5: anything)
+template <class X>
+FTS_HD q2 sq_fixed_line_nv(const X& x, const q2& f, const LineCoef29& q, const f29& v, bool inf) {
+  const int k = x.k;
+  f29 a = (k == 0) ? q.r1.c0 : (k == 1) ? q.r1.c1 : (k == 2) ? q.r2.c0 : q.r2.c1;
+  f29 prod = f29_mulb(a, v);
+  x.put(SX_P + k, {prod, prod});
+  x.sync();
+  q2 l1 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
+  q2 l3 = {x.get(SX_P + 2).c0, x.get(SX_P + 3).c0};
+  sq_pub(x, SX_A, f);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 2; t++) {
+    int j = k - (t == 0 ? 1 : 3);
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w29_mac(w, t == 0 ? l1 : l3, x.get(sb));
+  }
+  x.sync();
+  q2 r = w29_reduce(w);
+  q2 g = {f29_lin2(f.c0, 1, r.c0, 1), f29_lin2(f.c1, 1, r.c1, 1)};
+  return q2_sel(inf, f, g);
+}
+
+// the lane's multiplicand of a normalised fixed line at P (pn = (xP/yP, 1/yP))
+FTS_HD f29 sq_line_mult(int k, const G1Dev& pn) {
+  fp v;
+#pragma unroll
+  for (int i = 0; i < 8; i++) v.v[i] = k < 2 ? pn.x[i] : pn.y[i];
+  return f29_breduce(f29_from_fp(v));
+}
+
+// The prover's fixed-pair Miller product f(C, Q) f(A, PK1) f(B, PK2): all three
+// G2 arguments fixed, their lines precomputed and normalised by r0 (each pair's
+// Fp2 factor is sent to 1 by the final exponentiation); the squarings are shared
+template <class X>
+FTS_HD q2 sq_miller_f3n(const X& x, const LineCoef29* l0, const LineCoef29* l1, const LineCoef29* l2,
+                        const G1Dev& pn0, const G1Dev& pn1, const G1Dev& pn2, bool inf0, bool inf1, bool inf2) {
+  const f29 v0 = sq_line_mult(x.k, pn0), v1 = sq_line_mult(x.k, pn1), v2 = sq_line_mult(x.k, pn2);
+  q2 one = {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1};
+  q2 f = q2_sel(x.k == 0, one, q2_zero());
+#pragma nounroll
+  for (int s = 0; s < MILLER_LINES; s++) {
+    bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
+    if (sq) f = sq_sqr(x, f);
+    // one copy of the line step in the loop (three inlined copies spilled)
+#pragma nounroll
+    for (int t = 0; t < 3; t++) {
+      const LineCoef29* L = t == 0 ? l0 : (t == 1 ? l1 : l2);
+      f29 v;
+#pragma unroll
+      for (int i = 0; i < 9; i++) v.l[i] = t == 0 ? v0.l[i] : (t == 1 ? v1.l[i] : v2.l[i]);
+      f = sq_fixed_line_nv(x, f, L[s], v, t == 0 ? inf0 : (t == 1 ? inf1 : inf2));
+    }
+  }
+  return f;
+}
+
 // 2-pair Miller loop with the normalised fixed-Q lines (same GT value after
 // the final exponentiation as sq_miller_f; the Miller value differs by a
 // factor in Fp2*)

@@ -732,7 +732,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
       g2.fscal[2] = sc_h;
       g2.out = pl.n_g2out++;
       pl.g2.push_back(g2);
-      pl.pr.push_back({p1, d.R, g2.out, d.slot + 128});
+      pl.pr.push_back({p1, d.R, g2.out, d.slot + 128, NONE});
       HashJob h;
       h.seg_start = (uint32_t)pl.seg.size();
       seg(CONST_FLAG | C_PED0, 128);
@@ -1256,7 +1256,8 @@ void relocate_into(const Plan& b, const PieceBase& o, bool p2_g1out, bool keep_c
   for (PairJob j : b.pr) {
     j.p1 += o_g1;
     j.p2 += p2_g1out ? o_g1 : o_pts;
-    j.q2 += o_g2;
+    j.q2 = rel(j.q2, o_g2);
+    j.p3 = rel(j.p3, o_g1);
     j.bytes += o_arena;
     *pr++ = j;
   }
@@ -1643,6 +1644,22 @@ std::string validate_pp(const uint8_t* p, size_t n, const char* label) {
 
 // crypto.PublicParams.Deserialize (setup.go:134-151) + the structural subset
 // of Validate (setup.go:238-273) the verifier relies on.
+// every Miller line of the fixed G2 point has r0 != 0 (the normalised-line
+// Miller kernels divide by it); false for a point that does not decode
+static bool g2_lines_normalisable(const std::vector<uint8_t>& raw) {
+  std::vector<uint8_t> b = raw;
+  b.resize(std::max<size_t>(b.size(), 128) + 64, 0);
+  G2Dev d;
+  if (!decode_g2(b.data(), 128, d, nullptr)) return false;
+  g2a q = g2_load(d);
+  if (q.inf) return false;
+  std::vector<LineCoef> l(MILLER_LINES);
+  int n = precompute_lines(l.data(), q);
+  for (int i = 0; i < n; i++)
+    if (f2_is_zero(l[i].r0)) return false;
+  return n == MILLER_LINES;
+}
+
 bool pp_sig_tables(const PPInfo& pp) {
   if (pp.base == 0 || pp.base > G1B_SIG_MAX_DIGITS || pp.sig_r.size() != pp.base || pp.sig_s.size() != pp.base)
     return false;
@@ -1719,6 +1736,8 @@ std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out)
     if (pw >= 9223372036854775808.0) return "range proof exponent overflows int64";
     out.pow.push_back((uint64_t)(int64_t)pw);
   }
+  out.fixed_pairs = pp_sig_tables(out) && g2_lines_normalisable(out.q) && g2_lines_normalisable(out.pk[1]) &&
+                    g2_lines_normalisable(out.pk[2]);
   return "";
 }
 

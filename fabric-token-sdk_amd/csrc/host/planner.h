@@ -34,6 +34,9 @@ struct PPInfo {
   int64_t curve = 0;
   std::string label;
   std::vector<uint64_t> pow;                      // base^i, i < exponent
+  // the prover's membership commitments as three fixed-G2 pairings (Q, PK1,
+  // PK2; parse_pp: every line of the three normalisable and pp_sig_tables)
+  bool fixed_pairs = false;
 };
 // The prover multiplies by the PS signature points of the digits through fixed-
 // base tables (G1B_SIG0 ..) when every digit fits the 8-bit base index and no

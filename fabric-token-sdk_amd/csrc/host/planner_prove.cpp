@@ -372,8 +372,9 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       // R' = rr*R, S'' = rr*S + blinding*P  (obfuscateSignature, :196-222)
       uint32_t Rp;
       if (sigtab) {  // (R, S) = SignedValues[d]: fixed bases of the prover's table set
-        Rp = g1job({{(uint8_t)(G1B_SIG0 + 2 * d), rr}}, NONE, NONE, rp_bytes, slot + 448 + 27, true);
-        note_base(true, 0, 0, k * e + i);
+        // with fixed pairs R' feeds no pairing (below), only the proof bytes
+        Rp = g1job({{(uint8_t)(G1B_SIG0 + 2 * d), rr}}, NONE, NONE, rp_bytes, slot + 448 + 27, !pp.fixed_pairs);
+        note_base(!pp.fixed_pairs, 0, 0, k * e + i);
         g1job({{G1B_PEDGEN, blinding}, {(uint8_t)(G1B_SIG0 + 2 * d + 1), rr}}, NONE, NONE, obfs_bytes,
               slot + 448 + 27 + 88 + 29, false);
         note_base(false, 1, 1, k * e + i);
@@ -393,16 +394,27 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
       uint32_t rv = rnd(mt + "/r_value"), rh = rnd(mt + "/r_hash"), rsbf = rnd(mt + "/r_sigbf");
       // GT = FExp(e(R', rv*PK1 + rh*PK2) * e(rsbf*P, Q))   (computeCommitment, :225-257)
       uint32_t p1 = g1job({{G1B_PEDGEN, rsbf}}, NONE, NONE, NONE, NONE, true);
-      G2Job g2;
-      memset(&g2, 0, sizeof(g2));
-      g2.nfix = 2;
-      g2.fbase[0] = G2B_PK1;
-      g2.fscal[0] = rv;
-      g2.fbase[1] = G2B_PK2;
-      g2.fscal[1] = rh;
-      g2.out = pl.n_g2out++;
-      pl.g2.push_back(g2);
-      pl.pr.push_back({p1, Rp, g2.out, slot + 64});
+      if (sigtab && pp.fixed_pairs) {
+        // bilinearity: e(R', rv PK1 + rh PK2) = e((rv rr) R_d, PK1) e((rh rr) R_d, PK2), the
+        // same GT element with every G2 argument fixed (precomputed lines, no G2 work)
+        // and both G1 arguments fixed-base products of R_d
+        uint32_t a = g1job({{(uint8_t)(G1B_SIG0 + 2 * d), sc(SOP_MUL, rv, rr)}}, NONE, NONE, NONE, NONE, true);
+        note_base(true, 0, 0, k * e + i);
+        uint32_t b = g1job({{(uint8_t)(G1B_SIG0 + 2 * d), sc(SOP_MUL, rh, rr)}}, NONE, NONE, NONE, NONE, true);
+        note_base(true, 0, 0, k * e + i);
+        pl.pr.push_back({p1, a, NONE, slot + 64, b});
+      } else {
+        G2Job g2;
+        memset(&g2, 0, sizeof(g2));
+        g2.nfix = 2;
+        g2.fbase[0] = G2B_PK1;
+        g2.fscal[0] = rv;
+        g2.fbase[1] = G2B_PK2;
+        g2.fscal[1] = rh;
+        g2.out = pl.n_g2out++;
+        pl.g2.push_back(g2);
+        pl.pr.push_back({p1, Rp, g2.out, slot + 64, NONE});
+      }
       uint32_t rcb = rnd(mt + "/r_combf");
       g1job({{G1B_PED0, rv}, {G1B_PED1, rcb}}, NONE, NONE, slot, NONE, false);
       // challenge (computeChallenge, membership.go:260-277)

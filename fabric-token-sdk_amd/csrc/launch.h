@@ -83,6 +83,8 @@ __global__ void k_miller(const PairJob* jobs, uint32_t n, const LineCoef29* qlin
 __global__ void k_qlines(const G2Dev* q, LineCoef* out, LineCoef29* out29, LineCoef29* out29n, int* n, int* norm);
 __global__ void k_miller_n(const PairJob* jobs, uint32_t n, const LineCoef29* qlines_n, const EvLineDev* lines2,
                            const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
+__global__ void k_miller_f3(const PairJob* jobs, uint32_t n, const LineCoef29* qlines_n, const LineCoef29* pklines_n,
+                            const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
 // final exponentiation phases (k_fexp.hip); park: fexp_park_bytes(n) of scratch (dev/sx29.h Park)
 __global__ void k_fexp_easy(uint32_t n, const F12Dev* fbuf, int32_t* park);
 __global__ void k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps);

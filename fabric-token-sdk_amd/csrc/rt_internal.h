@@ -105,6 +105,9 @@ struct ftz_ctx {
   std::mutex ptab_mu;
   DBuf<G1Dev> g1tab_p;
   bool ptab_ready = false;
+  // pp.fixed_pairs: the normalised Miller lines of PK1 then PK2 (k_miller_f3)
+  std::vector<G2Dev> pp_g2;          // decoded PK0, PK1, PK2, Q
+  DBuf<LineCoef29> pklines29n;
   DBuf<G2Dev> g2tab;
   DBuf<LineCoef> qlines;
   DBuf<LineCoef29> qlines29;         // the same lines in the balanced 29-bit form (k_miller)

@@ -177,6 +177,11 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
       fail(FTZ_E_PP, "public parameters hold an invalid curve point");
       break;
     }
+    c->pp_g2.resize(4);
+    if (hipMemcpy(c->pp_g2.data(), d_g2.p, 4 * sizeof(G2Dev), hipMemcpyDeviceToHost) != hipSuccess) {
+      fail(FTZ_E_DEVICE, "copy failed");
+      break;
+    }
     c->const_bytes.assign(C_SIZE, 0);
     memcpy(&c->const_bytes[C_PEDGEN], &g1b[0], 64);
     memcpy(&c->const_bytes[C_PED0], &g1b[64], 192);
@@ -405,7 +410,9 @@ static int slot_finish_plan(ftz_batch* b, size_t n, bool p2_g1out) {
   std::string e = flat_layout(b->work, p2_g1out, b->fp);
   if (!e.empty()) return set_err(FTZ_E_INVALID, e);
   if (b->fp.n_items != n) return set_err(FTZ_E_INVALID, "planner: item count mismatch");
-  if (b->fp.cnt[PS_G2] != b->fp.cnt[PS_PR]) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
+  const bool fixed3 = p2_g1out && c->pp.fixed_pairs;  // the prover's pairings take no G2 jobs
+  if (!fixed3 && b->fp.cnt[PS_G2] != b->fp.cnt[PS_PR])
+    return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   b->n = n;
   HC(b->h_blob.reserve(b->fp.bytes));
   flat_write(b->work, b->fp, b->h_blob.p, c->const_bytes.data(), *c->pool);
@@ -413,7 +420,8 @@ static int slot_finish_plan(ftz_batch* b, size_t n, bool p2_g1out) {
   const PairJob* pr = b->fp.ptr<PairJob>(b->h_blob.p, PS_PR);
   const G2Job* g2 = b->fp.ptr<G2Job>(b->h_blob.p, PS_G2);
   for (size_t i = 0; i < b->fp.cnt[PS_PR]; i++)
-    if (pr[i].q2 != g2[i].out) return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
+    if (fixed3 ? (pr[i].q2 != NONE || pr[i].p3 == NONE) : pr[i].q2 != g2[i].out)
+      return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   scratch_layout(b);
   HC(b->d_blob.reserve(b->fp.bytes));
   HC(b->d_scr.reserve(b->sl.total));
@@ -464,6 +472,26 @@ static int ensure_prover_tables(ftz_ctx* c) {
     }
     HC(hipGetLastError());
     HC(hipStreamSynchronize(s));  // the scratch buffers go out of scope
+  }
+  if (c->pp.fixed_pairs) {  // PK1, PK2 lines for k_miller_f3 (the host planner checked r0 != 0)
+    if (!c->qnorm) return set_err(FTZ_E_PP, "fixed-pair prover needs normalisable Q lines");
+    DBuf<G2Dev> d_q;
+    DBuf<LineCoef> d_l;
+    DBuf<LineCoef29> d_l29;
+    DBuf<int> d_n;
+    std::vector<G2Dev> pk = {c->pp_g2[G2B_PK1], c->pp_g2[G2B_PK2]};
+    if (d_q.upload(pk, s) != hipSuccess || d_l.alloc(MILLER_LINES) != hipSuccess ||
+        d_l29.alloc(MILLER_LINES) != hipSuccess || d_n.alloc(4) != hipSuccess ||
+        c->pklines29n.alloc(2 * MILLER_LINES) != hipSuccess)
+      return set_err(FTZ_E_NOMEM, "prover line allocation failed");
+    for (int t = 0; t < 2; t++)
+      k_qlines<<<1, 64, 0, s>>>(d_q.p + t, d_l.p, d_l29.p, c->pklines29n.p + t * MILLER_LINES, d_n.p + 2 * t,
+                                d_n.p + 2 * t + 1);
+    int nl[4] = {0, 0, 0, 0};
+    HC(hipMemcpyAsync(nl, d_n.p, sizeof(nl), hipMemcpyDeviceToHost, s));
+    HC(hipStreamSynchronize(s));
+    if (nl[0] != MILLER_LINES || nl[2] != MILLER_LINES || !nl[1] || !nl[3])
+      return set_err(FTZ_E_PP, "PK1 / PK2 lines are not normalisable");
   }
   HC(hipGetLastError());
   HC(hipStreamSynchronize(s));
@@ -901,7 +929,8 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
     k_g1_combine<<<blocks_for(p.n_g1p, 256), 256, 0, s>>>(p.g1p, p.n_g1p, p.part1p, p.g1out, p.arena, p.pnorm);
   }
   HC(hipEventRecord(e[5], s));
-  // st[2]: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out)
+  // st[2]: t = rv PK1 + rh PK2 and its lines evaluated at R' (pair 2 reads g1out);
+  // none with fixed pairs (every G2 argument is a PP point with precomputed lines)
   HC(hipStreamWaitEvent(s3, e[5], 0));
   HC(hipEventRecord(e[14], s3));
   if (p.n_g2)
@@ -909,7 +938,10 @@ int prover_submit(ftz_batch* b, bool upload, bool fetch) {
   HC(hipEventRecord(e[15], s3));
   HC(hipStreamWaitEvent(s, e[15], 0));
   HC(hipEventRecord(e[6], s));
-  if (p.n_pr)
+  if (p.n_pr && p.n_g2 == 0 && c->pp.fixed_pairs && c->ptab_ready)  // e(C, Q) e(A, PK1) e(B, PK2)
+    k_miller_f3<<<blocks_for(p.n_pr, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.pr, p.n_pr, c->qlines29n.p, c->pklines29n.p,
+                                                                    p.g1out, p.pnorm, p.fbuf);
+  else if (p.n_pr)
     launch_miller(c, p, s);
   HC(hipEventRecord(e[7], s));
   launch_fexp(c, p, s);
