@@ -986,10 +986,10 @@ FTS_HD void job_miller(const PairJob& j, const LineCoef* qlines, const G1Dev* g1
 
 // the prover's fixed-pair product f(C, Q) f(A, PK1) f(B, PK2) (host emulation;
 // the device runs k_miller_f3 on precomputed normalised lines of all three)
-FTS_HD void job_miller3(const PairJob& j, const LineCoef* qlines, const G1Dev* g1out, const G2Dev* g2pp,
-                        F12Dev* fout, uint32_t idx) {
-  fp12 f = miller_2(qlines, g1_load(g1out[j.p1]), g1_load(g1out[j.p2]), g2_load(g2pp[G2B_PK1]));
-  f = f * miller_1(g1_load(g1out[j.p3]), g2_load(g2pp[G2B_PK2]));
+FTS_HD void job_miller3(const PairJob& j, const LineCoef* qlines, const LineCoef* pk1lines, const LineCoef* pk2lines,
+                        const G1Dev* g1out, F12Dev* fout, uint32_t idx) {
+  fp12 f = miller_fixed3(qlines, g1_load(g1out[j.p1]), pk1lines, g1_load(g1out[j.p2]), pk2lines,
+                         g1_load(g1out[j.p3]));
   f12_store(fout[idx], f);
 }
 

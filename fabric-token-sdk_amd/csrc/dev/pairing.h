@@ -187,6 +187,33 @@ FTS_HDN fp12 miller_2(const LinePtr qlines, const g1a& P1, const g1a& P2, const 
   return f;
 }
 
+// Miller loop of three pairs with precomputed lines each (the prover's
+// fixed-pair membership commitment on the host: Q, PK1, PK2 all fixed)
+template <class LinePtr>
+FTS_HDN fp12 miller_fixed3(const LinePtr l0, const g1a& P0, const LinePtr l1, const g1a& P1, const LinePtr l2,
+                           const g1a& P2) {
+  fp12 f = f12_one();
+  const LinePtr L[3] = {l0, l1, l2};
+  const g1a* P[3] = {&P0, &P1, &P2};
+  int n = 0;
+#pragma nounroll
+  for (int i = 64; i >= 0; i--) {
+    if (i != 64) f = f12_sqr(f);
+    for (int t = 0; t < 3; t++)
+      if (!P[t]->inf) f = line_mul(f, L[t][n], *P[t]);
+    n++;
+    if (naf_digit(i) != 0) {
+      for (int t = 0; t < 3; t++)
+        if (!P[t]->inf) f = line_mul(f, L[t][n], *P[t]);
+      n++;
+    }
+  }
+  for (int e = 0; e < 2; e++, n++)
+    for (int t = 0; t < 3; t++)
+      if (!P[t]->inf) f = line_mul(f, L[t][n], *P[t]);
+  return f;
+}
+
 // Miller loop for one pair with on-the-fly lines (used for tests / prover).
 FTS_HDN fp12 miller_1(const g1a& P, const g2a& Q) {
   fp12 f = f12_one();

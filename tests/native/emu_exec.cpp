@@ -30,7 +30,7 @@ struct EmuCtx {
   std::mutex sig_mu;
   bool sig_ready = false;
   std::vector<G2Dev> g2tab;
-  std::vector<G2Dev> g2pp;  // PK0, PK1, PK2, Q (the prover's fixed-pair Miller loops)
+  std::vector<LineCoef> pklines;  // PK1 then PK2 (the prover's fixed-pair Miller loops)
   std::vector<LineCoef> qlines;
   int fexp = 0;  // 0: exact (FTZ_FEXP_EXACT), 1: Fuentes
 };
@@ -111,7 +111,9 @@ void* emu_ctx_create(const uint8_t* pp, size_t len, char* err, size_t errlen) {
   par_for(n2, [&](uint32_t i) { job_tab_g2(i, g2.data(), c->g2tab.data()); });
   c->qlines.resize(MILLER_LINES);
   precompute_lines(c->qlines.data(), g2_load(g2[3]));
-  c->g2pp = g2;
+  c->pklines.resize(2 * MILLER_LINES);
+  precompute_lines(c->pklines.data(), g2_load(g2[G2B_PK1]));
+  precompute_lines(c->pklines.data() + MILLER_LINES, g2_load(g2[G2B_PK2]));
   return c;
 }
 
@@ -299,7 +301,8 @@ static long run_prove_plan(EmuCtx* c, Plan& p, size_t n, uint8_t* buf, size_t ca
   // pair 2 of a prover pairing job is R' = rr R (a G1 job output)
   par_for((uint32_t)p.pr.size(), [&](uint32_t i) {
     if (p.pr[i].p3 != NONE)  // fixed pairs (k_miller_f3 on the device)
-      job_miller3(p.pr[i], c->qlines.data(), g1out.data(), c->g2pp.data(), fbuf.data(), i);
+      job_miller3(p.pr[i], c->qlines.data(), c->pklines.data(), c->pklines.data() + MILLER_LINES, g1out.data(),
+                  fbuf.data(), i);
     else
       job_miller(p.pr[i], c->qlines.data(), g1out.data(), g1out.data(), g2out.data(), fbuf.data(), i);
   });
