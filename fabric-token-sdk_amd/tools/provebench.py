@@ -26,20 +26,22 @@ def main():
     ap.add_argument("--threads", type=int, default=None, help="host planning threads (ftz_options.threads)")
     ap.add_argument("--slots", type=int, default=None, help="passes in flight (ftz_options.slots)")
     ap.add_argument("--layout", default=None, help="prover t' / line stage layout: one_lane | sextet")
+    ap.add_argument("--batch", type=int, default=None, help="proofs per device pass (ftz_options.batch)")
     ap.add_argument("--no-split", action="store_true")
     a = ap.parse_args()
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     import time
 
     from zkatdlog import workload as W
-    with zkatdlog.Context(g["pp"].encode(), device=0, threads=a.threads, slots=a.slots) as ctx:
+    with zkatdlog.Context(g["pp"].encode(), device=0, threads=a.threads, slots=a.slots, batch=a.batch) as ctx:
         if a.serial:
             ctx.set_serial(True)
         if a.layout:
             ctx.set_layout("prover_g2lines", a.layout)
-        bench.prover_bench(ctx, 4096, 1)  # warm-up: slots and tables
+        bench.prover_bench(ctx, 4096, 2)  # warm-up: slots and tables
         ctx.prover_stats(reset=True)
         r = bench.prover_bench(ctx, 4096, a.steps)
+        r["pass_proofs"] = min(ctx.options["batch"], 8192)
         r["threads"] = ctx.options["threads"]
         r["slots"] = ctx.options["slots"]
         r["layout"] = a.layout or "default"
