@@ -1107,7 +1107,7 @@ static int prove_chunked(ftz_ctx* c, size_t n, const W* w, int kind, uint8_t* bu
   // responses) planned on the calling thread, and 8192-witness passes fill the
   // slots too slowly (65536 proofs: 298k/s vs 426k/s, profiles/r02g_prover_layout.txt);
   // opt.slots of them in flight (clamped to [2, 8])
-  const size_t K = std::max<size_t>(2, std::min<size_t>(c->opt.slots, 8)), B = std::min<size_t>(c->opt.batch, 8192);
+  const size_t K = std::max<size_t>(2, std::min<size_t>(c->opt.slots, 8)), B = std::min<size_t>(c->opt.batch, 4096);
   while (c->pslots.size() < K) {
     ftz_prover* p = new ftz_prover();
     p->ctx = c;

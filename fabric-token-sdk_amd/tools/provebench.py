@@ -41,7 +41,7 @@ def main():
         bench.prover_bench(ctx, 4096, 2)  # warm-up: slots and tables
         ctx.prover_stats(reset=True)
         r = bench.prover_bench(ctx, 4096, a.steps)
-        r["pass_proofs"] = min(ctx.options["batch"], 8192)
+        r["pass_proofs"] = min(ctx.options["batch"], 4096)
         r["threads"] = ctx.options["threads"]
         r["slots"] = ctx.options["slots"]
         r["layout"] = a.layout or "default"
