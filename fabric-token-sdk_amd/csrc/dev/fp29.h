@@ -456,6 +456,9 @@ FTS_HD j29 j29_add(const j29& p, const j29& q) {
 }
 
 // ---------------------------------------------------- XYZZ bucket accumulator
+// (products in the column-sum form f29_mul_c / f29_sqr_c: the same limbs as
+// f29_mul / f29_sqr with 17 independent accumulators instead of one running
+// sum, so the dependent chains of these long runs of additions are short)
 // x = X / ZZ, y = Y / ZZZ with ZZ^3 = ZZZ^2: the mixed addition needs 8M + 2S
 // (madd-2008-s) against 7M + 4S and the doublings of the Jacobian one -- the
 // MSM bucket sums are long runs of mixed additions.  Coordinates between
@@ -469,13 +472,13 @@ struct x29 {
 FTS_HD x29 x29_dbl_aff(const f29& x0, const f29& y0) {
   f29 x = f29_reduce(x0), y = f29_reduce(y0);      // (1.5, 1)
   f29 U = f29_norm(f29_add(y, y));                 // (3, 1)
-  f29 V = f29_sqr(U);                              // (2, 1)
-  f29 W = f29_mul(U, V);                           // (2, 1)
-  f29 S = f29_mul(x, V);                           // (2, 1)
-  f29 xx = f29_sqr(x);
+  f29 V = f29_sqr_c(U);                              // (2, 1)
+  f29 W = f29_mul_c(U, V);                           // (2, 1)
+  f29 S = f29_mul_c(x, V);                           // (2, 1)
+  f29 xx = f29_sqr_c(x);
   f29 M = f29_norm(f29_add(f29_add(xx, xx), xx));  // (6, 1)
-  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sqr(M), S), S));         // (40, 3) -> (1.5, 1)
-  f29 Y3 = f29_reduce(f29_sub(f29_mul(M, f29_norm(f29_sub(S, X3))), f29_mul(W, y)));  // (4, 2)
+  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sqr_c(M), S), S));         // (40, 3) -> (1.5, 1)
+  f29 Y3 = f29_reduce(f29_sub(f29_mul_c(M, f29_norm(f29_sub(S, X3))), f29_mul_c(W, y)));  // (4, 2)
   return {X3, Y3, V, W, false};
 }
 
@@ -487,8 +490,8 @@ FTS_HD x29 x29_madd(const x29& p, const f29& x2, const f29& y2) {
     f29 one = f29_reduce(f29_from_fp(fe_one<ModP>()));
     return {f29_reduce(x2), f29_reduce(y2), one, one, false};
   }
-  f29 U2 = f29_mul(x2, p.zz);                      // 32 x 2: (2, 1)
-  f29 S2 = f29_mul(y2, p.zzz);                     // (2, 1)
+  f29 U2 = f29_mul_c(x2, p.zz);                      // 32 x 2: (2, 1)
+  f29 S2 = f29_mul_c(y2, p.zzz);                     // (2, 1)
   f29 P = f29_norm(f29_sub(U2, p.x));              // (4, 1)
   f29 R = f29_norm(f29_sub(S2, p.y));              // (4, 1)
   if (f29_is_zero(P)) {
@@ -497,13 +500,13 @@ FTS_HD x29 x29_madd(const x29& p, const f29& x2, const f29& y2) {
     o.inf = true;
     return o;
   }
-  f29 PP = f29_sqr(P);                             // 16: (2, 1)
-  f29 PPP = f29_mul(P, PP);                        // 8: (2, 1)
-  f29 Q = f29_mul(p.x, PP);                        // 4: (2, 1)
-  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sub(f29_sqr(R), PPP), Q), Q));  // (8, 4) -> (1.5, 1)
-  f29 Y3a = f29_mul(R, f29_norm(f29_sub(Q, X3)));  // 4 x 3.5: (2, 1)
-  f29 Y3 = f29_reduce(f29_sub(Y3a, f29_mul(p.y, PPP)));            // (4, 2) -> (1.5, 1)
-  return {X3, Y3, f29_mul(p.zz, PP), f29_mul(p.zzz, PPP), false};
+  f29 PP = f29_sqr_c(P);                             // 16: (2, 1)
+  f29 PPP = f29_mul_c(P, PP);                        // 8: (2, 1)
+  f29 Q = f29_mul_c(p.x, PP);                        // 4: (2, 1)
+  f29 X3 = f29_reduce(f29_sub(f29_sub(f29_sub(f29_sqr_c(R), PPP), Q), Q));  // (8, 4) -> (1.5, 1)
+  f29 Y3a = f29_mul_c(R, f29_norm(f29_sub(Q, X3)));  // 4 x 3.5: (2, 1)
+  f29 Y3 = f29_reduce(f29_sub(Y3a, f29_mul_c(p.y, PPP)));            // (4, 2) -> (1.5, 1)
+  return {X3, Y3, f29_mul_c(p.zz, PP), f29_mul_c(p.zzz, PPP), false};
 }
 
 // to Jacobian without an inversion: Z' = ZZ ZZZ, X' = X ZZ ZZZ^2, Y' = Y ZZZ^4
