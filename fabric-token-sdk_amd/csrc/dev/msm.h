@@ -344,6 +344,16 @@ FTS_HD bool g1_from_raw(const uint8_t* b, g1a& a) {
 // and a final add").  Returns n, or the index of the first point that does not
 // decode (out untouched).  Exceptional cases (identity, P + P, P - P) go
 // through jac_add_aff.
+// Jacobian -> affine -> gnark RawBytes (infinity: 64 zero bytes)
+FTS_HD void g1j_to_raw(const g1j& acc, uint8_t out[64]) {
+  g1a r;
+  r.inf = is_zero(acc.z);
+  fp zi = r.inf ? fe_one<ModP>() : fp_inv_var(acc.z), zi2 = sqr(zi);
+  r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
+  r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
+  g1_to_bytes(out, r);
+}
+
 FTS_HDN uint32_t g1_sum_raw(uint32_t n, const uint8_t* raw, uint8_t out[64]) {
   g1j acc = jac_inf<fp>();
   for (uint32_t i = 0; i < n; i++) {
@@ -351,12 +361,7 @@ FTS_HDN uint32_t g1_sum_raw(uint32_t n, const uint8_t* raw, uint8_t out[64]) {
     if (!g1_from_raw(raw + 64 * (size_t)i, a)) return i;
     acc = jac_add_aff(acc, a);
   }
-  g1a r;
-  r.inf = is_zero(acc.z);
-  fp zi = r.inf ? fe_one<ModP>() : fp_inv_var(acc.z), zi2 = sqr(zi);
-  r.x = r.inf ? fe_zero<ModP>() : acc.x * zi2;
-  r.y = r.inf ? fe_zero<ModP>() : acc.y * zi2 * zi;
-  g1_to_bytes(out, r);
+  g1j_to_raw(acc, out);
   return n;
 }
 

@@ -358,11 +358,13 @@ __device__ __forceinline__ void coop29_add(f29& X, f29& Y, f29& Z, bool& inf, co
 }
 
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
-// on one wave with the 4-lane cooperative carry-free point ops; the last call
-// (w_lo = 0) converts to affine (binary-EEA inverse) and gnark RawBytes.  With
-// pre (one reduction window) this is the affine conversion alone.
+// on one wave with the 4-lane cooperative carry-free point ops, the Jacobian
+// result in acc_buf.  The affine conversion (one binary-EEA inverse: ~40k
+// instructions issued by a single lane) runs on the host after the 96-byte
+// read-back (msm_rt.hip g1j_to_raw).  With pre (one reduction window) this is a
+// copy of the window sum.
 __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
-                                                   G1JDev* acc_buf, G1Dev* res, uint8_t* bytes) {
+                                                   G1JDev* acc_buf) {
   if (blockIdx.x != 0) return;
   j29 a0 = w_hi == p.rw ? j29_inf() : j29_ld(*acc_buf);
   f29 X = a0.x, Y = a0.y, Z = a0.z;
@@ -373,19 +375,7 @@ __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uin
     coop29_add(X, Y, Z, inf, j29_ld(wsum[w]));
   }
   if (threadIdx.x != 0) return;
-  g1j a = j29_to({X, Y, Z, inf});
-  g1j_store(*acc_buf, a);
-  if (w_lo == 0) {
-    g1a r;
-    r.inf = is_zero(a.z);
-    fp zi = fp_inv_var(a.z), zi2 = sqr(zi);
-    r.x = r.inf ? fe_zero<ModP>() : a.x * zi2;
-    r.y = r.inf ? fe_zero<ModP>() : a.y * zi2 * zi;
-    G1Dev d;
-    g1_store(d, r);
-    *res = d;
-    g1_to_bytes(bytes, r);
-  }
+  g1j_store(*acc_buf, j29_to({X, Y, Z, inf}));
 }
 
 // test points with known logs: P_i = (i + off) G from the generator's fixed-base
