@@ -241,6 +241,10 @@ __device__ __forceinline__ void coop29_sqr_level(const f29 (&a)[CNT], f29 (&out)
 
 template <int CNT>
 __device__ __forceinline__ void coop29_level(const f29 (&a)[CNT], const f29 (&b)[CNT], f29 (&out)[CNT]) {
+  if constexpr (CNT == 1) {  // every lane computes the one product: no select, no broadcast
+    out[0] = f29_mul_c(a[0], b[0]);
+    return;
+  }
   const int k = (int)(threadIdx.x & 3);  // every quad of lanes computes the level
   const f29& a1 = a[CNT > 1 ? 1 : 0];
   const f29& a2 = a[CNT > 2 ? 2 : 0];
