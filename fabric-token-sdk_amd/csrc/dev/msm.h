@@ -292,15 +292,21 @@ FTS_HD j29 j29_inf() {
 }
 FTS_HD j29 j29_ld(const G1JDev& d) { return j29_from(g1j_load(d)); }
 
-// small-scalar multiple (k < 2^32), from the top set bit
+// small-scalar multiple (k < 2^32) by 2-bit windows from the top one: P, 2P, 3P
+// in registers (selects, no indexed array), two doublings and at most one
+// addition per window.  The lanes of a wave take different k, so a per-bit
+// conditional addition ran in every bit position for the wave (16 doublings +
+// 16 additions for 16-bit k); windows halve the additions
 FTS_HD j29 j29_mul_small(const j29& p, uint32_t k) {
   if (!k) return j29_inf();
-  j29 acc = p;
-  int top = 31;
-  while (!((k >> top) & 1)) top--;
-  for (int i = top - 1; i >= 0; i--) {
-    acc = j29_dbl(acc);
-    if ((k >> i) & 1) acc = j29_add(acc, p);
+  const j29 p2 = j29_dbl(p), p3 = j29_add(p2, p);
+  const int top = 31 - __builtin_clz(k), w = top >> 1;
+  uint32_t d = (k >> (2 * w)) & 3u;
+  j29 acc = d == 1 ? p : (d == 2 ? p2 : p3);
+  for (int i = w - 1; i >= 0; i--) {
+    acc = j29_dbl(j29_dbl(acc));
+    d = (k >> (2 * i)) & 3u;
+    if (d) acc = j29_add(acc, d == 1 ? p : (d == 2 ? p2 : p3));
   }
   return acc;
 }
@@ -338,12 +344,6 @@ FTS_HD bool g1_from_raw(const uint8_t* b, g1a& a) {
   return canon && g1_on_curve(a);
 }
 
-// Sum of n RawBytes points into out (RawBytes): the final addition of a
-// point-split multi-GPU MSM, where each rank contributes the MSM of its slice
-// of the points (SURVEY.md 8(e): "each GPU returns one partial sum; one gather
-// and a final add").  Returns n, or the index of the first point that does not
-// decode (out untouched).  Exceptional cases (identity, P + P, P - P) go
-// through jac_add_aff.
 // Jacobian -> affine -> gnark RawBytes (infinity: 64 zero bytes)
 FTS_HD void g1j_to_raw(const g1j& acc, uint8_t out[64]) {
   g1a r;
@@ -354,6 +354,12 @@ FTS_HD void g1j_to_raw(const g1j& acc, uint8_t out[64]) {
   g1_to_bytes(out, r);
 }
 
+// Sum of n RawBytes points into out (RawBytes): the final addition of a
+// point-split multi-GPU MSM, where each rank contributes the MSM of its slice
+// of the points (SURVEY.md 8(e): "each GPU returns one partial sum; one gather
+// and a final add").  Returns n, or the index of the first point that does not
+// decode (out untouched).  Exceptional cases (identity, P + P, P - P) go
+// through jac_add_aff.
 FTS_HDN uint32_t g1_sum_raw(uint32_t n, const uint8_t* raw, uint8_t out[64]) {
   g1j acc = jac_inf<fp>();
   for (uint32_t i = 0; i < n; i++) {
