@@ -605,15 +605,24 @@ def ppb_leg(device, args, bad_b):
 
 
 def owner_signatures(ctx, n=8192, reps=5):
-    """Idemix owner-signature leg: n NymSignatures (two
-    input owners per ~9.5 KB request, one distinct message per request) verified
-    by ONE ftz_verify_owner_signatures call, end to end from host bytes (proto /
-    ASN.1 decoding, upload, k_nym_part + k_nym_fin, verdicts); best of `reps`.
-    Signatures: tests/golden/idemix_golden.json "bench" (made offline), tiled."""
+    """Idemix owner-signature leg on both idemix curves:
+    BN254 (the curve cmd/pp/dlog/gen.go:117 and the NWO topologies deploy; the
+    reference's tokengen issuer) and FP256BN_AMCL (the unit-test keys)."""
+    from zkatdlog import _abi as A
+    return {"BN254": owner_signatures_curve(ctx, "idemix_bn254_golden.json", A.FTZ_CURVE_BN254, "BN254", n, reps),
+            "FP256BN_AMCL": owner_signatures_curve(ctx, "idemix_golden.json", A.FTZ_CURVE_FP256BN_AMCL,
+                                                   "FP256BN_AMCL", n, reps)}
+
+
+def owner_signatures_curve(ctx, fixture, curve_id, curve_name, n, reps):
+    """n NymSignatures (two input owners per ~9.5 KB request, one distinct message
+    per request) verified by ONE ftz_verify_owner_signatures call, end to end from
+    host bytes (proto / ASN.1 decoding, upload, k_nym_part + k_nym_fin, verdicts);
+    best of `reps`.  Signatures: the fixture's "bench" entries (made offline), tiled."""
     import hashlib
 
     import zkatdlog
-    g = json.load(open(os.path.join(ROOT, "tests", "golden", "idemix_golden.json")))
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", fixture)))
     ent = g["bench"]
 
     def expand(seed, L):
@@ -633,7 +642,7 @@ def owner_signatures(ctx, n=8192, reps=5):
         m = bytes(bytearray(a[1]))
         items += [(a[0], m, a[2]), (b[0], m, b[2])]
     from zkatdlog import _abi as A
-    ix = zkatdlog.Idemix(ctx, bytes.fromhex(g["ipk"]))
+    ix = zkatdlog.Idemix(ctx, bytes.fromhex(g["ipk"]), curve_id=curve_id)
     arr, keep = A.pack_owner_sigs(items)  # the Go shim hands over its own buffers: packing is not timed
     codes = ix.verify_owner_signatures_packed(arr, n)  # warm-up
     ok = all(c == 0 for c in codes)
@@ -646,7 +655,7 @@ def owner_signatures(ctx, n=8192, reps=5):
         best = dt if best is None else min(best, dt)
     ix.close()
     return {"signatures_per_s": round(n / best, 1), "ms_per_call": round(best * 1e3, 3), "signatures": n,
-            "msg_bytes": len(base[0][1]), "all_accepted": ok, "curve": "FP256BN_AMCL"}
+            "msg_bytes": len(base[0][1]), "all_accepted": ok, "curve": curve_name}
 
 
 def main():

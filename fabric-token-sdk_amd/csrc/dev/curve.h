@@ -218,6 +218,70 @@ FTS_HD bool g1_on_curve(const g1a& a) {
   return fe_eq(sqr(a.y), sqr(a.x) * a.x + three);
 }
 
+// gnark G1Affine.SetBytes via mathlib NewG1FromBytes:
+// flags 00 uncompressed (coordinates reduced mod p, (0,0) = infinity, must be
+// on the curve), 01 infinity, 10/11 compressed (smallest/largest root); false
+// when SetBytes returns an error (a is then the point at infinity).
+FTS_HD bool g1_setbytes(const uint8_t* b, uint32_t len, g1a& a) {
+  a.inf = false;
+  bool ok = true;
+  uint8_t m = len >= 1 ? (b[0] & 0xC0) : 0;
+  if (len < 32) {
+    ok = false;
+    a.inf = true;
+  } else if (m == 0x40) {
+    a.inf = true;
+  } else if (m == 0x00) {
+    if (len < 64) {
+      ok = false;
+      a.inf = true;
+    } else {
+      uint32_t t[8];
+      be32_to_limbs_g(t, b);
+      a.x = fe_from_int<ModP>(t);
+      be32_to_limbs_g(t, b + 32);
+      a.y = fe_from_int<ModP>(t);
+      if (is_zero(a.x) && is_zero(a.y)) {
+        a.inf = true;
+      } else {
+        ok = g1_on_curve(a);
+      }
+    }
+  } else {
+    uint8_t xb[32];
+    for (int k = 0; k < 32; k++) xb[k] = b[k];
+    xb[0] &= 0x3F;
+    uint32_t t[8];
+    be32_to_limbs(t, xb);
+    uint32_t mm[8];
+    for (int k = 0; k < 8; k++) mm[k] = P_MOD[k];
+    uint32_t tmp[8];
+    if (!sub8(tmp, t, mm)) {
+      ok = false;  // X >= p
+      a.inf = true;
+    } else {
+      a.x = fe_from_int<ModP>(t);
+      fp three = fe_one<ModP>() + fe_one<ModP>() + fe_one<ModP>();
+      fp rhs = sqr(a.x) * a.x + three;
+      fp y;
+      if (!fp_sqrt(y, rhs)) {
+        ok = false;
+        a.inf = true;
+      } else {
+        // gnark LexicographicallyLargest: y > (p-1)/2 as integers
+        fp ny = fe_neg(y);
+        uint32_t yi[8], nyi[8], d[8];
+        fe_to_int(yi, y);
+        fe_to_int(nyi, ny);
+        bool largest = sub8(d, nyi, yi) != 0;  // y > -y
+        bool want_largest = (m == 0xC0);
+        a.y = (largest == want_largest) ? y : ny;
+      }
+    }
+  }
+  return ok;
+}
+
 FTS_HD bool g2_on_curve(const g2a& a) {
   if (a.inf) return true;
   return f2_eq(sqr(a.y), sqr(a.x) * a.x + f2_const(TWIST_B));

@@ -19,6 +19,7 @@
 #pragma once
 #include "fp29.h"
 #include "fp_wide.h"
+#include "glv.h"
 #include "pairing.h"
 #include "sha256.h"
 
@@ -264,70 +265,6 @@ FTS_HD void b64_encode(uint8_t* out, const uint8_t* in, uint32_t len) {
 }
 
 // ------------------------------------------------------------------ jobs
-// gnark G1Affine.SetBytes via mathlib NewG1FromBytes:
-// flags 00 uncompressed (coordinates reduced mod p, (0,0) = infinity, must be
-// on the curve), 01 infinity, 10/11 compressed (smallest/largest root); false
-// when SetBytes returns an error (a is then the point at infinity).
-FTS_HD bool g1_setbytes(const uint8_t* b, uint32_t len, g1a& a) {
-  a.inf = false;
-  bool ok = true;
-  uint8_t m = len >= 1 ? (b[0] & 0xC0) : 0;
-  if (len < 32) {
-    ok = false;
-    a.inf = true;
-  } else if (m == 0x40) {
-    a.inf = true;
-  } else if (m == 0x00) {
-    if (len < 64) {
-      ok = false;
-      a.inf = true;
-    } else {
-      uint32_t t[8];
-      be32_to_limbs_g(t, b);
-      a.x = fe_from_int<ModP>(t);
-      be32_to_limbs_g(t, b + 32);
-      a.y = fe_from_int<ModP>(t);
-      if (is_zero(a.x) && is_zero(a.y)) {
-        a.inf = true;
-      } else {
-        ok = g1_on_curve(a);
-      }
-    }
-  } else {
-    uint8_t xb[32];
-    for (int k = 0; k < 32; k++) xb[k] = b[k];
-    xb[0] &= 0x3F;
-    uint32_t t[8];
-    be32_to_limbs(t, xb);
-    uint32_t mm[8];
-    for (int k = 0; k < 8; k++) mm[k] = P_MOD[k];
-    uint32_t tmp[8];
-    if (!sub8(tmp, t, mm)) {
-      ok = false;  // X >= p
-      a.inf = true;
-    } else {
-      a.x = fe_from_int<ModP>(t);
-      fp three = fe_one<ModP>() + fe_one<ModP>() + fe_one<ModP>();
-      fp rhs = sqr(a.x) * a.x + three;
-      fp y;
-      if (!fp_sqrt(y, rhs)) {
-        ok = false;
-        a.inf = true;
-      } else {
-        // gnark LexicographicallyLargest: y > (p-1)/2 as integers
-        fp ny = fe_neg(y);
-        uint32_t yi[8], nyi[8], d[8];
-        fe_to_int(yi, y);
-        fe_to_int(nyi, ny);
-        bool largest = sub8(d, nyi, yi) != 0;  // y > -y
-        bool want_largest = (m == 0xC0);
-        a.y = (largest == want_largest) ? y : ny;
-      }
-    }
-  }
-  return ok;
-}
-
 FTS_HD uint8_t job_decode(const DecodeJob& j, const uint8_t* wire, G1Dev* pts, uint8_t* arena) {
   g1a a;
   bool ok = g1_setbytes(wire + j.raw, j.len, a);
@@ -578,60 +515,6 @@ FTS_HD g1j g1_fixed_acc_fp(g1j acc, const G1Dev* tab, int base, const uint32_t s
     }
   }
   return acc;
-}
-
-// ---- GLV variable-base multiplication on G1 (phi(x, y) = (beta x, y) = [lambda]).
-// r[na + nb] = a[na] * b[nb]  (schoolbook, small operands)
-FTS_HD void mul_small(uint32_t* r, const uint32_t* a, int na, const uint32_t* b, int nb) {
-  for (int i = 0; i < na + nb; i++) r[i] = 0;
-  for (int i = 0; i < na; i++) {
-    uint32_t c = 0;
-    for (int j = 0; j < nb; j++) {
-      uint64_t t = (uint64_t)a[i] * b[j] + r[i + j] + c;
-      r[i + j] = (uint32_t)t;
-      c = (uint32_t)(t >> 32);
-    }
-    r[i + nb] = c;
-  }
-}
-
-// k = k1 + k2 lambda (mod r) with |k1|, |k2| < 2^128 (constants from
-// gen_constants.py: c1 = (k g1) >> 256, c2 = (k g2) >> 256, k2 = c1 |b1| - c2 b2,
-// k1 = k - k2 lambda mod r taken in (-r/2, r/2]).
-FTS_HD void glv_split(const uint32_t k[8], uint32_t k1[4], bool& n1, uint32_t k2[4], bool& n2) {
-  uint32_t g[8], w[16], c1[4], c2[4];
-  for (int i = 0; i < 8; i++) g[i] = GLV_G1[i];
-  mul_wide(w, k, g);
-  for (int i = 0; i < 4; i++) c1[i] = w[8 + i];
-  for (int i = 0; i < 8; i++) g[i] = GLV_G2[i];
-  mul_wide(w, k, g);
-  for (int i = 0; i < 4; i++) c2[i] = w[8 + i];
-  uint32_t b1[2] = {GLV_B1ABS[0], GLV_B1ABS[1]}, b2[4] = {GLV_B2[0], GLV_B2[1], GLV_B2[2], GLV_B2[3]};
-  uint32_t t1[6], t2[6], d[6];
-  mul_small(t1, c1, 4, b1, 2);
-  mul_small(t2, c2, 2, b2, 4);
-  uint32_t br = 0;
-  for (int i = 0; i < 6; i++) d[i] = subb32(t1[i], t2[i], br, &br);
-  n2 = br != 0;  // |t1 - t2| < 2^128 <<< 2^192: the borrow is the sign
-  if (n2) {
-    uint32_t c = 1;
-    for (int i = 0; i < 6; i++) d[i] = addc32(~d[i], 0, c, &c);
-  }
-  for (int i = 0; i < 4; i++) k2[i] = d[i];
-  // k1 = k - k2 lambda  (mod r)
-  uint32_t k2f[8] = {k2[0], k2[1], k2[2], k2[3], 0, 0, 0, 0};
-  fr t = fe_from_int<ModR>(k2f) * fe_const<ModR>(GLV_LAMBDA);
-  fr K = fe_from_int<ModR>(k);
-  fr r1 = n2 ? K + t : K - t;
-  uint32_t v[8], u[8], h[8], rm[8];
-  fe_to_int(v, r1);
-  for (int i = 0; i < 8; i++) {
-    h[i] = R_HALF[i];
-    rm[i] = R_MOD[i];
-  }
-  n1 = sub8(u, h, v) != 0;  // v > (r-1)/2
-  if (n1) sub8(v, rm, v);
-  for (int i = 0; i < 4; i++) k1[i] = v[i];
 }
 
 // k P for affine P and a scalar k < r.  Joint double-and-add over the two

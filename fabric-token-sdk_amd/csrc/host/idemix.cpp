@@ -344,8 +344,67 @@ std::string parse_ipk(const uint8_t* p, size_t n, IdemixIpk& out) {
   return "";
 }
 
+namespace {
+// strip leading zero bytes of a big-endian integer
+void be_strip(const uint8_t*& p, size_t& n) {
+  while (n && *p == 0) {
+    p++;
+    n--;
+  }
+}
+// big-endian integer of at most 32 significant bytes -> 32 bytes; false if wider
+bool be_to32(const uint8_t* p, size_t n, uint8_t out[32]) {
+  be_strip(p, n);
+  if (n > 32) return false;
+  memset(out, 0, 32 - n);
+  if (n) memcpy(out + 32 - n, p, n);
+  return true;
+}
+bool be32_geq_r(const uint8_t b[32]) {
+  uint32_t v[8], t[8], rm[8];
+  fts::be32_to_limbs(v, b);
+  for (int i = 0; i < 8; i++) rm[i] = fts::R_MOD[i];
+  return fts::sub8(t, v, rm) == 0;
+}
+void canon_xy(const fts::g1a& a, uint8_t x[32], uint8_t y[32]) {
+  uint32_t t[8];
+  if (a.inf) {
+    memset(x, 0, 32);
+    memset(y, 0, 32);
+    return;
+  }
+  fts::fe_to_int(t, a.x);
+  fts::limbs_to_be32(x, t);
+  fts::fe_to_int(t, a.y);
+  fts::limbs_to_be32(y, t);
+}
+}  // namespace
+
+void be_mod_r(const uint8_t* p, size_t n, uint8_t out[32]) {
+  using namespace fts;
+  be_strip(p, n);
+  uint32_t w[8] = {0, 1, 0, 0, 0, 0, 0, 0};
+  const fr two32 = fe_from_int<ModR>(w);
+  fr acc = fe_zero<ModR>();
+  size_t lead = n % 4;
+  auto word = [&](uint32_t v) {
+    uint32_t a[8] = {v, 0, 0, 0, 0, 0, 0, 0};
+    acc = acc * two32 + fe_from_int<ModR>(a);
+  };
+  if (lead) {
+    uint32_t v = 0;
+    for (size_t i = 0; i < lead; i++) v = (v << 8) | p[i];
+    word(v);
+  }
+  for (size_t i = lead; i < n; i += 4)
+    word(((uint32_t)p[i] << 24) | ((uint32_t)p[i + 1] << 16) | ((uint32_t)p[i + 2] << 8) | p[i + 3]);
+  uint32_t t[8];
+  fe_to_int(t, acc);
+  limbs_to_be32(out, t);
+}
+
 void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_t* sig, size_t sig_len,
-                            NymDecoded& out) {
+                            NymDecoded& out, int curve) {
   out.code = 0;
   out.why.clear();
   auto fail = [&](int code, const char* why) {
@@ -377,13 +436,21 @@ void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_
   // an empty NymX / NymY is nil even when it is on the wire (common.go:52 nil check)
   if (!pr[0] || !pr[1] || v[0].len == 0 || v[1].len == 0)
     return fail(FTZ_ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid");
-  // NymPublicKey import: raw = NymX || NymY split in halves, FromBytes reads 32 bytes of each
+  // NymPublicKey import: raw = NymX || NymY split in halves.  FP256BN: FromBytes
+  // reads 32 bytes of each (NewECPbigs later); BN254: G1FromProto wants halves of
+  // exactly 32 bytes and gnark SetBytes must accept X || Y
   size_t tot = v[0].len + v[1].len, half = tot / 2;
-  if (half < 32) return fail(FTZ_ERR_OWNER, "failed to import nym public key");
+  bool bn = curve == FTZ_CURVE_BN254;
+  if (half < 32 || (bn && tot != 64)) return fail(FTZ_ERR_OWNER, "failed to import nym public key");
   auto raw_at = [&](size_t i) { return i < v[0].len ? v[0].p[i] : v[1].p[i - v[0].len]; };
   for (int i = 0; i < 32; i++) {
     out.ints[0][i] = raw_at(i);
     out.ints[1][i] = raw_at(half + i);
+  }
+  if (bn) {
+    fts::g1a a;
+    if (!fts::bn_point_from_xy(out.ints[0], out.ints[1], a)) return fail(FTZ_ERR_OWNER, "failed to import nym public key");
+    canon_xy(a, out.ints[0], out.ints[1]);
   }
   PbField ou = v[2], role = v[3];
   bool has_ou = pr[2], has_role = pr[3];
@@ -400,6 +467,24 @@ void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_
   if (!pe.empty()) {
     out.code = FTZ_ERR_SIGNATURE;
     out.why = "error unmarshalling signature: " + pe;
+    return;
+  }
+  if (bn) {  // big.Int SetBytes over each whole field (absent = 0)
+    const uint8_t* fp_[4];
+    size_t fl[4];
+    for (int q = 0; q < 4; q++) {
+      fp_[q] = pr[q] ? v[q].p : nullptr;
+      fl[q] = pr[q] ? v[q].len : 0;
+    }
+    // Zr.Bytes() of the Nonce (common.BigToBytes): an integer >= 2^256 panics
+    if (!be_to32(fp_[3], fl[3], out.ints[5]))
+      return fail(FTZ_ERR_SIGNATURE, "failure [runtime error: makeslice: len out of range]");
+    uint8_t cr[32];
+    be_mod_r(fp_[0], fl[0], cr);
+    if (!be_to32(fp_[0], fl[0], out.ints[2]) || be32_geq_r(out.ints[2])) memset(out.ints[2], 0xff, 32);
+    be_mod_r(fp_[1], fl[1], out.ints[3]);
+    be_mod_r(fp_[2], fl[2], out.ints[4]);
+    nym_glv_split_bn(cr, out.glv);
     return;
   }
   for (int q = 0; q < 4; q++) {
@@ -481,8 +566,23 @@ void nym_glv_split(const uint8_t kb[32], uint32_t out[12]) {
   out[11] = 0;
 }
 
-void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymLayout& L) {
-  constexpr size_t PER_JOB = fts::NYM_SC_BYTES + 176;
+void nym_glv_split_bn(const uint8_t kb[32], uint32_t out[12]) {
+  uint32_t k[8], k1[4], k2[4];
+  bool n1, n2;
+  fts::be32_to_limbs(k, kb);
+  fts::glv_split(k, k1, n1, k2, n2);
+  for (int i = 0; i < 4; i++) {
+    out[i] = k1[i];
+    out[5 + i] = k2[i];
+  }
+  out[4] = out[9] = 0;
+  out[10] = (n1 ? 1u : 0u) | (n2 ? 2u : 0u);
+  out[11] = 0;
+}
+
+void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymLayout& L, int curve) {
+  constexpr size_t PER_JOB = fts::NYM_SC_BYTES + fts::NYM_PRE_SLOT;
+  const size_t align = (curve == FTZ_CURVE_BN254 ? fts::NymCurve<fts::fp>::PRE : fts::NymCurve<fts::fq>::PRE) % 16;
   size_t off = ((m * sizeof(fts::NymJob) + 15) & ~(size_t)15) + m * PER_JOB;
   std::map<std::pair<const uint8_t*, size_t>, uint32_t> at;
   L.msg_off.resize(m);
@@ -492,7 +592,7 @@ void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymL
     auto key = std::make_pair(q.msg, q.msg_len);
     auto it = at.find(key);
     if (it == at.end()) {
-      off = ((off + 15) & ~(size_t)15) + 6;
+      off = ((off + 15) & ~(size_t)15) + align;
       it = at.emplace(key, (uint32_t)off).first;
       L.distinct.push_back({(uint32_t)off, (uint32_t)k});
       off += q.msg_len;
@@ -503,9 +603,14 @@ void nym_plan_layout(const ftz_owner_sig* s, const uint32_t* idx, size_t m, NymL
 }
 
 void nym_fill(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDecoded* dec,
-              const uint8_t hash_slot[32], const NymLayout& L, uint8_t* blob,
-              const std::function<void(size_t, const std::function<void(size_t)>&)>& par) {
-  constexpr size_t SC = fts::NYM_SC_BYTES, PRE = 176, PIECE = 256;
+              const std::vector<uint8_t>& ipk_hash, const NymLayout& L, uint8_t* blob,
+              const std::function<void(size_t, const std::function<void(size_t)>&)>& par, int curve) {
+  constexpr size_t SC = fts::NYM_SC_BYTES, PRE = fts::NYM_PRE_SLOT, PIECE = 256;
+  const bool bn = curve == FTZ_CURVE_BN254;
+  // copy(proofData[4 + 2 G:], ipk.Hash): the 32-byte slot after t and Nym (G = 65 / 64)
+  const size_t hash_at = bn ? 4 + 2 * 64 : 4 + 2 * 65, tail_at = fts::NymCurve<fts::fp>::PRE;
+  uint8_t hash_slot[32] = {};
+  memcpy(hash_slot, ipk_hash.data(), ipk_hash.size() < 32 ? ipk_hash.size() : 32);
   size_t base = (m * sizeof(fts::NymJob) + 15) & ~(size_t)15;
   size_t jp = (m + PIECE - 1) / PIECE, mp = (L.distinct.size() + 15) / 16;
   par(jp + mp, [&](size_t p) {
@@ -522,7 +627,12 @@ void nym_fill(const ftz_owner_sig* s, const uint32_t* idx, size_t m, const NymDe
         uint8_t* pre = blob + j.pre;
         memset(pre, 0, PRE);
         memcpy(pre, "sign", 4);
-        memcpy(pre + 134, hash_slot, 32);
+        memcpy(pre + hash_at, hash_slot, 32);
+        if (bn)  // BN254: the 2 bytes after the message are ipk.Hash's bytes there, if it is that long, else 0
+          for (size_t q = 0; q < 2; q++) {
+            size_t hi = 32 + j.msg_len + q;
+            pre[tail_at + q] = hi < ipk_hash.size() ? ipk_hash[hi] : 0;
+          }
       }
     } else {
       size_t d0 = (p - jp) * 16;
@@ -554,16 +664,23 @@ std::string merge_ecp(const PbField& f, std::vector<uint8_t>& x, std::vector<uin
   return "";
 }
 
-// mathlib Zr UnmarshalJSON on FP256BN_AMCL: D_NIL, D_OK (32 raw bytes, FromBytes
-// reads the first 32), D_ERR (Unmarshal error), D_PANIC (foreign curve / short element)
-DecStatus zr_json(const JDoc& d, int64_t node, uint8_t out[32]) {
+// mathlib Zr UnmarshalJSON on the idemix curve: D_NIL, D_OK, D_ERR (Unmarshal
+// error), D_PANIC (a Zr of another curve: the driver's type assertion on use).
+// FP256BN_AMCL: FromBytes reads the first 32 raw bytes (a shorter element
+// panics); BN254: big.Int SetBytes over the whole element, out = its value mod r.
+DecStatus zr_json(const JDoc& d, int64_t node, uint8_t out[32], int want_curve) {
   if (node < 0 || d.at((uint32_t)node).type == J_NULL) return D_NIL;
   if (d.at((uint32_t)node).type != J_OBJ) return D_ERR;
   int64_t curve = 0;
   if (dec_int(d, d.field((uint32_t)node, "curve"), curve) == D_ERR) return D_ERR;
   std::vector<uint8_t> raw;
   if (dec_bytes(d, d.field((uint32_t)node, "element"), raw) == D_ERR) return D_ERR;
-  if (curve != FTZ_CURVE_FP256BN_AMCL || raw.size() < 32) return D_PANIC;
+  if (curve != want_curve) return D_PANIC;
+  if (want_curve == FTZ_CURVE_BN254) {
+    be_mod_r(raw.data(), raw.size(), out);
+    return D_OK;
+  }
+  if (raw.size() < 32) return D_PANIC;
   memcpy(out, raw.data(), 32);
   return D_OK;
 }
@@ -573,7 +690,7 @@ DecStatus zr_json(const JDoc& d, int64_t node, uint8_t out[32]) {
 // crypto/audit/auditor.go:252-274 InspectTokenOwner up to the curve arithmetic
 // of AuditInfo.Match (identity/msp/idemix/audit.go:51-83); see idemix.h
 void decode_owner_audit(const uint8_t* owner, size_t owner_len, const uint8_t* ai, size_t ai_len, size_t n_hattrs,
-                        EidDecoded& out) {
+                        EidDecoded& out, int curve) {
   out = EidDecoded();
   auto fail = [&](int code, const std::string& why) {
     out.code = code;
@@ -598,8 +715,8 @@ void decode_owner_audit(const uint8_t* owner, size_t owner_len, const uint8_t* a
   bool attrs_nil = true;
   if (!nil_ai) {
     uint8_t tmp[32];
-    rs = zr_json(d, d.field(root, "RNymEid"), out.rnym);
-    DecStatus es = zr_json(d, d.field(root, "EID"), tmp);
+    rs = zr_json(d, d.field(root, "RNymEid"), out.rnym, curve);
+    DecStatus es = zr_json(d, d.field(root, "EID"), tmp, curve);
     if (rs == D_ERR || es == D_ERR) return fail(FTZ_ERR_OWNER, "failed to get owner matcher");
     int64_t an = d.field(root, "Attributes");
     if (an >= 0 && d.at((uint32_t)an).type != J_NULL) {
@@ -656,10 +773,20 @@ void decode_owner_audit(const uint8_t* owner, size_t owner_len, const uint8_t* a
   if (!eid_nym || !nym_seen) return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: no EidNym provided");
   if (n_hattrs <= 2)
     return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: could not access H_a_eid in array");
-  if (nil_ai || rs == D_NIL) return fail(FTZ_ERR_PANIC, "panic: nil RNymEid");
-  if (ex.size() < 32 || ey.size() < 32) return fail(FTZ_ERR_PANIC, "panic: index out of range");
-  memcpy(out.nym_x, ex.data(), 32);
-  memcpy(out.nym_y, ey.data(), 32);
+  if (curve == FTZ_CURVE_BN254) {
+    // AuditNymEid on BN254: EidNym through G1FromProto (an error is a Match
+    // error) before Mul2 dereferences RNymEid
+    fts::g1a a;
+    if (ex.size() != 32 || ey.size() != 32 || !fts::bn_point_from_xy(ex.data(), ey.data(), a))
+      return fail(FTZ_ERR_AUDIT, "error while verifying the nym eid: could not deserialize EidNym");
+    if (nil_ai || rs == D_NIL) return fail(FTZ_ERR_PANIC, "panic: nil RNymEid");
+    canon_xy(a, out.nym_x, out.nym_y);
+  } else {
+    if (nil_ai || rs == D_NIL) return fail(FTZ_ERR_PANIC, "panic: nil RNymEid");
+    if (ex.size() < 32 || ey.size() < 32) return fail(FTZ_ERR_PANIC, "panic: index out of range");
+    memcpy(out.nym_x, ex.data(), 32);
+    memcpy(out.nym_y, ey.data(), 32);
+  }
   // HashToZr(EnrollmentID): SHA-256 read big-endian, reduced mod n on the device
   fts::Sha256 h;
   h.init();

@@ -1661,7 +1661,7 @@ static bool g2_lines_normalisable(const std::vector<uint8_t>& raw) {
 }
 
 bool pp_sig_tables(const PPInfo& pp) {
-  if (pp.base == 0 || pp.base > G1B_SIG_MAX_DIGITS || pp.sig_r.size() != pp.base || pp.sig_s.size() != pp.base)
+  if (pp.no_sigtab || pp.base == 0 || pp.base > G1B_SIG_MAX_DIGITS || pp.sig_r.size() != pp.base || pp.sig_s.size() != pp.base)
     return false;
   auto zero = [](const std::vector<uint8_t>& v) {
     for (uint8_t b : v)

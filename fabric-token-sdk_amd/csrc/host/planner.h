@@ -37,6 +37,9 @@ struct PPInfo {
   // the prover's membership commitments as three fixed-G2 pairings (Q, PK1,
   // PK2; parse_pp: every line of the three normalisable and pp_sig_tables)
   bool fixed_pairs = false;
+  // the runtime's copy for planning WITHOUT the prover's table set (not built:
+  // ftz_options.prover_tables = 0, or its allocation failed): pp_sig_tables false
+  bool no_sigtab = false;
 };
 // The prover multiplies by the PS signature points of the digits through fixed-
 // base tables (G1B_SIG0 ..) when every digit fits the 8-bit base index and no

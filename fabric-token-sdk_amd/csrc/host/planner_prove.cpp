@@ -697,10 +697,17 @@ struct WitView {
   const uint64_t* vals;  // output values (digits)
 };
 
+// digit i of v in base b the way PB::range decomposes it (repeated division):
+// not v / pp.pow[i], whose float64 math.Pow entries are inexact above 2^53
+static uint32_t digit_of(uint64_t v, uint32_t base, uint32_t i) {
+  for (uint32_t k = 0; k < i; k++) v /= base;
+  return (uint32_t)(v % base);
+}
+
 static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& o, const WitView& w, Plan& pl) {
   const uint32_t e = (uint32_t)pp.exponent;
   for (const BasePatch& q : t.bpatches) {
-    uint32_t d = (uint32_t)((w.vals[q.k / e] / pp.pow[q.k % e]) % pp.base);
+    uint32_t d = digit_of(w.vals[q.k / e], pp.base, q.k % e);
     G1Job& j = q.g1p ? pl.g1p[o.sec[PS_G1P] + q.job] : pl.g1[o.sec[PS_G1] + q.job];
     j.fbase[q.slot] = (uint8_t)(G1B_SIG0 + 2 * d + q.s);
   }
@@ -708,7 +715,7 @@ static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& 
     const uint8_t* src = nullptr;
     uint8_t tmp[32];
     uint32_t d = 0;
-    if (q.kind >= SRC_SIG_R) d = (uint32_t)((w.vals[q.k / e] / pp.pow[q.k % e]) % pp.base);
+    if (q.kind >= SRC_SIG_R) d = digit_of(w.vals[q.k / e], pp.base, q.k % e);
     switch (q.kind) {
       case SRC_SEED: src = w.seed; break;
       case SRC_IN_PT: src = w.in_pt + 64 * q.k; break;

@@ -1,7 +1,7 @@
 // C ABI of idemix owner-signature verification (include/ftsamd.h, SURVEY 8(f)
-// row 3): owner identity and signature protos decoded on the calling thread
-// (host/idemix.cpp), NymSignature.Ver's curve arithmetic and hashes on the GPU
-// (k_nym, one lane per signature).
+// row 3) on BN254 or FP256BN_AMCL: owner identity and signature protos decoded
+// on the host pool (host/idemix.cpp), NymSignature.Ver's curve arithmetic and
+// hashes on the GPU (k_nym_part/_fin, _bn for BN254; dev/idemix.h).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -24,7 +24,8 @@ struct NymSlot {
 
 struct ftz_idemix {
   ftz_ctx* ctx = nullptr;
-  uint8_t hash_slot[32] = {};  // copy(proofData[index:], ipk.Hash) into the 32-byte slot
+  int curve = FTZ_CURVE_FP256BN_AMCL;
+  std::vector<uint8_t> ipk_hash;  // IssuerPublicKey.Hash (copy(proofData[index:], ipk.Hash))
   DBuf<QDev> tab;              // HSk, HRand (and HAttrs[2]) fixed-base tables
   size_t n_hattrs = 0;         // len(IssuerPublicKey.HAttrs)
   bool heid_ok = false;        // HAttrs[2] decoded on the curve (its table exists)
@@ -46,21 +47,37 @@ struct ftz_idemix {
 
 extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curve_id, ftz_idemix** out) {
   if (!ctx || !out || (!ipk && ipk_len)) return set_err(FTZ_E_INVALID, "null argument");
-  if (curve_id != FTZ_CURVE_FP256BN_AMCL)
-    return set_err(FTZ_E_INVALID, "unsupported idemix curve id " + std::to_string(curve_id) + " (FP256BN_AMCL only)");
+  if (curve_id != FTZ_CURVE_FP256BN_AMCL && curve_id != FTZ_CURVE_BN254)
+    return set_err(FTZ_E_INVALID, "unsupported idemix curve id " + std::to_string(curve_id) +
+                                      " (BN254 = 1 or FP256BN_AMCL = 0)");
   if (ipk_len == 0) return set_err(FTZ_E_PP, "empty idemix issuer public key");
   ftsh::IdemixIpk k;
   std::string e = ftsh::parse_ipk(ipk, ipk_len, k);
   if (!e.empty()) return set_err(FTZ_E_PP, e);
-  q1a bases[3];
-  if (!nym_point_from_be(k.hsk_x.data(), k.hsk_y.data(), bases[0]) ||
-      !nym_point_from_be(k.hrand_x.data(), k.hrand_y.data(), bases[1]))
-    return set_err(FTZ_E_PP, "issuer public key: HSk / HRand not on FP256BN");
-  // HAttrs[2] (the enrollment-id base of the auditor's EidNym check)
-  bool heid = k.hattrs_x.size() > 2 && k.hattrs_x[2].size() >= 32 && k.hattrs_y[2].size() >= 32 &&
-              nym_point_from_be(k.hattrs_x[2].data(), k.hattrs_y[2].data(), bases[2]);
-  std::vector<QDev> tab((heid ? 3 : 2) * NYM_TAB_PER_BASE);
-  nym_build_tables(bases, heid ? 3 : 2, tab.data());
+  bool heid = false;
+  std::vector<QDev> tab;
+  if (curve_id == FTZ_CURVE_BN254) {
+    // gurvy G1FromProto: exactly 32-byte coordinates, gnark SetBytes
+    g1a bases[3];
+    auto dec = [](const std::vector<uint8_t>& x, const std::vector<uint8_t>& y, g1a& a) {
+      return x.size() == 32 && y.size() == 32 && bn_point_from_xy(x.data(), y.data(), a) && !a.inf;
+    };
+    if (!dec(k.hsk_x, k.hsk_y, bases[0]) || !dec(k.hrand_x, k.hrand_y, bases[1]))
+      return set_err(FTZ_E_PP, "issuer public key: HSk / HRand not a finite BN254 point");
+    heid = k.hattrs_x.size() > 2 && dec(k.hattrs_x[2], k.hattrs_y[2], bases[2]);
+    tab.resize((heid ? 3 : 2) * NYM_TAB_PER_BASE);
+    nym_build_tables(bases, heid ? 3 : 2, tab.data());
+  } else {
+    q1a bases[3];
+    if (!nym_point_from_be(k.hsk_x.data(), k.hsk_y.data(), bases[0]) ||
+        !nym_point_from_be(k.hrand_x.data(), k.hrand_y.data(), bases[1]))
+      return set_err(FTZ_E_PP, "issuer public key: HSk / HRand not on FP256BN");
+    // HAttrs[2] (the enrollment-id base of the auditor's EidNym check)
+    heid = k.hattrs_x.size() > 2 && k.hattrs_x[2].size() >= 32 && k.hattrs_y[2].size() >= 32 &&
+           nym_point_from_be(k.hattrs_x[2].data(), k.hattrs_y[2].data(), bases[2]);
+    tab.resize((heid ? 3 : 2) * NYM_TAB_PER_BASE);
+    nym_build_tables(bases, heid ? 3 : 2, tab.data());
+  }
   HC(hipSetDevice(ctx->device));
   ftz_idemix* ix = new ftz_idemix();
   ix->ctx = ctx;
@@ -72,7 +89,8 @@ extern "C" int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_le
       return set_err(FTZ_E_DEVICE, std::string("hipStreamCreate failed: ") + hipGetErrorString(se));
     }
   }
-  memcpy(ix->hash_slot, k.hash.data(), k.hash.size() < 32 ? k.hash.size() : 32);
+  ix->curve = curve_id;
+  ix->ipk_hash = k.hash;
   ix->n_hattrs = k.hattrs_x.size();
   ix->heid_ok = heid;
   hipError_t he = ix->tab.upload(tab, ctx->stream);
@@ -113,11 +131,12 @@ int nym_chunk(ftz_idemix* ix, NymSlot& q, const ftz_owner_sig* s, size_t a, size
   std::vector<ftsh::NymDecoded> dec(n);
   ix->pool->run((n + 63) / 64, [&](size_t p) {
     for (size_t i = p * 64; i < n && i < (p + 1) * 64; i++)
-      ftsh::decode_owner_signature(s[a + i].owner, s[a + i].owner_len, s[a + i].sig, s[a + i].sig_len, dec[i]);
+      ftsh::decode_owner_signature(s[a + i].owner, s[a + i].owner_len, s[a + i].sig, s[a + i].sig_len, dec[i],
+                                 ix->curve);
   });
   std::vector<uint32_t> idx;  // chunk-relative
   for (size_t i = 0; i < n; i++) {
-    if (ix->strict_nym && dec[i].code == 0) {
+    if (ix->strict_nym && ix->curve == FTZ_CURVE_FP256BN_AMCL && dec[i].code == 0) {
       q1a nym;
       if (!nym_point_from_be(dec[i].ints[0], dec[i].ints[1], nym)) {
         dec[i].code = FTZ_ERR_OWNER;
@@ -130,20 +149,26 @@ int nym_chunk(ftz_idemix* ix, NymSlot& q, const ftz_owner_sig* s, size_t a, size
   if (idx.empty()) return FTZ_SUCCESS;
   size_t m = idx.size();
   ftsh::NymLayout L;
-  ftsh::nym_plan_layout(s + a, idx.data(), m, L);
+  ftsh::nym_plan_layout(s + a, idx.data(), m, L, ix->curve);
   HC(q.h_blob.reserve(L.total));
   HC(q.d_blob.reserve(L.total));
   HC(q.h_ok.reserve(m));
   HC(q.d_ok.reserve(m));
   HC(q.d_part.reserve(4 * m * sizeof(QJDev)));
   WorkPool* pool = ix->pool;
-  ftsh::nym_fill(s + a, idx.data(), m, dec.data(), ix->hash_slot, L, q.h_blob.p,
-                 [pool](size_t k, const std::function<void(size_t)>& f) { pool->run(k, f); });
+  ftsh::nym_fill(s + a, idx.data(), m, dec.data(), ix->ipk_hash, L, q.h_blob.p,
+                 [pool](size_t k, const std::function<void(size_t)>& f) { pool->run(k, f); }, ix->curve);
   const NymJob* jobs = reinterpret_cast<const NymJob*>(q.d_blob.p);
   QJDev* part = reinterpret_cast<QJDev*>(q.d_part.p);
   HC(hipMemcpyAsync(q.d_blob.p, q.h_blob.p, L.total, hipMemcpyHostToDevice, q.st));
-  k_nym_part<<<(uint32_t)((4 * m + 63) / 64), 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, ix->tab.p, part);
-  k_nym_fin<<<(uint32_t)((m + 63) / 64), 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, part, q.d_ok.p);
+  const uint32_t gp = (uint32_t)((4 * m + 63) / 64), gf = (uint32_t)((m + 63) / 64);
+  if (ix->curve == FTZ_CURVE_BN254) {
+    k_nym_part_bn<<<gp, 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, ix->tab.p, part);
+    k_nym_fin_bn<<<gf, 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, part, q.d_ok.p);
+  } else {
+    k_nym_part<<<gp, 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, ix->tab.p, part);
+    k_nym_fin<<<gf, 64, 0, q.st>>>(jobs, (uint32_t)m, q.d_blob.p, part, q.d_ok.p);
+  }
   HC(hipGetLastError());
   HC(hipMemcpyAsync(q.h_ok.p, q.d_ok.p, m, hipMemcpyDeviceToHost, q.st));
   q.idx.resize(m);
@@ -193,12 +218,12 @@ extern "C" int ftz_audit_owners(ftz_idemix* ix, size_t n, const ftz_owner_audit*
     if ((!it[i].owner && it[i].owner_len) || (!it[i].audit_info && it[i].audit_info_len))
       return set_err(FTZ_E_INVALID, "null buffer with non-zero length");
   if (n > (1u << 26)) return set_err(FTZ_E_INVALID, "too many tokens in one call");
-  if (ix->n_hattrs > 2 && !ix->heid_ok) return set_err(FTZ_E_PP, "issuer public key: HAttrs[2] not on FP256BN");
+  if (ix->n_hattrs > 2 && !ix->heid_ok) return set_err(FTZ_E_PP, "issuer public key: HAttrs[2] not on the idemix curve");
   std::vector<ftsh::EidDecoded> dec(n);
   ix->pool->run((n + 63) / 64, [&](size_t p) {
     for (size_t i = p * 64; i < n && i < (p + 1) * 64; i++)
       ftsh::decode_owner_audit(it[i].owner, it[i].owner_len, it[i].audit_info, it[i].audit_info_len, ix->n_hattrs,
-                               dec[i]);
+                               dec[i], ix->curve);
   });
   std::vector<uint32_t> idx;
   for (size_t i = 0; i < n; i++) {
@@ -223,7 +248,10 @@ extern "C" int ftz_audit_owners(ftz_idemix* ix, size_t n, const ftz_owner_audit*
   }
   hipStream_t st = ix->slot[0].st;
   HC(hipMemcpyAsync(ix->d_eid.p, ix->h_eid.p, m * EID_JOB_BYTES, hipMemcpyHostToDevice, st));
-  k_eid<<<(uint32_t)((m + 63) / 64), 64, 0, st>>>(ix->d_eid.p, (uint32_t)m, ix->tab.p, ix->d_eid_ok.p);
+  if (ix->curve == FTZ_CURVE_BN254)
+    k_eid_bn<<<(uint32_t)((m + 63) / 64), 64, 0, st>>>(ix->d_eid.p, (uint32_t)m, ix->tab.p, ix->d_eid_ok.p);
+  else
+    k_eid<<<(uint32_t)((m + 63) / 64), 64, 0, st>>>(ix->d_eid.p, (uint32_t)m, ix->tab.p, ix->d_eid_ok.p);
   HC(hipGetLastError());
   HC(hipMemcpyAsync(ix->h_eid_ok.p, ix->d_eid_ok.p, m, hipMemcpyDeviceToHost, st));
   HC(hipStreamSynchronize(st));

@@ -154,3 +154,6 @@ __global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const 
 __global__ void k_nym_part(const NymJob* jobs, uint32_t n, const uint8_t* blob, const QDev* tab, QJDev* part);
 __global__ void k_nym_fin(const NymJob* jobs, uint32_t n, uint8_t* blob, const QJDev* part, uint8_t* ok);
 __global__ void k_eid(const uint8_t* in, uint32_t n, const QDev* tab, uint8_t* ok);
+__global__ void k_nym_part_bn(const NymJob* jobs, uint32_t n, const uint8_t* blob, const QDev* tab, QJDev* part);
+__global__ void k_nym_fin_bn(const NymJob* jobs, uint32_t n, uint8_t* blob, const QJDev* part, uint8_t* ok);
+__global__ void k_eid_bn(const uint8_t* in, uint32_t n, const QDev* tab, uint8_t* ok);

@@ -97,6 +97,7 @@ struct ftz_ctx {
   int device = 0;
   hipStream_t stream = nullptr;  // context-level work (setup, MSM)
   PPInfo pp;
+  PPInfo pp_var;                     // pp without the prover's table set (no_sigtab, no fixed pairs)
   std::vector<uint8_t> const_bytes;  // C_SIZE bytes, canonical PP RawBytes
   DBuf<G1Dev> g1tab;
   // the prover's table set: g1tab's bases, then the PS signature points of the
@@ -105,6 +106,7 @@ struct ftz_ctx {
   std::mutex ptab_mu;
   DBuf<G1Dev> g1tab_p;
   bool ptab_ready = false;
+  bool ptab_failed = false;          // its allocation failed once: the prover stays on the variable-base path
   // pp.fixed_pairs: the normalised Miller lines of PK1 then PK2 (k_miller_f3)
   std::vector<G2Dev> pp_g2;          // decoded PK0, PK1, PK2, Q
   DBuf<LineCoef29> pklines29n;
@@ -122,6 +124,8 @@ struct ftz_ctx {
   // fixed-base tables (round 3) its passes fill the device and one lane is ahead
   // (profiles/r03s_prover_layout.txt)
   int g2lanes = FTZ_LAYOUT_ONE_LANE;
+  bool g2lanes_set = false;
+  std::atomic<const uint8_t*> debug_poison{nullptr};  // ftz_ctx_debug_poison (engine failure-isolation tests)  // ftz_ctx_set_layout chose it: small passes keep it too
   int g2lanes_prover = FTZ_LAYOUT_ONE_LANE;
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)

@@ -54,6 +54,7 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->hold_inflight = 2;
   o->small_pass = 4096;
   o->msm_glv = 1;
+  o->prover_tables = 1;
 }
 
 extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {
@@ -74,7 +75,8 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     if (o.fexp != FTZ_FEXP_EXACT && o.fexp != FTZ_FEXP_FUENTES) return set_err(FTZ_E_INVALID, "unknown fexp variant");
     if (o.batch > (1u << 20) || o.slots > 64) return set_err(FTZ_E_INVALID, "batch / slots out of range");
     if (o.msm_window_bits > 24) return set_err(FTZ_E_INVALID, "msm_window_bits out of range (0..24)");
-    if (o.msm_glv > 1 || o.msm_precompute > 1) return set_err(FTZ_E_INVALID, "msm_glv / msm_precompute must be 0 or 1");
+    if (o.msm_glv > 1 || o.msm_precompute > 1 || o.prover_tables > 1)
+      return set_err(FTZ_E_INVALID, "msm_glv / msm_precompute / prover_tables must be 0 or 1");
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -98,6 +100,9 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     ftz_ctx_destroy(c);
     return set_err(FTZ_E_PP, e);
   }
+  c->pp_var = c->pp;
+  c->pp_var.no_sigtab = true;
+  c->pp_var.fixed_pairs = false;
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, prio_hi) != hipSuccess) {
@@ -315,11 +320,19 @@ extern "C" int ftz_ctx_set_serial(ftz_ctx* c, int serial) {
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_ctx_debug_poison(ftz_ctx* c, const uint8_t* proof) {
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  c->debug_poison.store(proof);
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
   if (!c) return set_err(FTZ_E_INVALID, "null context");
   if (layout != FTZ_LAYOUT_ONE_LANE && layout != FTZ_LAYOUT_SEXTET) return set_err(FTZ_E_INVALID, "unknown layout");
-  if (stage == FTZ_STAGE_G2LINES)
+  if (stage == FTZ_STAGE_G2LINES) {
     c->g2lanes = layout;
+    c->g2lanes_set = true;
+  }
   else if (stage == FTZ_STAGE_PROVER_G2LINES)
     c->g2lanes_prover = layout;
   else
@@ -410,7 +423,7 @@ static int slot_finish_plan(ftz_batch* b, size_t n, bool p2_g1out) {
   std::string e = flat_layout(b->work, p2_g1out, b->fp);
   if (!e.empty()) return set_err(FTZ_E_INVALID, e);
   if (b->fp.n_items != n) return set_err(FTZ_E_INVALID, "planner: item count mismatch");
-  const bool fixed3 = p2_g1out && c->pp.fixed_pairs;  // the prover's pairings take no G2 jobs
+  const bool fixed3 = p2_g1out && c->pp.fixed_pairs && c->ptab_ready;  // the prover's pairings take no G2 jobs
   if (!fixed3 && b->fp.cnt[PS_G2] != b->fp.cnt[PS_PR])
     return set_err(FTZ_E_INVALID, "planner: G2 and pairing jobs out of step");
   b->n = n;
@@ -431,6 +444,10 @@ static int slot_finish_plan(ftz_batch* b, size_t n, bool p2_g1out) {
 }
 
 int slot_plan_items(ftz_batch* b, size_t n, const PlanItem* items) {
+  if (const uint8_t* poison = b->ctx->debug_poison.load())
+    for (size_t i = 0; i < n; i++)
+      if ((items[i].kind == 0 && items[i].t.proof == poison) || (items[i].kind == 1 && items[i].i.proof == poison))
+        return set_err(FTZ_E_INVALID, "poisoned item (ftz_ctx_debug_poison)");
   plan_items(b->ctx->pp, n, items, b->work, *b->ctx->pool);
   return slot_finish_plan(b, n, false);
 }
@@ -438,15 +455,23 @@ int slot_plan_items(ftz_batch* b, size_t n, const PlanItem* items) {
 // The prover's G1 table set (ftz_ctx.g1tab_p): g1tab's bases, then R_d, S_d of
 // every digit (PP SignedValues), 32 MB per base with 16-bit windows (6.4 GB
 // for b = 100), built once -- in groups of 16 bases, the same kernels as g1tab
-// -- on the first proving call of a context whose PP qualify (pp_sig_tables).
+// -- on the first proving call of a context whose PP qualify (pp_sig_tables)
+// and whose ftz_options.prover_tables is 1.  When the tables cannot be
+// allocated the context records it once and proves on the variable-base path
+// (prover_plan plans with pp_var), as it does with prover_tables = 0.
 static int ensure_prover_tables(ftz_ctx* c) {
   std::lock_guard<std::mutex> lk(c->ptab_mu);
-  if (c->ptab_ready || !pp_sig_tables(c->pp)) return FTZ_SUCCESS;
+  if (c->ptab_ready || c->ptab_failed || !c->opt.prover_tables || !pp_sig_tables(c->pp)) return FTZ_SUCCESS;
   HC(hipSetDevice(c->device));
   const uint32_t nsig = 2 * c->pp.base, nb = G1B_SIG0 + nsig;
   const size_t per = (size_t)G1TAB_WINDOWS * G1TAB_DIGITS;
   if (c->pp_g1.size() != G1B_COUNT + (size_t)nsig) return set_err(FTZ_E_PP, "signature points not decoded");
-  if (c->g1tab_p.alloc(nb * per) != hipSuccess) return set_err(FTZ_E_NOMEM, "prover table allocation failed");
+  if (c->g1tab_p.alloc(nb * per) != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky allocation error
+    (void)c->g1tab_p.alloc(0);
+    c->ptab_failed = true;
+    return FTZ_SUCCESS;
+  }
   hipStream_t s = c->stream;
   HC(hipMemcpyAsync(c->g1tab_p.p, c->g1tab.p, G1B_COUNT * per * sizeof(G1Dev), hipMemcpyDeviceToDevice, s));
   std::vector<G1Dev> sig(c->pp_g1.begin() + G1B_COUNT, c->pp_g1.end());  // R_0, S_0, R_1, S_1, ...
@@ -506,9 +531,10 @@ int prover_plan(ftz_batch* b, size_t n, const void* wit, int kind) {
   ftz_ctx* c = b->ctx;
   int trc = ensure_prover_tables(c);
   if (trc != FTZ_SUCCESS) return trc;
+  const PPInfo& pp = c->ptab_ready ? c->pp : c->pp_var;  // the table set's bases only when it exists
   std::string e = kind == 0
-                      ? plan_prove_items_transfers(c->pp, n, static_cast<const TransferWit*>(wit), b->work, *c->pool)
-                      : plan_prove_items_issues(c->pp, n, static_cast<const IssueWit*>(wit), b->work, *c->pool);
+                      ? plan_prove_items_transfers(pp, n, static_cast<const TransferWit*>(wit), b->work, *c->pool)
+                      : plan_prove_items_issues(pp, n, static_cast<const IssueWit*>(wit), b->work, *c->pool);
   if (!e.empty()) return set_err(FTZ_E_INVALID, e);
   return slot_finish_plan(b, n, true);
 }
@@ -634,9 +660,10 @@ static hipError_t upload_plan(ftz_batch* b, hipStream_t s) {
 // sextet layout (k_g2lines); same bytes either way
 static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipStream_t s, bool prover) {
   // small passes (few callers waiting) take the low-latency sextet layout: six lanes
-  // per job cut the stage's per-job chain, which bounds a small pass's latency
+  // per job cut the stage's per-job chain, which bounds a small pass's latency --
+  // unless ftz_ctx_set_layout chose the verifier's layout explicitly
   int layout = prover ? c->g2lanes_prover : c->g2lanes;
-  if (!prover && p.n_g2 <= c->opt.small_pass) layout = FTZ_LAYOUT_SEXTET;
+  if (!prover && !c->g2lanes_set && p.n_g2 <= c->opt.small_pass) layout = FTZ_LAYOUT_SEXTET;
   if (layout == FTZ_LAYOUT_ONE_LANE) {
     k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);

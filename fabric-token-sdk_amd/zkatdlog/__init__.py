@@ -502,10 +502,12 @@ def transfer_zkproof_validate(ctx, input_commitments, output_commitments, proof)
 
 
 class Idemix:
-    """Idemix owner-signature verification on FP256BN: the
-    deserializer built from PublicParams.IdemixIssuerPK / IdemixCurveID
+    """Idemix owner-signature verification: the deserializer
+    built from PublicParams.IdemixIssuerPK / IdemixCurveID
     (zkatdlog/nogh/deserializer.go:45-61, identity/msp/idemix/deserializer.go:33-75)
-    with its Verify path on the GPU."""
+    with its Verify path on the GPU.  curve_id = FTZ_CURVE_BN254 (the curve
+    cmd/pp/dlog/gen.go:117 and the NWO topologies deploy, gurvy translator) or
+    FTZ_CURVE_FP256BN_AMCL (amcl translator, the reference's unit-test keys)."""
 
     def __init__(self, ctx, ipk, curve_id=_abi.FTZ_CURVE_FP256BN_AMCL):
         self.ctx = ctx

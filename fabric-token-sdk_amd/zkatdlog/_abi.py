@@ -41,6 +41,7 @@ FTZ_ERR_OWNER = 9
 FTZ_ERR_SIGNATURE = 10
 FTZ_ERR_UNSUPPORTED = 11
 FTZ_CURVE_FP256BN_AMCL = 0
+FTZ_CURVE_BN254 = 1
 
 
 class OwnerSig(ctypes.Structure):
@@ -96,7 +97,7 @@ class Options(ctypes.Structure):
                 ("hold_inflight", ctypes.c_uint32), ("small_pass", ctypes.c_uint32),
                 ("msm_window_bits", ctypes.c_uint32), ("msm_slot_cap", ctypes.c_uint32),
                 ("msm_seg_slots", ctypes.c_uint32), ("msm_glv", ctypes.c_uint32),
-                ("msm_precompute", ctypes.c_uint32)]
+                ("msm_precompute", ctypes.c_uint32), ("prover_tables", ctypes.c_uint32)]
 
 
 HOLD_NEVER = 0xFFFFFFFF
@@ -249,7 +250,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
-           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_set_layout", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
+           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_debug_poison", "ftz_ctx_set_layout", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
            "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
@@ -277,6 +278,7 @@ def load():
     lib.ftz_ctx_create.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(vp)]
     lib.ftz_ctx_create_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(vp)]
     lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
+    lib.ftz_ctx_debug_poison.argtypes = [vp, ctypes.c_void_p]
     lib.ftz_ctx_set_layout.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     lib.ftz_ctx_options.argtypes = [vp, ctypes.POINTER(Options)]
     lib.ftz_pp_validate.argtypes = [ctypes.c_char_p, sz]

@@ -107,9 +107,10 @@ typedef struct {
                            only while at least this many batches are in flight
                            (default 2; 0: always, also with the GPU idle -- closed-loop
                            callers resubmit together; FTZ_HOLD_NEVER: ship at once)       */
-  uint32_t small_pass;  /* device passes of at most this many proofs run the low-latency
+  uint32_t small_pass;  /* device passes of at most this many G2 jobs run the low-latency
                            layout of the t' / pair-2 line stage (six lanes per job
-                           instead of one; same bytes); default 4096, 0 = never          */
+                           instead of one; same bytes); default 4096, 0 = never; an
+                           explicit ftz_ctx_set_layout(FTZ_STAGE_G2LINES) overrides it  */
   uint32_t msm_window_bits; /* MSM planner overrides (ftz_msm_*), 0 = the planner's choice: */
   uint32_t msm_slot_cap;    /*   window bits c, bucket slot cap T, slots per segment S    */
   uint32_t msm_seg_slots;
@@ -118,6 +119,13 @@ typedef struct {
                            for every window w (W x the point memory) and runs use one shared
                            bucket set and no Horner chain; for fixed bases (ftz_msm_set_scalars)
                            0 (default): plain variable-base Pippenger                      */
+  uint32_t prover_tables; /* 1 (default): the first ftz_prove_* call builds fixed-base tables
+                           of the PP's digit signatures R_d, S_d (32 MB per point with
+                           16-bit windows: 2 x base x 32 MB, 6.4 GB at base 100, once per
+                           context) and proves through them and fixed-G2 pairings; if
+                           that allocation fails the context proves on the
+                           variable-base path instead (same bytes, slower) and does not
+                           retry.  0: never build them (variable-base path).            */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
@@ -138,6 +146,12 @@ int ftz_ctx_set_threads(ftz_ctx* ctx, int threads);
 /* profiling: 1 = run every kernel of a batch on one stream (per-kernel times
  * without overlap), 0 = the normal three-stream schedule */
 int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
+/* testing the job engine's failure isolation: planning a device pass that
+ * holds an item whose proof pointer equals `proof` fails (FTZ_E_INVALID,
+ * "poisoned item"), as a planner limit would; NULL clears it.  The engine must
+ * then deliver that error to the one request holding the item and the right
+ * codes to every other caller whose items shared the pass. */
+int ftz_ctx_debug_poison(ftz_ctx* ctx, const uint8_t* proof);
 /* profiling: kernel layout of a pipeline stage (results are identical; only
  * speed differs).  stage FTZ_STAGE_G2LINES (the verifier's t' = c PK0 + v PK1
  * + h PK2 and its 88 pair-2 Miller lines; default one lane) or
@@ -285,7 +299,7 @@ typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, con
 int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
                               int32_t* codes, int32_t* failed_action);
 
-/* ---- idemix owner signatures, FP256BN_AMCL.
+/* ---- idemix owner signatures, on BN254 or FP256BN_AMCL.
  * Replaces, per input token of a transfer, what TransferSignatureValidate
  * (crypto/validator/validator_transfer.go:42-82) runs after loading the token:
  * ctx.Deserializer.GetOwnerVerifier(tok.Owner) (nogh/deserializer.go:64-66 ->
@@ -296,13 +310,20 @@ int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz
  * owner = the token's Owner bytes (ASN.1 RawOwner), msg = the signed request
  * bytes, sig = the NymSignature proto.  ftz_idemix_create takes
  * PublicParams.IdemixIssuerPK (setup.go:36) -- the IssuerPublicKey proto -- and
- * IdemixCurveID (only FP256BN_AMCL = 0; the IPK's own proof is checked once by
- * the Go deserializer, NewDeserializer, and is not re-checked here). */
+ * PublicParams.IdemixCurveID, which selects the translator as
+ * identity/msp/idemix/deserializer.go:40-51 does: FTZ_CURVE_BN254 (1, the
+ * curve cmd/pp/dlog/gen.go:117 and every NWO topology deploy: gurvy
+ * translator, gnark point decoding, 64-byte G1 in the transcript) or
+ * FTZ_CURVE_FP256BN_AMCL (0, amcl translator).  The IPK's own proof is checked
+ * once by the Go deserializer (NewDeserializer) and is not re-checked here; an
+ * IPK whose HSk / HRand do not decode on the curve, or are the point at
+ * infinity, is refused with FTZ_E_PP. */
 #define FTZ_ERR_OWNER 9        /* the owner identity does not deserialize (RawOwner, idemix identity, nym) */
 #define FTZ_ERR_SIGNATURE 10   /* the signature does not unmarshal, or "pseudonym signature invalid"       */
 #define FTZ_ERR_UNSUPPORTED 11 /* owner type verified in Go (an HTLC script owner)                          */
 #define FTZ_ERR_AUDIT 12       /* the token owner does not match its audit info (AuditInfo.Match failed)    */
 #define FTZ_CURVE_FP256BN_AMCL 0
+#define FTZ_CURVE_BN254 1
 typedef struct ftz_idemix ftz_idemix;
 typedef struct {
   const uint8_t* owner; /* token.Token.Owner: asn1(RawOwner{Type, Identity})                  */
@@ -315,7 +336,8 @@ typedef struct {
 int ftz_idemix_create(ftz_ctx* ctx, const uint8_t* ipk, size_t ipk_len, int curve_id, ftz_idemix** out);
 /* codes[i] = FTZ_OK, FTZ_ERR_OWNER, FTZ_ERR_SIGNATURE or FTZ_ERR_UNSUPPORTED; thread-safe */
 int ftz_verify_owner_signatures(ftz_idemix* ix, size_t n, const ftz_owner_sig* s, int32_t* codes);
-/* Strict nym import (opt-in, default off).  amcl NewECPbigs turns an off-curve
+/* Strict nym import (opt-in, default off; FP256BN only -- on BN254 gnark's
+ * SetBytes already refuses an off-curve nym, FTZ_ERR_OWNER).  amcl NewECPbigs turns an off-curve
  * NymX/NymY into the point at infinity [EXT, unpinned: amcl is not in the
  * reference], and NymSignature.Ver then accepts a signature made against the
  * identity without any secret; parity with that reading is the default.  With

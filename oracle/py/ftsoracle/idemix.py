@@ -768,3 +768,267 @@ def signature_with_eid_nym(nym_eid, extra=b""):
     """an idemix Signature proto carrying eid_nym (and `extra` encoded fields) for fixtures"""
     ecp = pb_field(1, 2, nym_eid[0].to_bytes(32, "big")) + pb_field(2, 2, nym_eid[1].to_bytes(32, "big"))
     return extra + pb_field(18, 2, pb_field(1, 2, ecp) + pb_field(2, 2, bytes(32)))
+
+
+# ------------------------------------------------------------------ BN254 (gurvy translator)
+# The curve the reference DEPLOYS for idemix: cmd/pp/dlog/gen.go:117
+# (crypto.Setup(..., math3.BN254)), integration/nwo/token/platform.go:56,
+# fabric/fabric.go:81, orion/orion.go:72, the wallet's identity/msp/idemix/
+# lm.go:153; identity/msp/idemix/deserializer.go:40-51 picks the translator
+# by curve (math.BN254 -> amcl.Gurvy{C: curve}).  [EXT] IBM/idemix and
+# IBM/mathlib (go.mod:6-7; gnark-crypto v0.6.0 underneath, go.mod:53) are not
+# vendored; restated:
+#  * Gurvy.G1FromProto(ECP{X, Y}): len(X) and len(Y) must both be FieldBytes
+#    (32) -- else "invalid marshalled length" --, then mathlib NewG1FromBytes
+#    (X || Y) = gnark G1Affine.SetBytes behind a recover (bn254.g1_from_bytes:
+#    flags, mod-p coordinates, on-curve, (0,0) = infinity, compressed forms);
+#  * the nym import (NymPublicKeyImporter -> User.NewPublicNymFromBytes ->
+#    Translator.G1FromRawBytes): raw = NymX || NymY split at len/2 and read by
+#    G1FromProto, so only a 64-byte total decodes; a decoding error is an
+#    import error (amcl read an off-curve nym as infinity, gnark rejects it);
+#  * Zr from bytes: big.Int SetBytes over the WHOLE slice (any length, empty =
+#    0), no reduction; Equals compares the integers; G1 Mul by any big.Int = (k
+#    mod r) P (gnark GLV: the lattice rounding error does not grow with k);
+#    Zr.Bytes = common.BigToBytes, 32 bytes, and a value >= 2^256 panics there
+#    (make with a negative length), recovered into "failure [...]";
+#  * G1 Bytes = gnark RawBytes, 64 bytes (infinity = 64 zero bytes), while
+#    NymSignature still sizes proofData for 65-byte G1s:
+#    4 + 2*(2*32+1) + 32 + len(msg) bytes, filled as "sign" | t (64) | Nym (64)
+#    | ipk.Hash at 132 | msg at 164, the last 2 bytes left zero -- the same
+#    sizing the reference-held BN254 IssuerPublicKey proof has (18*32+3 bytes,
+#    576 used; issuer_key_check_bn254 accepts both tokengen keys with it);
+#  * HashToZr = SHA-256 mod r (pinned by those keys).
+BN254_CURVE_ID = 1
+
+
+def _bn():
+    from . import bn254 as C
+    return C
+
+
+class G1ProtoError(Exception):
+    pass
+
+
+def bn_g1_from_proto(x, y):
+    """Gurvy.G1FromProto(&ECP{X: x, Y: y}): the point (None = infinity) or G1ProtoError"""
+    C = _bn()
+    if x is None or y is None or len(x) != 32 or len(y) != 32:
+        raise G1ProtoError("invalid marshalled length")
+    try:
+        return C.g1_from_bytes(bytes(x) + bytes(y))
+    except C.DecodeError as e:
+        raise G1ProtoError("failure [set bytes failed [%s]]" % e)
+
+
+class IssuerPKBn254:
+    """an IssuerPublicKey proto read with the Gurvy translator; bad HSk / HRand /
+    HAttrs are None (the Go importer, IssuerPublicKey.Check, would refuse the key)"""
+
+    def __init__(self, raw):
+        m = pb_decode(raw, IPK_S)
+        self.raw = raw
+        self.fields = m
+
+        def pt(e):
+            try:
+                return ("ok", bn_g1_from_proto((e or {}).get(1), (e or {}).get(2)))
+            except G1ProtoError:
+                return ("bad", None)
+        self.hsk_s, self.hsk = pt(m.get(2))
+        self.hrand_s, self.hrand = pt(m.get(3))
+        self.hattrs_s = [pt(e) for e in m.get(4, [])]
+        self.hattrs = [p for _, p in self.hattrs_s]
+        self.hash = m.get(10, b"")
+
+
+def bn_zr(b):
+    """mathlib gurvy NewZrFromBytes: the whole slice big-endian, unreduced"""
+    return int.from_bytes(b or b"", "big")
+
+
+def bn_proof_data(t, nym, ipk_hash, msg):
+    C = _bn()
+    d = bytearray(len(SIGN_LABEL) + 2 * (2 * FIELD_BYTES + 1) + FIELD_BYTES + len(msg))
+    d[0:4] = SIGN_LABEL
+    d[4:68] = C.g1_bytes(t)
+    d[68:132] = C.g1_bytes(nym)
+    h = ipk_hash[:len(d) - 132]
+    d[132:132 + len(h)] = h  # copy(proofData[index:], ipk.Hash)
+    d[164:164 + len(msg)] = msg  # copy(proofData[index:], msg): 2 zero bytes stay at the end
+    return bytes(d)
+
+
+def bn_make_nym(ipk, sk, r_nym):
+    C = _bn()
+    return C.g1_add(C.g1_mul(ipk.hsk, sk), C.g1_mul(ipk.hrand, r_nym))
+
+
+def bn_nym_sign(ipk, sk, r_nym, nym, msg, r_sk, r_rnym, nonce):
+    """NewNymSignature on BN254 with injected randomness: the NymSignature proto"""
+    C = _bn()
+    t = C.g1_add(C.g1_mul(ipk.hsk, r_sk), C.g1_mul(ipk.hrand, r_rnym))
+    c = C.hash_to_zr(bn_proof_data(t, nym, ipk.hash, msg))
+    proof_c = C.hash_to_zr(c.to_bytes(32, "big") + nonce.to_bytes(32, "big"))
+    s_sk = (r_sk + proof_c * sk) % C.R
+    s_rnym = (r_rnym + proof_c * r_nym) % C.R
+    return b"".join(pb_field(k + 1, 2, v.to_bytes(32, "big")) for k, v in enumerate((proof_c, s_sk, s_rnym, nonce)))
+
+
+def bn_nym_verify(ipk, nym, sig, msg):
+    """NymSignature.Ver on BN254 behind the bridge's recover: (code, text)"""
+    C = _bn()
+    if len(sig) == 0:
+        return ERR_SIGNATURE, "invalid signature, it must not be empty"
+    try:
+        m = pb_decode(sig, NYMSIG_S)
+    except PbError as e:
+        return ERR_SIGNATURE, "error unmarshalling signature: %s" % e
+    proof_c, s_sk, s_rnym, nonce = (bn_zr(m.get(k)) for k in (1, 2, 3, 4))
+    t = C.g1_add(C.g1_add(C.g1_mul(ipk.hsk, s_sk), C.g1_mul(ipk.hrand, s_rnym)), C.g1_neg(C.g1_mul(nym, proof_c)))
+    c = C.hash_to_zr(bn_proof_data(t, nym, ipk.hash, msg))
+    if nonce >= 1 << 256:
+        return ERR_SIGNATURE, "failure [runtime error: makeslice: len out of range]"
+    if proof_c != C.hash_to_zr(c.to_bytes(32, "big") + nonce.to_bytes(32, "big")):
+        return ERR_SIGNATURE, "pseudonym signature invalid: zero-knowledge proof is invalid"
+    return OK, ""
+
+
+def bn_deserialize_idemix_identity(raw):
+    """common.go:40-117 Deserialize(raw, false) with the Gurvy translator"""
+    try:
+        si = pb_decode(raw, SERIALIZED_IDENTITY_S)
+    except PbError:
+        return None, (ERR_OWNER, "failed to unmarshal to msp.SerializedIdentity{}")
+    try:
+        ser = pb_decode(si.get(2, b""), SERIALIZED_IDEMIX_S)
+    except PbError:
+        return None, (ERR_OWNER, "could not deserialize a SerializedIdemixIdentity")
+    if not ser.get(1) or not ser.get(2):
+        return None, (ERR_OWNER, "unable to deserialize idemix identity: pseudonym is invalid")
+    raw_nym = ser[1] + ser[2]
+    half = len(raw_nym) // 2
+    try:
+        nym = bn_g1_from_proto(raw_nym[:half], raw_nym[half:])
+    except G1ProtoError:
+        return None, (ERR_OWNER, "failed to import nym public key")
+    try:
+        pb_decode(ser.get(3, b""), OU_S)
+    except PbError:
+        return None, (ERR_OWNER, "cannot deserialize the OU of the identity")
+    try:
+        pb_decode(ser.get(4, b""), ROLE_S)
+    except PbError:
+        return None, (ERR_OWNER, "cannot deserialize the role of the identity")
+    return nym, None
+
+
+def bn_owner_verify(ipk, owner, msg, sig):
+    """one input of TransferSignatureValidate on a BN254 idemix deployment: (code, text)"""
+    try:
+        typ, ident = raw_owner_decode(owner)
+    except RQ.Asn1Error:
+        return ERR_OWNER, "failed to unmarshal RawOwner"
+    if typ == "htlc":
+        return ERR_UNSUPPORTED, "htlc script owner: verified in Go"
+    if typ != "si":
+        return ERR_OWNER, "failed to deserialize RawOwner: Unknown owner type %s" % typ
+    nym, err = bn_deserialize_idemix_identity(ident)
+    if err:
+        return err
+    return bn_nym_verify(ipk, nym, sig, msg)
+
+
+def bn_serialize_idemix_identity(nym, **kw):
+    """as serialize_idemix_identity, with the nym's gnark coordinates (infinity = zeros)"""
+    C = _bn()
+    raw = C.g1_bytes(nym)
+    kw.setdefault("nymx", raw[:32])
+    kw.setdefault("nymy", raw[32:])
+    return serialize_idemix_identity((0, 0), **kw)
+
+
+def _bn_zr_json(v):
+    """mathlib Zr UnmarshalJSON on BN254: None for null / absent, "panic" for a
+    Zr of another curve id (the gurvy driver's type assertion on use), else the
+    raw integer of the element (any length)"""
+    from . import gojson as J
+    if v is None or v[0] == "null":
+        return None
+    curve, raw = J.dec_elem(v)
+    if curve != BN254_CURVE_ID:
+        return "panic"
+    return bn_zr(raw)
+
+
+def bn_audit_owner_match(ipk, owner, audit_info):
+    """InspectTokenOwner for one token on a BN254 idemix deployment: (code, text).
+    AuditNymEid order [EXT]: EidNym present, len(HAttrs) > 2, H_a_eid / HRand /
+    EidNym through G1FromProto (an error is a Match error), then
+    H_a_eid^HashToZr(eid) * HRand^RNymEid (a nil RNymEid panics here) == EidNym."""
+    from . import gojson as J
+    C = _bn()
+    if len(owner) == 0:
+        return ERR_OWNER, "token is a redeem token, cannot inspect ownership"
+    if len(audit_info) == 0:
+        return ERR_OWNER, "failed to inspect owner: owner info is nil"
+    try:
+        typ, ident = raw_owner_decode(owner)
+    except RQ.Asn1Error:
+        return ERR_OWNER, "owner cannot be unwrapped"
+    if typ != "si":
+        return ERR_UNSUPPORTED, "script owner: inspected in Go"
+    try:
+        v = J.parse(audit_info)
+        if v[0] == "null":
+            rnym, attrs = None, None
+        elif v[0] != "obj":
+            raise J.GoJSONError("cannot unmarshal into AuditInfo")
+        else:
+            rnym = _bn_zr_json(J.field(v, "RNymEid"))
+            eid_zr = _bn_zr_json(J.field(v, "EID"))
+            attrs = J.dec_list(J.field(v, "Attributes"), J.dec_bytes)
+            if "panic" in (rnym, eid_zr):
+                return ERR_PANIC, "panic: mathlib Zr of another curve"
+    except J.GoJSONError:
+        return ERR_OWNER, "failed to get owner matcher"
+    try:
+        si = pb_decode(ident, SERIALIZED_IDENTITY_S)
+    except PbError:
+        return ERR_AUDIT, "failed to unmarshal to msp.SerializedIdentity{}"
+    try:
+        ser = pb_decode(si.get(2, b""), SERIALIZED_IDEMIX_S)
+    except PbError:
+        return ERR_AUDIT, "could not deserialize a SerializedIdemixIdentity"
+    if attrs is None or len(attrs) <= EID_INDEX:
+        return ERR_PANIC, "panic: index out of range"
+    eid = attrs[EID_INDEX] or b""
+    try:
+        sig = pb_decode(ser.get(5, b""), SIGNATURE_S)
+    except PbError as e:
+        return ERR_AUDIT, "error while verifying the nym eid: %s" % e
+    en = sig.get(18)
+    if en is None or en.get(1) is None:
+        return ERR_AUDIT, "error while verifying the nym eid: no EidNym provided"
+    if len(ipk.hattrs) <= EID_INDEX:
+        return ERR_AUDIT, "error while verifying the nym eid: could not access H_a_eid in array"
+    if ipk.hattrs_s[EID_INDEX][0] != "ok" or ipk.hrand_s != "ok":
+        return ERR_AUDIT, "error while verifying the nym eid: could not deserialize H_a_eid / HRand"
+    try:
+        nym_eid = bn_g1_from_proto(en[1].get(1), en[1].get(2))
+    except G1ProtoError:
+        return ERR_AUDIT, "error while verifying the nym eid: could not deserialize EidNym"
+    if rnym is None:
+        return ERR_PANIC, "panic: nil RNymEid"
+    want = C.g1_add(C.g1_mul(ipk.hattrs[EID_INDEX], C.hash_to_zr(eid)), C.g1_mul(ipk.hrand, rnym))
+    if want != nym_eid:
+        return ERR_AUDIT, "error while verifying the nym eid: eid nym does not match"
+    return OK, ""
+
+
+def bn_signature_with_eid_nym(nym_eid, extra=b""):
+    """an idemix Signature proto carrying eid_nym (gnark coordinates) for fixtures"""
+    C = _bn()
+    raw = C.g1_bytes(nym_eid)
+    ecp = pb_field(1, 2, raw[:32]) + pb_field(2, 2, raw[32:])
+    return extra + pb_field(18, 2, pb_field(1, 2, ecp) + pb_field(2, 2, bytes(32)))

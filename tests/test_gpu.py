@@ -55,6 +55,21 @@ def test_golden_verdicts_every_layout(zk, golden, pp, g2lines):
         assert got == {c_["name"]: c_["expect"] for c_ in cases}
 
 
+@pytest.mark.parametrize("pp", ["pp_a", "pp_b"])
+def test_golden_tiled_past_small_pass_default_layout(zk, golden, pp):
+    """the default layout path of production-size passes: the golden transfer
+    cases tiled to > ftz_options.small_pass G2 jobs per device pass (so the
+    one-lane k_g2_part + k_g2lines1 stage runs, not the small-pass sextet one),
+    no set_layout call, every verdict at its position"""
+    cases = [c for c in golden[pp]["cases"] if c["kind"] == "transfer"]
+    with zk.Context(golden[pp]["pp"].encode(), device=0) as c:
+        assert c.options["small_pass"] == 4096
+        n = 4096 if pp == "pp_a" else 1024  # PP-A 8, PP-B 64 G2 jobs per transfer that reaches the pairings
+        sel = [k % len(cases) for k in range(n)]
+        got = c.verify_transfers([case_tuple(cases[k]) for k in sel])
+        assert list(got) == [cases[k]["expect"] for k in sel]
+
+
 def test_set_layout_rejects_unknown_values(zk, ctx_a):
     """ftz_ctx_set_layout: unknown stage or layout -> FTZ_E_INVALID, the context unchanged"""
     lib = ctx_a._lib

@@ -191,6 +191,61 @@ def test_engine_errors_do_not_wedge(ctx, zk, valid_set):
     assert ctx.verify_transfers([]) == []
 
 
+def test_engine_failure_isolation_requeue(zk, golden, valid_set, bad_set):
+    """ADVICE r03 (engine.hip requeue_solo): a device pass that fails to plan --
+    here an item poisoned with ftz_ctx_debug_poison, as a planner limit would --
+    is handed back and every request in it re-planned solo.  16 concurrent
+    callers (5..150 items, valid and tampered rows at known positions) share
+    64-item passes; one caller's 150-item request carries the poisoned item at
+    position 100, so that request is split across passes that plan fine
+    (in flight or done) and the failing one.  The poisoned caller gets the error,
+    every other caller its exact codes, and the engine keeps serving."""
+    from zkatdlog import _abi as A
+    rng = np.random.default_rng(64)
+    reqs = []
+    for k in range(16):
+        n = 150 if k == 5 else int(rng.integers(5, 150))
+        its, want = [], []
+        for i in range(n):
+            if rng.random() < 0.1:
+                j = int(rng.integers(bad_set.n))
+                its.append(bad_set.item(j))
+                want.append(int(bad_set.expect[j]))
+            else:
+                its.append(valid_set.item(int(rng.integers(valid_set.n))))
+                want.append(0)
+        arr, keep = A.pack_transfers(its)
+        reqs.append((arr, keep, n, want))
+    with zk.Context(golden["pp_a"]["pp"].encode(), device=0, batch=64, slots=3, window_us=20000,
+                    hold_inflight=0) as c:
+        for rnd in range(2):
+            poison = reqs[5][0][100].proof
+            assert c._lib.ftz_ctx_debug_poison(c._h, poison) == 0
+            go = threading.Barrier(len(reqs))
+            res = [None] * len(reqs)
+
+            def call(k):
+                arr, keep, n, want = reqs[k]
+                go.wait()
+                try:
+                    res[k] = list(c.verify_transfers_packed(arr, n))
+                except zk.DeviceError as e:
+                    res[k] = e
+            th = [threading.Thread(target=call, args=(k,)) for k in range(len(reqs))]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=120)
+            assert not any(t.is_alive() for t in th), "a caller is wedged"
+            assert isinstance(res[5], zk.DeviceError) and "poisoned item" in str(res[5]), res[5]
+            for k, (arr, keep, n, want) in enumerate(reqs):
+                if k != 5:
+                    assert res[k] == want, (rnd, k)
+        assert c._lib.ftz_ctx_debug_poison(c._h, None) == 0
+        arr, keep, n, want = reqs[5]
+        assert list(c.verify_transfers_packed(arr, n)) == want
+
+
 def test_prove_repeatedly_no_leak(ctx):
     """ftz_prove_transfers reuses the context's prover slots: 40 one-shot calls
     (no stream/event growth) and each result verifies."""

@@ -188,6 +188,26 @@ def test_gpu_proofs_match_oracle_every_layout(golden, pp_a, layout):
 
 
 @pytest.mark.gpu
+def test_gpu_proofs_without_prover_tables_match_oracle(golden, pp_a):
+    """ftz_options.prover_tables = 0 (the fallback a context takes
+    when the digit-signature table set cannot be allocated): the variable-base
+    R_d / S_d path with G2 jobs gives the same bytes as the oracle, for
+    transfers and issues"""
+    import zkatdlog
+    _, pp = pp_a
+    ws = [witness(pp, 330 + i, 2, 2) for i in range(2)]
+    iw = [issue_witness(pp, 430, 2)]
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, prover_tables=0) as c:
+        assert c.options["prover_tables"] == 0
+        proofs, codes = c.prove_transfers(ws)
+        iproofs, icodes = c.prove_issues(iw)
+    assert codes == [0, 0] and icodes == [0]
+    for w, p in zip(ws, proofs):
+        assert p == oracle_transfer(pp, w)
+    assert iproofs[0] == oracle_issue(pp, iw[0])
+
+
+@pytest.mark.gpu
 def test_gpu_issue_proofs_match_oracle(gctx, pp_a):
     _, pp = pp_a
     ws = [issue_witness(pp, 400, 2), issue_witness(pp, 401, 1, ttype="USD", anonymous=True)]
