@@ -28,6 +28,7 @@ import os as _os
 if int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
     _os.environ["GPU_MAX_HW_QUEUES"] = "16"
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -604,6 +605,46 @@ def ppb_leg(device, args, bad_b):
             "pp": "b=16,e=16 (values < 2^64)", "roofline": roof}, (pp, job, bases)
 
 
+def requests_leg(ctx, valid, n_req=100000, per=2):
+    """Block-level binding (the recommended drop-in): ONE
+    ftz_verify_token_requests_batched call over n_req raw asn1(TokenRequest)
+    requests of `per` transfer actions each (GPU-made proofs, 1/97 of the
+    requests spending a key missing from the ledger), end to end from request
+    bytes: ASN.1 + action JSON decoding, ledger lookups through a NATIVE
+    get_states callback (one call per 8192-request chunk, a hash map --
+    tools/callers.cpp), element checks, ZK verification in the job engine,
+    verdicts.  Then the same call with the one-key-at-a-time get_state."""
+    import numpy as np
+
+    import zkatdlog
+    from zkatdlog import workload as W
+    t0 = time.perf_counter()
+    rs = W.RequestSet(valid, n_req, per=per)
+    led = zkatdlog.NativeLedger(rs.ledger)
+    t_build = time.perf_counter() - t0
+    i32 = ctypes.POINTER(ctypes.c_int32)
+    out = {"requests": n_req, "transfers": n_req * per, "request_bytes": rs.nbytes(), "setup_s": round(t_build, 1)}
+    for batched in (True, False):
+        codes = np.zeros(n_req, dtype=np.int32)
+        failed = np.zeros(n_req, dtype=np.int32)
+        w = min(n_req, 8192)  # warm-up: the request threads, check buffers, engine slots
+        ctx.verify_token_requests_packed(rs.ptr(), w, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
+                                         batched=batched)
+        c0 = led.counts()
+        t0 = time.perf_counter()
+        ctx.verify_token_requests_packed(rs.ptr(), n_req, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
+                                         batched=batched)
+        dt = time.perf_counter() - t0
+        c1 = led.counts()
+        ok = bool(np.array_equal(codes, rs.expect) and np.array_equal(failed, rs.failed))
+        out["batched_get_states" if batched else "per_key_get_state"] = {
+            "requests_per_s": round(n_req / dt, 1), "transfers_per_s": round(n_req * per / dt, 1),
+            "s": round(dt, 3), "verdicts_bit_exact": ok, "callback_calls": c1[0] - c0[0],
+            "keys_looked_up": c1[1] - c0[1]}
+    led.close()
+    return out
+
+
 def owner_signatures(ctx, n=8192, reps=5):
     """Idemix owner-signature leg on both idemix curves:
     BN254 (the curve cmd/pp/dlog/gen.go:117 and the NWO topologies deploy; the
@@ -760,6 +801,9 @@ def main():
                                                 inflight=1 if args.serial else 4)
             extras["roofline"] = roofline(ctx, job, db, local, value, keep_serial=args.serial)
             extras["owner_signatures"] = owner_signatures(ctx)
+            extras["token_requests"] = requests_leg(ctx, valid)
+            extras["token_requests"]["vs_verify_transfers"] = round(
+                extras["token_requests"]["batched_get_states"]["transfers_per_s"] / value, 3)
         msm = [msm_latency(ctx, int(x)) for x in args.msm.split(",") if x]
         msm_res = None
         if args.msm and not args.no_extras:  # resident-point mode, its own context (ftz_options differ)

@@ -3,6 +3,9 @@
 
 #include <string.h>
 
+#include <algorithm>
+#include <deque>
+#include <memory>
 #include <thread>
 
 #include "gojson.h"
@@ -287,113 +290,207 @@ void for_unmarshal_elems(const ReqState& s, F f) {
 
 }  // namespace
 
-int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h, int32_t* codes, int32_t* failed,
-                          std::string& err) {
-  std::vector<ReqState> st(n);
-  // 1. decode: ASN.1, then every issue action, then every transfer action
-  //    (validator.go unmarshalIssueActions / unmarshalTransferActions)
-  for (size_t r = 0; r < n; r++) {
-    ReqState& s = st[r];
-    std::vector<Slice> f[4];
-    std::string e = der_token_request(reqs[r].p, reqs[r].len, f);
-    if (e.empty()) {
-      s.is.resize(f[0].size());
-      for (size_t k = 0; k < f[0].size() && e.empty(); k++) e = dec_issue_action(f[0][k].p, f[0][k].len, s.is[k], s.pool);
-      s.tr.resize(f[1].size());
-      for (size_t k = 0; k < f[1].size() && e.empty(); k++)
-        e = dec_transfer_action(f[1][k].p, f[1][k].len, s.tr[k], s.pool);
-    }
-    if (!e.empty()) {
+namespace {
+
+struct TRef {
+  size_t r, t, in_off, out_off;
+};
+struct IRef {
+  size_t r, k, out_off;
+};
+
+// One pipeline step: requests [r0, r1) from decode to the engine's verdicts.
+struct Chunk {
+  size_t r0 = 0, r1 = 0;
+  std::vector<ReqState> st;
+  std::vector<uint8_t> coms;  // contiguous 64-byte commitments per action
+  std::vector<TRef> trefs;
+  std::vector<IRef> irefs;
+  std::vector<ftz_transfer> tv;
+  std::vector<ftz_issue> iv;
+  std::vector<int32_t> tcodes, icodes;
+  int trc = FTZ_SUCCESS, irc = FTZ_SUCCESS;
+  std::thread th_t, th_i;
+  void join() {
+    if (th_t.joinable()) th_t.join();
+    if (th_i.joinable()) th_i.join();
+  }
+};
+
+void run_par(const RequestHooks& h, size_t k, const std::function<void(size_t)>& f) {
+  if (h.par && k > 1) {
+    h.par(k, f);
+  } else {
+    for (size_t i = 0; i < k; i++) f(i);
+  }
+}
+
+// element checks of the slots `who` names (request, pool offset); a rejected
+// slot marks its request failed (unmarshal) or its transfer's input bad (ledger)
+int check_slots(const RequestHooks& h, Chunk& c, const std::vector<std::pair<size_t, size_t>>& who,
+                const std::vector<size_t>& tr_of, std::string& err) {
+  if (who.empty()) return FTZ_SUCCESS;
+  std::vector<uint8_t> slots(64 * who.size()), ok(who.size());
+  for (size_t k = 0; k < who.size(); k++)
+    memcpy(slots.data() + 64 * k, c.st[who[k].first].pool.data() + who[k].second, 64);
+  int rc = h.check(who.size(), slots.data(), ok.data());
+  if (rc != FTZ_SUCCESS) {
+    err = "element check failed";
+    return rc;
+  }
+  for (size_t k = 0; k < who.size(); k++) {
+    if (ok[k]) continue;
+    ReqState& s = c.st[who[k].first];
+    if (tr_of.empty()) {
       s.failed = true;
       s.code = FTZ_ERR_PARSE;
+    } else {
+      s.tr_pre[tr_of[k]] = FTZ_ERR_INPUT;
     }
   }
+  return FTZ_SUCCESS;
+}
+
+// steps 1-3 of a chunk and the start of its ZK verification
+int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::string& err) {
+  const size_t m = c.r1 - c.r0;
+  c.st.resize(m);
+  // 1. decode: ASN.1, then every issue action, then every transfer action
+  //    (validator.go unmarshalIssueActions / unmarshalTransferActions)
+  constexpr size_t PIECE = 32;
+  run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
+    for (size_t i = p * PIECE; i < m && i < (p + 1) * PIECE; i++) {
+      ReqState& s = c.st[i];
+      const ftz_bytes& q = reqs[c.r0 + i];
+      std::vector<Slice> f[4];
+      std::string e = der_token_request(q.p, q.len, f);
+      if (e.empty()) {
+        s.is.resize(f[0].size());
+        for (size_t k = 0; k < f[0].size() && e.empty(); k++) e = dec_issue_action(f[0][k].p, f[0][k].len, s.is[k], s.pool);
+        s.tr.resize(f[1].size());
+        for (size_t k = 0; k < f[1].size() && e.empty(); k++)
+          e = dec_transfer_action(f[1][k].p, f[1][k].len, s.tr[k], s.pool);
+      }
+      if (!e.empty()) {
+        s.failed = true;
+        s.code = FTZ_ERR_PARSE;
+      }
+    }
+  });
   // 2. curve checks of the elements decoded at unmarshal (math.G1 UnmarshalJSON
-  //    -> gnark SetBytes), one device pass over every request
+  //    -> gnark SetBytes), one device pass over the chunk
   {
-    std::vector<uint8_t> slots;
-    std::vector<std::pair<size_t, size_t>> who;  // (request, slot offset)
-    for (size_t r = 0; r < n; r++) {
-      if (st[r].failed) continue;
-      for_unmarshal_elems(st[r], [&](const ElemRef& e) {
-        if (e.st != D_OK) return;
-        slots.insert(slots.end(), st[r].pool.begin() + e.off, st[r].pool.begin() + e.off + 64);
-        who.push_back({r, e.off});
+    std::vector<std::pair<size_t, size_t>> who;
+    for (size_t r = 0; r < m; r++) {
+      if (c.st[r].failed) continue;
+      for_unmarshal_elems(c.st[r], [&](const ElemRef& e) {
+        if (e.st == D_OK) who.push_back({r, e.off});
       });
     }
-    if (!who.empty()) {
-      std::vector<uint8_t> ok(who.size());
-      int rc = h.check(who.size(), slots.data(), ok.data());
-      if (rc != FTZ_SUCCESS) {
-        err = "element check failed";
-        return rc;
-      }
-      for (size_t k = 0; k < who.size(); k++)
-        if (!ok[k]) {
-          st[who[k].first].failed = true;
-          st[who[k].first].code = FTZ_ERR_PARSE;
-        }
-    }
+    int rc = check_slots(h, c, who, {}, err);
+    if (rc != FTZ_SUCCESS) return rc;
   }
   // 3. ledger inputs of every transfer (TransferSignatureValidate's loads,
-  //    validator_transfer.go:42-81), then their Data elements' curve checks
-  std::vector<uint8_t> lslots;
-  std::vector<std::pair<size_t, size_t>> lwho;  // (request, transfer)
-  for (size_t r = 0; r < n; r++) {
-    ReqState& s = st[r];
+  //    validator_transfer.go:42-81) on the calling thread, values copied; then
+  //    decoded as token.Token in parallel, then their Data elements checked
+  struct Need {
+    size_t r, t;
+  };
+  std::vector<Need> need;     // transfers whose inputs are looked up
+  std::vector<ftz_bytes> keys;
+  std::vector<size_t> key_at;  // first key index of need[k]
+  for (size_t r = 0; r < m; r++) {
+    ReqState& s = c.st[r];
     if (s.failed) continue;
     s.ins.resize(s.tr.size());
     s.tr_pre.assign(s.tr.size(), 0);
     s.is_pre.assign(s.is.size(), 0);
     for (size_t t = 0; t < s.tr.size(); t++) {
-      for (const std::string& key : s.tr[t].inputs) {
-        const uint8_t* val = nullptr;
-        size_t vlen = 0;
-        if (!h.get_state || h.get_state(h.user, key.data(), key.size(), &val, &vlen) != 0 || vlen == 0) {
-          s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to retrieve input" / "does not exists"
-          break;
-        }
-        ElemRef d;
-        if (!dec_token(val, vlen, d, s.pool).empty()) {
-          s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to deserialize input to spend"
-          break;
-        }
-        s.ins[t].push_back(d);
+      need.push_back({r, t});
+      key_at.push_back(keys.size());
+      for (const std::string& key : s.tr[t].inputs)
+        keys.push_back(ftz_bytes{reinterpret_cast<const uint8_t*>(key.data()), key.size()});
+    }
+  }
+  key_at.push_back(keys.size());
+  std::vector<uint8_t> vbuf;                          // copied values
+  std::vector<std::pair<size_t, size_t>> vref(keys.size(), {0, SIZE_MAX});  // (offset, len); len SIZE_MAX: missing
+  if (!keys.empty()) {
+    if (h.get_states) {
+      std::vector<ftz_bytes> vals(keys.size(), ftz_bytes{nullptr, 0});
+      if (h.get_states(h.user, keys.size(), keys.data(), vals.data()) == 0) {
+        size_t tot = 0;
+        for (const ftz_bytes& v : vals) tot += v.p ? v.len : 0;
+        vbuf.reserve(tot);
+        for (size_t k = 0; k < keys.size(); k++)
+          if (vals[k].p && vals[k].len) {
+            vref[k] = {vbuf.size(), vals[k].len};
+            vbuf.insert(vbuf.end(), vals[k].p, vals[k].p + vals[k].len);
+          }
       }
-      if (s.tr_pre[t]) continue;
-      for (const ElemRef& d : s.ins[t])
-        if (d.st == D_OK) {
-          lslots.insert(lslots.end(), s.pool.begin() + d.off, s.pool.begin() + d.off + 64);
-          lwho.push_back({r, t});
+    } else {
+      for (size_t q = 0; q < need.size(); q++)
+        for (size_t k = key_at[q]; k < key_at[q + 1]; k++) {
+          const uint8_t* val = nullptr;
+          size_t vlen = 0;
+          if (!h.get_state || h.get_state(h.user, reinterpret_cast<const char*>(keys[k].p), keys[k].len, &val, &vlen) != 0 ||
+              vlen == 0)
+            break;  // "failed to retrieve input" / "does not exists": the transfer's later inputs are not read
+          vref[k] = {vbuf.size(), vlen};
+          vbuf.insert(vbuf.end(), val, val + vlen);
         }
     }
   }
-  if (!lwho.empty()) {
-    std::vector<uint8_t> ok(lwho.size());
-    int rc = h.check(lwho.size(), lslots.data(), ok.data());
-    if (rc != FTZ_SUCCESS) {
-      err = "element check failed";
-      return rc;
+  // token decoding per request (a request's pool is written by one thread)
+  std::vector<size_t> need_of(m + 1, 0);  // need[] range of request r: [need_of[r], need_of[r+1])
+  for (size_t q = 0; q < need.size(); q++) need_of[need[q].r + 1] = q + 1;
+  for (size_t r = 1; r <= m; r++) need_of[r] = std::max(need_of[r], need_of[r - 1]);
+  run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
+    for (size_t r = p * PIECE; r < m && r < (p + 1) * PIECE; r++) {
+      ReqState& s = c.st[r];
+      for (size_t q = need_of[r]; q < need_of[r + 1]; q++) {
+        size_t t = need[q].t;
+        for (size_t k = key_at[q]; k < key_at[q + 1]; k++) {
+          if (vref[k].second == SIZE_MAX) {
+            s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to retrieve input" / "does not exists"
+            break;
+          }
+          ElemRef d;
+          if (!dec_token(vbuf.data() + vref[k].first, vref[k].second, d, s.pool).empty()) {
+            s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to deserialize input to spend"
+            break;
+          }
+          s.ins[t].push_back(d);
+        }
+      }
     }
-    for (size_t k = 0; k < lwho.size(); k++)
-      if (!ok[k]) st[lwho[k].first].tr_pre[lwho[k].second] = FTZ_ERR_INPUT;
+  });
+  {
+    std::vector<std::pair<size_t, size_t>> who;
+    std::vector<size_t> tr_of;
+    for (const Need& q : need) {
+      ReqState& s = c.st[q.r];
+      if (s.tr_pre[q.t]) continue;
+      for (const ElemRef& d : s.ins[q.t])
+        if (d.st == D_OK) {
+          who.push_back({q.r, d.off});
+          tr_of.push_back(q.t);
+        }
+    }
+    int rc = check_slots(h, c, who, tr_of, err);
+    if (rc != FTZ_SUCCESS) return rc;
   }
-  // 4. the ZK checks of every action still open, in shared device batches.
+  // 4. the ZK checks of every action still open, through the job engine.
   //    A nil or foreign-curve commitment reaches the verifier and the reference
   //    panics on it (G1 use / driver type assertion); a nil issue output fails
   //    GetCommitments ("failed to verify issue", validator.go verifyIssue).
-  std::vector<uint8_t> coms;  // contiguous 64-byte commitments per action
-  struct TRef { size_t r, t, in_off, out_off; };
-  struct IRef { size_t r, k, out_off; };
-  std::vector<TRef> trefs;
-  std::vector<IRef> irefs;
   auto put = [&](const ReqState& s, const ElemRef& e) {
-    size_t o = coms.size();
-    coms.resize(o + 64, 0);
-    memcpy(coms.data() + o, s.pool.data() + e.off, 64);
+    size_t o = c.coms.size();
+    c.coms.resize(o + 64, 0);
+    memcpy(c.coms.data() + o, s.pool.data() + e.off, 64);
   };
-  for (size_t r = 0; r < n; r++) {
-    ReqState& s = st[r];
+  for (size_t r = 0; r < m; r++) {
+    ReqState& s = c.st[r];
     if (s.failed) continue;
     for (size_t k = 0; k < s.is.size(); k++) {
       const IssueAct& a = s.is[k];
@@ -407,9 +504,9 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
         s.is_pre[k] = FTZ_ERR_PANIC;
         continue;
       }
-      size_t o = coms.size();
+      size_t o = c.coms.size();
       for (const ElemRef& e : a.out.data) put(s, e);
-      irefs.push_back({r, k, o});
+      c.irefs.push_back({r, k, o});
     }
     for (size_t t = 0; t < s.tr.size(); t++) {
       if (s.tr_pre[t]) continue;
@@ -421,48 +518,50 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
         s.tr_pre[t] = FTZ_ERR_PANIC;
         continue;
       }
-      size_t io = coms.size();
+      size_t io = c.coms.size();
       for (const ElemRef& e : s.ins[t]) put(s, e);
-      size_t oo = coms.size();
+      size_t oo = c.coms.size();
       for (const ElemRef& e : a.out.data) put(s, e);
-      trefs.push_back({r, t, io, oo});
+      c.trefs.push_back({r, t, io, oo});
     }
   }
-  std::vector<ftz_issue> iv(irefs.size());
-  for (size_t k = 0; k < irefs.size(); k++) {
-    const IssueAct& a = st[irefs[k].r].is[irefs[k].k];
-    iv[k] = ftz_issue{coms.data() + irefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(), a.proof.size(),
-                      (uint8_t)(a.anonymous ? 1 : 0)};
+  c.iv.resize(c.irefs.size());
+  for (size_t k = 0; k < c.irefs.size(); k++) {
+    const IssueAct& a = c.st[c.irefs[k].r].is[c.irefs[k].k];
+    c.iv[k] = ftz_issue{c.coms.data() + c.irefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(),
+                        a.proof.size(), (uint8_t)(a.anonymous ? 1 : 0)};
   }
-  std::vector<ftz_transfer> tv(trefs.size());
-  for (size_t k = 0; k < trefs.size(); k++) {
-    const ReqState& s = st[trefs[k].r];
-    const TransferAct& a = s.tr[trefs[k].t];
-    tv[k] = ftz_transfer{coms.data() + trefs[k].in_off, (uint32_t)s.ins[trefs[k].t].size(),
-                         coms.data() + trefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(), a.proof.size()};
+  c.tv.resize(c.trefs.size());
+  for (size_t k = 0; k < c.trefs.size(); k++) {
+    const ReqState& s = c.st[c.trefs[k].r];
+    const TransferAct& a = s.tr[c.trefs[k].t];
+    c.tv[k] = ftz_transfer{c.coms.data() + c.trefs[k].in_off, (uint32_t)s.ins[c.trefs[k].t].size(),
+                           c.coms.data() + c.trefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(),
+                           a.proof.size()};
   }
-  std::vector<int32_t> icodes(iv.size()), tcodes(tv.size());
-  // issues on a helper thread while the transfers go in from this one: the job
-  // engine coalesces both into the same device batches
-  int irc = FTZ_SUCCESS, trc = FTZ_SUCCESS;
-  std::thread ith;
-  if (!iv.empty()) {
-    if (tv.empty())
-      irc = h.verify_issues(iv.size(), iv.data(), icodes.data());
-    else
-      ith = std::thread([&] { irc = h.verify_issues(iv.size(), iv.data(), icodes.data()); });
+  c.icodes.resize(c.iv.size());
+  c.tcodes.resize(c.tv.size());
+  // issues and transfers on helper threads: the job engine coalesces them (and
+  // the other chunks in flight) into shared device batches
+  Chunk* cp = &c;
+  if (!c.iv.empty())
+    c.th_i = std::thread([&h, cp] { cp->irc = h.verify_issues(cp->iv.size(), cp->iv.data(), cp->icodes.data()); });
+  if (!c.tv.empty())
+    c.th_t = std::thread([&h, cp] { cp->trc = h.verify_transfers(cp->tv.size(), cp->tv.data(), cp->tcodes.data()); });
+  return FTZ_SUCCESS;
+}
+
+// 5. the chunk's verdicts: first failure in the reference's order, issues then transfers
+int finish_chunk(Chunk& c, int32_t* codes, int32_t* failed, std::string& err) {
+  c.join();
+  if (c.irc != FTZ_SUCCESS || c.trc != FTZ_SUCCESS) {
+    err = c.irc != FTZ_SUCCESS ? "issue verification failed" : "transfer verification failed";
+    return c.irc != FTZ_SUCCESS ? c.irc : c.trc;
   }
-  if (!tv.empty()) trc = h.verify_transfers(tv.size(), tv.data(), tcodes.data());
-  if (ith.joinable()) ith.join();
-  if (irc != FTZ_SUCCESS || trc != FTZ_SUCCESS) {
-    err = irc != FTZ_SUCCESS ? "issue verification failed" : "transfer verification failed";
-    return irc != FTZ_SUCCESS ? irc : trc;
-  }
-  for (size_t k = 0; k < irefs.size(); k++) st[irefs[k].r].is_pre[irefs[k].k] = icodes[k];
-  for (size_t k = 0; k < trefs.size(); k++) st[trefs[k].r].tr_pre[trefs[k].t] = tcodes[k];
-  // 5. first failure in the reference's order: issues, then transfers
-  for (size_t r = 0; r < n; r++) {
-    const ReqState& s = st[r];
+  for (size_t k = 0; k < c.irefs.size(); k++) c.st[c.irefs[k].r].is_pre[c.irefs[k].k] = c.icodes[k];
+  for (size_t k = 0; k < c.trefs.size(); k++) c.st[c.trefs[k].r].tr_pre[c.trefs[k].t] = c.tcodes[k];
+  for (size_t i = 0; i < c.st.size(); i++) {
+    const ReqState& s = c.st[i];
     int32_t code = s.failed ? s.code : FTZ_OK, at = -1;
     if (!s.failed) {
       for (size_t k = 0; k < s.is.size() && code == FTZ_OK; k++)
@@ -470,10 +569,43 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
       for (size_t t = 0; t < s.tr.size() && code == FTZ_OK; t++)
         if (s.tr_pre[t]) code = s.tr_pre[t], at = (int32_t)(s.is.size() + t);
     }
-    codes[r] = code;
-    if (failed) failed[r] = at;
+    codes[c.r0 + i] = code;
+    if (failed) failed[c.r0 + i] = at;
   }
   return FTZ_SUCCESS;
+}
+
+}  // namespace
+
+int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h, int32_t* codes, int32_t* failed,
+                          std::string& err) {
+  const size_t CH = h.chunk ? h.chunk : 8192, IN = h.inflight ? h.inflight : 1;
+  std::deque<std::unique_ptr<Chunk>> fly;
+  int rc = FTZ_SUCCESS;
+  for (size_t r0 = 0; r0 < n && rc == FTZ_SUCCESS; r0 += CH) {
+    while (fly.size() >= IN) {  // bound the memory held by chunks in flight
+      rc = finish_chunk(*fly.front(), codes, failed, err);
+      fly.pop_front();
+      if (rc != FTZ_SUCCESS) break;
+    }
+    if (rc != FTZ_SUCCESS) break;
+    fly.emplace_back(new Chunk());
+    Chunk& c = *fly.back();
+    c.r0 = r0;
+    c.r1 = std::min(n, r0 + CH);
+    rc = prepare_chunk(reqs, h, c, err);
+  }
+  // drain (also after an error: every helper thread is joined before returning)
+  while (!fly.empty()) {
+    std::string e2;
+    int r2 = finish_chunk(*fly.front(), codes, failed, e2);
+    if (rc == FTZ_SUCCESS && r2 != FTZ_SUCCESS) {
+      rc = r2;
+      err = e2;
+    }
+    fly.pop_front();
+  }
+  return rc;
 }
 
 }  // namespace ftsh

@@ -76,16 +76,29 @@ namespace ftsh {
 struct RequestHooks {
   // gnark SetBytes check of n 64-byte element slots: ok[i] = 1 / 0; FTZ_SUCCESS or an API error
   std::function<int(size_t n, const uint8_t* slots, uint8_t* ok)> check;
+  // thread-safe: called from helper threads, several requests in flight at once
   std::function<int(size_t n, const ftz_transfer* tx, int32_t* codes)> verify_transfers;
   std::function<int(size_t n, const ftz_issue* is, int32_t* codes)> verify_issues;
+  // ledger: one key at a time (get_state) or a chunk's keys in one call
+  // (get_states, preferred when set); both on the calling thread only
   ftz_get_state_fn get_state = nullptr;
+  ftz_get_states_fn get_states = nullptr;
   void* user = nullptr;
+  // parallel for over [0, k) (decoding); unset: serial on the calling thread
+  std::function<void(size_t k, const std::function<void(size_t)>& f)> par;
+  size_t chunk = 8192;  // requests decoded per pipeline step
+  size_t inflight = 4;  // chunks whose ZK verification may be in flight at once
 };
 
 // codes[r]: FTZ_OK or the first failing check of request r in the reference's
 // order; failed[r] (optional): the failing action's index (issues first, then
 // transfers), -1 for a request-level failure or none.  Returns FTZ_SUCCESS or
 // an API error (err set).
+//
+// Pipelined over chunks of h.chunk requests: chunk k+1 is decoded (h.par), its
+// elements checked (h.check) and its ledger inputs loaded (get_state(s), the
+// calling thread) while the ZK verification of chunks k, k-1, ... runs in the
+// job engine (h.verify_*, one helper thread per chunk and action kind).
 int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h, int32_t* codes, int32_t* failed,
                           std::string& err);
 

@@ -291,18 +291,25 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
 }
 
 // gnark SetBytes check of n 64-byte slots on the context's device (rt_internal.h)
+// gnark SetBytes checks of n 64-byte slots on the device, on a stream and
+// grow-only buffers of their own: a check never waits on the job engine's
+// batches (no hipMalloc / hipFree per call) nor on MSM / setup work
 int g1_check_slots(ftz_ctx* c, size_t n, const uint8_t* slots, uint8_t* ok) {
   if (!n) return FTZ_SUCCESS;
-  std::lock_guard<std::mutex> lk(c->mu);
+  if (n > (1u << 26)) return set_err(FTZ_E_INVALID, "too many elements in one check");
+  std::lock_guard<std::mutex> lk(c->chk_mu);
   HC(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
-  DBuf<uint8_t> buf;
-  HC(buf.alloc(65 * n));
-  HC(hipMemcpyAsync(buf.p, slots, 64 * n, hipMemcpyHostToDevice, s));
-  k_g1_check<<<blocks(n, 256), 256, 0, s>>>((uint32_t)n, buf.p, buf.p + 64 * n);
+  if (!c->chk_stream) HC(hipStreamCreateWithFlags(&c->chk_stream, hipStreamNonBlocking));
+  hipStream_t s = c->chk_stream;
+  HC(c->chk_h.reserve(65 * n));
+  HC(c->chk_d.reserve(65 * n));
+  memcpy(c->chk_h.p, slots, 64 * n);
+  HC(hipMemcpyAsync(c->chk_d.p, c->chk_h.p, 64 * n, hipMemcpyHostToDevice, s));
+  k_g1_check<<<blocks(n, 256), 256, 0, s>>>((uint32_t)n, c->chk_d.p, c->chk_d.p + 64 * n);
   HC(hipGetLastError());
-  HC(hipMemcpyAsync(ok, buf.p + 64 * n, n, hipMemcpyDeviceToHost, s));
+  HC(hipMemcpyAsync(c->chk_h.p + 64 * n, c->chk_d.p + 64 * n, n, hipMemcpyDeviceToHost, s));
   HC(hipStreamSynchronize(s));
+  memcpy(ok, c->chk_h.p + 64 * n, n);
   return FTZ_SUCCESS;
 }
 

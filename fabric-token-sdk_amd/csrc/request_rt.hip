@@ -1,9 +1,11 @@
 // C ABI of the raw token-request path (include/ftsamd.h, host/request.h):
-// ASN.1 + action JSON decoding on the calling thread, element checks on the
-// device, ZK verification of every action through the context's job engine.
+// ASN.1 + action JSON decoding on the context's request threads, element checks
+// on the device, ZK verification of every action through the context's job
+// engine -- pipelined over chunks of requests (ftsh::verify_token_requests).
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <thread>
 #include <vector>
@@ -27,15 +29,26 @@ extern "C" int ftz_token_request_decode(const uint8_t* raw, size_t len, size_t c
   return FTZ_SUCCESS;
 }
 
-extern "C" int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
-                                         void* user, int32_t* codes, int32_t* failed_action) {
+namespace {
+int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
+                    ftz_get_states_fn get_states, void* user, int32_t* codes, int32_t* failed_action) {
   if (!ctx || (n && (!reqs || !codes))) return set_err(FTZ_E_INVALID, "null argument");
+  for (size_t i = 0; i < n; i++)
+    if (!reqs[i].p && reqs[i].len) return set_err(FTZ_E_INVALID, "null request with non-zero length");
+  WorkPool* pool;
+  {
+    std::lock_guard<std::mutex> lk(ctx->req_mu);
+    if (!ctx->req_pool) ctx->req_pool = new WorkPool((int)std::max<uint32_t>(4, ctx->opt.threads / 2));
+    pool = ctx->req_pool;
+  }
   ftsh::RequestHooks h;
   h.check = [ctx](size_t m, const uint8_t* slots, uint8_t* ok) { return g1_check_slots(ctx, m, slots, ok); };
   h.verify_transfers = [ctx](size_t m, const ftz_transfer* tx, int32_t* c) { return ftz_verify_transfers(ctx, m, tx, c); };
   h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return ftz_verify_issues(ctx, m, is, c); };
   h.get_state = get_state;
+  h.get_states = get_states;
   h.user = user;
+  h.par = [pool](size_t k, const std::function<void(size_t)>& f) { pool->run(k, f); };
   std::string err;
   int rc = ftsh::verify_token_requests(n, reqs, h, codes, failed_action, err);
   if (rc != FTZ_SUCCESS && !err.empty()) {
@@ -43,4 +56,17 @@ extern "C" int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes
     return set_err(rc, err + (last.empty() ? "" : ": " + last));
   }
   return rc;
+}
+}  // namespace
+
+extern "C" int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
+                                         void* user, int32_t* codes, int32_t* failed_action) {
+  return verify_requests(ctx, n, reqs, get_state, nullptr, user, codes, failed_action);
+}
+
+extern "C" int ftz_verify_token_requests_batched(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs,
+                                                 ftz_get_states_fn get_states, void* user, int32_t* codes,
+                                                 int32_t* failed_action) {
+  if (!get_states) return set_err(FTZ_E_INVALID, "null get_states");
+  return verify_requests(ctx, n, reqs, nullptr, get_states, user, codes, failed_action);
 }

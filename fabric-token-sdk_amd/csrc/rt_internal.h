@@ -129,6 +129,15 @@ struct ftz_ctx {
   int g2lanes_prover = FTZ_LAYOUT_ONE_LANE;
   WorkPool* pool = nullptr;          // host planning threads
   std::mutex mu;                     // context-level device work (MSM, setup)
+  // raw token requests: decoding threads of their own (the engine plans on `pool`
+  // concurrently) and grow-only element-check buffers (no hipMalloc / hipFree --
+  // which would wait on the engine's device work -- per call)
+  std::mutex req_mu;
+  WorkPool* req_pool = nullptr;
+  hipStream_t chk_stream = nullptr;
+  std::mutex chk_mu;
+  PinnedMem chk_h;
+  DevMem chk_d;
   // Stream triples (pairing chain / side G1 jobs / G2 + lines) shared by every
   // batch slot of the context round-robin, so the number of HIP streams -- and
   // of hardware queues they need (GPU_MAX_HW_QUEUES) -- stays 3 x opt.slots + 1

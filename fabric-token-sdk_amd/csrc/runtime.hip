@@ -300,7 +300,12 @@ extern "C" void ftz_ctx_destroy(ftz_ctx* c) {
   c->qlines29.alloc(0);
   c->qlines29n.alloc(0);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->chk_stream) {
+    (void)hipStreamSynchronize(c->chk_stream);
+    (void)hipStreamDestroy(c->chk_stream);
+  }
   delete c->pool;
+  delete c->req_pool;
   delete c;
 }
 

@@ -92,3 +92,63 @@ extern "C" int ftz_callers_run(ftz_ctx* ctx, const ftz_transfer* pool, const int
   out[5] = (double)all.back();
   return FTZ_SUCCESS;
 }
+
+// ---- a native ledger for the block-level binding leg (bench.py "requests"):
+// what a committer's state snapshot hands the library -- a hash map from the
+// token key to json(token.Token), read by ftz_get_state_fn / ftz_get_states_fn
+// callbacks that cost what a native lookup costs (no Python in the timed call).
+#include <string>
+#include <unordered_map>
+
+namespace {
+struct Ledger {
+  std::unordered_map<std::string, std::string> kv;
+  uint64_t lookups = 0;  // calls (get_state) / keys (get_states), for the bench's report
+  uint64_t calls = 0;
+};
+}  // namespace
+
+extern "C" void* ftz_ledger_create(size_t n, const ftz_bytes* keys, const ftz_bytes* vals) {
+  Ledger* l = new Ledger();
+  l->kv.reserve(n);
+  for (size_t i = 0; i < n; i++)
+    l->kv.emplace(std::string((const char*)keys[i].p, keys[i].len), std::string((const char*)vals[i].p, vals[i].len));
+  return l;
+}
+
+extern "C" void ftz_ledger_destroy(void* p) { delete (Ledger*)p; }
+
+extern "C" void ftz_ledger_counts(void* p, uint64_t* calls, uint64_t* lookups) {
+  Ledger* l = (Ledger*)p;
+  *calls = l->calls;
+  *lookups = l->lookups;
+}
+
+extern "C" int ftz_ledger_get_state(void* user, const char* key, size_t key_len, const uint8_t** val,
+                                    size_t* val_len) {
+  Ledger* l = (Ledger*)user;
+  l->calls++;
+  l->lookups++;
+  auto it = l->kv.find(std::string(key, key_len));
+  if (it == l->kv.end()) {
+    *val = nullptr;
+    *val_len = 0;
+    return 0;  // GetState of a missing key: nil value, no error
+  }
+  *val = (const uint8_t*)it->second.data();
+  *val_len = it->second.size();
+  return 0;
+}
+
+extern "C" int ftz_ledger_get_states(void* user, size_t n, const ftz_bytes* keys, ftz_bytes* vals) {
+  Ledger* l = (Ledger*)user;
+  l->calls++;
+  l->lookups += n;
+  std::string k;
+  for (size_t i = 0; i < n; i++) {
+    k.assign((const char*)keys[i].p, keys[i].len);
+    auto it = l->kv.find(k);
+    vals[i] = it == l->kv.end() ? ftz_bytes{nullptr, 0} : ftz_bytes{(const uint8_t*)it->second.data(), it->second.size()};
+  }
+  return 0;
+}

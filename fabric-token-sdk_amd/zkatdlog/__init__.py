@@ -231,18 +231,32 @@ class Context:
         finally:
             m.close()
 
-    def verify_token_requests(self, requests, ledger):
+    def verify_token_requests(self, requests, ledger, batched=False):
         """Raw token requests (asn1 TokenRequest bytes) validated as
         Validator.VerifyTokenRequestFromRaw does minus the Go-side signature /
         HTLC / metadata checks; ledger: dict key -> token.Token JSON bytes (or a
-        callable).  Returns (codes, failed_action) lists."""
+        callable), or a NativeLedger.  batched: the one-callback-per-chunk
+        lookup (ftz_verify_token_requests_batched).  Returns (codes,
+        failed_action) lists."""
         arr, keep = _abi.pack_bytes(requests)
         n = len(keep)
-        cb = _abi.get_state_callback(ledger)
         codes = (ctypes.c_int32 * max(1, n))()
         failed = (ctypes.c_int32 * max(1, n))()
-        _check(self._lib.ftz_verify_token_requests(self._h, n, arr, cb, None, codes, failed), self._lib)
+        self.verify_token_requests_packed(arr, n, ledger, codes, failed, batched=batched)
         return list(codes)[:n], list(failed)[:n]
+
+    def verify_token_requests_packed(self, arr, n, ledger, codes, failed, batched=False):
+        """as verify_token_requests over a packed ftz_bytes array and caller-owned
+        int32 code arrays (bench: the packing stays out of the timed call)"""
+        if isinstance(ledger, NativeLedger):
+            fn, user = ledger.fn(batched), ledger.handle
+            keep_cb = None
+        else:
+            keep_cb = (_abi.get_states_callback if batched else _abi.get_state_callback)(ledger)
+            fn, user = ctypes.cast(keep_cb, ctypes.c_void_p), None
+        call = self._lib.ftz_verify_token_requests_batched if batched else self._lib.ftz_verify_token_requests
+        _check(call(self._h, n, arr, fn, user, codes, failed), self._lib)
+        del keep_cb
 
     def g1_sum(self, points):
         """Sum of RawBytes G1 points (n x 64 bytes, the identity = 64 zero
@@ -499,6 +513,47 @@ def transfer_zkproof_validate(ctx, input_commitments, output_commitments, proof)
     inputs are the commitments of the ledger tokens, not the action's own
     InputCommitments."""
     TransferVerifier(input_commitments, output_commitments, ctx).verify(proof)
+
+
+class NativeLedger:
+    """A ledger snapshot served by native callbacks (tools/callers.cpp
+    ftz_ledger_*): key -> json(token.Token), looked up without Python in the
+    call -- what a committer's state database hands the library."""
+
+    def __init__(self, items):
+        import os
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libftscallers.so"))
+        lib.ftz_ledger_create.restype = ctypes.c_void_p
+        lib.ftz_ledger_create.argtypes = [ctypes.c_size_t, ctypes.POINTER(_abi.Bytes), ctypes.POINTER(_abi.Bytes)]
+        lib.ftz_ledger_destroy.argtypes = [ctypes.c_void_p]
+        lib.ftz_ledger_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.POINTER(ctypes.c_uint64)]
+        items = list(items.items()) if isinstance(items, dict) else list(items)
+        ks, kk = _abi.pack_bytes([k.encode() if isinstance(k, str) else k for k, _ in items])
+        vs, vk = _abi.pack_bytes([v for _, v in items])
+        self._lib = lib
+        self.handle = lib.ftz_ledger_create(len(items), ks, vs)
+
+    def fn(self, batched):
+        return ctypes.cast(self._lib.ftz_ledger_get_states if batched else self._lib.ftz_ledger_get_state,
+                           ctypes.c_void_p)
+
+    def counts(self):
+        """(callback calls, keys looked up) so far"""
+        c, k = ctypes.c_uint64(), ctypes.c_uint64()
+        self._lib.ftz_ledger_counts(self.handle, ctypes.byref(c), ctypes.byref(k))
+        return c.value, k.value
+
+    def close(self):
+        if self.handle:
+            self._lib.ftz_ledger_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Idemix:

@@ -115,6 +115,7 @@ class Bytes(ctypes.Structure):
 # int (*)(void* user, const char* key, size_t key_len, const uint8_t** val, size_t* val_len)
 GET_STATE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t))
+GET_STATES_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p)
 FTZ_ERR_INPUT = 8
 
 
@@ -149,6 +150,29 @@ def get_state_callback(ledger):
         val_len[0] = len(ent[0])
         return 0
     return GET_STATE_FN(cb)
+
+
+def get_states_callback(ledger):
+    """A GET_STATES_FN (batched lookup) over a dict key(str) -> bytes; the
+    returned object must stay referenced during the call."""
+    lookup = ledger.get if isinstance(ledger, dict) else ledger
+    hold = []
+
+    def cb(user, n, keys, vals):
+        ks = ctypes.cast(keys, ctypes.POINTER(Bytes))
+        vs = ctypes.cast(vals, ctypes.POINTER(Bytes))
+        hold.clear()
+        for i in range(n):
+            k = ctypes.string_at(ks[i].p, ks[i].len).decode("utf-8", errors="surrogateescape")
+            v = lookup(k)
+            if v is None or len(v) == 0:
+                vs[i] = Bytes(None, 0)
+                continue
+            b = ctypes.create_string_buffer(bytes(v), len(v))
+            hold.append(b)
+            vs[i] = Bytes(ctypes.cast(b, ctypes.c_void_p), len(v))
+        return 0
+    return GET_STATES_FN(cb)
 
 
 def pack_openings(openings):
@@ -255,7 +279,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
-           "ftz_token_request_decode", "ftz_verify_token_requests",
+           "ftz_token_request_decode", "ftz_verify_token_requests", "ftz_verify_token_requests_batched",
            "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_ctx_prover_stats", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
@@ -325,8 +349,11 @@ def load():
     lib.ftz_idemix_destroy.argtypes = [vp]
     lib.ftz_idemix_destroy.restype = None
     lib.ftz_token_request_decode.argtypes = [ctypes.c_char_p, sz, ctypes.POINTER(sz), ctypes.POINTER(Bytes), sz]
-    lib.ftz_verify_token_requests.argtypes = [vp, sz, ctypes.POINTER(Bytes), GET_STATE_FN, vp,
+    # the callback as a plain function pointer: a ctypes GET_STATE(S)_FN or a native one
+    lib.ftz_verify_token_requests.argtypes = [vp, sz, ctypes.POINTER(Bytes), vp, vp,
                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    lib.ftz_verify_token_requests_batched.argtypes = [vp, sz, ctypes.POINTER(Bytes), vp, vp,
+                                                      ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     szp = ctypes.POINTER(ctypes.c_size_t)
     i32p = ctypes.POINTER(ctypes.c_int32)
     lib.ftz_prove_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), u8p, sz, szp, i32p]

@@ -169,3 +169,100 @@ def mixed_job(valid, bad, n, rate=1 / 64, seed=2024, offset=0):
         rows[pick] = bad.rows[which[pick]]
         expect[pick] = bad.expect[which[pick]]
     return Job(rows, expect, [valid, bad])
+
+
+# ---------------------------------------------------------------- raw token requests
+# asn1.Marshal(driver.TokenRequest) (token/driver/request.go:24-38) of transfer
+# actions json.Marshal(transfer.TransferAction) (crypto/transfer/sender.go:105-116:
+# Inputs, InputCommitments, OutputTokens, Proof, Metadata) whose G1 fields are
+# mathlib's curveElement JSON {"curve":1,"element":base64(RawBytes)}; ledger
+# values json.Marshal(token.Token{Owner, Data}) (crypto/token/token.go:20-25).
+BENCH_OWNER = base64.b64encode(b"owner-identity").decode()
+
+
+def _der_len(n):
+    if n < 0x80:
+        return bytes([n])
+    b = n.to_bytes((n.bit_length() + 7) // 8, "big")
+    return bytes([0x80 | len(b)]) + b
+
+
+def _der(tag, body):
+    return bytes([tag]) + _der_len(len(body)) + body
+
+
+def _elem(raw):
+    return '{"curve":1,"element":"%s"}' % base64.b64encode(raw).decode()
+
+
+def token_json(raw):
+    return ('{"Owner":"%s","Data":%s}' % (BENCH_OWNER, _elem(raw))).encode()
+
+
+def transfer_action_json(keys, ins, outs, proof):
+    """json(TransferAction) with 64-byte RawBytes input / output commitments"""
+    return ('{"Inputs":[%s],"InputCommitments":[%s],"OutputTokens":[%s],"Proof":"%s","Metadata":null}' % (
+        ",".join('"%s"' % k for k in keys),
+        ",".join(_elem(ins[64 * i:64 * i + 64]) for i in range(len(ins) // 64)),
+        ",".join('{"Owner":"%s","Data":%s}' % (BENCH_OWNER, _elem(outs[64 * i:64 * i + 64]))
+                 for i in range(len(outs) // 64)),
+        base64.b64encode(proof).decode())).encode()
+
+
+def token_request(transfers, issues=(), sigs=(), auditor_sigs=()):
+    """asn1.Marshal(TokenRequest{Issues, Transfers, Signatures, AuditorSignatures})"""
+    def seq_of(items):
+        return _der(0x30, b"".join(_der(0x04, x) for x in items))
+    return _der(0x30, seq_of(issues) + seq_of(transfers) + seq_of(sigs) + seq_of(auditor_sigs))
+
+
+class RequestSet:
+    """n raw token requests of `per` transfer actions each (GPU-made proofs of a
+    TransferSet, tiled), flat in one buffer, with the ledger holding their
+    inputs.  Every `missing_every`-th request's last action spends a key that is
+    not on the ledger (FTZ_ERR_INPUT at that action); all other requests verify.
+    rows = a packed ftz_bytes numpy array pointing into the buffer."""
+
+    def __init__(self, valid, n, per=2, missing_every=97, tag="blk"):
+        parts, ledger, off = [], {}, [0]
+        self.expect = np.zeros(n, dtype=np.int32)
+        self.failed = np.full(n, -1, dtype=np.int32)
+        sig = [b"\x30" * 72] * per  # signatures travel in the request; verified in Go
+        cache = {}  # distinct proof -> (its action JSON after the Inputs list, ledger token JSONs)
+
+        def tail(j):
+            if j not in cache:
+                ins, outs, proof = valid.item(j)
+                act = transfer_action_json([], ins, outs, proof)
+                cache[j] = (act[len(b'{"Inputs":[]'):], [token_json(ins[64 * i:64 * i + 64])
+                                                         for i in range(len(ins) // 64)])
+            return cache[j]
+        for r in range(n):
+            acts = []
+            for a in range(per):
+                rest, toks = tail((r * per + a) % valid.n)
+                keys = ["%s%07d:%d:%d" % (tag, r, a, i) for i in range(len(toks))]
+                missing = missing_every and r % missing_every == missing_every - 1 and a == per - 1
+                for i, k in enumerate(keys):
+                    if not (missing and i == 0):
+                        ledger[k] = toks[i]
+                acts.append(b'{"Inputs":[' + ",".join('"%s"' % k for k in keys).encode() + b"]" + rest)
+                if missing:
+                    self.expect[r] = _abi.FTZ_ERR_INPUT
+                    self.failed[r] = a
+            raw = token_request(acts, sigs=sig)
+            parts.append(raw)
+            off.append(off[-1] + len(raw))
+        self.buf = np.frombuffer(b"".join(parts), dtype=np.uint8)
+        self.off = np.asarray(off, dtype=np.int64)
+        self.n, self.per, self.ledger = n, per, ledger
+        addr, self._keep = _abi.buffer_address(self.buf)
+        self.rows = np.zeros(n, dtype=[("p", np.uint64), ("len", np.uint64)])
+        self.rows["p"] = addr + self.off[:-1]
+        self.rows["len"] = self.off[1:] - self.off[:-1]
+
+    def ptr(self):
+        return ctypes.cast(self.rows.ctypes.data, ctypes.POINTER(_abi.Bytes))
+
+    def nbytes(self):
+        return int(self.off[-1])

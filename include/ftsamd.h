@@ -282,8 +282,19 @@ int ftz_token_request_decode(const uint8_t* raw, size_t len, size_t counts[4], f
 /* Ledger lookup (driver.GetStateFnc, validator.go:45; the Go shim passes a cgo
  * export over getState): 0 and *val / *val_len (valid until the next call on
  * the same thread), or non-zero when the state cannot be read.  Called on the
- * calling thread only, in the reference's order. */
+ * thread that called ftz_verify_token_requests only, never concurrently; the
+ * library copies each value before the next call. */
 typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, const uint8_t** val, size_t* val_len);
+/* Batched ledger lookup (one cgo crossing per pipeline chunk instead of one per
+ * input): vals[i] = the value of keys[i], {NULL, 0} when it does not exist.
+ * Returns 0, or non-zero when the states cannot be read (every transfer with
+ * an input in this call then fails with FTZ_ERR_INPUT, as a GetState error
+ * does).  Called on the thread that called ftz_verify_token_requests_batched
+ * only, never concurrently; the values must stay valid until the next
+ * get_states call or the return of ftz_verify_token_requests_batched (the
+ * library copies them before either).  The Go side may look the keys up
+ * concurrently itself. */
+typedef int (*ftz_get_states_fn)(void* user, size_t n, const ftz_bytes* keys, ftz_bytes* vals);
 #define FTZ_ERR_INPUT 8 /* an input to spend is missing on the ledger or is not a token.Token */
 /* ZK validation of n raw token requests as Validator.VerifyTokenRequestFromRaw
  * performs it (crypto/validator/validator.go:45-108) minus the checks that stay
@@ -295,9 +306,17 @@ typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, con
  * transfer.Verifier) in order; all actions of all requests are verified in
  * shared device batches.  codes[i] = FTZ_OK or the first failing check of
  * request i; failed_action (may be NULL) = that action's index (issues first,
- * then transfers), -1 if none or request-level. */
+ * then transfers), -1 if none or request-level.
+ * Pipelined: requests are decoded on the library's own host threads in chunks,
+ * and while chunk k's actions are verified on the device, chunk k+1 is decoded
+ * and its inputs looked up (on the calling thread).  Thread-safe: calls on one
+ * context from several threads share the device batches. */
 int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
                               int32_t* codes, int32_t* failed_action);
+/* The same with the batched ledger lookup (recommended for block-level
+ * binding: one callback per chunk of up to 8192 requests). */
+int ftz_verify_token_requests_batched(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_states_fn get_states,
+                                      void* user, int32_t* codes, int32_t* failed_action);
 
 /* ---- idemix owner signatures, on BN254 or FP256BN_AMCL.
  * Replaces, per input token of a transfer, what TransferSignatureValidate

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -452,6 +453,36 @@ int emu_verify_token_requests(void* ctx, size_t n, const ftz_bytes* reqs, ftz_ge
   h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return emu_verify_issues(ctx, m, is, c); };
   h.get_state = get_state;
   h.user = user;
+  std::string err;
+  return ftsh::verify_token_requests(n, reqs, h, codes, failed, err);
+}
+
+// the same with the pipeline's knobs: batched lookups, chunk size, chunks in
+// flight, and `par_threads` decoding threads (0: serial)
+int emu_verify_token_requests_ex(void* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
+                                 ftz_get_states_fn get_states, void* user, size_t chunk, size_t inflight,
+                                 int par_threads, int32_t* codes, int32_t* failed) {
+  ftsh::RequestHooks h;
+  h.check = [](size_t m, const uint8_t* slots, uint8_t* ok) {
+    for (size_t i = 0; i < m; i++) {
+      g1a a;
+      ok[i] = g1_setbytes(slots + 64 * i, 64, a) ? 1 : 0;
+    }
+    return 0;
+  };
+  h.verify_transfers = [ctx](size_t m, const ftz_transfer* tx, int32_t* c) { return emu_verify_transfers(ctx, m, tx, c); };
+  h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return emu_verify_issues(ctx, m, is, c); };
+  h.get_state = get_state;
+  h.get_states = get_states;
+  h.user = user;
+  h.chunk = chunk;
+  h.inflight = inflight;
+  std::unique_ptr<WorkPool> pool;
+  if (par_threads > 0) {
+    pool.reset(new WorkPool(par_threads));
+    WorkPool* pp = pool.get();
+    h.par = [pp](size_t k, const std::function<void(size_t)>& f) { pp->run(k, f); };
+  }
   std::string err;
   return ftsh::verify_token_requests(n, reqs, h, codes, failed, err);
 }

@@ -74,6 +74,35 @@ def test_oracle_verdicts_real_zk_sample(fx):
     assert seen == len(pick)
 
 
+@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("chunk,inflight,threads", [(1, 1, 0), (3, 2, 3), (7, 4, 4), (8192, 4, 2)])
+def test_emu_request_pipeline_knobs(emu, fx, batched, chunk, inflight, threads):
+    """the pipelined request path (chunks decoded on a thread pool while earlier
+    chunks are being verified, lookups one key at a time or one call per chunk)
+    gives every fixture verdict and failing index, whatever the chunking; the
+    fixture's requests tiled 3x so that chunks straddle request kinds"""
+    from zkatdlog import _abi as A
+    emu.emu_verify_token_requests_ex.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Bytes),
+                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                 ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                                                 ctypes.POINTER(ctypes.c_int32)]
+    pp = fx["pp"].encode()
+    ctx = emu.emu_ctx_create(pp, len(pp), ctypes.create_string_buffer(256), 256)
+    rq = fx["requests"] * 3
+    try:
+        arr, keep = A.pack_bytes([r["raw_b"] for r in rq])
+        cb = (A.get_states_callback if batched else A.get_state_callback)(fx["ledger_b"])
+        fn = ctypes.cast(cb, ctypes.c_void_p)
+        n = len(rq)
+        codes = (ctypes.c_int32 * n)()
+        failed = (ctypes.c_int32 * n)()
+        assert emu.emu_verify_token_requests_ex(ctx, n, arr, None if batched else fn, fn if batched else None, None,
+                                                chunk, inflight, threads, codes, failed) == 0
+    finally:
+        emu.emu_ctx_destroy(ctx)
+    assert [(codes[k], failed[k]) for k in range(n)] == [(r["expect"], r["failed_action"]) for r in rq]
+
+
 def test_emu_request_path_matches_fixture(emu, fx):
     """the product's request orchestration (host/request.cpp) over the host
     build of the job code reproduces every fixture verdict and failing index"""
@@ -104,6 +133,28 @@ def gctx(fx):
     c = zkatdlog.Context(fx["pp"].encode(), device=0)
     yield c
     c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batched", [False, True])
+def test_gpu_requests_native_ledger_tiled(gctx, fx, batched):
+    """ftz_verify_token_requests(_batched) with a native ledger callback over the
+    fixture tiled past several 8192-request pipeline chunks: every verdict and
+    failing index at its position, and every key looked up on the calling
+    thread (one callback per chunk when batched)"""
+    import zkatdlog
+    rq = fx["requests"] * (20000 // len(fx["requests"]) + 1)
+    led = zkatdlog.NativeLedger(fx["ledger_b"])
+    try:
+        codes, failed = gctx.verify_token_requests([r["raw_b"] for r in rq], led, batched=batched)
+        calls, keys = led.counts()
+    finally:
+        led.close()
+    assert list(zip(codes, failed)) == [(r["expect"], r["failed_action"]) for r in rq]
+    if batched:
+        assert calls <= (len(rq) + 8191) // 8192
+    else:
+        assert calls == keys
 
 
 @pytest.mark.gpu
@@ -164,3 +215,43 @@ def test_asn1_decoder_mutation_fuzz(fx):
         assert got == want, (k, mode, raw[:16].hex())
         agree += 1
     assert agree == 2000
+
+
+def test_bench_request_workload_encoding(fx, emu):
+    """zkatdlog.workload.RequestSet (the bench's block-level leg) writes requests
+    the oracle decodes as TokenRequest / TransferAction with the intended keys,
+    commitments and proofs, and whose verdicts through the product's request
+    orchestration (host emulation) are the ones it expects, including the
+    missing-input rows"""
+    import base64
+
+    from ftsoracle import request as R
+    from zkatdlog import _abi as A
+    from zkatdlog import workload as W
+    g = json.load(open(os.path.join(HERE, "golden", "zkatdlog_golden.json")))["pp_a"]
+    good = [c for c in g["cases"] if c["kind"] == "transfer" and c["expect"] == 0 and len(c["inputs"]) == 256
+            and len(c["outputs"]) == 256][:2]
+    items = [(bytes.fromhex(c["inputs"]), bytes.fromhex(c["outputs"]), base64.b64decode(c["proof"])) for c in good]
+    vs = W.TransferSet.from_items(items, [0] * len(items))
+    rs = W.RequestSet(vs, 7, per=2, missing_every=3)
+    raw0 = bytes(rs.buf[rs.off[0]:rs.off[1]])
+    f = R.der_token_request(raw0)
+    assert [len(x) for x in f] == [0, 2, 2, 0]
+    a = R.decode_transfer_action(f[1][1])
+    assert a is not None
+    assert json.loads(f[1][1])["Inputs"] == ["blk0000000:1:0", "blk0000000:1:1"]
+    assert base64.b64decode(json.loads(f[1][1])["Proof"]) == items[1][2]
+    assert list(rs.expect) == [0, 0, 8, 0, 0, 8, 0] and list(rs.failed) == [-1, -1, 1, -1, -1, 1, -1]
+    emu.emu_verify_token_requests.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(A.Bytes),
+                                              A.GET_STATE_FN, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                              ctypes.POINTER(ctypes.c_int32)]
+    pp = g["pp"].encode()
+    ctx = emu.emu_ctx_create(pp, len(pp), ctypes.create_string_buffer(256), 256)
+    try:
+        cb = A.get_state_callback({k: v for k, v in rs.ledger.items()})
+        codes = (ctypes.c_int32 * rs.n)()
+        failed = (ctypes.c_int32 * rs.n)()
+        assert emu.emu_verify_token_requests(ctx, rs.n, rs.ptr(), cb, None, codes, failed) == 0
+    finally:
+        emu.emu_ctx_destroy(ctx)
+    assert list(codes) == list(rs.expect) and list(failed) == list(rs.failed)
