@@ -590,19 +590,22 @@ def ppb_leg(device, args, bad_b):
         t0 = time.perf_counter()
         valid = W.prove_distinct(ctx, n_prove, tag=b"ppb", bases=bases)
         t_prove = time.perf_counter() - t0
-        job = W.mixed_job(valid, bad_b, 8 * n_prove, seed=5)
-        ctx.verify_transfers_packed(job.ptr(), 2 * ctx.options["batch"])  # warm the engine slots
+        # the engine sizes passes by pairing jobs: 4 x batch of them, the pairings of a
+        # PP-A pass -- 1024 PP-B transfers (2 outputs x 16 digits each) per pass
+        pass_n = max(1, 4 * ctx.options["batch"] // (2 * ctx.exponent))
+        job = W.mixed_job(valid, bad_b, 64 * pass_n, seed=5)  # 64 device passes
+        ctx.verify_transfers_packed(job.ptr(), (ctx.options["slots"] + 1) * pass_n)  # warm the engine slots
         t0 = time.perf_counter()
         codes = ctx.verify_transfers_packed(job.ptr(), job.n)
         dt = time.perf_counter() - t0
         ok = bool(np.array_equal(codes, job.expect))
         rate = job.n / dt
-        roof = roofline(ctx, job, min(ctx.options["batch"], job.n), device, rate, pp_key="pp_b")
+        roof = roofline(ctx, job, min(pass_n, job.n), device, rate, pp_key="pp_b")
     finally:
         ctx.close()
     return {"verify_transfers_per_s": round(rate, 1), "verify_transfers": job.n, "verdicts_bit_exact": ok,
             "prove_proofs_per_s": round(n_prove / t_prove, 1), "proofs": n_prove,
-            "pp": "b=16,e=16 (values < 2^64)", "roofline": roof}, (pp, job, bases)
+            "pp": "b=16,e=16 (values < 2^64)", "device_pass_transfers": pass_n, "roofline": roof}, (pp, job, bases)
 
 
 def requests_leg(ctx, valid, n_req=100000, per=2):

@@ -99,6 +99,12 @@ static PlanItem item_of(const Request* r, size_t i) {
   return it;
 }
 
+// membership proofs (= pairing jobs) an item brings: one per range-proof digit
+// of every output (range/proof.go:228-257)
+static uint64_t item_pairs(const Request* r, size_t i, uint64_t exponent) {
+  return exponent * (r->tx ? r->tx[i].n_out : r->is[i].n_out);
+}
+
 static size_t item_bytes(const Request* r, size_t i) {
   return r->tx ? r->tx[i].proof_len + 64 * ((size_t)r->tx[i].n_in + r->tx[i].n_out)
                : r->is[i].proof_len + 64 * (size_t)r->is[i].n_out;
@@ -184,20 +190,30 @@ void Engine::dispatcher() {
     free_slots.pop_front();
     b->parts.clear();
     b->items.clear();
+    // a pass closes at B items, BATCH_PROOF_BYTES of proofs, or B * 4 pairing
+    // jobs -- a PP-A pass of B 2-output transfers (e = 2): wider range proofs
+    // (PP-B: e = 16, 8x the pairings per transfer) get proportionally fewer
+    // proofs per pass, so their passes cost what a PP-A pass costs
     size_t bytes = 0;
-    while (!q.empty() && b->items.size() < B) {
+    uint64_t pairs = 0;
+    const uint64_t pair_budget = 4 * (uint64_t)B, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);
+    auto room = [&]() {
+      return b->items.empty() || (bytes < BATCH_PROOF_BYTES && pairs < pair_budget);
+    };
+    while (!q.empty() && b->items.size() < B && room()) {
       Request* r = q.front();
       if (r->solo && !b->items.empty()) break;  // a solo request never shares a batch
       size_t start = r->next;
-      while (r->next < r->n && b->items.size() < B && (bytes < BATCH_PROOF_BYTES || b->items.empty())) {
+      while (r->next < r->n && b->items.size() < B && room()) {
         bytes += item_bytes(r, r->next);
+        pairs += item_pairs(r, r->next, ex);
         b->items.push_back(item_of(r, r->next));
         r->next++;
         pending--;
       }
       if (r->next > start) b->parts.push_back({r, start, r->next - start});
       if (r->next == r->n) q.pop_front();
-      if (bytes >= BATCH_PROOF_BYTES || r->solo) break;
+      if (!room() || r->solo) break;
     }
     lk.unlock();
     Clock::time_point t0 = Clock::now();
