@@ -80,6 +80,24 @@ bool hex4(const uint8_t* s, size_t n, size_t i, uint32_t& v) {
   return true;
 }
 
+// first index at or after j (< n) whose byte is '"', '\\', < 0x20 or >= 0x80,
+// 32 bytes per step; n if none
+__attribute__((target("avx2"))) static size_t scan_plain_avx2(const uint8_t* s, size_t n, size_t j) {
+  const __m256i quote = _mm256_set1_epi8('"'), bslash = _mm256_set1_epi8('\\'), c1f = _mm256_set1_epi8(0x1f);
+  while (j + 32 <= n) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + j));
+    // signed compare: bytes >= 0x80 are negative, so v <= 0x1f catches them and the control bytes
+    __m256i hit = _mm256_or_si256(_mm256_cmpeq_epi8(v, quote), _mm256_cmpeq_epi8(v, bslash));
+    hit = _mm256_or_si256(hit, _mm256_cmpgt_epi8(_mm256_add_epi8(c1f, _mm256_set1_epi8(1)), v));
+    uint32_t m = (uint32_t)_mm256_movemask_epi8(hit);
+    if (m) return j + (size_t)__builtin_ctz(m);
+    j += 32;
+  }
+  return j;
+}
+
+static const bool g_avx2_scan = __builtin_cpu_supports("avx2");
+
 struct Parser {
   const uint8_t* s;
   size_t n, i;
@@ -91,6 +109,10 @@ struct Parser {
 
   // index of the first byte at or after j that is '"', '\\', < 0x20 or >= 0x80
   size_t scan_plain(size_t j) const {
+    if (g_avx2_scan) {
+      j = scan_plain_avx2(s, n, j);
+      if (j + 32 <= n) return j;  // a hit inside a full block
+    }
     const uint64_t ones = 0x0101010101010101ull, high = 0x8080808080808080ull;
     while (j + 8 <= n) {
       uint64_t v;
@@ -724,7 +746,12 @@ DecStatus dec_bytes(const JDoc& d, int64_t node, std::vector<uint8_t>& out) {
   out.clear();
   if (node < 0 || d.at((uint32_t)node).type == J_NULL) return D_NIL;
   if (d.at((uint32_t)node).type != J_STR) return D_ERR;
-  if (!b64_decode(d.str((uint32_t)node), d.len((uint32_t)node), out)) return D_ERR;
+  const char* s = d.str((uint32_t)node);
+  size_t n = d.len((uint32_t)node);
+  // canonical text (the Go encoder's output) through the vector decoder, anything
+  // else through the lenient one: same bytes where both accept
+  if (b64_decode_strict_append(s, n, out)) return D_OK;
+  if (!b64_decode(s, n, out)) return D_ERR;
   return D_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <deque>
 #include <memory>
 #include <thread>
@@ -317,6 +318,17 @@ struct Chunk {
   }
 };
 
+// accumulates the calling thread's time since the last mark into one stage
+struct StageClock {
+  RequestStats* st;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(double RequestStats::*field) {
+    auto now = std::chrono::steady_clock::now();
+    if (st) st->*field += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+};
+
 void run_par(const RequestHooks& h, size_t k, const std::function<void(size_t)>& f) {
   if (h.par && k > 1) {
     h.par(k, f);
@@ -325,173 +337,197 @@ void run_par(const RequestHooks& h, size_t k, const std::function<void(size_t)>&
   }
 }
 
-// element checks of the slots `who` names (request, pool offset); a rejected
-// slot marks its request failed (unmarshal) or its transfer's input bad (ledger)
-int check_slots(const RequestHooks& h, Chunk& c, const std::vector<std::pair<size_t, size_t>>& who,
-                const std::vector<size_t>& tr_of, std::string& err) {
-  if (who.empty()) return FTZ_SUCCESS;
-  std::vector<uint8_t> slots(64 * who.size()), ok(who.size());
-  for (size_t k = 0; k < who.size(); k++)
-    memcpy(slots.data() + 64 * k, c.st[who[k].first].pool.data() + who[k].second, 64);
-  int rc = h.check(who.size(), slots.data(), ok.data());
-  if (rc != FTZ_SUCCESS) {
-    err = "element check failed";
-    return rc;
-  }
-  for (size_t k = 0; k < who.size(); k++) {
-    if (ok[k]) continue;
-    ReqState& s = c.st[who[k].first];
-    if (tr_of.empty()) {
-      s.failed = true;
-      s.code = FTZ_ERR_PARSE;
-    } else {
-      s.tr_pre[tr_of[k]] = FTZ_ERR_INPUT;
-    }
-  }
-  return FTZ_SUCCESS;
+// exclusive prefix sums in place: v[0] = 0, v[i + 1] = v[i] + (count of item i)
+void prefix(std::vector<size_t>& v) {
+  v[0] = 0;
+  for (size_t i = 1; i < v.size(); i++) v[i] += v[i - 1];
 }
 
-// steps 1-3 of a chunk and the start of its ZK verification
+// steps 1-4 of a chunk and the start of its ZK verification.  Every per-request
+// stage runs on h.par (a request's state is written by one thread); the
+// calling thread does the prefix sums, the device checks and the ledger
+// callbacks.
 int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::string& err) {
   const size_t m = c.r1 - c.r0;
+  StageClock clk{h.stats};
   c.st.resize(m);
-  // 1. decode: ASN.1, then every issue action, then every transfer action
-  //    (validator.go unmarshalIssueActions / unmarshalTransferActions)
   constexpr size_t PIECE = 32;
-  run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
-    for (size_t i = p * PIECE; i < m && i < (p + 1) * PIECE; i++) {
-      ReqState& s = c.st[i];
-      const ftz_bytes& q = reqs[c.r0 + i];
-      std::vector<Slice> f[4];
-      std::string e = der_token_request(q.p, q.len, f);
-      if (e.empty()) {
-        s.is.resize(f[0].size());
-        for (size_t k = 0; k < f[0].size() && e.empty(); k++) e = dec_issue_action(f[0][k].p, f[0][k].len, s.is[k], s.pool);
-        s.tr.resize(f[1].size());
-        for (size_t k = 0; k < f[1].size() && e.empty(); k++)
-          e = dec_transfer_action(f[1][k].p, f[1][k].len, s.tr[k], s.pool);
-      }
-      if (!e.empty()) {
-        s.failed = true;
-        s.code = FTZ_ERR_PARSE;
-      }
+  auto each = [&](const std::function<void(size_t)>& f) {
+    run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
+      for (size_t r = p * PIECE; r < m && r < (p + 1) * PIECE; r++) f(r);
+    });
+  };
+  std::vector<size_t> cnt(m + 1, 0);
+  // 1. decode: ASN.1, then every issue action, then every transfer action
+  //    (validator.go unmarshalIssueActions / unmarshalTransferActions);
+  //    cnt = the request's elements decoded at unmarshal
+  each([&](size_t i) {
+    ReqState& s = c.st[i];
+    const ftz_bytes& q = reqs[c.r0 + i];
+    std::vector<Slice> f[4];
+    std::string e = der_token_request(q.p, q.len, f);
+    if (e.empty()) {
+      s.is.resize(f[0].size());
+      for (size_t k = 0; k < f[0].size() && e.empty(); k++) e = dec_issue_action(f[0][k].p, f[0][k].len, s.is[k], s.pool);
+      s.tr.resize(f[1].size());
+      for (size_t k = 0; k < f[1].size() && e.empty(); k++) e = dec_transfer_action(f[1][k].p, f[1][k].len, s.tr[k], s.pool);
     }
+    if (!e.empty()) {
+      s.failed = true;
+      s.code = FTZ_ERR_PARSE;
+      return;
+    }
+    size_t k = 0;
+    for_unmarshal_elems(s, [&](const ElemRef& x) { k += x.st == D_OK; });
+    cnt[i + 1] = k;
   });
+  clk.mark(&RequestStats::decode);
   // 2. curve checks of the elements decoded at unmarshal (math.G1 UnmarshalJSON
   //    -> gnark SetBytes), one device pass over the chunk
-  {
-    std::vector<std::pair<size_t, size_t>> who;
-    for (size_t r = 0; r < m; r++) {
-      if (c.st[r].failed) continue;
-      for_unmarshal_elems(c.st[r], [&](const ElemRef& e) {
-        if (e.st == D_OK) who.push_back({r, e.off});
+  prefix(cnt);
+  if (cnt[m]) {
+    std::vector<uint8_t> slots(64 * cnt[m]), ok(cnt[m]);
+    each([&](size_t r) {
+      size_t o = cnt[r];
+      if (c.st[r].failed) return;  // a request that failed to decode counted none
+      for_unmarshal_elems(c.st[r], [&](const ElemRef& x) {
+        if (x.st == D_OK) memcpy(slots.data() + 64 * o++, c.st[r].pool.data() + x.off, 64);
       });
+    });
+    int rc = h.check(cnt[m], slots.data(), ok.data());
+    if (rc != FTZ_SUCCESS) {
+      err = "element check failed";
+      return rc;
     }
-    int rc = check_slots(h, c, who, {}, err);
-    if (rc != FTZ_SUCCESS) return rc;
+    each([&](size_t r) {
+      for (size_t k = cnt[r]; k < cnt[r + 1]; k++)
+        if (!ok[k]) {
+          c.st[r].failed = true;
+          c.st[r].code = FTZ_ERR_PARSE;
+        }
+    });
   }
+  clk.mark(&RequestStats::check);
   // 3. ledger inputs of every transfer (TransferSignatureValidate's loads,
-  //    validator_transfer.go:42-81) on the calling thread, values copied; then
-  //    decoded as token.Token in parallel, then their Data elements checked
-  struct Need {
-    size_t r, t;
-  };
-  std::vector<Need> need;     // transfers whose inputs are looked up
-  std::vector<ftz_bytes> keys;
-  std::vector<size_t> key_at;  // first key index of need[k]
-  for (size_t r = 0; r < m; r++) {
+  //    validator_transfer.go:42-81) through the callbacks on the calling thread
+  std::vector<size_t> kat(m + 1, 0);  // the request's first key index
+  each([&](size_t r) {
     ReqState& s = c.st[r];
-    if (s.failed) continue;
+    if (s.failed) return;
     s.ins.resize(s.tr.size());
     s.tr_pre.assign(s.tr.size(), 0);
     s.is_pre.assign(s.is.size(), 0);
-    for (size_t t = 0; t < s.tr.size(); t++) {
-      need.push_back({r, t});
-      key_at.push_back(keys.size());
-      for (const std::string& key : s.tr[t].inputs)
-        keys.push_back(ftz_bytes{reinterpret_cast<const uint8_t*>(key.data()), key.size()});
-    }
-  }
-  key_at.push_back(keys.size());
-  std::vector<uint8_t> vbuf;                          // copied values
-  std::vector<std::pair<size_t, size_t>> vref(keys.size(), {0, SIZE_MAX});  // (offset, len); len SIZE_MAX: missing
+    size_t k = 0;
+    for (const TransferAct& t : s.tr) k += t.inputs.size();
+    kat[r + 1] = k;
+  });
+  prefix(kat);
+  std::vector<ftz_bytes> keys(kat[m]);
+  each([&](size_t r) {
+    size_t k = kat[r];
+    if (c.st[r].failed) return;
+    for (const TransferAct& t : c.st[r].tr)
+      for (const std::string& key : t.inputs) keys[k++] = ftz_bytes{reinterpret_cast<const uint8_t*>(key.data()), key.size()};
+  });
+  std::vector<ftz_bytes> vals(keys.size(), ftz_bytes{nullptr, 0});  // {NULL, 0}: missing / not read
+  std::vector<uint8_t> vbuf;  // the one-key form's values, copied (each is valid until the next call)
   if (!keys.empty()) {
     if (h.get_states) {
-      std::vector<ftz_bytes> vals(keys.size(), ftz_bytes{nullptr, 0});
-      if (h.get_states(h.user, keys.size(), keys.data(), vals.data()) == 0) {
-        size_t tot = 0;
-        for (const ftz_bytes& v : vals) tot += v.p ? v.len : 0;
-        vbuf.reserve(tot);
-        for (size_t k = 0; k < keys.size(); k++)
-          if (vals[k].p && vals[k].len) {
-            vref[k] = {vbuf.size(), vals[k].len};
-            vbuf.insert(vbuf.end(), vals[k].p, vals[k].p + vals[k].len);
-          }
-      }
+      // values valid until the next get_states call: the tokens are decoded below, before it
+      if (h.get_states(h.user, keys.size(), keys.data(), vals.data()) != 0)
+        for (ftz_bytes& v : vals) v = ftz_bytes{nullptr, 0};
     } else {
-      for (size_t q = 0; q < need.size(); q++)
-        for (size_t k = key_at[q]; k < key_at[q + 1]; k++) {
-          const uint8_t* val = nullptr;
-          size_t vlen = 0;
-          if (!h.get_state || h.get_state(h.user, reinterpret_cast<const char*>(keys[k].p), keys[k].len, &val, &vlen) != 0 ||
-              vlen == 0)
-            break;  // "failed to retrieve input" / "does not exists": the transfer's later inputs are not read
-          vref[k] = {vbuf.size(), vlen};
-          vbuf.insert(vbuf.end(), val, val + vlen);
-        }
-    }
-  }
-  // token decoding per request (a request's pool is written by one thread)
-  std::vector<size_t> need_of(m + 1, 0);  // need[] range of request r: [need_of[r], need_of[r+1])
-  for (size_t q = 0; q < need.size(); q++) need_of[need[q].r + 1] = q + 1;
-  for (size_t r = 1; r <= m; r++) need_of[r] = std::max(need_of[r], need_of[r - 1]);
-  run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
-    for (size_t r = p * PIECE; r < m && r < (p + 1) * PIECE; r++) {
-      ReqState& s = c.st[r];
-      for (size_t q = need_of[r]; q < need_of[r + 1]; q++) {
-        size_t t = need[q].t;
-        for (size_t k = key_at[q]; k < key_at[q + 1]; k++) {
-          if (vref[k].second == SIZE_MAX) {
-            s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to retrieve input" / "does not exists"
-            break;
+      std::vector<std::pair<size_t, size_t>> at(keys.size(), {0, 0});
+      for (size_t r = 0; r < m; r++) {
+        const ReqState& s = c.st[r];
+        if (s.failed) continue;
+        size_t k = kat[r];
+        for (const TransferAct& t : s.tr) {
+          size_t k1 = k + t.inputs.size();
+          for (; k < k1; k++) {
+            const uint8_t* val = nullptr;
+            size_t vlen = 0;
+            if (!h.get_state ||
+                h.get_state(h.user, reinterpret_cast<const char*>(keys[k].p), keys[k].len, &val, &vlen) != 0 ||
+                vlen == 0)
+              break;  // "failed to retrieve input" / "does not exists": the transfer's later inputs are not read
+            at[k] = {vbuf.size(), vlen};
+            vbuf.insert(vbuf.end(), val, val + vlen);
           }
-          ElemRef d;
-          if (!dec_token(vbuf.data() + vref[k].first, vref[k].second, d, s.pool).empty()) {
-            s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to deserialize input to spend"
-            break;
-          }
-          s.ins[t].push_back(d);
+          k = k1;
         }
       }
+      for (size_t k = 0; k < keys.size(); k++)
+        if (at[k].second) vals[k] = ftz_bytes{vbuf.data() + at[k].first, at[k].second};
     }
-  });
-  {
-    std::vector<std::pair<size_t, size_t>> who;
-    std::vector<size_t> tr_of;
-    for (const Need& q : need) {
-      ReqState& s = c.st[q.r];
-      if (s.tr_pre[q.t]) continue;
-      for (const ElemRef& d : s.ins[q.t])
-        if (d.st == D_OK) {
-          who.push_back({q.r, d.off});
-          tr_of.push_back(q.t);
-        }
-    }
-    int rc = check_slots(h, c, who, tr_of, err);
-    if (rc != FTZ_SUCCESS) return rc;
   }
+  clk.mark(&RequestStats::lookup);
+  // token decoding per request; cnt = the request's ledger Data elements to check
+  std::fill(cnt.begin(), cnt.end(), 0);
+  each([&](size_t r) {
+    ReqState& s = c.st[r];
+    if (s.failed) return;
+    size_t k = kat[r], nd = 0;
+    for (size_t t = 0; t < s.tr.size(); t++) {
+      size_t k1 = k + s.tr[t].inputs.size();
+      for (; k < k1; k++) {
+        if (!vals[k].p || !vals[k].len) {
+          s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to retrieve input" / "does not exists"
+          break;
+        }
+        ElemRef d;
+        if (!dec_token(vals[k].p, vals[k].len, d, s.pool).empty()) {
+          s.tr_pre[t] = FTZ_ERR_INPUT;  // "failed to deserialize input to spend"
+          break;
+        }
+        s.ins[t].push_back(d);
+      }
+      k = k1;
+      if (!s.tr_pre[t])
+        for (const ElemRef& d : s.ins[t]) nd += d.st == D_OK;
+    }
+    cnt[r + 1] = nd;
+  });
+  clk.mark(&RequestStats::tokens);
+  prefix(cnt);
+  if (cnt[m]) {
+    std::vector<uint8_t> slots(64 * cnt[m]), ok(cnt[m]);
+    std::vector<uint32_t> tr_of(cnt[m]);
+    each([&](size_t r) {
+      const ReqState& s = c.st[r];
+      size_t o = cnt[r];
+      if (s.failed) return;
+      for (size_t t = 0; t < s.tr.size(); t++) {
+        if (s.tr_pre[t]) continue;
+        for (const ElemRef& d : s.ins[t])
+          if (d.st == D_OK) {
+            memcpy(slots.data() + 64 * o, s.pool.data() + d.off, 64);
+            tr_of[o++] = (uint32_t)t;
+          }
+      }
+    });
+    int rc = h.check(cnt[m], slots.data(), ok.data());
+    if (rc != FTZ_SUCCESS) {
+      err = "element check failed";
+      return rc;
+    }
+    each([&](size_t r) {
+      for (size_t k = cnt[r]; k < cnt[r + 1]; k++)
+        if (!ok[k]) c.st[r].tr_pre[tr_of[k]] = FTZ_ERR_INPUT;
+    });
+  }
+  clk.mark(&RequestStats::check);
   // 4. the ZK checks of every action still open, through the job engine.
   //    A nil or foreign-curve commitment reaches the verifier and the reference
   //    panics on it (G1 use / driver type assertion); a nil issue output fails
   //    GetCommitments ("failed to verify issue", validator.go verifyIssue).
-  auto put = [&](const ReqState& s, const ElemRef& e) {
-    size_t o = c.coms.size();
-    c.coms.resize(o + 64, 0);
-    memcpy(c.coms.data() + o, s.pool.data() + e.off, 64);
-  };
-  for (size_t r = 0; r < m; r++) {
+  //    Per request: the pre-verifier codes and the counts, then prefix sums,
+  //    then every request fills its commitments / jobs in place.
+  std::vector<size_t> ncom(m + 1, 0), nis(m + 1, 0), ntr(m + 1, 0);
+  each([&](size_t r) {
     ReqState& s = c.st[r];
-    if (s.failed) continue;
+    if (s.failed) return;
+    size_t nc = 0, ni = 0, nt = 0;
     for (size_t k = 0; k < s.is.size(); k++) {
       const IssueAct& a = s.is[k];
       if (a.out.nil_token) {
@@ -504,9 +540,8 @@ int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::s
         s.is_pre[k] = FTZ_ERR_PANIC;
         continue;
       }
-      size_t o = c.coms.size();
-      for (const ElemRef& e : a.out.data) put(s, e);
-      c.irefs.push_back({r, k, o});
+      nc += a.out.data.size();
+      ni++;
     }
     for (size_t t = 0; t < s.tr.size(); t++) {
       if (s.tr_pre[t]) continue;
@@ -518,29 +553,53 @@ int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::s
         s.tr_pre[t] = FTZ_ERR_PANIC;
         continue;
       }
-      size_t io = c.coms.size();
-      for (const ElemRef& e : s.ins[t]) put(s, e);
-      size_t oo = c.coms.size();
-      for (const ElemRef& e : a.out.data) put(s, e);
-      c.trefs.push_back({r, t, io, oo});
+      nc += s.ins[t].size() + a.out.data.size();
+      nt++;
     }
-  }
-  c.iv.resize(c.irefs.size());
-  for (size_t k = 0; k < c.irefs.size(); k++) {
-    const IssueAct& a = c.st[c.irefs[k].r].is[c.irefs[k].k];
-    c.iv[k] = ftz_issue{c.coms.data() + c.irefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(),
-                        a.proof.size(), (uint8_t)(a.anonymous ? 1 : 0)};
-  }
-  c.tv.resize(c.trefs.size());
-  for (size_t k = 0; k < c.trefs.size(); k++) {
-    const ReqState& s = c.st[c.trefs[k].r];
-    const TransferAct& a = s.tr[c.trefs[k].t];
-    c.tv[k] = ftz_transfer{c.coms.data() + c.trefs[k].in_off, (uint32_t)s.ins[c.trefs[k].t].size(),
-                           c.coms.data() + c.trefs[k].out_off, (uint32_t)a.out.data.size(), a.proof.data(),
-                           a.proof.size()};
-  }
+    ncom[r + 1] = nc;
+    nis[r + 1] = ni;
+    ntr[r + 1] = nt;
+  });
+  prefix(ncom);
+  prefix(nis);
+  prefix(ntr);
+  c.coms.resize(64 * ncom[m]);
+  c.irefs.resize(nis[m]);
+  c.trefs.resize(ntr[m]);
+  c.iv.resize(nis[m]);
+  c.tv.resize(ntr[m]);
+  each([&](size_t r) {
+    const ReqState& s = c.st[r];
+    if (s.failed) return;
+    size_t o = 64 * ncom[r], ki = nis[r], kt = ntr[r];
+    auto put = [&](const ElemRef& e) {
+      memcpy(c.coms.data() + o, s.pool.data() + e.off, 64);
+      o += 64;
+    };
+    for (size_t k = 0; k < s.is.size(); k++) {
+      if (s.is_pre[k]) continue;
+      const IssueAct& a = s.is[k];
+      size_t oo = o;
+      for (const ElemRef& e : a.out.data) put(e);
+      c.irefs[ki] = {r, k, oo};
+      c.iv[ki++] = ftz_issue{c.coms.data() + oo, (uint32_t)a.out.data.size(), a.proof.data(), a.proof.size(),
+                             (uint8_t)(a.anonymous ? 1 : 0)};
+    }
+    for (size_t t = 0; t < s.tr.size(); t++) {
+      if (s.tr_pre[t]) continue;
+      const TransferAct& a = s.tr[t];
+      size_t io = o;
+      for (const ElemRef& e : s.ins[t]) put(e);
+      size_t oo = o;
+      for (const ElemRef& e : a.out.data) put(e);
+      c.trefs[kt] = {r, t, io, oo};
+      c.tv[kt++] = ftz_transfer{c.coms.data() + io, (uint32_t)s.ins[t].size(), c.coms.data() + oo,
+                                (uint32_t)a.out.data.size(), a.proof.data(), a.proof.size()};
+    }
+  });
   c.icodes.resize(c.iv.size());
   c.tcodes.resize(c.tv.size());
+  clk.mark(&RequestStats::build);
   // issues and transfers on helper threads: the job engine coalesces them (and
   // the other chunks in flight) into shared device batches
   Chunk* cp = &c;
@@ -583,11 +642,13 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
   std::deque<std::unique_ptr<Chunk>> fly;
   int rc = FTZ_SUCCESS;
   for (size_t r0 = 0; r0 < n && rc == FTZ_SUCCESS; r0 += CH) {
+    StageClock clk{h.stats};
     while (fly.size() >= IN) {  // bound the memory held by chunks in flight
       rc = finish_chunk(*fly.front(), codes, failed, err);
       fly.pop_front();
       if (rc != FTZ_SUCCESS) break;
     }
+    clk.mark(&RequestStats::drain);
     if (rc != FTZ_SUCCESS) break;
     fly.emplace_back(new Chunk());
     Chunk& c = *fly.back();
@@ -596,6 +657,7 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
     rc = prepare_chunk(reqs, h, c, err);
   }
   // drain (also after an error: every helper thread is joined before returning)
+  StageClock clk{h.stats};
   while (!fly.empty()) {
     std::string e2;
     int r2 = finish_chunk(*fly.front(), codes, failed, e2);
@@ -605,6 +667,7 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
     }
     fly.pop_front();
   }
+  clk.mark(&RequestStats::drain);
   return rc;
 }
 

@@ -73,6 +73,11 @@ std::string dec_token(const uint8_t* p, size_t n, ElemRef& data, std::vector<uin
 
 namespace ftsh {
 
+// calling-thread time per pipeline stage, ms (optional, RequestHooks.stats)
+struct RequestStats {
+  double decode = 0, check = 0, lookup = 0, tokens = 0, build = 0, drain = 0;
+};
+
 struct RequestHooks {
   // gnark SetBytes check of n 64-byte element slots: ok[i] = 1 / 0; FTZ_SUCCESS or an API error
   std::function<int(size_t n, const uint8_t* slots, uint8_t* ok)> check;
@@ -88,6 +93,7 @@ struct RequestHooks {
   std::function<void(size_t k, const std::function<void(size_t)>& f)> par;
   size_t chunk = 8192;  // requests decoded per pipeline step
   size_t inflight = 4;  // chunks whose ZK verification may be in flight at once
+  RequestStats* stats = nullptr;
 };
 
 // codes[r]: FTZ_OK or the first failing check of request r in the reference's

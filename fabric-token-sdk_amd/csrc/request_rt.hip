@@ -38,7 +38,7 @@ int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state
   WorkPool* pool;
   {
     std::lock_guard<std::mutex> lk(ctx->req_mu);
-    if (!ctx->req_pool) ctx->req_pool = new WorkPool((int)std::max<uint32_t>(4, ctx->opt.threads / 2));
+    if (!ctx->req_pool) ctx->req_pool = new WorkPool((int)std::max<uint32_t>(4, ctx->opt.threads));
     pool = ctx->req_pool;
   }
   ftsh::RequestHooks h;

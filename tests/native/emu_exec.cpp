@@ -457,6 +457,42 @@ int emu_verify_token_requests(void* ctx, size_t n, const ftz_bytes* reqs, ftz_ge
   return ftsh::verify_token_requests(n, reqs, h, codes, failed, err);
 }
 
+// host-side throughput of the request pipeline alone (tools, not a test of
+// verdicts): element checks and ZK verification answered "ok" at once, the
+// decoding / lookup / token / build stages real.  stats[6] = RequestStats (ms).
+int emu_request_host_bench(size_t n, const ftz_bytes* reqs, ftz_get_states_fn get_states, void* user, size_t chunk,
+                           int par_threads, int32_t* codes, double* stats) {
+  ftsh::RequestHooks h;
+  h.check = [](size_t m, const uint8_t*, uint8_t* ok) {
+    memset(ok, 1, m);
+    return 0;
+  };
+  h.verify_transfers = [](size_t m, const ftz_transfer*, int32_t* c) {
+    memset(c, 0, m * sizeof(int32_t));
+    return 0;
+  };
+  h.verify_issues = [](size_t m, const ftz_issue*, int32_t* c) {
+    memset(c, 0, m * sizeof(int32_t));
+    return 0;
+  };
+  h.get_states = get_states;
+  h.user = user;
+  h.chunk = chunk;
+  std::unique_ptr<WorkPool> pool;
+  if (par_threads > 0) {
+    pool.reset(new WorkPool(par_threads));
+    WorkPool* pp = pool.get();
+    h.par = [pp](size_t k, const std::function<void(size_t)>& f) { pp->run(k, f); };
+  }
+  ftsh::RequestStats st;
+  h.stats = &st;
+  std::string err;
+  int rc = ftsh::verify_token_requests(n, reqs, h, codes, nullptr, err);
+  double v[6] = {st.decode, st.check, st.lookup, st.tokens, st.build, st.drain};
+  memcpy(stats, v, sizeof v);
+  return rc;
+}
+
 // the same with the pipeline's knobs: batched lookups, chunk size, chunks in
 // flight, and `par_threads` decoding threads (0: serial)
 int emu_verify_token_requests_ex(void* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
