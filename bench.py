@@ -634,16 +634,23 @@ def requests_leg(ctx, valid, n_req=100000, per=2):
         ctx.verify_token_requests_packed(rs.ptr(), w, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
                                          batched=batched)
         c0 = led.counts()
+        ctx.request_stats(reset=True)
+        est0 = ctx.engine_stats(reset=True)
         t0 = time.perf_counter()
         ctx.verify_token_requests_packed(rs.ptr(), n_req, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
                                          batched=batched)
         dt = time.perf_counter() - t0
         c1 = led.counts()
+        stages = ctx.request_stats(reset=True)
+        est = ctx.engine_stats()
         ok = bool(np.array_equal(codes, rs.expect) and np.array_equal(failed, rs.failed))
         out["batched_get_states" if batched else "per_key_get_state"] = {
             "requests_per_s": round(n_req / dt, 1), "transfers_per_s": round(n_req * per / dt, 1),
             "s": round(dt, 3), "verdicts_bit_exact": ok, "callback_calls": c1[0] - c0[0],
-            "keys_looked_up": c1[1] - c0[1]}
+            "keys_looked_up": c1[1] - c0[1], "calling_thread_ms": stages,
+            "engine": {"batches": est["batches"], "max_in_flight": est["max_in_flight"],
+                       "plan_ms_per_batch": round(est["plan_ms"] / max(1, est["batches"]), 3),
+                       "device_ms_per_batch": round(est["device_ms"] / max(1, est["batches"]), 3)}}
     led.close()
     return out
 

@@ -49,8 +49,15 @@ int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state
   h.get_states = get_states;
   h.user = user;
   h.par = [pool](size_t k, const std::function<void(size_t)>& f) { pool->run(k, f); };
+  ftsh::RequestStats st;
+  h.stats = &st;
   std::string err;
   int rc = ftsh::verify_token_requests(n, reqs, h, codes, failed_action, err);
+  {
+    std::lock_guard<std::mutex> lk(ctx->req_mu);
+    const double v[6] = {st.decode, st.check, st.lookup, st.tokens, st.build, st.drain};
+    for (int k = 0; k < 6; k++) ctx->req_ms[k] += v[k];
+  }
   if (rc != FTZ_SUCCESS && !err.empty()) {
     std::string last = ftz_last_error();
     return set_err(rc, err + (last.empty() ? "" : ": " + last));
@@ -58,6 +65,16 @@ int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state
   return rc;
 }
 }  // namespace
+
+extern "C" int ftz_ctx_request_stats(ftz_ctx* ctx, double ms[6], int reset) {
+  if (!ctx || !ms) return set_err(FTZ_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(ctx->req_mu);
+  for (int k = 0; k < 6; k++) {
+    ms[k] = ctx->req_ms[k];
+    if (reset) ctx->req_ms[k] = 0;
+  }
+  return FTZ_SUCCESS;
+}
 
 extern "C" int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state,
                                          void* user, int32_t* codes, int32_t* failed_action) {

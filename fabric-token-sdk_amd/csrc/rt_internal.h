@@ -134,6 +134,7 @@ struct ftz_ctx {
   // which would wait on the engine's device work -- per call)
   std::mutex req_mu;
   WorkPool* req_pool = nullptr;
+  double req_ms[6] = {};  // ftz_ctx_request_stats (under req_mu)
   hipStream_t chk_stream = nullptr;
   std::mutex chk_mu;
   PinnedMem chk_h;

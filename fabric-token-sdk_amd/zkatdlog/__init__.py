@@ -245,6 +245,12 @@ class Context:
         self.verify_token_requests_packed(arr, n, ledger, codes, failed, batched=batched)
         return list(codes)[:n], list(failed)[:n]
 
+    def request_stats(self, reset=False):
+        """calling-thread ms per request-pipeline stage (ftz_ctx_request_stats)"""
+        ms = (ctypes.c_double * 6)()
+        _check(self._lib.ftz_ctx_request_stats(self._h, ms, 1 if reset else 0), self._lib)
+        return dict(zip(("decode", "check", "lookup", "tokens", "build", "drain"), (round(x, 2) for x in ms)))
+
     def verify_token_requests_packed(self, arr, n, ledger, codes, failed, batched=False):
         """as verify_token_requests over a packed ftz_bytes array and caller-owned
         int32 code arrays (bench: the packing stays out of the timed call)"""

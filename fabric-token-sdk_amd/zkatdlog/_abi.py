@@ -279,7 +279,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
            "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
-           "ftz_token_request_decode", "ftz_verify_token_requests", "ftz_verify_token_requests_batched",
+           "ftz_token_request_decode", "ftz_verify_token_requests", "ftz_verify_token_requests_batched", "ftz_ctx_request_stats",
            "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_ctx_prover_stats", "ftz_prover_load_transfers", "ftz_prover_load_issues",
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
@@ -354,6 +354,7 @@ def load():
                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
     lib.ftz_verify_token_requests_batched.argtypes = [vp, sz, ctypes.POINTER(Bytes), vp, vp,
                                                       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]
+    lib.ftz_ctx_request_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]
     szp = ctypes.POINTER(ctypes.c_size_t)
     i32p = ctypes.POINTER(ctypes.c_int32)
     lib.ftz_prove_transfers.argtypes = [vp, sz, ctypes.POINTER(TransferWitness), u8p, sz, szp, i32p]

@@ -317,6 +317,12 @@ int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz
  * binding: one callback per chunk of up to 8192 requests). */
 int ftz_verify_token_requests_batched(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_states_fn get_states,
                                       void* user, int32_t* codes, int32_t* failed_action);
+/* profiling: the calling thread's time in each stage of the request pipeline,
+ * summed over the context's ftz_verify_token_requests* calls, in ms: ms[0]
+ * decode (ASN.1 + action JSON, parallel), [1] element checks (device), [2]
+ * ledger callbacks, [3] token decoding (parallel), [4] job building, [5]
+ * waiting for the verdicts of earlier chunks; reset != 0 zeroes them after. */
+int ftz_ctx_request_stats(ftz_ctx* ctx, double ms[6], int reset);
 
 /* ---- idemix owner signatures, on BN254 or FP256BN_AMCL.
  * Replaces, per input token of a transfer, what TransferSignatureValidate
