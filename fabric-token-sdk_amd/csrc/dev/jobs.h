@@ -91,8 +91,12 @@ struct ScalJob {
 struct VTerm {
   uint32_t pt;        // pts index
   uint32_t w_lo, w_hi;
-  uint32_t pad;
+  uint32_t flags;     // VT_HORNER on a job's first term
 };
+// The job's variable part is sum_i b^i P_i given in Horner order: terms
+// P_{e-1}, ..., P_0, each weight = b, computed as V = b V + P_t (PP-B range
+// equality: 15 x (4 doublings + 1 addition) instead of 16 64-bit multiples)
+static constexpr uint32_t VT_HORNER = 1;
 
 struct G1Job {
   uint32_t fscal[3];
@@ -792,6 +796,14 @@ FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* 
     const VTerm& v0 = vterms[j.vstart];
     if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
       Va = g1_load(pts[v0.pt]);
+    } else if (v0.flags & VT_HORNER) {
+      const uint64_t b = ((uint64_t)v0.w_hi << 32) | v0.w_lo;
+      g1j V = jac_from_aff(g1_load(pts[v0.pt]));
+      for (uint32_t t = 1; t < j.vcount; t++) {
+        V = jac_mul_u64(V, b);
+        V = jac_add_aff(V, g1_load(pts[vterms[j.vstart + t].pt]));
+      }
+      Va = jac_to_aff(V);
     } else {
       g1j V = jac_inf<fp>();
       for (uint32_t t = 0; t < j.vcount; t++) {

@@ -372,7 +372,7 @@ class Builder {
     v.pt = pt;
     v.w_lo = (uint32_t)w;
     v.w_hi = (uint32_t)(w >> 32);
-    v.pad = 0;
+    v.flags = 0;
     return v;
   }
 
@@ -777,7 +777,12 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
   for (uint32_t j = 0; j < n; j++) {
     uint32_t scb = scalar(r.eq_cbf[j]);
     std::vector<VTerm> terms;
-    for (uint32_t i = 0; i < e; i++) terms.push_back(vterm(com_pt[j][i], pp.pow[i]));
+    if (pp.pow_exact && e > 1) {  // sum_i b^i com_i in Horner order (VT_HORNER): same point
+      for (uint32_t i = e; i-- > 0;) terms.push_back(vterm(com_pt[j][i], pp.base));
+      terms[0].flags = VT_HORNER;
+    } else {
+      for (uint32_t i = 0; i < e; i++) terms.push_back(vterm(com_pt[j][i], pp.pow[i]));
+    }
     g1job({{G1B_PED0, sv[j]}, {G1B_PED1, scb}}, terms, sc_rc, rg_bytes + 64 * (n + j));
   }
   HashJob h;
@@ -1735,6 +1740,14 @@ std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out)
     (void)acc;
     if (pw >= 9223372036854775808.0) return "range proof exponent overflows int64";
     out.pow.push_back((uint64_t)(int64_t)pw);
+  }
+  // the Horner form of sum_i pow[i] com_i needs pow[i] == base^i exactly
+  out.pow_exact = true;
+  unsigned __int128 bi = 1;
+  for (size_t i = 0; i < out.pow.size(); i++) {
+    if (i) bi *= out.base;
+    if (bi >> 64 || (uint64_t)bi != out.pow[i]) out.pow_exact = false;
+    if (bi >> 64) break;
   }
   out.fixed_pairs = pp_sig_tables(out) && g2_lines_normalisable(out.q) && g2_lines_normalisable(out.pk[1]) &&
                     g2_lines_normalisable(out.pk[2]);

@@ -34,6 +34,7 @@ struct PPInfo {
   int64_t curve = 0;
   std::string label;
   std::vector<uint64_t> pow;                      // base^i, i < exponent
+  bool pow_exact = false;                         // every pow[i] is base^i exactly (float64 math.Pow was exact)
   // the prover's membership commitments as three fixed-G2 pairings (Q, PK1,
   // PK2; parse_pp: every line of the three normalisable and pp_sig_tables)
   bool fixed_pairs = false;

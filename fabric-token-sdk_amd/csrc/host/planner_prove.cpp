@@ -230,7 +230,7 @@ struct PB {
       v.pt = var_pt;
       v.w_lo = 1;
       v.w_hi = 0;
-      v.pad = 0;
+      v.flags = 0;
       pl.vt.push_back(v);
       j.vcount = 1;
       j.vscal = vscal;
