@@ -91,8 +91,8 @@ struct RequestHooks {
   void* user = nullptr;
   // parallel for over [0, k) (decoding); unset: serial on the calling thread
   std::function<void(size_t k, const std::function<void(size_t)>& f)> par;
-  size_t chunk = 8192;  // requests decoded per pipeline step
-  size_t inflight = 4;  // chunks whose ZK verification may be in flight at once
+  size_t chunk = 4096;  // requests decoded per pipeline step
+  size_t inflight = 8;  // chunks whose ZK verification may be in flight at once
   RequestStats* stats = nullptr;
 };
 

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <thread>
 #include <vector>
@@ -42,7 +43,35 @@ int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state
     pool = ctx->req_pool;
   }
   ftsh::RequestHooks h;
-  h.check = [ctx](size_t m, const uint8_t* slots, uint8_t* ok) { return g1_check_slots(ctx, m, slots, ok); };
+  // gnark SetBytes checks: uncompressed and infinity-flag encodings on the host
+  // threads (a few field products each), compressed ones -- a square root each,
+  // rare on the wire -- in one device pass
+  h.check = [ctx, pool](size_t m, const uint8_t* slots, uint8_t* ok) {
+    std::atomic<size_t> ncomp{0};
+    pool->run((m + 255) / 256, [&](size_t p) {
+      for (size_t i = p * 256; i < m && i < (p + 1) * 256; i++) {
+        if (slots[64 * i] & 0x80) {
+          ok[i] = 2;
+          ncomp.fetch_add(1, std::memory_order_relaxed);
+          continue;
+        }
+        fts::g1a a;
+        ok[i] = fts::g1_setbytes(slots + 64 * i, 64, a) ? 1 : 0;
+      }
+    });
+    if (ncomp.load() == 0) return (int)FTZ_SUCCESS;
+    std::vector<uint32_t> at;
+    std::vector<uint8_t> cs;
+    for (size_t i = 0; i < m; i++)
+      if (ok[i] == 2) {
+        at.push_back((uint32_t)i);
+        cs.insert(cs.end(), slots + 64 * i, slots + 64 * i + 64);
+      }
+    std::vector<uint8_t> cok(at.size());
+    int rc = g1_check_slots(ctx, at.size(), cs.data(), cok.data());
+    for (size_t k = 0; k < at.size(); k++) ok[at[k]] = rc == FTZ_SUCCESS ? cok[k] : 0;
+    return rc;
+  };
   h.verify_transfers = [ctx](size_t m, const ftz_transfer* tx, int32_t* c) { return ftz_verify_transfers(ctx, m, tx, c); };
   h.verify_issues = [ctx](size_t m, const ftz_issue* is, int32_t* c) { return ftz_verify_issues(ctx, m, is, c); };
   h.get_state = get_state;

@@ -98,11 +98,13 @@ extern "C" int ftz_callers_run(ftz_ctx* ctx, const ftz_transfer* pool, const int
 // token key to json(token.Token), read by ftz_get_state_fn / ftz_get_states_fn
 // callbacks that cost what a native lookup costs (no Python in the timed call).
 #include <string>
+#include <string_view>
 #include <unordered_map>
 
 namespace {
 struct Ledger {
-  std::unordered_map<std::string, std::string> kv;
+  std::string store;  // every key and value, back to back
+  std::unordered_map<std::string_view, std::pair<size_t, size_t>> kv;  // key -> (value offset, length)
   uint64_t lookups = 0;  // calls (get_state) / keys (get_states), for the bench's report
   uint64_t calls = 0;
 };
@@ -110,9 +112,19 @@ struct Ledger {
 
 extern "C" void* ftz_ledger_create(size_t n, const ftz_bytes* keys, const ftz_bytes* vals) {
   Ledger* l = new Ledger();
+  size_t tot = 0;
+  for (size_t i = 0; i < n; i++) tot += keys[i].len + vals[i].len;
+  l->store.reserve(tot);
+  std::vector<std::pair<size_t, size_t>> ko(n);
+  for (size_t i = 0; i < n; i++) {
+    ko[i] = {l->store.size(), keys[i].len};
+    l->store.append((const char*)keys[i].p, keys[i].len);
+    l->store.append((const char*)vals[i].p, vals[i].len);
+  }
   l->kv.reserve(n);
   for (size_t i = 0; i < n; i++)
-    l->kv.emplace(std::string((const char*)keys[i].p, keys[i].len), std::string((const char*)vals[i].p, vals[i].len));
+    l->kv.emplace(std::string_view(l->store.data() + ko[i].first, ko[i].second),
+                  std::make_pair(ko[i].first + ko[i].second, vals[i].len));
   return l;
 }
 
@@ -129,14 +141,14 @@ extern "C" int ftz_ledger_get_state(void* user, const char* key, size_t key_len,
   Ledger* l = (Ledger*)user;
   l->calls++;
   l->lookups++;
-  auto it = l->kv.find(std::string(key, key_len));
+  auto it = l->kv.find(std::string_view(key, key_len));
   if (it == l->kv.end()) {
     *val = nullptr;
     *val_len = 0;
     return 0;  // GetState of a missing key: nil value, no error
   }
-  *val = (const uint8_t*)it->second.data();
-  *val_len = it->second.size();
+  *val = (const uint8_t*)l->store.data() + it->second.first;
+  *val_len = it->second.second;
   return 0;
 }
 
@@ -144,11 +156,10 @@ extern "C" int ftz_ledger_get_states(void* user, size_t n, const ftz_bytes* keys
   Ledger* l = (Ledger*)user;
   l->calls++;
   l->lookups += n;
-  std::string k;
   for (size_t i = 0; i < n; i++) {
-    k.assign((const char*)keys[i].p, keys[i].len);
-    auto it = l->kv.find(k);
-    vals[i] = it == l->kv.end() ? ftz_bytes{nullptr, 0} : ftz_bytes{(const uint8_t*)it->second.data(), it->second.size()};
+    auto it = l->kv.find(std::string_view((const char*)keys[i].p, keys[i].len));
+    vals[i] = it == l->kv.end() ? ftz_bytes{nullptr, 0}
+                                : ftz_bytes{(const uint8_t*)l->store.data() + it->second.first, it->second.second};
   }
   return 0;
 }

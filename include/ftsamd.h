@@ -314,7 +314,7 @@ typedef int (*ftz_get_states_fn)(void* user, size_t n, const ftz_bytes* keys, ft
 int ftz_verify_token_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state_fn get_state, void* user,
                               int32_t* codes, int32_t* failed_action);
 /* The same with the batched ledger lookup (recommended for block-level
- * binding: one callback per chunk of up to 8192 requests). */
+ * binding: one callback per pipeline chunk of up to 4096 requests). */
 int ftz_verify_token_requests_batched(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_states_fn get_states,
                                       void* user, int32_t* codes, int32_t* failed_action);
 /* profiling: the calling thread's time in each stage of the request pipeline,

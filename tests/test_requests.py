@@ -141,7 +141,7 @@ def test_gpu_requests_native_ledger_tiled(gctx, fx, batched):
     """ftz_verify_token_requests(_batched) with a native ledger callback over the
     fixture tiled past several 8192-request pipeline chunks: every verdict and
     failing index at its position, and every key looked up on the calling
-    thread (one callback per chunk when batched)"""
+    thread (one callback per 4096-request chunk when batched)"""
     import zkatdlog
     rq = fx["requests"] * (20000 // len(fx["requests"]) + 1)
     led = zkatdlog.NativeLedger(fx["ledger_b"])
@@ -152,7 +152,7 @@ def test_gpu_requests_native_ledger_tiled(gctx, fx, batched):
         led.close()
     assert list(zip(codes, failed)) == [(r["expect"], r["failed_action"]) for r in rq]
     if batched:
-        assert calls <= (len(rq) + 8191) // 8192
+        assert calls <= (len(rq) + 4095) // 4096
     else:
         assert calls == keys
 
