@@ -627,12 +627,15 @@ def requests_leg(ctx, valid, n_req=100000, per=2):
     t_build = time.perf_counter() - t0
     i32 = ctypes.POINTER(ctypes.c_int32)
     out = {"requests": n_req, "transfers": n_req * per, "request_bytes": rs.nbytes(), "setup_s": round(t_build, 1)}
+    codes = np.zeros(n_req, dtype=np.int32)
+    failed = np.zeros(n_req, dtype=np.int32)
+    # warm-up over the whole set (untimed): the request threads' per-thread parse
+    # buffers, the engine slots, and the first touch of the request bytes
+    ctx.verify_token_requests_packed(rs.ptr(), n_req, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
+                                     batched=True)
     for batched in (True, False):
-        codes = np.zeros(n_req, dtype=np.int32)
-        failed = np.zeros(n_req, dtype=np.int32)
-        w = min(n_req, 8192)  # warm-up: the request threads, check buffers, engine slots
-        ctx.verify_token_requests_packed(rs.ptr(), w, led, codes.ctypes.data_as(i32), failed.ctypes.data_as(i32),
-                                         batched=batched)
+        codes[:] = 0
+        failed[:] = 0
         c0 = led.counts()
         ctx.request_stats(reset=True)
         est0 = ctx.engine_stats(reset=True)
@@ -731,6 +734,7 @@ def main():
     ap.add_argument("--serial", action="store_true",
                     help="profiling: every kernel on one stream for the whole run (ftz_ctx_set_serial), so that a "
                          "rocprofv3 kernel trace gives per-kernel durations without overlap")
+    ap.add_argument("--opt", default="", help="A/B: extra ftz_options fields, e.g. 'pass_shaping=0,small_pass=0'")
     ap.add_argument("--layout", default=os.environ.get("FTZ_LAYOUT", ""),
                     help="kernel layouts, e.g. 'g2lines=sextet,pairing=one_lane' (ftz_ctx_set_layout)")
     args = ap.parse_args()
@@ -752,7 +756,9 @@ def main():
     from zkatdlog.dist import bitmap_of, verify_shard
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
-    ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads)
+    extra_opt = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, args.opt.split(",")))}
+    ctx = zkatdlog.Context(pp_json, device=local, batch=args.device_batch, slots=args.slots, threads=args.threads,
+                           **extra_opt)
     db = ctx.options["batch"]  # proofs per device pass: the engine cuts the job into passes of db
     if args.serial:
         ctx.set_serial(True)

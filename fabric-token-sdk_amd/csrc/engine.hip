@@ -190,21 +190,34 @@ void Engine::dispatcher() {
     free_slots.pop_front();
     b->parts.clear();
     b->items.clear();
-    // a pass closes at B items, BATCH_PROOF_BYTES of proofs, or B * 4 pairing
-    // jobs -- a PP-A pass of B 2-output transfers (e = 2): wider range proofs
+    // Pass size Bp: B, except (a) the first pass onto an idle device takes B/4,
+    // so that the device starts after a quarter of the planning, and (b) once
+    // fewer than slots x B items are pending, passes of pending / slots (>= B/4),
+    // so that the last passes of a job run side by side instead of one long pass
+    // alone at the end (fill and drain of a 10-pass job were ~10 % of its time).
+    // A pass closes at Bp items, BATCH_PROOF_BYTES of proofs, or Bp * 4 pairing
+    // jobs -- a PP-A pass of Bp 2-output transfers (e = 2): wider range proofs
     // (PP-B: e = 16, 8x the pairings per transfer) get proportionally fewer
     // proofs per pass, so their passes cost what a PP-A pass costs
+    const size_t slots_n = ctx->opt.slots ? ctx->opt.slots : 1, Bmin = std::max<size_t>(1, B / 4);
+    size_t Bp = B;
+    if (ctx->opt.pass_shaping) {
+      if (inflight.empty() && pending > Bmin)
+        Bp = Bmin;
+      else if (pending < slots_n * B)
+        Bp = std::min(B, std::max(Bmin, (pending + slots_n - 1) / slots_n));
+    }
     size_t bytes = 0;
     uint64_t pairs = 0;
-    const uint64_t pair_budget = 4 * (uint64_t)B, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);
+    const uint64_t pair_budget = 4 * (uint64_t)Bp, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);
     auto room = [&]() {
       return b->items.empty() || (bytes < BATCH_PROOF_BYTES && pairs < pair_budget);
     };
-    while (!q.empty() && b->items.size() < B && room()) {
+    while (!q.empty() && b->items.size() < Bp && room()) {
       Request* r = q.front();
       if (r->solo && !b->items.empty()) break;  // a solo request never shares a batch
       size_t start = r->next;
-      while (r->next < r->n && b->items.size() < B && room()) {
+      while (r->next < r->n && b->items.size() < Bp && room()) {
         bytes += item_bytes(r, r->next);
         pairs += item_pairs(r, r->next, ex);
         b->items.push_back(item_of(r, r->next));
