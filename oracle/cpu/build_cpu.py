@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 LIB = os.path.join(HERE, "libftscpu.so")
 PKG = os.path.join(ROOT, "fabric-token-sdk_amd", "csrc")
 SRCS = [os.path.join(ROOT, "tests", "native", f) for f in ("emu.cpp", "emu_exec.cpp", "msm_emu.cpp", "sx_emu.cpp")] + \
+       [os.path.join(HERE, "msm_pippenger.cpp")] + \
        [os.path.join(PKG, "host", f) for f in ("planner.cpp", "planner_prove.cpp", "gojson.cpp", "request.cpp")]
 
 

@@ -279,3 +279,26 @@ def test_gpu_msm_point_split_2_20(ctx):
             m.close()
     got = ctx.g1_sum(b"".join(parts))
     assert got == C.g1_bytes(C.g1_mul(C.G1_GEN, _known_log_sum(kb, n, off)))
+
+
+@pytest.mark.parametrize("n,c,threads", [(1, 0, 1), (6, 3, 2), (40, 5, 3), (300, 0, 4), (2000, 0, 8)])
+def test_cpu_pippenger_baseline(n, c, threads):
+    """oracle/cpu msm_pippenger.cpp (the bench's CPU MSM baseline: XYZZ buckets,
+    signed windows over GLV halves, tasks of window x point slice) against the
+    oracle's sum, with repeated / cancelling points and zero / -1 scalars"""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle", "cpu"))
+    import build_cpu
+    lib = ctypes.CDLL(build_cpu.build())
+    lib.cpu_msm_pippenger.argtypes = [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                      ctypes.c_uint32, ctypes.c_char_p]
+    pts, ks = rnd_case(n, 100 + n)
+    ks = [k % C.R for k in ks]
+    pb, kb = pack(pts, ks)
+    out = ctypes.create_string_buffer(64)
+    assert lib.cpu_msm_pippenger(n, pb, kb, threads, c, out) == 0
+    want = None
+    for p, k in zip(pts, ks):
+        want = C.g1_add(want, C.g1_mul(p, k))
+    assert out.raw == C.g1_bytes(want)
