@@ -190,23 +190,14 @@ void Engine::dispatcher() {
     free_slots.pop_front();
     b->parts.clear();
     b->items.clear();
-    // Pass size Bp: B, except (a) the first pass onto an idle device takes B/4,
-    // so that the device starts after a quarter of the planning, and (b) once
-    // fewer than slots x B items are pending, passes of pending / slots (>= B/4),
-    // so that the last passes of a job run side by side instead of one long pass
-    // alone at the end (fill and drain of a 10-pass job were ~10 % of its time).
-    // A pass closes at Bp items, BATCH_PROOF_BYTES of proofs, or Bp * 4 pairing
-    // jobs -- a PP-A pass of Bp 2-output transfers (e = 2): wider range proofs
+    // A pass closes at B items, BATCH_PROOF_BYTES of proofs, or B * 4 pairing
+    // jobs -- a PP-A pass of B 2-output transfers (e = 2): wider range proofs
     // (PP-B: e = 16, 8x the pairings per transfer) get proportionally fewer
-    // proofs per pass, so their passes cost what a PP-A pass costs
-    const size_t slots_n = ctx->opt.slots ? ctx->opt.slots : 1, Bmin = std::max<size_t>(1, B / 4);
-    size_t Bp = B;
-    if (ctx->opt.pass_shaping) {
-      if (inflight.empty() && pending > Bmin)
-        Bp = Bmin;
-      else if (pending < slots_n * B)
-        Bp = std::min(B, std::max(Bmin, (pending + slots_n - 1) / slots_n));
-    }
+    // proofs per pass, so their passes cost what a PP-A pass costs.  (Smaller
+    // first / tail passes to shorten a job's fill and drain were measured:
+    // 420-442k vs 676-688k transfers/s on a 20-step job -- a pass's planning and
+    // kernel chain have a fixed latency that smaller passes do not shed.)
+    const size_t Bp = B;
     size_t bytes = 0;
     uint64_t pairs = 0;
     const uint64_t pair_budget = 4 * (uint64_t)Bp, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);

@@ -126,10 +126,6 @@ typedef struct {
                            that allocation fails the context proves on the
                            variable-base path instead (same bytes, slower) and does not
                            retry.  0: never build them (variable-base path).            */
-  uint32_t pass_shaping;  /* 1 (default): the engine's first pass onto an idle device takes
-                           batch / 4 items and, once fewer than slots x batch items are
-                           pending, passes take pending / slots (>= batch / 4), so a
-                           job's pipeline fills and drains faster; 0: passes of batch. */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
