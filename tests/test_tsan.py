@@ -42,8 +42,19 @@ def test_host_code_is_race_free_under_tsan(golden, tmp_path):
         o, s = bytes.fromhex(c["owner"]), bytes.fromhex(c["sig"])
         own += struct.pack("<2I", len(o), len(s)) + o + s
     (tmp_path / "own.bin").write_bytes(bytes(own))
+    # the pipelined raw-request path (host/request.cpp) with its ledger
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "token_requests.json")))
+    rq = bytearray()
+    for k, v in fx["ledger"].items():
+        kb, vb = k.encode(), base64.b64decode(v)
+        rq += struct.pack("<3I", 1, len(kb), len(vb)) + kb + vb
+    for r_ in fx["requests"] * 2:
+        raw = base64.b64decode(r_["raw"])
+        rq += struct.pack("<3I", 0, 0, len(raw)) + raw
+    (tmp_path / "req.bin").write_bytes(bytes(rq))
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
-    r = subprocess.run([str(exe), str(tmp_path / "pp.json"), str(tmp_path / "tx.bin"), str(tmp_path / "own.bin")],
+    r = subprocess.run([str(exe), str(tmp_path / "pp.json"), str(tmp_path / "tx.bin"), str(tmp_path / "own.bin"),
+                        str(tmp_path / "req.bin")],
                        capture_output=True, text=True, env=env, timeout=600)
     assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-2000:])
