@@ -1,0 +1,88 @@
+"""The Go binding under go/gpu (the cgo shim a maintainer drops into
+token/core/zkatdlog/crypto/validator/gpu) stays in step with
+the C ABI: there is no Go toolchain in this image, so this checks statically
+that every C function, constant, struct and struct field the Go and C files
+name is declared in include/ftsamd.h, that the exported callbacks match the
+ABI's callback shapes, and that the registration patch names the shim's API."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GO = os.path.join(ROOT, "go", "gpu")
+HDR = open(os.path.join(ROOT, "include", "ftsamd.h")).read()
+
+
+def _go_sources():
+    return {f: open(os.path.join(GO, f)).read() for f in sorted(os.listdir(GO)) if f.endswith((".go", ".c"))}
+
+
+def _structs():
+    out = {}
+    for body, name in re.findall(r"typedef struct \{(.*?)\}\s*(\w+);", HDR, re.S):
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        out[name] = set(re.findall(r"(\w+)\s*(?:\[[^\]]*\])?;", body))
+    return out
+
+
+def test_every_c_name_is_declared():
+    srcs = _go_sources()
+    assert {"ftz.go", "prover.go", "owner.go", "block.go", "callbacks.c", "gpu_test.go"} <= set(srcs)
+    funcs = set(re.findall(r"\b(ftz_\w+)\s*\(", HDR))
+    consts = set(re.findall(r"#define\s+(FTZ_\w+)", HDR))
+    types = set(_structs()) | {"ftz_ctx", "ftz_idemix", "ftz_prover", "ftz_batch", "ftz_msm",
+                               "ftz_get_state_fn", "ftz_get_states_fn"}
+    shim_fns = {"ftz_go_get_state_fn", "ftz_go_get_states_fn"}
+    seen = set()
+    for f, s in srcs.items():
+        if f.endswith("_test.go"):
+            assert 'import "C"' not in s  # cgo is not allowed in test files
+            continue
+        for name in re.findall(r"\bC\.(\w+)", s):
+            seen.add(name)
+            if name.startswith("FTZ_"):
+                assert name in consts, (f, name)
+            elif name.startswith("ftz_"):
+                assert name in funcs or name in types or name in shim_fns, (f, name)
+    # the shim covers the verifier, prover, idemix and request entry points
+    for fn in ("ftz_ctx_create_ex", "ftz_verify_transfers", "ftz_verify_issues", "ftz_prover_load_transfers",
+               "ftz_prover_load_issues", "ftz_prover_proofs", "ftz_idemix_create", "ftz_verify_owner_signatures",
+               "ftz_audit_owners", "ftz_verify_token_requests", "ftz_verify_token_requests_batched"):
+        assert fn in seen, fn
+
+
+def test_struct_literal_fields_exist():
+    structs = _structs()
+    n = 0
+    for f, s in _go_sources().items():
+        for name, body in re.findall(r"C\.(ftz_\w+)\{([^{}]*)\}", s):
+            for key in re.findall(r"(\w+):", body):
+                key = key[1:] if key == "_type" else key  # cgo renames the Go keyword
+                assert key in structs[name], (f, name, key)
+                n += 1
+        for key in re.findall(r"\bopt\.(\w+)\s*=", s):
+            assert key in structs["ftz_options"], (f, key)
+            n += 1
+    assert n >= 30
+
+
+def test_callbacks_match_the_abi():
+    c = _go_sources()["callbacks.c"]
+    assert "static int get_state_tramp(void* u, const char* k, size_t kl, const uint8_t** v, size_t* vl)" in c
+    assert "static int get_states_tramp(void* u, size_t n, const ftz_bytes* keys, ftz_bytes* vals)" in c
+    assert "typedef int (*ftz_get_state_fn)(void* user, const char* key, size_t key_len, const uint8_t** val, " \
+           "size_t* val_len);" in HDR
+    assert "typedef int (*ftz_get_states_fn)(void* user, size_t n, const ftz_bytes* keys, ftz_bytes* vals);" in HDR
+    b = _go_sources()["block.go"]
+    assert "//export goGetState\n" in b and "//export goGetStates\n" in b
+    # a file with //export may only declare in its preamble
+    pre = b.split('import "C"')[0]
+    assert "{" not in pre.replace("/*", "").split("*/")[0]
+
+
+def test_registration_patch_uses_the_shim_api():
+    p = open(os.path.join(ROOT, "go", "patches", "0001-zkatdlog-gpu-validator.patch")).read()
+    srcs = "".join(_go_sources().values())
+    for sym in ("DeviceFromEnv", "NewVerifier", "NewOwnerVerifier", "VerifyIssue", "TransferSignatureValidate",
+                "TransferZKProofValidate"):
+        assert sym in p
+        assert re.search(r"func (\([^)]*\) )?%s\(" % sym, srcs), sym
