@@ -211,21 +211,6 @@ FTS_HDN Jac<F> aff_mul_u64(const Aff<F>& p, uint64_t k) {
   return acc;
 }
 
-// k V for a Jacobian V and a small scalar k >= 1 (left-to-right binary from
-// the top bit: k = 16 is four doublings)
-template <class F>
-FTS_HDN Jac<F> jac_mul_u64(const Jac<F>& v, uint64_t k) {
-  Jac<F> acc = v;
-  int top = 63;
-  while (top > 0 && !((k >> top) & 1)) top--;
-#pragma nounroll
-  for (int i = top - 1; i >= 0; i--) {
-    acc = jac_dbl(acc);
-    if ((k >> i) & 1) acc = jac_add(acc, v);
-  }
-  return k ? acc : jac_inf<F>();
-}
-
 // curve membership of an affine point (Montgomery coordinates)
 FTS_HD bool g1_on_curve(const g1a& a) {
   if (a.inf) return true;

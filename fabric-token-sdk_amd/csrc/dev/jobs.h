@@ -797,10 +797,19 @@ FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* 
     if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
       Va = g1_load(pts[v0.pt]);
     } else if (v0.flags & VT_HORNER) {
+      // sum_t b^(count-1-t) P_t in Horner order, b = the first term's weight;
+      // the multiple b V by an inline double-and-add from b's top bit (a call
+      // of its own here cost k_g1_part 31 VGPRs and a wave per SIMD)
       const uint64_t b = ((uint64_t)v0.w_hi << 32) | v0.w_lo;
+      const int top = 63 - __builtin_clzll(b);
       g1j V = jac_from_aff(g1_load(pts[v0.pt]));
       for (uint32_t t = 1; t < j.vcount; t++) {
-        V = jac_mul_u64(V, b);
+        const g1j V1 = V;
+#pragma nounroll
+        for (int q = top - 1; q >= 0; q--) {
+          V = jac_dbl(V);
+          if ((b >> q) & 1) V = jac_add(V, V1);
+        }
         V = jac_add_aff(V, g1_load(pts[vterms[j.vstart + t].pt]));
       }
       Va = jac_to_aff(V);
