@@ -23,10 +23,13 @@ verdict-bitmap all-gather over RCCL (configs[3]).  Prints ONE JSON line.
 import os as _os
 
 # Hardware queues per process: the engine keeps 4 batches in flight on 3 streams
-# each; HIP's default of 4 queues would serialise them (set before the HIP
-# runtime initialises; <= 32).
-if int(_os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# each (9 high- and 4 low-priority streams per context); HIP's default of 4
+# queues would serialise them (set before the HIP runtime initialises).  12, not
+# more: HIP caps each priority level at this many queues, and with 16 two live
+# contexts (the PP-B leg's beside the headline's) mapped more queues than the
+# hardware scheduler holds at once -- it then time-slices them and a kernel
+# stalls ~10.7 ms every few passes (profiles/r04/hwqueue_stalls.txt).
+_os.environ["GPU_MAX_HW_QUEUES"] = "12"
 import argparse
 import ctypes
 import json

@@ -6,8 +6,8 @@ import os
 import sys
 import time
 
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+if True:  # as bench.py: 12 (16 oversubscribes the hardware scheduler with two contexts)
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
 import json  # noqa: E402
