@@ -6,9 +6,13 @@
 //
 // Pipeline (k_msm.hip; every stage one lane per item):
 //   keys      k_i -> W signed digits d in [-2^(c-1), 2^(c-1)]; sort key = the
-//             global bucket w B + |d| - 1, value = virtual point | sign
-//   sort      stable LSD radix sort of the (key, value) pairs (rocPRIM)
-//   bounds    bucket ranges [start, end) read off the sorted keys
+//             bucket |d| - 1 within the window (c - 1 bits), value = the
+//             entry index t = w nv + v | sign (| ZERO for a zero digit)
+//   sort      stable LSD radix sort of the (key, value) pairs (rocPRIM); the
+//             entries are generated window-major, so stability keeps each
+//             bucket's entries grouped by window
+//   bounds    (window, bucket) ranges [start, end) read off the sorted keys and
+//             the windows of the sorted values
 //   slots     bucket b gets m_b = max(1, ceil(count_b / T)) slots of at most T
 //             points (scan of m_b -> slot offsets, slot -> bucket owner map), so
 //             that heavy buckets (the top window's few buckets, skewed scalars)
@@ -47,7 +51,8 @@ struct MsmPlan {
   uint32_t pre;        // 1: resident-point mode (points 2^(c w) P_v precomputed, one bucket set)
   uint32_t rw;         // reduction windows: W, or 1 with pre
   uint32_t per;        // sort entries per reduction window: nv, or W nv with pre
-  uint32_t pts;        // resident points: nv, or W nv + 1 with pre (last = the identity)
+  uint32_t pts;        // resident points: nv + 1, or W nv + 1 with pre (last = the identity)
+  uint64_t nv_magic;   // floor(2^32 / nv) + 1: the window of an entry t without a division
 };
 
 // window bits for n (virtual) points: floor(log2 n / 2) + 7 clamped to [8, 20]
@@ -91,7 +96,8 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   p.pre = pre ? 1 : 0;
   p.rw = pre ? 1 : p.windows;
   p.per = pre ? p.windows * p.nv : p.nv;
-  p.pts = pre ? p.windows * p.nv + 1 : p.nv;
+  p.pts = pre ? p.windows * p.nv + 1 : p.nv + 1;
+  p.nv_magic = (1ull << 32) / p.nv + 1;
   // the default cap keeps the per-window mean (about as many bucket lanes per
   // point as without pre)
   if (!slot_cap) {
@@ -101,7 +107,13 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   if (slot_cap > 1023) slot_cap = 1023;  // length bins of the slot ordering (k_msm.hip)
   p.slot_cap = slot_cap;
   p.max_slots = p.buckets + (uint32_t)((p.per + slot_cap - 1) / slot_cap);
-  if (!seg_len && pre) seg_len = 16;  // measured at 2^20 (2.71 ms against 2.81 with 4)
+  if (!seg_len && pre) {
+    // 16 measured at 2^20 (2.71 ms against 2.81 with 4 and 2.85 with 32); at
+    // 2^24 (3.1M slots) 64: 26.0 ms against 26.7 with 16 -- longer runs once
+    // the segments would exceed 64k lanes
+    seg_len = 16;
+    while (seg_len < 64 && p.max_slots / seg_len > 65536) seg_len *= 2;
+  }
   if (!seg_len) {
     uint64_t tot = (uint64_t)p.rw * p.max_slots;
     seg_len = 4;
@@ -126,35 +138,32 @@ FTS_HD int32_t msm_digit(const uint32_t k[8], uint32_t c, uint32_t w, uint32_t& 
   return (int32_t)raw;
 }
 
-// Sort keys of point i (both GLV halves): for window w and virtual point vi the
-// entry t = w nv + vi gets key[t] = w B + |d| - 1 (= the global bucket index g)
-// and val[t] = vi | sign << 31, or key[t] = MSM_KEY_NONE for a zero digit.  A
-// stable radix sort of (key, val) over msm_key_bits(p) bits then lists every
-// bucket's points contiguously (zero digits last) and msm_job_bounds reads the
-// bucket ranges off the sorted keys: no atomics, coalesced writes.
-static constexpr uint32_t MSM_KEY_NONE = 0xFFFFFFFFu;
+// Sort keys of point i (both GLV halves): window w's entry t = w nv + vi gets
+// key[t] = |d| - 1, the bucket within the window, and val[t] = t | sign << 31.
+// A zero digit goes to bucket 0 with the identity: val = t | MSM_ZERO (the
+// bucket pass loads the identity point for it and skips it; pre: the value is
+// the index of the identity point).  Keys are c - 1 bits -- one radix pass
+// fewer than keys w B + b with a sort-last bit for zero digits (2^20: 16
+// bits, two passes instead of three) -- and the stable sort keeps each
+// bucket's entries in window order, so msm_job_bounds reads the (window,
+// bucket) ranges off (key, window of the value): no atomics, coalesced writes.
+// Non-pre values hold t in 30 bits: W nv < 2^30 (msm_rt.hip checks it).
+static constexpr uint32_t MSM_ZERO = 0x40000000u;
+static constexpr uint32_t MSM_T_MASK = 0x3FFFFFFFu;
 
-// key bits the sort must look at: g < W B plus one bit so that NONE sorts last
-// (pre: g < B and no NONE keys)
-FTS_HD uint32_t msm_key_bits(const MsmPlan& p) {
-  uint64_t top = (uint64_t)p.rw * p.buckets;
-  uint32_t b = 0;
-  while ((1ull << b) < top) b++;
-  return p.pre ? (b ? b : 1) : b + 1;
-}
+// key bits the sort must look at: the bucket within a window (c - 1 bits)
+FTS_HD uint32_t msm_key_bits(const MsmPlan& p) { return p.c > 1 ? p.c - 1 : 1; }
 
 FTS_HD void msm_put_key(const MsmPlan& p, uint32_t w, uint32_t vi, int32_t d, bool neg, uint32_t* key,
                         uint32_t* val) {
   size_t t = (size_t)w * p.nv + vi;
   if (d == 0) {
-    // pre: bucket 0 with the identity (the last resident point)
-    key[t] = p.pre ? 0u : MSM_KEY_NONE;
-    val[t] = p.pre ? p.pts - 1 : 0u;
+    key[t] = 0;
+    val[t] = p.pre ? p.pts - 1 : (uint32_t)t | MSM_ZERO;
     return;
   }
-  uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1;
-  key[t] = p.pre ? b : w * p.buckets + b;
-  val[t] = (p.pre ? (uint32_t)t : vi) | (((d < 0) != neg) ? 0x80000000u : 0u);
+  key[t] = (uint32_t)(d < 0 ? -d : d) - 1;
+  val[t] = (uint32_t)t | (((d < 0) != neg) ? 0x80000000u : 0u);
 }
 
 FTS_HD void msm_job_keys(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val) {
@@ -174,13 +183,35 @@ FTS_HD void msm_job_keys(const MsmPlan& p, uint32_t i, const uint32_t (*scal)[8]
   }
 }
 
-// sorted entry t: a bucket's first entry records start[g] = t, its last one
-// end[g] = t + 1 (start/end zeroed beforehand, so an empty bucket reads 0, 0)
-FTS_HD void msm_job_bounds(uint64_t t, uint64_t total, const uint32_t* skey, uint32_t* start, uint32_t* end) {
-  uint32_t k = skey[t];
-  if (k == MSM_KEY_NONE) return;
-  if (t == 0 || skey[t - 1] != k) start[k] = (uint32_t)t;
-  if (t + 1 == total || skey[t + 1] != k) end[k] = (uint32_t)(t + 1);
+// the window of entry index x = w nv + v (x < 2^30): x nv_magic / 2^32 is
+// floor(x / nv) or one more (x / 2^32 < 1/4 of slack), one compare fixes it
+FTS_HD uint32_t msm_window_of(const MsmPlan& p, uint32_t x) {
+  uint32_t w = (uint32_t)(((uint64_t)x * p.nv_magic) >> 32);
+  return (uint64_t)w * p.nv > x ? w - 1 : w;
+}
+
+// global bucket of sorted entry t: w B + key (pre: one bucket set, g = key)
+FTS_HD uint32_t msm_entry_bucket(const MsmPlan& p, uint64_t t, const uint32_t* skey, const uint32_t* sval) {
+  if (p.pre) return skey[t];
+  return msm_window_of(p, sval[t] & MSM_T_MASK) * p.buckets + skey[t];
+}
+
+// sorted entry t and its successor: where the (window, bucket) changes, the
+// one ends (end[g] = t + 1) and the next starts (start[g'] = t + 1); start /
+// end zeroed beforehand, so an empty bucket reads 0, 0
+FTS_HD void msm_job_bounds(const MsmPlan& p, uint64_t t, uint64_t total, const uint32_t* skey, const uint32_t* sval,
+                           uint32_t* start, uint32_t* end) {
+  uint32_t g = msm_entry_bucket(p, t, skey, sval);
+  if (t == 0) start[g] = 0;
+  if (t + 1 == total) {
+    end[g] = (uint32_t)total;
+    return;
+  }
+  uint32_t g1 = msm_entry_bucket(p, t + 1, skey, sval);
+  if (g1 != g) {
+    end[g] = (uint32_t)(t + 1);
+    start[g1] = (uint32_t)(t + 1);
+  }
 }
 
 // virtual point v of the resident array: P_v for v < n, phi(P_(v-n)) =
@@ -248,8 +279,14 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
   const uint32_t* e = perm + start[g];
   g1j acc = jac_inf<fp>();
   if (lo >= hi) return acc;
+  // entry -> resident point: pre values are point indices; otherwise t - w nv,
+  // and a zero digit loads the identity (the last point)
+  const uint32_t base = p.pre ? 0u : (g / p.buckets) * p.nv, ident = p.pts - 1;
+  auto point_of = [&](uint32_t v) -> uint32_t {
+    return p.pre ? (v & 0x7FFFFFFFu) : ((v & MSM_ZERO) ? ident : (v & MSM_T_MASK) - base);
+  };
   uint32_t v = e[lo];
-  G1Dev nxt = pts[v & 0x7FFFFFFFu];
+  G1Dev nxt = pts[point_of(v)];
 #if FTS_G1_F29
   // the additions in the carry-free XYZZ form (dev/fp29.h), one conversion per slot
   x29 a{};
@@ -261,7 +298,7 @@ FTS_HD g1j msm_job_slot(const MsmPlan& p, uint32_t j, const uint32_t* owner, con
     uint32_t sign = v >> 31;
     if (q + 1 < hi) {
       v = e[q + 1];
-      nxt = pts[v & 0x7FFFFFFFu];
+      nxt = pts[point_of(v)];
     }
     g1a P = g1_load(cur);
 #if FTS_G1_F29

@@ -52,11 +52,11 @@ __global__ void __launch_bounds__(256) k_msm_keys(MsmPlan p, const uint32_t (*sc
 }
 
 // one lane per sorted entry: bucket ranges
-__global__ void __launch_bounds__(256) k_msm_bounds(uint64_t total, const uint32_t* skey, uint32_t* start,
-                                                    uint32_t* end) {
+__global__ void __launch_bounds__(256) k_msm_bounds(MsmPlan p, uint64_t total, const uint32_t* skey,
+                                                    const uint32_t* sval, uint32_t* start, uint32_t* end) {
   uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
-  msm_job_bounds(t, total, skey, start, end);
+  msm_job_bounds(p, t, total, skey, sval, start, end);
 }
 
 // count[g] = end[g] - start[g] and the bucket's slot count

@@ -24,14 +24,26 @@ struct ftz_msm {
   hipEvent_t ev[2];
   bool ev_init = false;
   float last_ms = 0;
+  uint32_t radix_bits = 8;  // digit bits per radix-sort pass (8: rocPRIM's gfx950 default; 9: Radix9)
 };
 
 static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
 
 // The (key, value) sort uses rocPRIM's gfx950 onesweep default (8 key bits per
-// pass, three passes for 17..24-bit keys).  An 11-bit config (2048 digit bins,
-// 256-thread blocks, match ranking, two passes) measured slower: 2^20 3.29 ->
-// 4.33 ms, 2^24 29.0 -> 44.6 ms.
+// pass) or, where 9-bit digits save a pass (17- and 18-bit keys: 2^24 points at
+// c = 19), the same kernel shape with 512 digit bins.  An 11-bit config (2048
+// digit bins, 256-thread blocks, match ranking) measured slower in round 3:
+// 2^20 3.29 -> 4.33 ms, 2^24 29.0 -> 44.6 ms.
+using Radix9 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 12>, rocprim::kernel_config<1024, 12>, 9,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+static hipError_t msm_sort(ftz_msm* m, void* tmp, size_t& tb, size_t wn, hipStream_t s) {
+  if (m->radix_bits == 9)
+    return rocprim::radix_sort_pairs<Radix9>(tmp, tb, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s);
+  return rocprim::radix_sort_pairs(tmp, tb, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s);
+}
 
 static int msm_alloc(ftz_msm* m, size_t n) {
   const MsmPlan& p = m->p;
@@ -46,8 +58,10 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->start.alloc(wb));
   HC(m->end.alloc(wb));
   m->key_bits = msm_key_bits(p);
-  HC(rocprim::radix_sort_pairs(nullptr, m->sort_tmp_bytes, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0,
-                               m->key_bits, m->ctx->stream));
+  // 9-bit digits where they save a pass (17-18 bits: two passes instead of three)
+  const uint32_t rb = m->ctx->opt.msm_radix_bits;
+  m->radix_bits = rb ? rb : (m->key_bits > 16 && m->key_bits <= 18 ? 9u : 8u);
+  HC(msm_sort(m, nullptr, m->sort_tmp_bytes, wn, m->ctx->stream));
   HC(m->sort_tmp.alloc(m->sort_tmp_bytes ? m->sort_tmp_bytes : 1));
   HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
   HC(m->nsl.alloc(wb));
@@ -93,10 +107,14 @@ static int msm_new(ftz_ctx* c, size_t n, ftz_msm** out) {
   // segment; 0 = the planner's choice) and the GLV switch
   const ftz_options& o = c->opt;
   m->p = msm_make_plan(n, o.msm_window_bits, o.msm_slot_cap, o.msm_seg_slots, o.msm_glv != 0, o.msm_precompute != 0);
-  // sort values carry a point index in 31 bits
+  // sort values carry a point index in 31 bits (pre) or an entry index in 30
   if (m->p.pre && (uint64_t)m->p.windows * m->p.nv + 1 >= (1ull << 31)) {
     delete m;
     return set_err(FTZ_E_INVALID, "msm_precompute: windows x points exceeds 2^31 resident points");
+  }
+  if (!m->p.pre && (uint64_t)m->p.windows * m->p.nv >= (1ull << 30)) {
+    delete m;
+    return set_err(FTZ_E_INVALID, "MSM too large: windows x points exceeds 2^30 sort entries");
   }
   int rc = msm_alloc(m, n);
   if (rc != FTZ_SUCCESS) {
@@ -113,10 +131,8 @@ static int prepare_points(ftz_msm* m) {
   hipStream_t s = m->ctx->stream;
   const MsmPlan& p = m->p;
   if (p.glv) k_msm_phi<<<blocks(p.n, 256), 256, 0, s>>>(p, m->pts.p);
-  if (p.pre) {
-    k_msm_precompute<<<blocks(p.nv, 256), 256, 0, s>>>(p, m->pts.p);
-    HC(hipMemsetAsync(m->pts.p + (p.pts - 1), 0, sizeof(G1Dev), s));
-  }
+  if (p.pre) k_msm_precompute<<<blocks(p.nv, 256), 256, 0, s>>>(p, m->pts.p);
+  HC(hipMemsetAsync(m->pts.p + (p.pts - 1), 0, sizeof(G1Dev), s));  // the identity: zero digits
   HC(hipGetLastError());
   return FTZ_SUCCESS;
 }
@@ -225,10 +241,10 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   // (window, bucket)-sorted point lists: keys, stable radix sort, bucket ranges
   k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
   size_t tb = m->sort_tmp_bytes;
-  HC(rocprim::radix_sort_pairs(m->sort_tmp.p, tb, m->key.p, m->skey.p, m->val.p, m->perm.p, wn, 0, m->key_bits, s));
+  HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
   HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
   HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
-  k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>((uint64_t)wn, m->skey.p, m->start.p, m->end.p);
+  k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start.p, m->end.p);
   k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start.p, m->end.p, m->count.p, m->nsl.p);
   int rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;

@@ -126,6 +126,8 @@ typedef struct {
                            that allocation fails the context proves on the
                            variable-base path instead (same bytes, slower) and does not
                            retry.  0: never build them (variable-base path).            */
+  uint32_t msm_radix_bits; /* MSM sort digit bits per radix pass: 0 = the planner's choice
+                           (9 where it saves a pass, else 8), or 8 / 9                   */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);

@@ -45,7 +45,7 @@ extern "C" int emu_msm_ex(size_t n, const uint8_t* points, const uint8_t* scalar
   for (size_t t = 0; t < wn; t++) idx[t] = (uint32_t)t;
   std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return (key[a] & kmask) < (key[b] & kmask); });
   for (size_t t = 0; t < wn; t++) skey[t] = key[idx[t]], perm[t] = val[idx[t]];
-  for (uint64_t t = 0; t < wn; t++) msm_job_bounds(t, wn, skey.data(), start.data(), end.data());
+  for (uint64_t t = 0; t < wn; t++) msm_job_bounds(p, t, wn, skey.data(), perm.data(), start.data(), end.data());
   for (size_t g = 0; g < wb; g++) count[g] = end[g] - start[g];
   std::vector<uint32_t> soff(wb), owner((size_t)p.rw * p.max_slots, 0xFFFFFFFFu), wlo(p.rw), whi(p.rw);
   uint32_t run = 0;
