@@ -188,6 +188,37 @@ def test_gpu_msm_known_logs(ctx, lg, bits):
     assert info["window_bits"] == (lg + 1) // 2 + 7 and info["last_ms"] > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,radix", [(19, 0), (19, 8), (17, 9), (12, 9)])
+def test_gpu_msm_radix_digits(golden, c, radix):
+    """The sort's digit width (ftz_options.msm_radix_bits: 0 = the planner's
+    9 bits for 17-18-bit keys, else 8) changes only the number of passes: with
+    bucket-within-window keys and a stable sort every setting gives the known
+    discrete log, zero digits included (scalars with zero windows)."""
+    import zkatdlog
+    n, off = 1 << 18, 4242
+    rng = random.Random(c * 10 + radix)
+    ks = [rng.randrange(1 << 256) % C.R for _ in range(n)]
+    ks[:64] = [0, 1, C.R - 1] + [(1 << (19 * w)) for w in range(7)] + [rng.randrange(1 << 40) for _ in range(54)]
+    kb = b"".join(k.to_bytes(32, "big") for k in ks)
+    with zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_window_bits=c, msm_radix_bits=radix) as cx:
+        m = zkatdlog.Msm(cx, scalars=kb, gen_offset=off)
+        try:
+            got = m.run()
+            assert m.info()["window_bits"] == c
+        finally:
+            m.close()
+    want = C.g1_mul(C.G1_GEN, sum(k * (i + off) for i, k in enumerate(ks)) % C.R)
+    assert got == C.g1_bytes(want)
+
+
+@pytest.mark.gpu
+def test_gpu_msm_radix_bits_rejected(golden):
+    import zkatdlog
+    with pytest.raises(zkatdlog.DeviceError, match="msm_radix_bits"):
+        zkatdlog.Context(golden["pp_a"]["pp"].encode(), device=0, msm_radix_bits=7)
+
+
 def _known_log_sum(kb, n, off):
     """sum_i k_i (i + off) mod r for n big-endian 32-byte scalars, in 16-bit
     chunks with numpy (each chunk's dot product with i fits in uint64 for
