@@ -363,20 +363,34 @@ __device__ __forceinline__ void coop29_add(f29& X, f29& Y, f29& Z, bool& inf, co
 
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
 // on one wave with the 4-lane cooperative carry-free point ops, the Jacobian
-// result in acc_buf.  The affine conversion (one binary-EEA inverse: ~40k
-// instructions issued by a single lane) runs on the host after the 96-byte
-// read-back (msm_rt.hip g1j_to_raw).  With pre (one reduction window) this is a
-// copy of the window sum.
-__global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum,
-                                                   G1JDev* acc_buf) {
+// result in acc_buf.  W_w arrives as `per` partial sums (wparts[w per + k], the
+// last tree level's chunks): the wave's 16 quads first add up the windows'
+// partials in parallel (quad q takes windows q, q + 16, ...) and publish the
+// window sums through LDS, which replaces a tree launch of one block per
+// window.  The affine conversion (one binary-EEA inverse: ~40k instructions
+// issued by a single lane) runs on the host after the 96-byte read-back
+// (msm_rt.hip g1j_to_raw).  With pre (one reduction window) the chain is the
+// window sum itself.
+static constexpr uint32_t HORNER_MAX_WINDOWS = 32;
+__global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wparts,
+                                                   uint32_t per, G1JDev* acc_buf) {
+  __shared__ j29 ws[HORNER_MAX_WINDOWS];
   if (blockIdx.x != 0) return;
+  const uint32_t quad = threadIdx.x >> 2;
+  for (uint32_t w = w_lo + quad; w < w_hi; w += 16) {
+    f29 X{}, Y{}, Z{};
+    bool inf = true;
+    for (uint32_t k = 0; k < per; k++) coop29_add(X, Y, Z, inf, j29_ld(wparts[(size_t)w * per + k]));
+    if ((threadIdx.x & 3) == 0) ws[w - w_lo] = {X, Y, Z, inf};
+  }
+  __syncthreads();
   j29 a0 = w_hi == p.rw ? j29_inf() : j29_ld(*acc_buf);
   f29 X = a0.x, Y = a0.y, Z = a0.z;
   bool inf = a0.inf;
   for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
     if (w != (int)p.rw - 1 && !inf)
       for (uint32_t q = 0; q < p.c; q++) coop29_dbl(X, Y, Z);
-    coop29_add(X, Y, Z, inf, j29_ld(wsum[w]));
+    coop29_add(X, Y, Z, inf, ws[w - (int)w_lo]);
   }
   if (threadIdx.x != 0) return;
   g1j_store(*acc_buf, j29_to({X, Y, Z, inf}));

@@ -147,7 +147,8 @@ __global__ void k_msm_bucket(MsmPlan p, const uint32_t* whi, const uint32_t* ord
 __global__ void k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo, const uint32_t* whi,
                               const uint32_t* owner, const G1JDev* slot_sum, G1JDev* part);
 __global__ void k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out);
-__global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wsum, G1JDev* acc_buf);
+__global__ void k_msm_horner(MsmPlan p, uint32_t w_hi, uint32_t w_lo, const G1JDev* wparts, uint32_t per,
+                             G1JDev* acc_buf);
 __global__ void k_msm_genpoints(uint32_t n, uint32_t off, uint32_t chunk, const G1Dev* gtab, G1JDev* jtmp,
                                 uint32_t (*zs)[8], G1Dev* pts);
 

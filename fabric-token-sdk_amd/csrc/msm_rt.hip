@@ -19,7 +19,7 @@ struct ftz_msm {
   size_t sort_tmp_bytes = 0;
   uint32_t key_bits = 0;
   DBuf<G1JDev> slot_sum, part, tree;
-  DBuf<G1JDev> hacc, wsum;
+  DBuf<G1JDev> hacc;
   DBuf<uint8_t> ok;
   hipEvent_t ev[2];
   bool ev_init = false;
@@ -59,6 +59,7 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->end.alloc(wb));
   m->key_bits = msm_key_bits(p);
   // 9-bit digits where they save a pass (17-18 bits: two passes instead of three)
+  if (p.rw > 32) return set_err(FTZ_E_INVALID, "MSM plan has more than 32 windows");
   const uint32_t rb = m->ctx->opt.msm_radix_bits;
   m->radix_bits = rb ? rb : (m->key_bits > 16 && m->key_bits <= 18 ? 9u : 8u);
   HC(msm_sort(m, nullptr, m->sort_tmp_bytes, wn, m->ctx->stream));
@@ -76,7 +77,6 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->part.alloc((size_t)p.rw * p.segs));
   HC(m->tree.alloc((size_t)p.rw * ((p.segs + 255) / 256) * 2));
   HC(m->hacc.alloc(1));
-  HC(m->wsum.alloc(p.rw));
   HC(m->ok.alloc(n));
   for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
   m->ev_init = true;
@@ -260,20 +260,22 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
                                                m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
   k_msm_segment<<<blocks((size_t)p.rw * p.segs, 128), 128, 0, s>>>(p, 0, p.rw, m->wlo.p, m->whi.p,
                                                                        m->owner.p, m->slot_sum.p, m->part.p);
-  // tree passes: segs -> ceil(segs/256) -> ... -> 1 per window
+  // tree passes: segs -> ceil(segs/256) -> ... until at most HORNER_PARTS per
+  // window, which the Horner wave adds up itself (quads in parallel)
+  const uint32_t HORNER_PARTS = 8;
   G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.rw * ((p.segs + 255) / 256)};
   const G1JDev* in = m->part.p;
   uint32_t cnt = p.segs;
   int which = 0;
-  do {
+  while (cnt > HORNER_PARTS) {
     uint32_t chunks = (cnt + 255) / 256;
-    G1JDev* out = chunks == 1 ? m->wsum.p : bufs[which];
+    G1JDev* out = bufs[which];
     k_msm_tree<<<p.rw * chunks, 256, 0, s>>>(in, cnt, out);
     in = out;
     which ^= 1;
     cnt = chunks;
-  } while (cnt > 1);
-  k_msm_horner<<<1, 64, 0, s>>>(p, p.rw, 0, m->wsum.p, m->hacc.p);
+  }
+  k_msm_horner<<<1, 64, 0, s>>>(p, p.rw, 0, in, cnt, m->hacc.p);
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
   G1JDev acc;
