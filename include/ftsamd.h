@@ -398,7 +398,10 @@ int ftz_audit_owners(ftz_idemix* ix, size_t n, const ftz_owner_audit* items, int
  * bytes big-endian, reduced mod r.  The reference path has no MSM; this is the
  * operation mathlib exposes from gnark-crypto as G1Jac.MultiExp.  Pippenger
  * with signed windows over GLV half-scalars (k = k1 + k2 lambda, |k_i| < 2^128,
- * points P_i and phi(P_i)), c = floor(log2(2n) / 2) + 7 clamped to [8, 20]. */
+ * points P_i and phi(P_i)), c = floor(log2(2n) / 2) + 7 clamped to [8, 20].
+ * Sizes: n in [1, 2^28], and windows x 2n < 2^30 sort entries (n up to
+ * ~2^26; FTZ_E_INVALID beyond), or windows x 2n < 2^31 resident points with
+ * msm_precompute. */
 typedef struct ftz_msm ftz_msm;
 int ftz_msm_g1(ftz_ctx* ctx, size_t n, const uint8_t* points, const uint8_t* scalars, uint8_t out[64]);
 /* staged form: upload once, run on HBM-resident inputs (bench) */
