@@ -240,3 +240,23 @@ def test_msm_point_split_gloo(world, n):
     assert sorted((r[1], r[2]) for r in res)[-1][1] == n
     for rank, start, stop, out in res:
         assert out == want
+
+
+@pytest.mark.gpu
+def test_rccl_rank_path_on_one_gpu():
+    """bench.py's N > 1 path in the order a torchrun rank runs it: torch
+    initialises HIP and joins an RCCL ("nccl") group, then the library opens
+    its context in the same process (one HIP runtime: torch's, which the
+    library's code objects run on).  One rank on one GPU: the tx-sharded
+    verification, the verdict-bitmap all-gather, the MIN / MAX reduces and
+    the point-split MSM's 64-byte partial gather (tests/gpu_scripts/
+    dist_world1.py, a child process so that torch loads first)."""
+    import json
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, FTZ_TEST_PORT="29613")
+    r = subprocess.run([sys.executable, "-u", os.path.join(here, "gpu_scripts", "dist_world1.py")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out == {"verdicts_ok": True, "elapsed_max": 0.125, "msm_matches_single": True}
