@@ -108,11 +108,12 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   p.slot_cap = slot_cap;
   p.max_slots = p.buckets + (uint32_t)((p.per + slot_cap - 1) / slot_cap);
   if (!seg_len && pre) {
-    // 16 measured at 2^20 (2.71 ms against 2.81 with 4 and 2.85 with 32); at
-    // 2^24 (3.1M slots) 64: 26.0 ms against 26.7 with 16 -- longer runs once
-    // the segments would exceed 64k lanes
-    seg_len = 16;
-    while (seg_len < 64 && p.max_slots / seg_len > 65536) seg_len *= 2;
+    // at most ~24k segment lanes, S in [4, 64]: measured best at 2^16 (90k
+    // slots, S = 4: 0.63-0.65 ms against 0.84 with 16), 2^20 (328k slots,
+    // S = 16: 2.54 ms against 3.54 with 64 and 2.85 with 32) and 2^24 (8.4M
+    // slots, S = 64: 26.0 ms against 26.7 with 16)
+    seg_len = 4;
+    while (seg_len < 64 && p.max_slots / seg_len > 24576) seg_len *= 2;
   }
   if (!seg_len) {
     uint64_t tot = (uint64_t)p.rw * p.max_slots;
