@@ -114,7 +114,7 @@ func (v *Verifier) verifyBlock(l *blockLedger, raws [][]byte) ([]error, error) {
 	defer h.Delete()
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	reqs := (*[1 << 28]C.ftz_bytes)(C.malloc(C.size_t(len(raws)) * C.size_t(unsafe.Sizeof(C.ftz_bytes{}))))[:len(raws):len(raws)]
+	reqs := cArray[C.ftz_bytes](len(raws))
 	defer C.free(unsafe.Pointer(&reqs[0]))
 	for i, r := range raws {
 		reqs[i] = C.ftz_bytes{p: ptr(&pin, r), len: C.size_t(len(r))}

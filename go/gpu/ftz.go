@@ -158,6 +158,13 @@ func ptr(pin *runtime.Pinner, b []byte) *C.uint8_t {
 	return (*C.uint8_t)(unsafe.Pointer(&b[0]))
 }
 
+// cArray allocates n elements of T in C memory, where pinned Go pointers may
+// be stored (the ABI's descriptor arrays); release with C.free(&s[0]).
+func cArray[T any](n int) []T {
+	var z T
+	return unsafe.Slice((*T)(C.malloc(C.size_t(n)*C.size_t(unsafe.Sizeof(z)))), n)
+}
+
 // rawBytes flattens G1 points to the ABI's n x 64-byte gnark RawBytes.
 func rawBytes(ps []*math.G1) []byte {
 	b := make([]byte, 0, 64*len(ps))
@@ -242,7 +249,7 @@ func (v *Verifier) verifyTransfersRaw(in, out, proofs [][]byte) ([]int, error) {
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	// C.malloc'd descriptor array: it holds pinned Go pointers, which cgo allows in C memory
-	tx := (*[1 << 28]C.ftz_transfer)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.ftz_transfer{}))))[:n:n]
+	tx := cArray[C.ftz_transfer](n)
 	defer C.free(unsafe.Pointer(&tx[0]))
 	for i := range proofs {
 		tx[i] = C.ftz_transfer{inputs: ptr(&pin, in[i]), n_in: C.uint32_t(len(in[i]) / 64), outputs: ptr(&pin, out[i]),
@@ -324,7 +331,7 @@ func (v *Verifier) verifyIssuesRaw(out [][]byte, anonymous []bool, proofs [][]by
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	d := (*[1 << 28]C.ftz_issue)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(C.ftz_issue{}))))[:n:n]
+	d := cArray[C.ftz_issue](n)
 	defer C.free(unsafe.Pointer(&d[0]))
 	for i := range proofs {
 		var anon C.uint8_t

@@ -78,7 +78,7 @@ func (o *OwnerVerifier) Verify(items []OwnerSig) ([]int, error) {
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	d := (*[1 << 28]C.ftz_owner_sig)(C.malloc(C.size_t(len(items)) * C.size_t(unsafe.Sizeof(C.ftz_owner_sig{}))))[:len(items):len(items)]
+	d := cArray[C.ftz_owner_sig](len(items))
 	defer C.free(unsafe.Pointer(&d[0]))
 	for i, it := range items {
 		d[i] = C.ftz_owner_sig{owner: ptr(&pin, it.Owner), owner_len: C.size_t(len(it.Owner)),
@@ -184,7 +184,7 @@ func (o *OwnerVerifier) AuditOwners(items []OwnerAudit) ([]int, error) {
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	d := (*[1 << 28]C.ftz_owner_audit)(C.malloc(C.size_t(len(items)) * C.size_t(unsafe.Sizeof(C.ftz_owner_audit{}))))[:len(items):len(items)]
+	d := cArray[C.ftz_owner_audit](len(items))
 	defer C.free(unsafe.Pointer(&d[0]))
 	for i, it := range items {
 		d[i] = C.ftz_owner_audit{owner: ptr(&pin, it.Owner), owner_len: C.size_t(len(it.Owner)),

@@ -81,8 +81,7 @@ func (v *Verifier) ProveTransfers(ws []TransferWitness) ([][]byte, error) {
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	d := (*[1 << 28]C.ftz_transfer_witness)(C.malloc(C.size_t(len(ws)) *
-		C.size_t(unsafe.Sizeof(C.ftz_transfer_witness{}))))[:len(ws):len(ws)]
+	d := cArray[C.ftz_transfer_witness](len(ws))
 	defer C.free(unsafe.Pointer(&d[0]))
 	for i, w := range ws {
 		if len(w.InW) != len(w.In) || len(w.OutW) != len(w.Out) || len(w.InW) == 0 {
@@ -112,8 +111,7 @@ func (v *Verifier) ProveIssues(ws []IssueWitness) ([][]byte, error) {
 	}
 	var pin runtime.Pinner
 	defer pin.Unpin()
-	d := (*[1 << 28]C.ftz_issue_witness)(C.malloc(C.size_t(len(ws)) *
-		C.size_t(unsafe.Sizeof(C.ftz_issue_witness{}))))[:len(ws):len(ws)]
+	d := cArray[C.ftz_issue_witness](len(ws))
 	defer C.free(unsafe.Pointer(&d[0]))
 	for i, w := range ws {
 		if len(w.TW) != len(w.Tokens) || len(w.TW) == 0 {
