@@ -20,8 +20,9 @@ import torch.distributed as dist  # noqa: E402
 
 def main():
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get("FTZ_TEST_PORT", "29611"),
-                            rank=0, world_size=1)
+    import tempfile
+    store = os.path.join(tempfile.mkdtemp(prefix="ftz_dist_"), "store")  # a file rendezvous: no port to collide on
+    dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1)
     import numpy as np
 
     import zkatdlog

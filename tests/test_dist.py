@@ -254,9 +254,8 @@ def test_rccl_rank_path_on_one_gpu():
     import json
     import subprocess
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, FTZ_TEST_PORT="29613")
     r = subprocess.run([sys.executable, "-u", os.path.join(here, "gpu_scripts", "dist_world1.py")],
-                       capture_output=True, text=True, timeout=300, env=env)
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out == {"verdicts_ok": True, "elapsed_max": 0.125, "msm_matches_single": True}
