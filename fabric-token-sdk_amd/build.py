@@ -6,6 +6,11 @@ source/header mtimes.  Output: zkatdlog/_lib/libftsamd.so (in-tree, so it
 travels to the GPU box with the repo snapshot).
 
     python fabric-token-sdk_amd/build.py [-j N] [--force]
+    python fabric-token-sdk_amd/build.py --variant NAME --defs "-DFTS_SX_KARA=0"
+
+--variant builds an A/B library with extra defines into zkatdlog/_lib/ab/
+libftsamd_NAME.so (objects in build/obj_NAME); FTS_LIB=<path> makes
+zkatdlog._abi load it instead of the default library (same-box A/B runs).
 """
 import argparse
 import glob
@@ -42,17 +47,39 @@ def newest(paths):
     return max(os.path.getmtime(p) for p in paths if os.path.exists(p))
 
 
-def compile_one(src, force, hdr_time):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def compile_one(src, force, hdr_time, obj_dir=OBJ, extra=()):
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     if not force and os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_time):
         return obj, None
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas"] + DEFS + ["-c", src, "-o", obj]
+        cmd = [HIPCC, "-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas"] + DEFS + list(extra) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, "%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr)
     return obj, None
+
+
+def build_variant(name, defs, jobs=8, force=False):
+    """A/B library: the same sources with extra defines (see module doc)."""
+    obj_dir = os.path.join(HERE, "build", "obj_" + name)
+    lib = os.path.join(os.path.dirname(LIB), "ab", "libftsamd_%s.so" % name)
+    os.makedirs(obj_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
+    hdr_time = newest(headers())
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        results = list(ex.map(lambda s: compile_one(s, force, hdr_time, obj_dir, defs), SOURCES))
+    errs = [e for _, e in results if e]
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in results]
+    if force or not os.path.exists(lib) or os.path.getmtime(lib) < newest(objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    print("built", lib)
+    return lib
 
 
 def build(jobs=8, force=False, verbose=True):
@@ -93,9 +120,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", type=int, default=8)
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default=None)
+    ap.add_argument("--defs", default="")
     a = ap.parse_args()
     try:
-        build(a.j, a.force)
+        if a.variant:
+            build_variant(a.variant, a.defs.split(), a.j, a.force)
+        else:
+            build(a.j, a.force)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -26,6 +26,61 @@
 namespace fts {
 
 // ----------------------------------------------------------- accumulation
+// FTS_SX_KARA (default 1): the lane's Fp2 sum is kept as three Karatsuba rows
+//   U = sum a0 b0,  V = sum a1 b1,  W = sum (a0 + a1)(b0 + b1)
+// (3 x 81 MADs per Fp2 product instead of the schoolbook 4 x 81), and the two
+// rows the reduction needs are formed once per sum: re = U - V, im = W - U - V.
+// The rows are computed modulo 2^64 (unsigned: they may wrap, W in particular,
+// whose operands are unbalanced limb sums); re and im are the schoolbook
+// column sums exactly, whose bound (108 limb products of <= 2^56 per column)
+// is unchanged, so every reduced value -- and every GT byte -- is bit-identical
+// to the schoolbook accumulation.  A complex square s^2 adds s0^2, s1^2 and
+// (s0 + s1)^2 to the rows as three 45-MAD squarings (doubled cross products).
+#ifndef FTS_SX_KARA
+#define FTS_SX_KARA 1
+#endif
+#if FTS_SX_KARA
+struct W29 {
+  uint64_t u[17], v[17], w[17];
+};
+FTS_HD void w29_init(W29& w) {
+#pragma unroll
+  for (int i = 0; i < 17; i++) w.u[i] = w.v[i] = w.w[i] = 0;
+}
+FTS_HD uint64_t w29_p(int32_t a, int32_t b) { return (uint64_t)((int64_t)a * (int64_t)b); }
+// w += a b (a, b balanced, or limbs within 2^29)
+FTS_HD void w29_mac(W29& w, const q2& a, const q2& b) {
+  FTS_COUNT_MAD(192);  // the 32-bit equivalent (3 wide products), for opcounts
+  FTS_SCHED_FENCE();
+  const f29 sa = f29_add(a.c0, a.c1), sb = f29_add(b.c0, b.c1);
+#pragma unroll
+  for (int i = 0; i < 9; i++)
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      w.u[i + j] += w29_p(a.c0.l[i], b.c0.l[j]);
+      w.v[i + j] += w29_p(a.c1.l[i], b.c1.l[j]);
+      w.w[i + j] += w29_p(sa.l[i], sb.l[j]);
+    }
+}
+// row += x^2: cross products once with the doubled operand (|2 x_i| < 2^31)
+FTS_HD void w29_row_sqr(uint64_t r[17], const f29& x) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int32_t d = x.l[i] + x.l[i];
+    r[2 * i] += w29_p(x.l[i], x.l[i]);
+#pragma unroll
+    for (int j = i + 1; j < 9; j++) r[i + j] += w29_p(d, x.l[j]);
+  }
+}
+// w += s^2 (s balanced): 3 x 45 MADs
+FTS_HD void w29_sqr_acc(W29& w, const q2& s) {
+  FTS_COUNT_MAD(128);
+  FTS_SCHED_FENCE();
+  w29_row_sqr(w.u, s.c0);
+  w29_row_sqr(w.v, s.c1);
+  w29_row_sqr(w.w, f29_add(s.c0, s.c1));
+}
+#else
 struct W29 {
   int64_t re[17], im[17];
 };
@@ -48,6 +103,7 @@ FTS_HD void w29_mac(W29& w, const q2& a, const q2& b) {
       w.im[i + j] += (int64_t)a.c1.l[i] * b.c0.l[j];
     }
 }
+#endif
 // Montgomery reduction of one row, balanced digits and result
 FTS_HD f29 w29_redc(int64_t c[17]) {
   FTS_COUNT_MAD(72);
@@ -71,6 +127,17 @@ FTS_HD f29 w29_redc(int64_t c[17]) {
   r.l[8] = (int32_t)acc;
   return r;
 }
+#if FTS_SX_KARA
+FTS_HD q2 w29_reduce(W29& w) {
+  int64_t re[17], im[17];
+#pragma unroll
+  for (int i = 0; i < 17; i++) {
+    re[i] = (int64_t)(w.u[i] - w.v[i]);
+    im[i] = (int64_t)(w.w[i] - (w.u[i] + w.v[i]));
+  }
+  return {w29_redc(re), w29_redc(im)};
+}
+#else
 FTS_HD q2 w29_reduce(W29& w) { return {w29_redc(w.re), w29_redc(w.im)}; }
 // w += s^2 (s balanced) as (s0 + s1)(s0 - s1) + 2 s0 s1 u: two limb-product rows
 // instead of the four of w29_mac(w, s, s)
@@ -86,6 +153,7 @@ FTS_HD void w29_sqr_acc(W29& w, const q2& s) {
       w.im[i + j] += (int64_t)t.l[i] * s.c1.l[j];
     }
 }
+#endif
 
 FTS_HD q2 q2_mul(const q2& a, const q2& b) {
   W29 w;
@@ -397,6 +465,13 @@ FTS_HD f29 f29_mulb(const f29& a, const f29& b) {
   return w29_redc(c);
 }
 
+#if FTS_SX_KARA
+// the Karatsuba rows take the same three squarings as w29_sqr_acc
+FTS_HD void w29_sqr3_acc(W29& w, const q2& s) {
+  FTS_COUNT_MAD(32);  // the schoolbook variant's count (160), for opcounts
+  w29_sqr_acc(w, s);
+}
+#else
 // w += s^2 (s balanced) as s0 s0 - s1 s1 + (2 s0) s1 u: three limb-product rows
 // (the column bound stays that of w29_mac(w, s, s): 18 units of 2^56 per row)
 FTS_HD void w29_sqr3_acc(W29& w, const q2& s) {
@@ -412,6 +487,7 @@ FTS_HD void w29_sqr3_acc(W29& w, const q2& s) {
       w.im[i + j] += (int64_t)t.l[i] * s.c1.l[j];
     }
 }
+#endif
 
 // c = a^2 (as sx_sqr): a, xi a and 2 a published (2 a unreduced: its limbs
 // are within 2^29 and SX_SQR4_TAB gives every lane at most 6 operand units).
@@ -450,6 +526,25 @@ FTS_HD q2 sq_mul_line_r(const X& x, const q2& f, const q2& l0, const q2& l1, con
     int j = x.k - (t == 0 ? 0 : (t == 1 ? 1 : 3));
     int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
     w29_mac(w, t == 0 ? l0 : (t == 1 ? l1 : l3), x.get(sb));
+  }
+  x.sync();
+  return w29_reduce(w);
+}
+
+// f * (pair-2 line s), the three evaluated coefficients read from the line
+// buffer inside the term loop (one at a time: the Karatsuba rows leave no room
+// for all three next to the accumulator)
+template <class X>
+FTS_HD q2 sq_mul_evline(const X& x, const q2& f, const EvLineDev* l2, uint32_t s, uint32_t idx, uint32_t njobs) {
+  sq_pub(x, SX_A, f);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 3; t++) {
+    int j = x.k - (t == 0 ? 0 : (t == 1 ? 1 : 3));
+    int sb = j < 0 ? SX_AX + j + 6 : SX_A + j;
+    w29_mac(w, evline_ld29(l2, s, t, idx, njobs), x.get(sb));
   }
   x.sync();
   return w29_reduce(w);
@@ -585,8 +680,7 @@ FTS_HD q2 sq_miller_fn(const X& x, const LineCoef29* qlines_n, const g1a& P1, co
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sq_sqr(x, f);
     f = sq_fixed_line_n(x, f, qlines_n[s], xq, yi, P1.inf);
-    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
-                      evline_ld29(l2, s, 2, idx, njobs));
+    f = sq_mul_evline(x, f, l2, s, idx, njobs);
   }
   return f;
 }
@@ -603,8 +697,7 @@ FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sq_sqr(x, f);
     f = sq_fixed_line(x, f, qlines[s], yP, xP, P1.inf);
-    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
-                      evline_ld29(l2, s, 2, idx, njobs));
+    f = sq_mul_evline(x, f, l2, s, idx, njobs);
   }
   return f;
 }

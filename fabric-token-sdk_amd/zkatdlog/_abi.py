@@ -272,6 +272,8 @@ class Stats(ctypes.Structure):
 
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libftsamd.so")
+# same-box A/B runs load a variant build (build.py --variant) instead
+LIB_PATH = os.environ.get("FTS_LIB") or LIB_PATH
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
