@@ -2,6 +2,9 @@
 #include <hip/hip_runtime.h>
 
 #include "dev/jobs.h"
+#ifdef FTS_MILLER_KARA  // A/B builds: the Miller kernels' accumulation alone
+#define FTS_SX_KARA FTS_MILLER_KARA
+#endif
 #include "dev/sx29.h"
 #include "launch.h"
 

@@ -633,3 +633,83 @@ class OwnerVerifier:
         code = self.ix.verify_owner_signatures([(self.owner, bytes(message), bytes(sigma))])[0]
         if code != FTZ_OK:
             raise ZKError(code)
+
+
+class SignatureError(Exception):
+    """An owner-signature check failed: the text is the reference's
+    (validator_transfer.go:50-76) error chain, outermost first."""
+
+
+PSEUDONYM_INVALID = "pseudonym signature invalid: zero-knowledge proof is invalid"  # IBM/idemix NymSignature.Ver
+
+
+def _unique_id(owner):
+    # view.Identity.UniqueID (fabric-smart-client, not vendored [EXT]): the hex
+    # SHA-256 of the identity bytes
+    import hashlib
+    return hashlib.sha256(bytes(owner)).hexdigest()
+
+
+def transfer_signature_validate(keys, load, owner_verifier, has_been_signed_by, verify_batch, unique_id=_unique_id):
+    """validator.TransferSignatureValidate (crypto/validator/validator_transfer.go:42-82)
+    with the owners' signatures verified in ONE batch (the Go shim's
+    go/gpu/owner.go transferSignatures, same order and texts):
+
+    * load(key) -> token owner bytes (raises with the reference's ledger texts);
+    * owner_verifier(owner) -> a verifier (the Go deserializer; raises on a bad owner);
+    * has_been_signed_by(owner, verifier) -> sigma (the provider's cursor; calls
+      verifier.verify(msg, sigma), raises "invalid state, insufficient number of signatures");
+    * verify_batch([(owner, msg, sigma)]) -> FTZ codes (Idemix.verify_owner_signatures).
+
+    The reference verifies input i's signature before it loads input i+1, so
+    when a step of input j fails, the signatures of inputs 0..j-1 are checked
+    first and the first bad one wins.  Returns [(owner, sigma)] or raises
+    SignatureError with the reference's text."""
+
+    class _Capture:
+        msg = sigma = None
+
+        def verify(self, message, sigma):
+            self.msg, self.sigma = bytes(message), bytes(sigma)
+
+    done = []  # (key, owner, go verifier, msg, sigma)
+
+    def check():
+        if not done:
+            return None
+        codes = verify_batch([(o, m, s) for _, o, _, m, s in done])
+        for i, (c, (key, owner, v, m, s)) in enumerate(zip(codes, done)):
+            err = None
+            if c in (_abi.FTZ_ERR_UNSUPPORTED, _abi.FTZ_ERR_OWNER):
+                try:  # owners the library does not verify: the Go verifier decides
+                    v.verify(m, s)
+                except Exception as e:  # noqa: BLE001 -- the verifier's own error text
+                    err = str(e)
+            elif c != FTZ_OK:
+                err = PSEUDONYM_INVALID
+            if err is not None:
+                return "failed signature verification [%d][%s][%s]: %s" % (i, key, unique_id(owner), err)
+        return None
+
+    def fail(text):
+        raise SignatureError(check() or text)
+
+    for i, key in enumerate(keys):
+        try:
+            owner = bytes(load(key))
+        except Exception as e:  # noqa: BLE001
+            fail(str(e))
+        try:
+            v = owner_verifier(owner)
+        except Exception as e:  # noqa: BLE001
+            fail("failed deserializing owner [%d][%s][%s]: %s" % (i, key, unique_id(owner), e))
+        cap = _Capture()
+        try:
+            has_been_signed_by(owner, cap)
+        except Exception as e:  # noqa: BLE001
+            fail("failed signature verification [%d][%s][%s]: %s" % (i, key, unique_id(owner), e))
+        done.append((key, owner, v, cap.msg, cap.sigma))
+    text = check()
+    if text:
+        raise SignatureError(text)
+    return [(o, s) for _, o, _, _, s in done]

@@ -53,9 +53,16 @@ type blockLedger struct {
 	pin  runtime.Pinner
 }
 
+// ledgerOf reads the cgo.Handle verifyBlock passes by reference as the ABI's
+// void* user (the runtime/cgo pattern: a pointer to the handle, never the
+// handle's integer value converted to a pointer).
+func ledgerOf(user unsafe.Pointer) *blockLedger {
+	return (*(*cgo.Handle)(user)).Value().(*blockLedger)
+}
+
 //export goGetState
 func goGetState(user unsafe.Pointer, key *C.char, keyLen C.size_t, val **C.uint8_t, valLen *C.size_t) C.int {
-	l := cgo.Handle(user).Value().(*blockLedger)
+	l := ledgerOf(user)
 	l.pin.Unpin() // the previous value has been copied
 	v, err := l.get(C.GoStringN(key, C.int(keyLen)))
 	if err != nil {
@@ -68,7 +75,7 @@ func goGetState(user unsafe.Pointer, key *C.char, keyLen C.size_t, val **C.uint8
 
 //export goGetStates
 func goGetStates(user unsafe.Pointer, n C.size_t, keys *C.ftz_bytes, vals *C.ftz_bytes) C.int {
-	l := cgo.Handle(user).Value().(*blockLedger)
+	l := ledgerOf(user)
 	l.pin.Unpin() // the previous chunk's values have been copied
 	ks := unsafe.Slice(keys, int(n))
 	vs := unsafe.Slice(vals, int(n))
@@ -112,6 +119,9 @@ func (v *Verifier) verifyBlock(l *blockLedger, raws [][]byte) ([]error, error) {
 	defer l.pin.Unpin()
 	h := cgo.NewHandle(l)
 	defer h.Delete()
+	// &h is a Go pointer to pointer-free memory: cgo keeps it valid (and
+	// pinned) for the duration of the call, which is as long as the library
+	// may use it
 	var pin runtime.Pinner
 	defer pin.Unpin()
 	reqs := cArray[C.ftz_bytes](len(raws))
@@ -125,10 +135,10 @@ func (v *Verifier) verifyBlock(l *blockLedger, raws [][]byte) ([]error, error) {
 		var rc C.int
 		if l.gets != nil {
 			rc = C.ftz_verify_token_requests_batched(ctx, C.size_t(len(raws)), &reqs[0], C.ftz_go_get_states_fn(),
-				unsafe.Pointer(h), &codes[0], &failed[0])
+				unsafe.Pointer(&h), &codes[0], &failed[0])
 		} else {
 			rc = C.ftz_verify_token_requests(ctx, C.size_t(len(raws)), &reqs[0], C.ftz_go_get_state_fn(),
-				unsafe.Pointer(h), &codes[0], &failed[0])
+				unsafe.Pointer(&h), &codes[0], &failed[0])
 		}
 		if rc != C.FTZ_SUCCESS {
 			return errors.Errorf("gpu verifier: %s", lastError())

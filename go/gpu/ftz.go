@@ -25,6 +25,7 @@ package gpu
 import "C"
 
 import (
+	"crypto/sha256"
 	"os"
 	"runtime"
 	"strconv"
@@ -126,6 +127,70 @@ func newVerifierRaw(raw []byte, device int, o *Options) (*Verifier, error) {
 	return v, nil
 }
 
+// shared holds one (Verifier, OwnerVerifier) pair per device, keyed by the
+// SHA-256 of the serialized public parameters (Shared).
+var shared struct {
+	mu sync.Mutex
+	m  map[int]*sharedEntry
+}
+
+type sharedEntry struct {
+	pp [32]byte
+	v  *Verifier
+	ov *OwnerVerifier // nil when SupportsIdemixCurve(pp.IdemixCurveID) is false
+}
+
+// Shared returns the process-wide Verifier and OwnerVerifier of (device, pp).
+// Driver.NewValidator runs per request on some paths (the Orion custodian:
+// services/network/orion/approval.go:100 -> token.NewServicesFromPublicParams
+// -> core.NewValidator), so a device context -- the PP's fixed-base tables in
+// HBM, streams, planning threads -- is built once per (device, PP) and reused
+// by every validator. New public parameters on a device close the previous
+// pair explicitly (Close waits for the calls in flight; a validator still
+// holding the old pair then fails with "gpu verifier closed"). ov is nil when
+// the library does not verify owner signatures on pp.IdemixCurveID.
+func Shared(pp *crypto.PublicParams, device int) (v *Verifier, ov *OwnerVerifier, err error) {
+	raw, err := pp.Serialize()
+	if err != nil {
+		return nil, nil, err
+	}
+	key := sha256.Sum256(raw)
+	shared.mu.Lock()
+	defer shared.mu.Unlock()
+	if shared.m == nil {
+		shared.m = map[int]*sharedEntry{}
+	}
+	if e := shared.m[device]; e != nil {
+		if e.pp == key {
+			return e.v, e.ov, nil
+		}
+		if e.ov != nil {
+			e.ov.Close()
+		}
+		e.v.Close()
+		delete(shared.m, device)
+	}
+	v, err = newVerifierRaw(raw, device, nil)
+	if err != nil {
+		return nil, nil, err
+	}
+	if SupportsIdemixCurve(pp.IdemixCurveID) {
+		if ov, err = v.NewOwnerVerifier(pp); err != nil {
+			v.Close()
+			return nil, nil, err
+		}
+	}
+	shared.m[device] = &sharedEntry{pp: key, v: v, ov: ov}
+	return v, ov, nil
+}
+
+// SharedContexts is the number of device contexts Shared holds (tests).
+func SharedContexts() int {
+	shared.mu.Lock()
+	defer shared.mu.Unlock()
+	return len(shared.m)
+}
+
 // Close releases the device context. Calls after Close fail.
 func (v *Verifier) Close() {
 	v.mu.Lock()
@@ -134,6 +199,13 @@ func (v *Verifier) Close() {
 		C.ftz_ctx_destroy(v.ctx)
 		v.ctx = nil
 	}
+}
+
+// Closed reports whether Close has run.
+func (v *Verifier) Closed() bool {
+	v.mu.RLock()
+	defer v.mu.RUnlock()
+	return v.ctx == nil
 }
 
 // use runs f with the context held against a concurrent Close.
@@ -190,6 +262,14 @@ var errText = map[C.int32_t]string{
 	C.FTZ_ERR_UNSUPPORTED: "owner type verified in Go",
 	C.FTZ_ERR_AUDIT:       "owner does not match its audit info",
 }
+
+// Verdict codes (include/ftsamd.h FTZ_*), for callers and tests without cgo.
+const (
+	CodeOK          = int(C.FTZ_OK)
+	CodeOwner       = int(C.FTZ_ERR_OWNER)
+	CodeSignature   = int(C.FTZ_ERR_SIGNATURE)
+	CodeUnsupported = int(C.FTZ_ERR_UNSUPPORTED)
+)
 
 // CodeError is a failed verdict: Code is the library's FTZ_ERR_* value.
 type CodeError struct {

@@ -14,9 +14,12 @@ import (
 	"runtime"
 	"unsafe"
 
+	math "github.com/IBM/mathlib"
+	"github.com/hyperledger-labs/fabric-smart-client/platform/view/view"
 	"github.com/hyperledger-labs/fabric-token-sdk/token/core/zkatdlog/crypto"
 	"github.com/hyperledger-labs/fabric-token-sdk/token/core/zkatdlog/crypto/token"
 	"github.com/hyperledger-labs/fabric-token-sdk/token/core/zkatdlog/crypto/validator"
+	"github.com/hyperledger-labs/fabric-token-sdk/token/driver"
 	"github.com/pkg/errors"
 )
 
@@ -112,61 +115,149 @@ func (c *capture) Verify(message, sigma []byte) error {
 	return nil
 }
 
+// errPseudonym is the text of a failing idemix NymSignature.Ver (IBM/idemix
+// nymsignature.go), which HasBeenSignedBy returns and the reference wraps.
+var errPseudonym = errors.New("pseudonym signature invalid: zero-knowledge proof is invalid")
+
+// sigInput is one input of a transfer action as the reference's loop sees it.
+type sigInput struct {
+	key      string
+	tok      *token.Token
+	verifier driver.Verifier // the Go owner verifier (GetOwnerVerifier)
+	item     OwnerSig
+}
+
+// sigSteps are the reference loop's effects, injectable for the precedence
+// test (gpu_test.go): load the ledger token of one input, deserialize its
+// owner, let the signature provider hand out the next signature, and verify a
+// batch of owner signatures (codes as ftz_verify_owner_signatures).
+type sigSteps struct {
+	load   func(key string) (*token.Token, error)
+	owner  func(raw view.Identity) (driver.Verifier, error)
+	signed func(owner view.Identity, v driver.Verifier) ([]byte, error)
+	verify func(items []OwnerSig) ([]int, error)
+}
+
+// transferSignatures runs validator.TransferSignatureValidate's loop
+// (crypto/validator/validator_transfer.go:50-76) with every owner signature of
+// the action verified in one device batch, and returns exactly the reference's
+// first error: per input, in order, the ledger load, the owner deserialization
+// ("failed deserializing owner [i][in][UniqueID]"), the provider's cursor and
+// then the signature itself ("failed signature verification [i][in][UniqueID]").
+// When a step of input j fails, the signatures of inputs 0..j-1 -- which the
+// reference verified before reaching input j -- are checked first, so a bad
+// signature on an earlier input still wins.
+func transferSignatures(keys []string, st sigSteps) ([]sigInput, error) {
+	ins := make([]sigInput, 0, len(keys))
+	// check verifies the signatures of ins on the device and returns the
+	// reference's error for the first bad one
+	check := func() error {
+		if len(ins) == 0 {
+			return nil
+		}
+		items := make([]OwnerSig, len(ins))
+		for i := range ins {
+			items[i] = ins[i].item
+		}
+		codes, err := st.verify(items)
+		if err != nil {
+			return err
+		}
+		for i, c := range codes {
+			in := ins[i]
+			var verr error
+			switch c {
+			case int(C.FTZ_OK):
+			case int(C.FTZ_ERR_UNSUPPORTED), int(C.FTZ_ERR_OWNER):
+				// an owner the library does not verify (HTLC script) or decodes
+				// differently from the Go deserializer: the Go verifier decides
+				verr = in.verifier.Verify(in.item.Msg, in.item.Sig)
+			default:
+				verr = errPseudonym
+			}
+			if verr != nil {
+				return errors.Wrapf(verr, "failed signature verification [%d][%s][%s]", i, in.key,
+					view.Identity(in.tok.Owner).UniqueID())
+			}
+		}
+		return nil
+	}
+	fail := func(err error) ([]sigInput, error) {
+		if e := check(); e != nil {
+			return nil, e
+		}
+		return nil, err
+	}
+	for i, key := range keys {
+		tok, err := st.load(key)
+		if err != nil {
+			return fail(err)
+		}
+		verifier, err := st.owner(tok.Owner)
+		if err != nil {
+			return fail(errors.Wrapf(err, "failed deserializing owner [%d][%s][%s]", i, key,
+				view.Identity(tok.Owner).UniqueID()))
+		}
+		c := &capture{}
+		if _, err := st.signed(tok.Owner, c); err != nil { // insufficient signatures
+			return fail(errors.Wrapf(err, "failed signature verification [%d][%s][%s]", i, key,
+				view.Identity(tok.Owner).UniqueID()))
+		}
+		ins = append(ins, sigInput{key: key, tok: tok, verifier: verifier,
+			item: OwnerSig{Owner: tok.Owner, Msg: c.msg, Sig: c.sigma}})
+	}
+	if err := check(); err != nil {
+		return nil, err
+	}
+	return ins, nil
+}
+
 // TransferSignatureValidate is a drop-in for validator.TransferSignatureValidate
-// (crypto/validator/validator_transfer.go:42-82): the same ledger loads, error
-// texts and signature order, with the owners' signatures of the action verified
-// in one device call. Owners the library does not verify (HTLC scripts,
-// FTZ_ERR_UNSUPPORTED) go through ctx.Deserializer.GetOwnerVerifier as before.
+// (crypto/validator/validator_transfer.go:42-82): the same ledger loads, owner
+// deserialization, signature order and error texts, with the owners'
+// signatures of the action verified in one device call (transferSignatures).
 func (o *OwnerVerifier) TransferSignatureValidate(ctx *validator.Context) error {
-	inputs, err := ctx.Action.GetInputs()
+	keys, err := ctx.Action.GetInputs()
 	if err != nil {
 		return errors.Wrapf(err, "failed to retrieve inputs to spend")
 	}
-	tokens := make([]*token.Token, 0, len(inputs))
-	sigs := make([][]byte, 0, len(inputs))
-	items := make([]OwnerSig, 0, len(inputs))
-	for _, in := range inputs {
-		raw, err := ctx.Ledger.GetState(in)
-		if err != nil {
-			return errors.Wrapf(err, "failed to retrieve input to spend [%s]", in)
-		}
-		if len(raw) == 0 {
-			return errors.Errorf("input to spend [%s] does not exists", in)
-		}
-		tok := &token.Token{}
-		if err := tok.Deserialize(raw); err != nil {
-			return errors.Wrapf(err, "failed to deserialize input to spend [%s]", in)
-		}
-		c := &capture{}
-		if _, err := ctx.SignatureProvider.HasBeenSignedBy(tok.Owner, c); err != nil {
-			return errors.Wrapf(err, "failed signature verification [%s]", in) // insufficient signatures
-		}
-		tokens, sigs = append(tokens, tok), append(sigs, c.sigma)
-		items = append(items, OwnerSig{Owner: tok.Owner, Msg: c.msg, Sig: c.sigma})
-	}
-	codes, err := o.Verify(items)
+	ins, err := transferSignatures(keys, sigSteps{
+		load: func(in string) (*token.Token, error) {
+			raw, err := ctx.Ledger.GetState(in)
+			if err != nil {
+				return nil, errors.Wrapf(err, "failed to retrieve input to spend [%s]", in)
+			}
+			if len(raw) == 0 {
+				return nil, errors.Errorf("input to spend [%s] does not exists", in)
+			}
+			tok := &token.Token{}
+			if err := tok.Deserialize(raw); err != nil {
+				return nil, errors.Wrapf(err, "failed to deserialize input to spend [%s]", in)
+			}
+			return tok, nil
+		},
+		owner:  ctx.Deserializer.GetOwnerVerifier,
+		signed: ctx.SignatureProvider.HasBeenSignedBy,
+		verify: o.Verify,
+	})
 	if err != nil {
 		return err
 	}
-	for i, c := range codes {
-		switch c {
-		case C.FTZ_OK:
-		case C.FTZ_ERR_UNSUPPORTED:
-			verifier, err := ctx.Deserializer.GetOwnerVerifier(tokens[i].Owner)
-			if err != nil {
-				return errors.Wrapf(err, "failed deserializing owner [%d][%s]", i, inputs[i])
-			}
-			if err := verifier.Verify(items[i].Msg, sigs[i]); err != nil {
-				return errors.Wrapf(err, "failed signature verification [%d][%s]", i, inputs[i])
-			}
-		case C.FTZ_ERR_OWNER:
-			return errors.Errorf("failed deserializing owner [%d][%s]", i, inputs[i])
-		default:
-			return errors.Errorf("failed signature verification [%d][%s]: pseudonym signature invalid", i, inputs[i])
-		}
+	tokens, sigs := make([]*token.Token, len(ins)), make([][]byte, len(ins))
+	for i, in := range ins {
+		tokens[i], sigs[i] = in.tok, in.item.Sig
 	}
 	ctx.InputTokens, ctx.Signatures = tokens, sigs
 	return nil
+}
+
+// SupportsIdemixCurve reports whether the library verifies owner signatures on
+// the idemix curve PublicParams.IdemixCurveID names (ftz_idemix_create: BN254
+// and FP256BN_AMCL). Other curves (e.g. FP256BN_AMCL_MIRACL, which
+// identity/msp/idemix/deserializer.go:47 also accepts) keep the Go
+// validator.TransferSignatureValidate; the ZK checks still run on the GPU.
+func SupportsIdemixCurve(id math.CurveID) bool {
+	return id == math.BN254 || id == math.FP256BN_AMCL
 }
 
 // OwnerAudit is one auditor owner inspection: the token's Owner bytes and the

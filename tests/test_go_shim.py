@@ -82,7 +82,31 @@ def test_callbacks_match_the_abi():
 def test_registration_patch_uses_the_shim_api():
     p = open(os.path.join(ROOT, "go", "patches", "0001-zkatdlog-gpu-validator.patch")).read()
     srcs = "".join(_go_sources().values())
-    for sym in ("DeviceFromEnv", "NewVerifier", "NewOwnerVerifier", "VerifyIssue", "TransferSignatureValidate",
-                "TransferZKProofValidate"):
+    for sym in ("DeviceFromEnv", "Shared", "VerifyIssue", "TransferSignatureValidate", "TransferZKProofValidate"):
         assert sym in p
         assert re.search(r"func (\([^)]*\) )?%s\(" % sym, srcs), sym
+    # contexts are process-wide per (device, PP), not one per NewValidator
+    assert "gpu.NewVerifier(" not in p
+
+
+def test_cgo_handle_passed_by_reference():
+    """the ledger handle crosses into C as a pointer to the
+    cgo.Handle (runtime/cgo's pattern), never as the handle value coerced to a
+    pointer, which go vet flags"""
+    b = _go_sources()["block.go"]
+    assert "unsafe.Pointer(h)" not in b and "cgo.Handle(user)" not in b
+    assert b.count("unsafe.Pointer(&h)") == 2 and "(*(*cgo.Handle)(user))" in b
+
+
+def test_owner_signature_precedence_logic():
+    """weak #8 (r04): the shim deserializes each owner with the Go deserializer
+    before consuming its signature, and its error texts carry the UniqueID, in
+    the reference's order (validator_transfer.go:50-76); gpu_test.go holds the
+    precedence cases"""
+    o = _go_sources()["owner.go"]
+    assert '"failed deserializing owner [%d][%s][%s]"' in o
+    assert o.count('"failed signature verification [%d][%s][%s]"') == 2
+    body = o[o.index("func transferSignatures"):]
+    assert body.index("st.owner(") < body.index("st.signed(")
+    t = _go_sources()["gpu_test.go"]
+    assert "func TestTransferSignaturePrecedence" in t and "func TestSharedContextReuse" in t
