@@ -326,7 +326,7 @@ FTS_HD f29 f29_lin2(const f29& a, int32_t ca, const f29& b, int32_t cb) {
     if (i < 8) {
       const int32_t lo = f29_bdigit(acc);
       r.l[i] = lo;
-      acc = (acc - lo) >> 29;
+      acc = (acc + F29_HALF) >> 29;  // = (acc - lo) / 2^29: lo is acc's balanced low digit
     } else {
       r.l[8] = (int32_t)acc;
     }

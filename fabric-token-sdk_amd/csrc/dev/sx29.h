@@ -122,7 +122,7 @@ FTS_HD f29 w29_redc(int64_t c[17]) {
     acc += c[9 + i];
     const int32_t lo = f29_bdigit(acc);
     r.l[i] = lo;
-    acc = (acc - lo) >> 29;
+    acc = (acc + F29_HALF) >> 29;  // = (acc - lo) / 2^29: lo is acc's balanced low digit
   }
   r.l[8] = (int32_t)acc;
   return r;
