@@ -35,7 +35,24 @@ namespace fts {
 struct f29 {
   int32_t l[9];
 };
+
+// A 32-bit value the compiler must treat as produced here: a lane-dependent
+// multiplicand whose sign extension LLVM would otherwise hoist out of a loop
+// (or keep from another block) is then multiplied as a full int64 x int64
+// (v_mad_u64_u32 + 2 v_mul_lo_u32 + v_add3, 4 instructions) instead of one
+// v_mad_i64_i32.
+FTS_HD int32_t pin32(int32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
 static constexpr int32_t F29_MASK = (1 << 29) - 1;
+
+FTS_HD void pin29(f29& a) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) a.l[i] = pin32(a.l[i]);
+}
 
 FTS_HD f29 f29_add(const f29& a, const f29& b) {
   f29 r;
@@ -314,7 +331,12 @@ FTS_HD int32_t f29_bdigit(int64_t acc) {
 
 // ca a + cb b - q p, balanced (|result| <= p/2 + e).  |ca|, |cb| <= 16 and
 // inputs with |limb| <= 2^29: every term fits the 64-bit sweep.
-FTS_HD f29 f29_lin2(const f29& a, int32_t ca, const f29& b, int32_t cb) {
+FTS_HD f29 f29_lin2(const f29& a_, int32_t ca, const f29& b_, int32_t cb) {
+  if (!__builtin_constant_p(ca)) ca = pin32(ca);
+  if (!__builtin_constant_p(cb)) cb = pin32(cb);
+  f29 a = a_, b = b_;  // limbs as 32-bit values here (not sign-extended copies from elsewhere)
+  pin29(a);
+  pin29(b);
   double t = (double)ca * ((double)a.l[8] * 536870912.0 + (double)a.l[7]) +
              (double)cb * ((double)b.l[8] * 536870912.0 + (double)b.l[7]);
   const int32_t q = (int32_t)__builtin_rint(t * P29_TOP_INV);

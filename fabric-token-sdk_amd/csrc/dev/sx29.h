@@ -556,7 +556,9 @@ template <class X>
 FTS_HD q2 sq_fixed_line(const X& x, const q2& f, const LineCoef29& q, const f29& yP, const f29& xP, bool inf) {
   const int k = x.k;
   f29 a = (k == 0) ? q.r0.c0 : (k == 1) ? q.r0.c1 : (k == 2) ? q.r1.c0 : q.r1.c1;
-  f29 prod = f29_mulb(a, k < 2 ? yP : xP);
+  f29 m = k < 2 ? yP : xP;
+  pin29(m);
+  f29 prod = f29_mulb(a, m);
   x.put(SX_P + k, {prod, prod});
   x.sync();
   q2 l0 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
@@ -578,7 +580,9 @@ template <class X>
 FTS_HD q2 sq_fixed_line_n(const X& x, const q2& f, const LineCoef29& q, const f29& xq, const f29& yi, bool inf) {
   const int k = x.k;
   f29 a = (k == 0) ? q.r1.c0 : (k == 1) ? q.r1.c1 : (k == 2) ? q.r2.c0 : q.r2.c1;
-  f29 prod = f29_mulb(a, k < 2 ? xq : yi);
+  f29 m = k < 2 ? xq : yi;
+  pin29(m);
+  f29 prod = f29_mulb(a, m);
   x.put(SX_P + k, {prod, prod});
   x.sync();
   q2 l1 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
@@ -605,7 +609,9 @@ template <class X>
 FTS_HD q2 sq_fixed_line_nv(const X& x, const q2& f, const LineCoef29& q, const f29& v, bool inf) {
   const int k = x.k;
   f29 a = (k == 0) ? q.r1.c0 : (k == 1) ? q.r1.c1 : (k == 2) ? q.r2.c0 : q.r2.c1;
-  f29 prod = f29_mulb(a, v);
+  f29 m = v;
+  pin29(m);
+  f29 prod = f29_mulb(a, m);
   x.put(SX_P + k, {prod, prod});
   x.sync();
   q2 l1 = {x.get(SX_P + 0).c0, x.get(SX_P + 1).c0};
