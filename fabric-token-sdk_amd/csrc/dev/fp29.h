@@ -356,6 +356,63 @@ FTS_HD f29 f29_lin2(const f29& a_, int32_t ca, const f29& b_, int32_t cb) {
   return r;
 }
 
+// ca a + cb b without the quotient: one balanced carry sweep (limbs 0..7 in
+// [-2^28, 2^28), limb 8 the signed rest), the value unchanged -- for operands
+// that are only ever multiplied (|value| <= (|ca| + |cb|)(p/2 + e) stays far
+// inside the product's value budget, and the limbs inside its column budget)
+FTS_HD f29 f29_lin2_ns(const f29& a_, int32_t ca, const f29& b_, int32_t cb) {
+  f29 a = a_, b = b_;
+  pin29(a);
+  pin29(b);
+  f29 r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (int64_t)ca * a.l[i] + (int64_t)cb * b.l[i];
+    if (i < 8) {
+      r.l[i] = f29_bdigit(acc);
+      acc = (acc + F29_HALF) >> 29;
+    } else {
+      r.l[8] = (int32_t)acc;
+    }
+  }
+  return r;
+}
+
+// c0 x0 + c1 x1 + c2 x2 + c3 x3 - q p, balanced (|result| <= p/2 + e); |c_i|
+// <= 64 and balanced inputs (|limb| <= 2^29)
+FTS_HD f29 f29_lin4(const f29& x0_, int32_t c0, const f29& x1_, int32_t c1, const f29& x2_, int32_t c2,
+                    const f29& x3_, int32_t c3) {
+  f29 x0 = x0_, x1 = x1_, x2 = x2_, x3 = x3_;
+  pin29(x0);
+  pin29(x1);
+  pin29(x2);
+  pin29(x3);
+  c0 = pin32(c0);
+  c1 = pin32(c1);
+  c2 = pin32(c2);
+  c3 = pin32(c3);
+  double t = (double)c0 * ((double)x0.l[8] * 536870912.0 + (double)x0.l[7]) +
+             (double)c1 * ((double)x1.l[8] * 536870912.0 + (double)x1.l[7]) +
+             (double)c2 * ((double)x2.l[8] * 536870912.0 + (double)x2.l[7]) +
+             (double)c3 * ((double)x3.l[8] * 536870912.0 + (double)x3.l[7]);
+  const int32_t q = (int32_t)__builtin_rint(t * P29_TOP_INV);
+  f29 r;
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    acc += (int64_t)c0 * x0.l[i] + (int64_t)c1 * x1.l[i] + (int64_t)c2 * x2.l[i] + (int64_t)c3 * x3.l[i] -
+           (int64_t)q * P29B[i];
+    if (i < 8) {
+      r.l[i] = f29_bdigit(acc);
+      acc = (acc + F29_HALF) >> 29;
+    } else {
+      r.l[8] = (int32_t)acc;
+    }
+  }
+  return r;
+}
+
 FTS_HD q2 q2_neg(const q2& a) { return {f29_neg(a.c0), f29_neg(a.c1)}; }
 FTS_HD q2 q2_conj(const q2& a) { return {a.c0, f29_neg(a.c1)}; }
 FTS_HD q2 q2_zero() {
@@ -375,6 +432,9 @@ FTS_HD q2 q2_sel(bool c, const q2& a, const q2& b) {
 }
 // xi a = (9 a0 - a1) + (a0 + 9 a1) u, reduced
 FTS_HD q2 q2_mul_xi(const q2& a) { return {f29_lin2(a.c0, 9, a.c1, -1), f29_lin2(a.c0, 1, a.c1, 9)}; }
+// the same value carry-swept only (|value| <= 5 p + e): a multiplicand
+FTS_HD q2 q2_mul_xi_lazy(const q2& a) { return {f29_lin2_ns(a.c0, 9, a.c1, -1), f29_lin2_ns(a.c0, 1, a.c1, 9)}; }
+FTS_HD q2 q2_add(const q2& a, const q2& b) { return {f29_add(a.c0, b.c0), f29_add(a.c1, b.c1)}; }
 
 FTS_HD f29 f29_breduce(const f29& a) { return f29_lin2(a, 1, a, 0); }
 

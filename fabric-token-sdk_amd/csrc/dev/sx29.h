@@ -201,7 +201,7 @@ struct Sq {
 template <class X>
 FTS_HD void sq_pub(const X& x, int base, const q2& v) {
   x.put(base + x.k, v);
-  x.put(base + 6 + x.k, q2_mul_xi(v));
+  x.put(base + 6 + x.k, q2_mul_xi_lazy(v));  // xi v is only ever a multiplicand
 }
 
 // c = a * b, b published in SX_B / SX_BX (as sx_mul)
@@ -226,6 +226,47 @@ FTS_HD q2 sq_mulv(const X& x, const q2& a, const q2& b) {
   return sq_mul(x, a);
 }
 
+#ifndef FTS_SX_CYC2
+#define FTS_SX_CYC2 1
+#endif
+#if FTS_SX_CYC2
+// Granger-Scott cyclotomic squaring (as sx_cyc_sqr) with ONE Fp2 product per
+// lane.  The Fp4 pairs are (a_p, a_(p+3)); pair p's even lane (k = 2p) needs
+// a_p^2 + xi a_(p+3)^2, its odd lane (k = 3, 5, 1 for p = 0, 1, 2) the cross
+// product a_p a_(p+3).  The odd lane computes q = a_p a_(p+3) and hands it over
+// through LDS; the even lane computes P = (a_p + a_(p+3)) (a_p + xi a_(p+3)) =
+// a_p^2 + xi a_(p+3)^2 + (1 + xi) q, so
+//   even:   3 (P - (1 + xi) q) - 2 a_k
+//   k = 3, 5: 6 q + 2 a_k,   k = 1: 6 xi q + 2 a_k
+// (each a four-term linear map, f29_lin4).  The even lane's operands are
+// unreduced sums (limbs within 2^29: one product, 18 limb products of <= 2^58
+// per column).  Versus one general product plus one complex square per lane:
+// 3 x 81 limb products instead of 3 x 81 + 3 x 45.
+template <class X>
+FTS_HD q2 sq_cyc_sqr(X x, q2 a) {
+  const int k = x.k, odd = k & 1;
+  const int p = odd ? (k == 3 ? 0 : (k == 5 ? 1 : 2)) : (k >> 1);
+  sq_pub(x, SX_A, a);
+  x.sync();
+  q2 u = x.get(SX_A + p), v = x.get(SX_A + p + 3), xv = x.get(SX_AX + p + 3);
+  q2 s = q2_sel(odd, u, q2_add(u, v)), t = q2_sel(odd, v, q2_add(u, xv));
+  W29 w;
+  w29_init(w);
+  w29_mac(w, s, t);
+  q2 r = w29_reduce(w);
+  x.sync();                       // every lane has read the AX slots
+  if (odd) x.put(SX_AX + p, r);   // q of pair p
+  x.sync();
+  q2 q = x.get(SX_AX + p);
+  x.sync();  // q read before the next publish rewrites AX
+  // lane coefficients: out.c0 = cr r.c0 + b0 q.c0 + g0 q.c1 + ca a.c0,
+  //                    out.c1 = cr r.c1 + b1 q.c0 + g1 q.c1 + ca a.c1
+  int32_t cr = odd ? 0 : 3, ca = odd ? 2 : -2;
+  int32_t b0 = odd ? (k == 1 ? 54 : 6) : -30, g0 = odd ? (k == 1 ? -6 : 0) : 3;
+  int32_t b1 = odd ? (k == 1 ? 6 : 0) : -3, g1 = odd ? (k == 1 ? 54 : 6) : -30;
+  return {f29_lin4(r.c0, cr, q.c0, b0, q.c1, g0, a.c0, ca), f29_lin4(r.c1, cr, q.c0, b1, q.c1, g1, a.c1, ca)};
+}
+#else
 // Granger-Scott cyclotomic squaring (as sx_cyc_sqr): even lanes 3 r - 2 a,
 // odd lanes 6 r + 2 a, r the lane's one or two products.  Every lane runs one
 // general product (even lanes a_{m+3} (xi a_{m+3}), odd lanes their cross
@@ -248,6 +289,8 @@ FTS_HD q2 sq_cyc_sqr(X x, q2 a) {
   const int32_t cr = odd ? 6 : 3, ca = odd ? 2 : -2;
   return {f29_lin2(r.c0, cr, a.c0, ca), f29_lin2(r.c1, cr, a.c1, ca)};
 }
+
+#endif
 
 FTS_HD q2 sq_conj(int k, const q2& a) { return (k & 1) ? q2_neg(a) : a; }
 FTS_HD q2 sq_frob1(int k, const q2& a) { return q2_mul(q2_conj(a), q2_from_fp2(f2_const(FROB1[k]))); }

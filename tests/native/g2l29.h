@@ -28,7 +28,6 @@
 
 namespace fts {
 
-FTS_HD q2 q2_add(const q2& a, const q2& b) { return {f29_add(a.c0, b.c0), f29_add(a.c1, b.c1)}; }
 FTS_HD q2 q2_sub(const q2& a, const q2& b) { return {f29_sub(a.c0, b.c0), f29_sub(a.c1, b.c1)}; }
 // ca a + cb b, balanced
 FTS_HD q2 q2_lin(const q2& a, int32_t ca, const q2& b, int32_t cb) {
