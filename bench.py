@@ -278,6 +278,8 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     in HBM (P_i = (i + 1) G generated on the device, random 256-bit scalars),
     median wall-clock of `reps` synchronous runs after one warm-up; the result
     must be identical on every run (tests/test_msm.py checks it bit-exactly).
+    ms: scalars resident in HBM; ms_host_scalars: scalars copied from
+    page-locked host memory inside the timed call (ftz_msm_run_scalars).
     With ctx.options["msm_precompute"] the resident-point mode (window multiples
     stored at load, one bucket set, no Horner chain); load_s is the staging
     time including that precomputation."""
@@ -290,6 +292,7 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     t_load = time.perf_counter()
     m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
     t_load = time.perf_counter() - t_load
+    hbuf = None
     try:
         first = m.run()
         wall, dev = [], []
@@ -300,10 +303,25 @@ def msm_latency(ctx, lg, reps=5, seed=7):
             dev.append(m.info()["last_ms"])
             assert out == first, "MSM result changed between runs"
         info = m.info()
+        # the same MSM with the scalars starting in (page-locked) host memory:
+        # ftz_msm_run_scalars = chunked H2D copies overlapped with the fused key
+        # kernel, then the resident pipeline
+        hbuf = zkatdlog.HostBuffer(ctx, len(scal))
+        hbuf.write(scal)
+        assert m.run_scalars(hbuf) == first, "host-scalar MSM differs"
+        hwall = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = m.run_scalars(hbuf)
+            hwall.append((time.perf_counter() - t0) * 1e3)
+            assert out == first, "host-scalar MSM result changed between runs"
     finally:
         m.close()
+        if hbuf is not None:
+            hbuf.close()
     wall.sort()
     dev.sort()
+    hwall.sort()
     # algorithmic work of a GLV Pippenger with c-bit windows: one mixed addition
     # (7M + 4S) per (window, virtual point) and 2 Jacobian additions (12M + 4S)
     # per bucket in the running-sum reduction, in Montgomery products M
@@ -313,6 +331,8 @@ def msm_latency(ctx, lg, reps=5, seed=7):
     peak = madpeak(ctx.device)
     ach = m_prod * MAD_PER_M / (dev[reps // 2] * 1e-3)
     return {"n": n, "ms": round(wall[reps // 2], 3), "device_ms": round(dev[reps // 2], 3),
+            "ms_host_scalars": round(hwall[reps // 2], 3),
+            "host_scalars_note": "scalars in page-locked host memory: %d MB H2D inside the time" % (32 * n >> 20),
             "window_bits": c, "mode": "resident-point" if pre else "variable-base", "load_s": round(t_load, 3),
             "result": first.hex(),
             "roofline": {"bound": "valu", "achieved": round(ach / 1e12, 4), "peak": round(peak / 1e12, 4),

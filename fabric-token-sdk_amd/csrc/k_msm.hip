@@ -51,6 +51,19 @@ __global__ void __launch_bounds__(256) k_msm_keys(MsmPlan p, const uint32_t (*sc
   msm_job_keys(p, i, scal, key, val);
 }
 
+// the same from 32-byte big-endian scalars in HBM for points [i0, i1) (the
+// chunk a host copy has delivered): reduce mod r, keep the limbs for later runs,
+// and write the sort keys -- k_msm_load_scal and k_msm_keys in one pass
+__global__ void __launch_bounds__(256) k_msm_keys_raw(MsmPlan p, uint32_t i0, uint32_t i1, const uint8_t* raw,
+                                                      uint32_t (*scal)[8], uint32_t* key, uint32_t* val) {
+  uint32_t i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= i1) return;
+  uint32_t k[8];
+  be32_to_limbs_g(k, raw + 32 * (size_t)i);
+  fe_to_int(scal[i], fe_from_int<ModR>(k));
+  msm_job_keys(p, i, scal, key, val);
+}
+
 // one lane per sorted entry: bucket ranges
 __global__ void __launch_bounds__(256) k_msm_bounds(MsmPlan p, uint64_t total, const uint32_t* skey,
                                                     const uint32_t* sval, uint32_t* start, uint32_t* end) {

@@ -23,6 +23,13 @@ struct ftz_msm {
   DBuf<uint8_t> ok;
   hipEvent_t ev[2];
   bool ev_init = false;
+  // ftz_msm_run_scalars: raw big-endian scalars on the device, a copy stream and
+  // one event per chunk (created on first use)
+  DBuf<uint8_t> raw;
+  hipStream_t cstream = nullptr;
+  static constexpr int RAW_CHUNKS = 8;
+  hipEvent_t cev[RAW_CHUNKS + 1];
+  bool cev_init = false;
   float last_ms = 0;
   uint32_t radix_bits = 8;  // digit bits per radix-sort pass (8: rocPRIM's gfx950 default; 9: Radix9)
 };
@@ -227,19 +234,13 @@ extern "C" int ftz_msm_set_scalars(ftz_msm* m, const uint8_t* scalars) {
   return upload_scalars(m, scalars);
 }
 
-extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
-  if (!m || !out) return set_err(FTZ_E_INVALID, "null argument");
-  ftz_ctx* c = m->ctx;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HC(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
+// the pipeline after the sort keys (stream s, event ev[0] already recorded)
+static int msm_after_keys(ftz_msm* m, uint8_t out[64]) {
+  hipStream_t s = m->ctx->stream;
   const MsmPlan& p = m->p;
   size_t wb = (size_t)p.rw * p.buckets;
-  HC(hipEventRecord(m->ev[0], s));
-  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
   size_t wn = (size_t)p.windows * p.nv;
-  // (window, bucket)-sorted point lists: keys, stable radix sort, bucket ranges
-  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
+  // (window, bucket)-sorted point lists: stable radix sort, bucket ranges
   size_t tb = m->sort_tmp_bytes;
   HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
   HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
@@ -291,6 +292,69 @@ extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
+  if (!m || !out) return set_err(FTZ_E_INVALID, "null argument");
+  ftz_ctx* c = m->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const MsmPlan& p = m->p;
+  HC(hipEventRecord(m->ev[0], s));
+  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
+  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
+  return msm_after_keys(m, out);
+}
+
+// ftz_msm_run with the scalars copied from host memory in RAW_CHUNKS pieces on a
+// stream of the handle's own; the compute stream runs the key kernel of each
+// piece as soon as its copy has landed.  last_ms spans the first copy to the
+// result (events on both streams).
+extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t out[64]) {
+  if (!m || !scalars || !out) return set_err(FTZ_E_INVALID, "null argument");
+  ftz_ctx* c = m->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HC(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const MsmPlan& p = m->p;
+  if (!m->raw.p) HC(m->raw.alloc(32 * (size_t)p.n));
+  if (!m->cstream) HC(hipStreamCreateWithFlags(&m->cstream, hipStreamNonBlocking));
+  if (!m->cev_init) {
+    for (int k = 0; k <= ftz_msm::RAW_CHUNKS; k++) HC(hipEventCreateWithFlags(&m->cev[k], hipEventDisableTiming));
+    m->cev_init = true;
+  }
+  // the copies must not overwrite raw scalars a previous run still reads
+  HC(hipEventRecord(m->cev[ftz_msm::RAW_CHUNKS], s));
+  HC(hipStreamWaitEvent(m->cstream, m->cev[ftz_msm::RAW_CHUNKS], 0));
+  HC(hipEventRecord(m->ev[0], m->cstream));
+  uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(m->scal.p);
+  const uint32_t per = (p.n + ftz_msm::RAW_CHUNKS - 1) / ftz_msm::RAW_CHUNKS;
+  for (int k = 0; k < ftz_msm::RAW_CHUNKS; k++) {
+    uint32_t i0 = k * per, i1 = std::min<uint32_t>(p.n, i0 + per);
+    if (i0 >= i1) break;
+    HC(hipMemcpyAsync(m->raw.p + 32 * (size_t)i0, scalars + 32 * (size_t)i0, 32 * (size_t)(i1 - i0),
+                      hipMemcpyHostToDevice, m->cstream));
+    HC(hipEventRecord(m->cev[k], m->cstream));
+    HC(hipStreamWaitEvent(s, m->cev[k], 0));
+    k_msm_keys_raw<<<blocks(i1 - i0, 256), 256, 0, s>>>(p, i0, i1, m->raw.p, scal, m->key.p, m->val.p);
+  }
+  return msm_after_keys(m, out);
+}
+
+extern "C" int ftz_host_alloc(size_t bytes, void** out) {
+  if (!out) return set_err(FTZ_E_INVALID, "null argument");
+  *out = nullptr;
+  if (!bytes) return FTZ_SUCCESS;
+  if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+    *out = nullptr;
+    return set_err(FTZ_E_NOMEM, "page-locked host allocation failed");
+  }
+  return FTZ_SUCCESS;
+}
+
+extern "C" void ftz_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 extern "C" int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits) {
   if (!m) return set_err(FTZ_E_INVALID, "null argument");
   if (last_ms) *last_ms = m->last_ms;
@@ -304,6 +368,12 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
   if (m->ev_init)
   {
     for (int k = 0; k < 2; k++) (void)hipEventDestroy(m->ev[k]);
+  }
+  if (m->cev_init)
+    for (int k = 0; k <= ftz_msm::RAW_CHUNKS; k++) (void)hipEventDestroy(m->cev[k]);
+  if (m->cstream) {
+    (void)hipStreamSynchronize(m->cstream);
+    (void)hipStreamDestroy(m->cstream);
   }
   delete m;
 }

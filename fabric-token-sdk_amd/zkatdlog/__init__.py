@@ -371,6 +371,22 @@ class Msm:
         _check(self._lib.ftz_msm_run(self._h, out), self._lib)
         return bytes(out)
 
+    def run_scalars(self, scalars):
+        """set the scalars and run in one call (ftz_msm_run_scalars): scalars is
+        n x 32 bytes (bytes, or a HostBuffer for page-locked memory)"""
+        if isinstance(scalars, HostBuffer):
+            if scalars.size < 32 * self.n:
+                raise ValueError("scalars must be n x 32 bytes")
+            ptr, keep = scalars.ptr, None
+        else:
+            keep = bytes(scalars)
+            if len(keep) != 32 * self.n:
+                raise ValueError("scalars must be n x 32 bytes")
+            ptr = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p)
+        out = (ctypes.c_uint8 * 64)()
+        _check(self._lib.ftz_msm_run_scalars(self._h, ptr, out), self._lib)
+        return bytes(out)
+
     def info(self):
         ms, c = ctypes.c_float(), ctypes.c_uint32()
         _check(self._lib.ftz_msm_info(self._h, ctypes.byref(ms), ctypes.byref(c)), self._lib)
@@ -383,6 +399,32 @@ class Msm:
 
     def __del__(self):
         self.close()
+
+
+class HostBuffer:
+    """Page-locked host memory (ftz_host_alloc): inputs staged here copy to the
+    device at the full link rate."""
+
+    def __init__(self, ctx, size):
+        self._lib, self.size, self.ptr = ctx._lib, int(size), ctypes.c_void_p()
+        _check(self._lib.ftz_host_alloc(self.size, ctypes.byref(self.ptr)), self._lib)
+
+    def write(self, data, offset=0):
+        data = bytes(data)
+        if offset + len(data) > self.size:
+            raise ValueError("write past the end of the buffer")
+        ctypes.memmove(self.ptr.value + offset, data, len(data))
+
+    def close(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            self._lib.ftz_host_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Prover:

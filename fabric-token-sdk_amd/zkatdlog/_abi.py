@@ -281,7 +281,7 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
-           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
+           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_run_scalars", "ftz_host_alloc", "ftz_host_free", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_token_request_decode", "ftz_verify_token_requests", "ftz_verify_token_requests_batched", "ftz_ctx_request_stats",
            "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_ctx_prover_stats", "ftz_prover_load_transfers", "ftz_prover_load_issues",
@@ -341,6 +341,10 @@ def load():
     lib.ftz_msm_load_gen.argtypes = [vp, sz, u32, ctypes.c_char_p, ctypes.POINTER(vp)]
     lib.ftz_msm_run.argtypes = [vp, u8p]
     lib.ftz_msm_set_scalars.argtypes = [vp, ctypes.c_char_p]
+    lib.ftz_msm_run_scalars.argtypes = [vp, ctypes.c_void_p, u8p]
+    lib.ftz_host_alloc.argtypes = [sz, ctypes.POINTER(vp)]
+    lib.ftz_host_free.argtypes = [vp]
+    lib.ftz_host_free.restype = None
     lib.ftz_msm_info.argtypes = [vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(u32)]
     lib.ftz_msm_destroy.argtypes = [vp]
     lib.ftz_msm_destroy.restype = None

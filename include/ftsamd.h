@@ -412,6 +412,16 @@ int ftz_msm_run(ftz_msm* m, uint8_t out[64]);
 /* replace the scalars of a loaded MSM (n x 32 bytes big-endian); the points, and
  * with msm_precompute their window multiples, stay resident */
 int ftz_msm_set_scalars(ftz_msm* m, const uint8_t* scalars);
+/* set the scalars and run in one call, for scalars that start in host memory:
+ * the 32n bytes are copied in chunks on a copy stream while the key kernel of
+ * the chunks already on the device runs (big-endian -> reduced limbs -> GLV
+ * halves -> window digits in one pass), then the rest of ftz_msm_run.  The
+ * scalars stay loaded, as with ftz_msm_set_scalars.  Page-locked memory
+ * (ftz_host_alloc) copies at the full link rate. */
+int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t out[64]);
+/* page-locked host memory for staging large inputs (scalars, proof bytes) */
+int ftz_host_alloc(size_t bytes, void** out);
+void ftz_host_free(void* p);
 /* device time of the last ftz_msm_run in ms (HIP events) and the window size */
 int ftz_msm_info(const ftz_msm* m, float* last_ms, uint32_t* window_bits);
 void ftz_msm_destroy(ftz_msm* m);

@@ -167,6 +167,38 @@ def test_gpu_msm_rejects_bad_point(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True])
+def test_gpu_msm_run_scalars_from_host(ctx, pinned):
+    """ftz_msm_run_scalars (chunked host copies overlapped with the fused key
+    kernel): the known-log sum for new scalars, from pageable and page-locked
+    memory, with n not a multiple of the chunk count; the scalars stay loaded
+    for a following ftz_msm_run"""
+    import zkatdlog
+    n, off = (1 << 18) + 3, 777
+    rng = random.Random(99 + pinned)
+    k0 = [rng.randrange(C.R) for _ in range(n)]
+    k1 = [rng.randrange(1 << 256) for _ in range(n)]  # unreduced: the device reduces mod r
+    b0 = b"".join(k.to_bytes(32, "big") for k in k0)
+    b1 = b"".join(k.to_bytes(32, "big") for k in k1)
+    m = zkatdlog.Msm(ctx, scalars=b0, gen_offset=off)
+    buf = None
+    try:
+        if pinned:
+            buf = zkatdlog.HostBuffer(ctx, len(b1))
+            buf.write(b1)
+            got = m.run_scalars(buf)
+        else:
+            got = m.run_scalars(b1)
+        again = m.run()
+    finally:
+        m.close()
+        if buf is not None:
+            buf.close()
+    want = C.g1_mul(C.G1_GEN, sum(k * (i + off) for i, k in enumerate(k1)) % C.R)
+    assert got == C.g1_bytes(want) and again == got
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("lg,bits", [(16, 256), (20, 256), (16, 3), (18, 64)])
 def test_gpu_msm_known_logs(ctx, lg, bits):
     """bits < 256: skewed scalars (a few hot buckets, most windows empty)."""
