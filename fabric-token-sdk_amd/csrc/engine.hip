@@ -197,7 +197,10 @@ void Engine::dispatcher() {
     // first / tail passes to shorten a job's fill and drain were measured:
     // 420-442k vs 676-688k transfers/s on a 20-step job -- a pass's planning and
     // kernel chain have a fixed latency that smaller passes do not shed.)
-    const size_t Bp = B;
+    // the first pass of a job (nothing in flight) may be smaller: it reaches the
+    // device after a shorter planning step (ftz_options.first_pass)
+    const size_t fp1 = ctx->opt.first_pass;
+    const size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
     size_t bytes = 0;
     uint64_t pairs = 0;
     const uint64_t pair_budget = 4 * (uint64_t)Bp, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);

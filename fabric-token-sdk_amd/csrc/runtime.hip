@@ -53,6 +53,7 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->fexp = FTZ_FEXP_EXACT;
   o->hold_inflight = 2;
   o->small_pass = 4096;
+  o->first_pass = 4096;
   o->msm_glv = 1;
   o->prover_tables = 1;
 }

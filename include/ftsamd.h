@@ -128,6 +128,11 @@ typedef struct {
                            retry.  0: never build them (variable-base path).            */
   uint32_t msm_radix_bits; /* MSM sort digit bits per radix pass: 0 = the planner's choice
                            (9 where it saves a pass, else 8), or 8 / 9                   */
+  uint32_t first_pass;  /* proofs in a pass dispatched while no pass is in flight (the
+                           start of a job): default 4096, 0 = batch.  A smaller first
+                           pass reaches the device after half the planning step: a
+                           20-step bench job 707k -> 725k transfers/s (mean of 4 on one
+                           box, profiles/r05/first_pass_ab.txt)                        */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);

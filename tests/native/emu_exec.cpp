@@ -378,6 +378,47 @@ int emu_plan_prove_ms(void* ctx, size_t n, const ftz_transfer_witness* w, int th
   return 0;
 }
 
+// TEST-ONLY diagnostic: host time of one verifier pass's planning as the
+// engine runs it (plan_items on a pool of `threads`, then flat_layout +
+// flat_write into one blob), median of `reps`: out_ms[0] items, [1] layout +
+// write, [2] blob bytes, [3] bytes uploaded, [4 + s] bytes of section s.
+int emu_plan_verify_ms(void* ctx, size_t n, const ftz_transfer* tx, int threads, int reps, double* out_ms) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  std::vector<PlanItem> items(n);
+  for (size_t i = 0; i < n; i++) {
+    memset(&items[i], 0, sizeof(PlanItem));
+    items[i].kind = 0;
+    items[i].t = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+  }
+  WorkPool pool(threads);
+  PlanWork work;
+  FlatPlan fp;
+  std::vector<uint8_t> blob;
+  std::vector<double> a, b;
+  using Clk = std::chrono::steady_clock;
+  for (int r = 0; r < reps; r++) {
+    auto t0 = Clk::now();
+    plan_items(c->pp, n, items.data(), work, pool);
+    auto t1 = Clk::now();
+    std::string e = flat_layout(work, false, fp);
+    if (!e.empty()) return -2;
+    if (blob.size() < fp.bytes) blob.resize(fp.bytes);
+    flat_write(work, fp, blob.data(), c->const_bytes.data(), pool);
+    auto t2 = Clk::now();
+    a.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+    b.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+  }
+  std::sort(a.begin(), a.end());
+  std::sort(b.begin(), b.end());
+  out_ms[0] = a[a.size() / 2];
+  out_ms[1] = b[b.size() / 2];
+  out_ms[2] = (double)fp.bytes;
+  out_ms[3] = (double)fp.upload;
+  for (int k = 0; k < PS_COUNT; k++)
+    out_ms[4 + k] = (double)((k + 1 < PS_COUNT ? fp.off[k + 1] : fp.bytes) - fp.off[k]);
+  return 0;
+}
+
 long emu_prove_issues(void* ctx, size_t n, const ftz_issue_witness* w, uint8_t* buf, size_t cap, size_t* offsets,
                       int32_t* codes, char* err, size_t errlen) {
   EmuCtx* c = (EmuCtx*)ctx;
