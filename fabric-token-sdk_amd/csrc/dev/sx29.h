@@ -575,8 +575,12 @@ FTS_HD q2 sq_mul_line_r(const X& x, const q2& f, const q2& l0, const q2& l1, con
 }
 
 // f * (pair-2 line s), the three evaluated coefficients read from the line
-// buffer inside the term loop (one at a time: the Karatsuba rows leave no room
-// for all three next to the accumulator)
+// buffer inside the term loop, one at a time (FTS_MILLER_EVLINE_IN_LOOP; the
+// default loads all three before the product, sq_mul_line_r, which hides the
+// load latency and fits the registers since the multiplicands are pinned)
+#ifndef FTS_MILLER_EVLINE_IN_LOOP
+#define FTS_MILLER_EVLINE_IN_LOOP 0
+#endif
 template <class X>
 FTS_HD q2 sq_mul_evline(const X& x, const q2& f, const EvLineDev* l2, uint32_t s, uint32_t idx, uint32_t njobs) {
   sq_pub(x, SX_A, f);
@@ -729,7 +733,12 @@ FTS_HD q2 sq_miller_fn(const X& x, const LineCoef29* qlines_n, const g1a& P1, co
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sq_sqr(x, f);
     f = sq_fixed_line_n(x, f, qlines_n[s], xq, yi, P1.inf);
+#if FTS_MILLER_EVLINE_IN_LOOP
     f = sq_mul_evline(x, f, l2, s, idx, njobs);
+#else
+    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
+                      evline_ld29(l2, s, 2, idx, njobs));
+#endif
   }
   return f;
 }
@@ -746,7 +755,12 @@ FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const
     bool sq = s < 64 ? ((MILLER_SQR.lo >> s) & 1) : ((MILLER_SQR.hi >> (s - 64)) & 1);
     if (sq) f = sq_sqr(x, f);
     f = sq_fixed_line(x, f, qlines[s], yP, xP, P1.inf);
+#if FTS_MILLER_EVLINE_IN_LOOP
     f = sq_mul_evline(x, f, l2, s, idx, njobs);
+#else
+    f = sq_mul_line_r(x, f, evline_ld29(l2, s, 0, idx, njobs), evline_ld29(l2, s, 1, idx, njobs),
+                      evline_ld29(l2, s, 2, idx, njobs));
+#endif
   }
   return f;
 }
