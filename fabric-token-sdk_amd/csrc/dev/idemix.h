@@ -103,7 +103,10 @@ template <>
 struct NymCurve<fp> {
   static constexpr uint32_t G1_BYTES = 64;
   static constexpr uint32_t PRE = 4 + 64 + 64 + 32;  // 164, then the message, then TAIL bytes
-  static constexpr uint32_t TAIL = 2;                // proofData is sized for 65-byte points
+  // proofData is sized for 65-byte points, so two zero bytes follow the message
+  // [EXT, parity unpinned: the issuer key's own proof uses the same sizing, no
+  // reference file holds a BN254 NymSignature]
+  static constexpr uint32_t TAIL = 2;
   FTS_HD static fp beta() { return fe_const<ModP>(GLV_BETA); }
   FTS_HD static fp from_canon(const uint32_t a[8]) { return fe_from_int<ModP>(a); }
   FTS_HD static void to_int(uint32_t out[8], const fp& a) { fe_to_int(out, a); }

@@ -477,10 +477,14 @@ void decode_owner_signature(const uint8_t* owner, size_t owner_len, const uint8_
       fl[q] = pr[q] ? v[q].len : 0;
     }
     // Zr.Bytes() of the Nonce (common.BigToBytes): an integer >= 2^256 panics
+    // [EXT, parity unpinned: no reference file holds a BN254 NymSignature;
+    // tests/golden/idemix_bn254_golden.json "parity"]
     if (!be_to32(fp_[3], fl[3], out.ints[5]))
       return fail(FTZ_ERR_SIGNATURE, "failure [runtime error: makeslice: len out of range]");
     uint8_t cr[32];
     be_mod_r(fp_[0], fl[0], cr);
+    // ProofC >= r (or longer than 32 bytes) can never equal HashToZr(c || Nonce) < r:
+    // an all-ones sentinel that no hash matches [EXT, parity unpinned]
     if (!be_to32(fp_[0], fl[0], out.ints[2]) || be32_geq_r(out.ints[2])) memset(out.ints[2], 0xff, 32);
     be_mod_r(fp_[1], fl[1], out.ints[3]);
     be_mod_r(fp_[2], fl[2], out.ints[4]);

@@ -246,6 +246,14 @@ def main():
     out = {
         "comment": "idemix owner signatures on BN254, the deployed idemix curve (SURVEY 8(f) row 3); "
                    "issuer = cmd/tokengen/testdata/idemix/ca; made by make_idemix_bn254.py",
+        "parity": "UNPINNED for the signature transcript: no file under the reference holds a BN254 "
+                  "NymSignature, so the expected verdicts are the oracle's restatement of IBM/idemix + mathlib "
+                  "[EXT]; pinned by the reference's tokengen issuer key: HSk, HRand, HAttrs, W, ipk.Hash, the "
+                  "G1/G2 RawBytes encodings and HashToZr (tests/test_idemix.py issuer-key proof). The [EXT] "
+                  "choices a real Go-made NymSignature would confirm or refute: the 2-byte transcript tail "
+                  "(proofData sized for 65-byte points, dev/idemix.h NymCurve<fp>::TAIL), ProofC >= r never "
+                  "matching (host/idemix.cpp), and Nonce >= 2^256 mapped to a recovered panic "
+                  "(FTZ_ERR_SIGNATURE).",
         "ext_assumptions": {
             "nym_signature": "IBM/idemix NymSignature.Ver over mathlib BN254: t = HSk^SSk HRand^SRNym Nym^-C, "
                              "c = HashToZr('sign'||t||Nym||ipk.Hash@132||msg@164||00 00) "
