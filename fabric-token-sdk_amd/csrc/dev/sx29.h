@@ -39,6 +39,8 @@ namespace fts {
 #ifndef FTS_SX_KARA
 #define FTS_SX_KARA 1
 #endif
+// a limb product as an unsigned 64-bit term (rows that may wrap modulo 2^64)
+FTS_HD uint64_t w29_p(int32_t a, int32_t b) { return (uint64_t)((int64_t)a * (int64_t)b); }
 #if FTS_SX_KARA
 struct W29 {
   uint64_t u[17], v[17], w[17];
@@ -47,7 +49,6 @@ FTS_HD void w29_init(W29& w) {
 #pragma unroll
   for (int i = 0; i < 17; i++) w.u[i] = w.v[i] = w.w[i] = 0;
 }
-FTS_HD uint64_t w29_p(int32_t a, int32_t b) { return (uint64_t)((int64_t)a * (int64_t)b); }
 // w += a b (a, b balanced, or limbs within 2^29)
 FTS_HD void w29_mac(W29& w, const q2& a, const q2& b) {
   FTS_COUNT_MAD(192);  // the 32-bit equivalent (3 wide products), for opcounts
@@ -155,6 +156,32 @@ FTS_HD void w29_sqr_acc(W29& w, const q2& s) {
 }
 #endif
 
+// one Fp2 product a b (a, b limbs within 2^29), Karatsuba by columns: each
+// column's three sums U_c, V_c, W_c are formed and folded into re_c = U_c - V_c,
+// im_c = W_c - U_c - V_c at once, so only the two result rows stay live (68
+// VGPRs instead of the three accumulation rows' 102) -- for a lone product
+FTS_HD q2 w29_prod1(const q2& a, const q2& b) {
+  FTS_COUNT_MAD(192);  // as w29_mac (the reductions count themselves)
+  FTS_SCHED_FENCE();
+  const f29 sa = f29_add(a.c0, a.c1), sb = f29_add(b.c0, b.c1);
+  int64_t re[17], im[17];
+#pragma unroll
+  for (int c = 0; c < 17; c++) {
+    uint64_t u = 0, v = 0, w = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = c - i;
+      if (j < 0 || j > 8) continue;
+      u += w29_p(a.c0.l[i], b.c0.l[j]);
+      v += w29_p(a.c1.l[i], b.c1.l[j]);
+      w += w29_p(sa.l[i], sb.l[j]);
+    }
+    re[c] = (int64_t)(u - v);
+    im[c] = (int64_t)(w - (u + v));
+  }
+  return {w29_redc(re), w29_redc(im)};
+}
+
 FTS_HD q2 q2_mul(const q2& a, const q2& b) {
   W29 w;
   w29_init(w);
@@ -250,10 +277,7 @@ FTS_HD q2 sq_cyc_sqr(X x, q2 a) {
   x.sync();
   q2 u = x.get(SX_A + p), v = x.get(SX_A + p + 3), xv = x.get(SX_AX + p + 3);
   q2 s = q2_sel(odd, u, q2_add(u, v)), t = q2_sel(odd, v, q2_add(u, xv));
-  W29 w;
-  w29_init(w);
-  w29_mac(w, s, t);
-  q2 r = w29_reduce(w);
+  q2 r = w29_prod1(s, t);
   x.sync();                       // every lane has read the AX slots
   if (odd) x.put(SX_AX + p, r);   // q of pair p
   x.sync();
@@ -317,6 +341,9 @@ FTS_HD q2 sq_expt(X x, const P& pk, int src, int ps) {
 #pragma nounroll
   for (int i = 61; i >= 0; i--) {
     r = sq_cyc_sqr(x, r);
+    // in the 18-slot layout the multiplier's slots alias SX_AX, which the
+    // squaring overwrites: republish before every multiplication
+    if (X::B == SX_AX) cur = 0;
     if ((BN_X_W4_NZ >> i) & 1) {
       int m = ((BN_X_W4_M3 >> i) & 1) ? 3 : (((BN_X_W4_M5 >> i) & 1) ? 5 : (((BN_X_W4_M7 >> i) & 1) ? 7 : 1));
       if (m != cur) {

@@ -40,8 +40,20 @@ __global__ void __launch_bounds__(64, 2) k_fexp_easy(uint32_t n, const F12Dev* f
 // from slot ps (a is re-read from src).  24 LDS slots (A, AX, B, BX): 17.4 KB
 // per workgroup, so LDS admits the two waves per SIMD that the registers allow
 // (the 30-slot region's 21.7 KB admitted 1.75).
+#ifndef FTS_EXPT_SLOTS
+#define FTS_EXPT_SLOTS 24
+#endif
+#if FTS_EXPT_SLOTS == 18
+// 18 LDS slots (A, AX = B, BX: the multiplier republished after every
+// squaring), 13 KB per workgroup: LDS admits three waves per SIMD, but the
+// 168 VGPRs of three waves spill (164 B per lane) and the launch ran 4.02-4.06
+// against 3.56-3.58 ms per 8192-proof pass (profiles/r05/expt_slots_ab.txt)
+__global__ void __launch_bounds__(64, 3) k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps) {
+  SQ_KERNEL_PROLOGUE_B(n, 18, 6)
+#else
 __global__ void __launch_bounds__(64, 2) k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps) {
   SQ_KERNEL_PROLOGUE_B(n, 24, 12)
+#endif
   FEXP_PARK
   pk.put(dst, sq_expt(x, pk, src, ps));
 }
