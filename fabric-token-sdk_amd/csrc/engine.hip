@@ -70,6 +70,7 @@ struct Engine {
   std::deque<Request*> q;
   size_t pending = 0;        // proofs queued and not yet handed to a batch (under mu)
   bool disp_holding = false;  // the dispatcher is waiting out a window (under mu)
+  bool tail_split_done = false;  // the queue's last pass was cut in two (under mu; reset by new requests)
   std::vector<ftz_batch*> slots;
   std::deque<ftz_batch*> free_slots, inflight;
   ftz_engine_stats st{};
@@ -199,8 +200,14 @@ void Engine::dispatcher() {
     // kernel chain have a fixed latency that smaller passes do not shed.)
     // the first pass of a job (nothing in flight) may be smaller: it reaches the
     // device after a shorter planning step (ftz_options.first_pass)
-    const size_t fp1 = ctx->opt.first_pass;
-    const size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
+    const size_t fp1 = ctx->opt.first_pass, ts = ctx->opt.tail_split;
+    size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
+    // the queue's last pass in two halves whose kernel chains overlap
+    // (ftz_options.tail_split)
+    if (ts && !tail_split_done && !inflight.empty() && pending <= Bp && pending >= 2 * (size_t)ts) {
+      Bp = (pending + 1) / 2;
+      tail_split_done = true;  // the second half goes whole
+    }
     size_t bytes = 0;
     uint64_t pairs = 0;
     const uint64_t pair_budget = 4 * (uint64_t)Bp, ex = (uint64_t)std::max<int64_t>(1, ctx->pp.exponent);
@@ -351,6 +358,7 @@ int engine_verify(ftz_ctx* c, size_t n, const ftz_transfer* tx, const ftz_issue*
     if (e->stop) return set_err(FTZ_E_INVALID, "context is being destroyed");
     e->q.push_back(&r);
     e->pending += n;
+    e->tail_split_done = false;
     // a dispatcher waiting out a window only needs waking for a full batch
     if (!e->disp_holding || e->pending >= e->ctx->opt.batch) e->cv_q.notify_one();
   }

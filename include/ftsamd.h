@@ -133,6 +133,10 @@ typedef struct {
                            pass reaches the device after half the planning step: a
                            20-step bench job 707k -> 725k transfers/s (mean of 4 on one
                            box, profiles/r05/first_pass_ab.txt)                        */
+  uint32_t tail_split;  /* the last pass of the queue (pending <= batch) is cut in two
+                           halves of at least this many proofs, whose kernel chains then
+                           overlap: 0 (default) = off (measured no gain on the 20-step
+                           job, profiles/r05/tail_split_ab.txt)                         */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
