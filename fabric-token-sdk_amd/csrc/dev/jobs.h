@@ -620,9 +620,19 @@ FTS_HD void g1dev_get(const G1Dev& d, fp& a, fp& b) {
 // tb: 16 G1Dev entries at stride st (device: a per-batch buffer laid out
 // [entry][job] so that a wave's accesses coalesce; host: a local array).
 // Entries 0..7 hold the table, 8..15 the (Z, prefix) pairs while it is built.
+// g1_mul_glv16_iso: k V for V = (X:Y:Z) Jacobian on E, Z != 0, without
+// bringing V to affine first: (X, Y) is an affine point of the isomorphic curve
+// y^2 = x^3 + b Z^6 (psi(x, y) = (x Z^2, y Z^3) maps E onto it and commutes with
+// negation and phi(x, y) = (beta x, y)), so the same code runs on (X, Y) and
+// the result (X':Y':Z') there is (X':Y':Z' Z) on E -- one product for an
+// inversion.
+FTS_HD g1j g1_mul_glv16_iso(const g1a& p, const fp& zin, const uint32_t k[8], G1Dev* tb, size_t st);
 FTS_HD g1j g1_mul_glv16(const g1a& p, const uint32_t k[8], G1Dev* tb, size_t st) {
+  if (p.inf) return jac_inf<fp>();
+  return g1_mul_glv16_iso(p, fe_one<ModP>(), k, tb, st);
+}
+FTS_HD g1j g1_mul_glv16_iso(const g1a& p, const fp& zin, const uint32_t k[8], G1Dev* tb, size_t st) {
   g1j acc = jac_inf<fp>();
-  if (p.inf) return acc;
   uint32_t k1[4], k2[4];
   bool n1, n2;
   glv_split(k, k1, n1, k2, n2);
@@ -701,7 +711,7 @@ FTS_HD g1j g1_mul_glv16(const g1a& p, const uint32_t k[8], G1Dev* tb, size_t st)
     if (m2) acc = nacc;
   }
 #endif
-  acc.z = acc.z * Zc;  // back to E (the point at infinity keeps z = 0)
+  acc.z = acc.z * (Zc * zin);  // back to E (the point at infinity keeps z = 0)
   return acc;
 }
 
@@ -782,8 +792,64 @@ FTS_HD g1j g1j_load(const G1JDev& d) {
   return p;
 }
 
-// vtab: per-batch scratch of 16 n G1Dev entries for the variable parts'
-// window tables (device); the host emulation passes nullptr (local table).
+// The variable point V of a G1 job's variable term, in Jacobian form, formed
+// inline by doublings and mixed additions of the proof points (no call frames:
+// out-of-line point routines here cost k_g1_part 400 B of scratch per lane on
+// every launch) and handed to the GLV multiplication without an inversion
+// (g1_mul_glv16_iso).
+//   - a single unit-weight point;
+//   - sum_t b^(count-1-t) P_t (VT_HORNER, the range-equality commitment sum)
+//     with b a power of two (PP-B, b = 16): Horner, log2 b doublings a term;
+//   - otherwise sum_t c_t P_t (c_t = b^(count-1-t), which fits 64 bits when the
+//     planner marks the powers exact, or the explicit weights w_t) by one joint
+//     left-to-right double-and-add over the c_t's bits (PP-A, b = 100, e = 2:
+//     6 doublings and 4 additions).
+FTS_HD uint64_t vterm_w(const VTerm& v) { return ((uint64_t)v.w_hi << 32) | v.w_lo; }
+FTS_HD g1j g1_var_point(const G1Job& j, const VTerm* vterms, const G1Dev* pts) {
+  const VTerm& v0 = vterms[j.vstart];
+  const uint64_t b = vterm_w(v0);
+  const bool horner = (v0.flags & VT_HORNER) != 0;
+  if (j.vcount == 1 && (horner || b == 1)) return jac_from_aff(g1_load(pts[v0.pt]));
+  if (horner && (b & (b - 1)) == 0) {
+    const int top = b ? 63 - __builtin_clzll(b) : 0;
+    g1j V = jac_from_aff(g1_load(pts[v0.pt]));
+    for (uint32_t t = 1; t < j.vcount; t++) {
+#pragma nounroll
+      for (int q = 0; q < top; q++) V = jac_dbl(V);
+      V = jac_add_aff(V, g1_load(pts[vterms[j.vstart + t].pt]));
+    }
+    return b ? V : jac_from_aff(g1_load(pts[vterms[j.vstart + j.vcount - 1].pt]));
+  }
+  // joint double-and-add; term t's weight: horner b^(count-1-t), else w_t
+  uint64_t cmax = 0;
+  if (horner) {
+    cmax = 1;
+    for (uint32_t t = 1; t < j.vcount; t++) cmax *= b;
+  } else {
+    for (uint32_t t = 0; t < j.vcount; t++) cmax |= vterm_w(vterms[j.vstart + t]);
+  }
+  g1j V = jac_inf<fp>();
+  if (cmax == 0) return V;
+  const int top = 63 - __builtin_clzll(cmax);
+#pragma nounroll
+  for (int q = top; q >= 0; q--) {
+    if (q != top) V = jac_dbl(V);
+    uint64_t c = 1;
+#pragma nounroll
+    for (uint32_t t = j.vcount; t-- > 0;) {
+      const VTerm& vt = vterms[j.vstart + t];
+      const uint64_t w = horner ? c : vterm_w(vt);
+      if ((w >> q) & 1) V = jac_add_aff(V, g1_load(pts[vt.pt]));
+      c *= b;
+    }
+  }
+  return V;
+}
+
+// Part f of job jb (i = f n + jb): f < 3 the fixed-base term f, f = 3 the
+// variable term by GLV.  vtab: per-batch scratch of 16 n G1Dev entries for the
+// variable parts' window tables (device); the host emulation may pass nullptr
+// (a local table).
 FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* vterms, const G1Dev* pts,
                         const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part, G1Dev* vtab) {
   uint32_t f = i / n, jb = i - f * n;
@@ -792,47 +858,20 @@ FTS_HD void job_g1_part(const G1Job* jobs, uint32_t n, uint32_t i, const VTerm* 
   if (f < 3) {
     if (f < j.nfix) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
   } else if (j.vscal != NONE) {
-    g1a Va;
-    const VTerm& v0 = vterms[j.vstart];
-    if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
-      Va = g1_load(pts[v0.pt]);
-    } else if (v0.flags & VT_HORNER) {
-      // sum_t b^(count-1-t) P_t in Horner order, b = the first term's weight;
-      // the multiple b V by an inline double-and-add from b's top bit (a call
-      // of its own here cost k_g1_part 31 VGPRs and a wave per SIMD)
-      const uint64_t b = ((uint64_t)v0.w_hi << 32) | v0.w_lo;
-      const int top = 63 - __builtin_clzll(b);
-      g1j V = jac_from_aff(g1_load(pts[v0.pt]));
-      for (uint32_t t = 1; t < j.vcount; t++) {
-        const g1j V1 = V;
-#pragma nounroll
-        for (int q = top - 1; q >= 0; q--) {
-          V = jac_dbl(V);
-          if ((b >> q) & 1) V = jac_add(V, V1);
-        }
-        V = jac_add_aff(V, g1_load(pts[vterms[j.vstart + t].pt]));
-      }
-      Va = jac_to_aff(V);
-    } else {
-      g1j V = jac_inf<fp>();
-      for (uint32_t t = 0; t < j.vcount; t++) {
-        const VTerm& vt = vterms[j.vstart + t];
-        g1a P = g1_load(pts[vt.pt]);
-        uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
-        if (w == 1) {
-          V = jac_add_aff(V, P);
-        } else {
-          V = jac_add(V, aff_mul_u64(P, w));
-        }
-      }
-      Va = jac_to_aff(V);
-    }
-    if (j.vneg) Va = aff_neg(Va);
+    g1j V = g1_var_point(j, vterms, pts);
+    if (j.vneg) V = jac_neg(V);
+#if FTS_G1_VAR_W == 16
 #if defined(__HIP_DEVICE_COMPILE__)
-    acc = G1_MUL_VAR(Va, scal[j.vscal], vtab + jb, n);
+    G1Dev* tb = vtab + jb;
+    const size_t st = n;
 #else
     G1Dev loc[16];
-    acc = G1_MUL_VAR(Va, scal[j.vscal], vtab ? vtab + jb : loc, vtab ? n : 1);
+    G1Dev* tb = vtab ? vtab + jb : loc;
+    const size_t st = vtab ? n : 1;
+#endif
+    if (!is_zero(V.z)) acc = g1_mul_glv16_iso(g1a{V.x, V.y, false}, V.z, scal[j.vscal], tb, st);
+#else
+    acc = g1_mul_glv(jac_to_aff(V), scal[j.vscal]);
 #endif
   }
   g1j_store(part[i], acc);

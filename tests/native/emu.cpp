@@ -3,6 +3,7 @@
 // Lets the CPU test tier check every formula the HIP kernels run against the
 // independent Python oracle without a GPU.  Never loaded by the product.
 #include <string.h>
+#include <vector>
 #include "../../fabric-token-sdk_amd/csrc/dev/pairing.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sha256.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
@@ -75,6 +76,33 @@ int emu_g1_mul_glv(const uint8_t* p64, const uint8_t* k32, int which, uint8_t* o
   g1a p = ld_g1(p64);
   G1Dev tb[16];
   g1a r = jac_to_aff(which ? g1_mul_glv16(p, k, tb, 1) : g1_mul_glv(p, k));
+  g1_to_bytes(out64, r);
+  return g1_on_curve(r) ? 0 : 1;
+}
+// The variable part of one G1 job (job_g1_part, part 3): k (sum_t c_t P_t)
+// with c_t = base^(cnt-1-t) (horner) or w[t], negated when vneg.
+int emu_g1_var_part(const uint8_t* pts64, const uint64_t* w, uint32_t cnt, int horner, int vneg,
+                    const uint8_t* k32, uint8_t* out64) {
+  std::vector<G1Dev> pts(cnt);
+  std::vector<VTerm> vt(cnt);
+  for (uint32_t t = 0; t < cnt; t++) {
+    g1_store(pts[t], ld_g1(pts64 + 64 * t));
+    vt[t].pt = t;
+    vt[t].w_lo = (uint32_t)w[t];
+    vt[t].w_hi = (uint32_t)(w[t] >> 32);
+    vt[t].flags = (horner && t == 0) ? VT_HORNER : 0;
+  }
+  G1Job j{};
+  j.nfix = 0;
+  j.vstart = 0;
+  j.vcount = cnt;
+  j.vscal = 0;
+  j.vneg = (uint32_t)vneg;
+  uint32_t scal[1][8];
+  be32_to_limbs(scal[0], k32);
+  G1JDev part[4];
+  job_g1_part(&j, 1, 3, vt.data(), pts.data(), scal, nullptr, part, nullptr);
+  g1a r = jac_to_aff(g1j_load(part[3]));
   g1_to_bytes(out64, r);
   return g1_on_curve(r) ? 0 : 1;
 }

@@ -133,3 +133,52 @@ def test_g1_mul_glv_variants(emu):
             o = buf(64)
             assert emu.emu_g1_mul_glv(C.g1_bytes(P), (k % C.R).to_bytes(32, "big"), which, o) == 0
             assert o.raw == want, (k, which)
+
+
+def test_g1_variable_point_forms(emu):
+    """The variable part of a G1 job (dev/jobs.h g1_var_point + the GLV
+    multiplication on the isomorphic curve, g1_mul_glv16_iso) for every form the
+    planner emits (planner.cpp:777-787): a unit point, Horner sums with a
+    power-of-two base (PP-B, b = 16, e = 16) and a general base (PP-A, b = 100,
+    e = 2; b = 10, e = 19), explicit 64-bit weights (powers the planner could
+    not mark exact), zero weights, sums that cancel to the point at infinity,
+    and negation -- against the oracle."""
+    import ctypes
+    rng = random.Random(23)
+    emu.emu_g1_var_part.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p]
+    M64 = (1 << 64) - 1
+
+    def pts(n):
+        return [C.g1_mul(C.G1_GEN, rng.randrange(1, C.R)) for _ in range(n)]
+
+    G = C.G1_GEN
+    cases = [
+        (pts(1), [1], False),
+        (pts(1), [16], True),
+        (pts(16), [16] * 16, True),
+        (pts(2), [100, 100], True),
+        (pts(19), [10] * 19, True),
+        (pts(3), [1, 2, 3], True),
+        (pts(4), [1, 0, M64, 1 << 63], False),
+        (pts(3), [rng.randrange(1 << 64) for _ in range(3)], False),
+        (pts(2), [0, 0], False),
+        ([G, C.g1_neg(C.g1_mul(G, 100))], [1, 100], False),
+        ([C.g1_neg(C.g1_mul(G, 100)), G], [100, 100], True),
+        ([G, C.g1_neg(C.g1_mul(G, 100))], [100, 100], True),  # 100 G - 100 G = O
+        ([G, G], [1, 1], False),  # doubling inside the sum
+    ]
+    for n, (P, w, horner) in enumerate(cases):
+        cnt = len(P)
+        c = [w[0] ** (cnt - 1 - t) for t in range(cnt)] if horner else w
+        V = None
+        for Pt, ct in zip(P, c):
+            V = C.g1_add(V, C.g1_mul(Pt, ct % C.R))
+        for vneg in (0, 1):
+            k = rng.randrange(C.R) if n % 2 else C.R - 1
+            want = C.g1_mul(C.g1_neg(V) if vneg else V, k)
+            o = buf(64)
+            warr = (ctypes.c_uint64 * cnt)(*w)
+            assert emu.emu_g1_var_part(b"".join(C.g1_bytes(p) for p in P), warr, cnt, int(horner), vneg,
+                                       k.to_bytes(32, "big"), o) == 0
+            assert o.raw == C.g1_bytes(want), (n, vneg)
