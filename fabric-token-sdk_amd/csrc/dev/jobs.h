@@ -733,40 +733,6 @@ FTS_HD void g1_emit_bytes(const G1Job& j, const g1a& r, uint8_t* arena) {
   }
 }
 
-FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const uint32_t (*scal)[8],
-                   const G1Dev* tab, G1Dev* g1out, uint8_t* arena) {
-  g1j acc = jac_inf<fp>();
-  if (j.vscal != NONE) {
-    g1a Va;
-    const VTerm& v0 = vterms[j.vstart];
-    if (j.vcount == 1 && v0.w_lo == 1 && v0.w_hi == 0) {
-      Va = g1_load(pts[v0.pt]);  // a single unit-weight point is already affine
-    } else {
-      g1j V = jac_inf<fp>();
-      for (uint32_t t = 0; t < j.vcount; t++) {
-        const VTerm& vt = vterms[j.vstart + t];
-        g1a P = g1_load(pts[vt.pt]);
-        uint64_t w = ((uint64_t)vt.w_hi << 32) | vt.w_lo;
-        if (w == 1) {
-          V = jac_add_aff(V, P);
-        } else {
-          V = jac_add(V, aff_mul_u64(P, w));
-        }
-      }
-      Va = jac_to_aff(V);
-    }
-    if (j.vneg) Va = aff_neg(Va);
-    G1Dev loc[16];
-    acc = G1_MUL_VAR(Va, scal[j.vscal], loc, 1);
-  }
-  for (int f = 0; f < j.nfix; f++) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
-  g1a r = jac_to_aff(acc);
-  G1Dev d;
-  g1_store(d, r);
-  g1out[j.out] = d;
-  g1_emit_bytes(j, r, arena);
-}
-
 // ---- G1 jobs split into uniform parts (device path): item i of [0, 4n) is
 // fixed-base slot f = i / n (0..2) or the variable part (f = 3) of job i % n;
 // job_g1_combine adds the parts and converts to affine.  Same point as job_g1.
@@ -844,6 +810,25 @@ FTS_HD g1j g1_var_point(const G1Job& j, const VTerm* vterms, const G1Dev* pts) {
     }
   }
   return V;
+}
+
+// One lane per job (host emulation): the variable part then the fixed-base
+// slots, to affine.
+FTS_HD void job_g1(const G1Job& j, const VTerm* vterms, const G1Dev* pts, const uint32_t (*scal)[8],
+                   const G1Dev* tab, G1Dev* g1out, uint8_t* arena) {
+  g1j acc = jac_inf<fp>();
+  if (j.vscal != NONE) {
+    g1j V = g1_var_point(j, vterms, pts);
+    if (j.vneg) V = jac_neg(V);
+    G1Dev loc[16];
+    if (!is_zero(V.z)) acc = g1_mul_glv16_iso(g1a{V.x, V.y, false}, V.z, scal[j.vscal], loc, 1);
+  }
+  for (int f = 0; f < j.nfix; f++) acc = g1_fixed_acc(acc, tab, j.fbase[f], scal[j.fscal[f]]);
+  g1a r = jac_to_aff(acc);
+  G1Dev d;
+  g1_store(d, r);
+  g1out[j.out] = d;
+  g1_emit_bytes(j, r, arena);
 }
 
 // Part f of job jb (i = f n + jb): f < 3 the fixed-base term f, f = 3 the

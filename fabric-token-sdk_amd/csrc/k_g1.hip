@@ -10,13 +10,6 @@ using namespace fts;
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; \
   if (i >= (n)) return;
 
-__global__ void __launch_bounds__(128) k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
-                                            const uint32_t (*scal)[8], const G1Dev* tab, G1Dev* g1out,
-                                            uint8_t* arena) {
-  JOB_KERNEL_PROLOGUE(n);
-  job_g1(jobs[i], vt, pts, scal, tab, g1out, arena);
-}
-
 // Uniform parts of the G1 jobs (fixed-base slots and GLV variable parts), one
 // lane per part: lanes [f n, (f+1) n) all run the same code path.
 __global__ void __launch_bounds__(128) k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,

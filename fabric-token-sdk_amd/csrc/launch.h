@@ -60,8 +60,6 @@ __global__ void k_verdict(const TxChecks* tx, uint32_t n, const Check* ck, const
                           const uint8_t* hash_ok, int32_t* codes, uint32_t* bitmap);
 __global__ void k_pp_decode(const uint8_t* raw, const uint32_t* g1off, uint32_t n1, const uint32_t* g2off,
                             uint32_t n2, G1Dev* g1, G2Dev* g2, uint8_t* g1bytes, uint8_t* g2bytes, uint8_t* ok);
-__global__ void k_g1(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts, const uint32_t (*scal)[8],
-                     const G1Dev* tab, G1Dev* g1out, uint8_t* arena);
 __global__ void k_g1_part(const G1Job* jobs, uint32_t n, const VTerm* vt, const G1Dev* pts,
                           const uint32_t (*scal)[8], const G1Dev* tab, G1JDev* part, G1Dev* vtab);
 __global__ void k_g1_combine(const G1Job* jobs, uint32_t n, const G1JDev* part, G1Dev* g1out, uint8_t* arena,
