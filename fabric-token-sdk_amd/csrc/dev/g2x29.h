@@ -1,0 +1,134 @@
+// Fixed-base G2 partial sums (k_g2_part) on the carry-free balanced form of the
+// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_prod1): the XYZZ mixed
+// addition (madd-2008-s, 8M + 2S) over Fp2 instead of the 32-bit Jacobian one
+// (madd-2007-bl, 7M + 4S, curve.h).  One Fp2 product is w29_prod1 -- three
+// 81-MAD limb-product rows folded by columns into the two rows the balanced
+// reductions need -- against three 32-bit Montgomery products with a carry add
+// per MAD.  The partial leaves in Jacobian form through x2q_to_g2j, so
+// job_g2lines_parts (the one-lane line kernel) is unchanged; t' = the sum of
+// the four partials in affine form does not depend on their representatives,
+// so g2out and every line byte are identical to job_g2_part's.
+//
+// Bounds: coordinates between operations are balanced (w29_prod1 and f29_lin2 /
+// f29_lin4 outputs: limbs in [-2^28, 2^28], |value| <= p/2 + e); w29_prod1
+// takes operands with limbs within 2^29 (a difference of two balanced values),
+// q2_sqrb balanced ones.
+#pragma once
+#include "jobs.h"
+#include "sx29.h"
+
+namespace fts {
+
+// a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u (a balanced): two limb-product rows
+FTS_HD q2 q2_sqrb(const q2& a) {
+  FTS_COUNT_MAD(128);
+  FTS_SCHED_FENCE();
+  const f29 s = f29_add(a.c0, a.c1), d = f29_sub(a.c0, a.c1), t = f29_add(a.c0, a.c0);
+  int64_t re[17], im[17];
+#pragma unroll
+  for (int c = 0; c < 17; c++) {
+    int64_t r = 0, m = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = c - i;
+      if (j < 0 || j > 8) continue;
+      r += (int64_t)s.l[i] * d.l[j];
+      m += (int64_t)t.l[i] * a.c1.l[j];
+    }
+    re[c] = r;
+    im[c] = m;
+  }
+  return {w29_redc(re), w29_redc(im)};
+}
+FTS_HD q2 q2_lin2b(const q2& a, int32_t ca, const q2& b, int32_t cb) {
+  return {f29_lin2(a.c0, ca, b.c0, cb), f29_lin2(a.c1, ca, b.c1, cb)};
+}
+FTS_HD q2 q2_lin3b(const q2& a, int32_t ca, const q2& b, int32_t cb, const q2& c, int32_t cc) {
+  return {f29_lin4(a.c0, ca, b.c0, cb, c.c0, cc, c.c0, 0), f29_lin4(a.c1, ca, b.c1, cb, c.c1, cc, c.c1, 0)};
+}
+FTS_HD q2 q2_subr(const q2& a, const q2& b) { return {f29_sub(a.c0, b.c0), f29_sub(a.c1, b.c1)}; }
+FTS_HD bool q2_rzero(const q2& a) { return f29_reduced_zero(a.c0) && f29_reduced_zero(a.c1); }
+FTS_HD q2 q2_one_b() { return {f29_breduce(f29_from_fp(fe_one<ModP>())), q2_zero().c1}; }
+
+// x = X / ZZ, y = Y / ZZZ, ZZ^3 = ZZZ^2
+struct x2q {
+  q2 x, y, zz, zzz;
+  bool inf;
+};
+
+// 2 (x, y) for an affine point (balanced), mdbl-2008-s-1 (a = 0)
+FTS_HD x2q x2q_dbl_aff(const q2& x, const q2& y) {
+  const q2 U = q2_lin2b(y, 2, y, 0);
+  const q2 V = q2_sqrb(U);
+  const q2 W = w29_prod1(U, V);
+  const q2 S = w29_prod1(x, V);
+  const q2 M = q2_lin2b(q2_sqrb(x), 3, x, 0);
+  const q2 X3 = q2_lin3b(q2_sqrb(M), 1, S, -2, S, 0);
+  const q2 Y3 = q2_lin2b(w29_prod1(M, q2_subr(S, X3)), 1, w29_prod1(W, y), -1);
+  return {X3, Y3, V, W, false};
+}
+
+// p + (x2, y2), (x2, y2) affine (balanced) and not the identity: madd-2008-s.
+// P = U2 - X vanishes iff the x coordinates agree: the sum is then a doubling
+// (R = 0) or the identity.
+FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
+  if (p.inf) {
+    const q2 one = q2_one_b();
+    return {x2, y2, one, one, false};
+  }
+  const q2 P = q2_lin2b(w29_prod1(x2, p.zz), 1, p.x, -1);
+  const q2 R = q2_lin2b(w29_prod1(y2, p.zzz), 1, p.y, -1);
+  if (q2_rzero(P)) {
+    if (q2_rzero(R)) return x2q_dbl_aff(x2, y2);
+    x2q o = p;
+    o.inf = true;
+    return o;
+  }
+  // ordered so that each input dies at its last use (the accumulator, the
+  // operands and one product's 34 columns are live together)
+  const q2 PP = q2_sqrb(P);
+  const q2 ZZ3 = w29_prod1(p.zz, PP);
+  const q2 PPP = w29_prod1(P, PP);
+  const q2 ZZZ3 = w29_prod1(p.zzz, PPP);
+  const q2 Q = w29_prod1(p.x, PP);
+  const q2 X3 = q2_lin3b(q2_sqrb(R), 1, PPP, -1, Q, -2);
+  const q2 YP = w29_prod1(p.y, PPP);
+  const q2 Y3 = q2_lin2b(w29_prod1(R, q2_subr(Q, X3)), 1, YP, -1);
+  return {X3, Y3, ZZ3, ZZZ3, false};
+}
+
+// to 32-bit Jacobian without an inversion: Z' = ZZ ZZZ, X' = X ZZ ZZZ^2,
+// Y' = Y ZZZ^4 (X'/Z'^2 = X/ZZ and Y'/Z'^3 = Y/ZZZ since ZZ^3 = ZZZ^2)
+FTS_HD g2j x2q_to_g2j(const x2q& p) {
+  if (p.inf) return jac_inf<fp2>();
+  const q2 t = q2_sqrb(p.zzz);
+  const q2 X = w29_prod1(w29_prod1(p.x, p.zz), t);
+  const q2 Y = w29_prod1(p.y, q2_sqrb(t));
+  const q2 Z = w29_prod1(p.zz, p.zzz);
+  return {q2_to_fp2(X), q2_to_fp2(Y), q2_to_fp2(Z)};
+}
+
+// job_g2_part (dev/jobs.h) on this form: lane q of a job sums the table points
+// of the (base, window) positions q, q + 4, ...
+FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev& out) {
+  x2q acc;
+  acc.inf = true;
+  acc.x = acc.y = acc.zz = acc.zzz = q2_zero();
+#pragma nounroll
+  for (int p = q; p < 3 * G2TAB_WINDOWS; p += 4) {
+    int f = p / G2TAB_WINDOWS, w = p % G2TAB_WINDOWS;
+    if (f < g.nfix) {
+      int32_t d = sdigit_at(scal[g.fscal[f]], G2TAB_C, w);
+      if (d) {
+        g2a T = g2_load(tab[((size_t)g.fbase[f] * G2TAB_WINDOWS + w) * G2TAB_DIGITS + (uint32_t)(d < 0 ? -d : d) - 1]);
+        const q2 x2 = q2_from_fp2(T.x);
+        q2 y2 = q2_from_fp2(T.y);
+        if (d < 0) y2 = q2_neg(y2);
+        acc = x2q_madd(acc, x2, y2);
+      }
+    }
+  }
+  g2part_store(out, x2q_to_g2j(acc));
+}
+
+}  // namespace fts

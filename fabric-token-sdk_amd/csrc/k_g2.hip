@@ -1,10 +1,15 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
+#include "dev/g2x29.h"
 #include "dev/jobs.h"
 #include "launch.h"
 
 using namespace fts;
+
+#ifndef FTS_G2_PART_X29
+#define FTS_G2_PART_X29 1
+#endif
 
 #define JOB_KERNEL_PROLOGUE(n)                          \
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; \
@@ -27,6 +32,8 @@ __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJo
 }
 
 // The same in the one-lane layout, split (job_g2_part / job_g2lines_parts):
+// FTS_G2_PART_X29 (default 1) sums the parts in the carry-free XYZZ form
+// (dev/g2x29.h), 0 in the 32-bit Jacobian one.
 // four lanes per job sum the table points (part-major, so every wave runs one
 // part), then one lane per job adds the partials and emits the lines.
 __global__ void __launch_bounds__(64) k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8],
@@ -34,7 +41,11 @@ __global__ void __launch_bounds__(64) k_g2_part(const G2Job* g2, uint32_t n, con
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 4 * n) return;
   uint32_t q = i / n, job = i - q * n;
+#if FTS_G2_PART_X29
+  job_g2_part_x29(g2[job], (int)q, scal, tab, part[i]);
+#else
   job_g2_part(g2[job], (int)q, scal, tab, part[i]);
+#endif
 }
 __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n,
                                                  const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,

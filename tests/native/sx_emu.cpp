@@ -13,6 +13,7 @@
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
 #include "g2l29.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/g2x29.h"
 
 using namespace fts;
 
@@ -291,6 +292,15 @@ int sxe_g2lines(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalars)
   if (memcmp(o1.data(), o3.data(), sizeof(G2Dev))) return 100;
   for (int s = 0; s < MILLER_LINES; s++)
     if (memcmp(&l1[s], &l3[s], sizeof(EvLineDev))) return 101 + s;
+  // the XYZZ carry-free part kernel (dev/g2x29.h, the device default): other
+  // Jacobian representatives, the same t' and lines
+  for (int q = 0; q < 4; q++) job_g2_part_x29(g, q, scal, tab.data(), part[q]);
+  std::vector<G2Dev> o4(1);
+  std::vector<EvLineDev> l4(MILLER_LINES);
+  job_g2lines_parts(g, j, part.data(), o4.data(), &pt, l4.data(), 0, 1);
+  if (memcmp(o1.data(), o4.data(), sizeof(G2Dev))) return 300;
+  for (int s = 0; s < MILLER_LINES; s++)
+    if (memcmp(&l1[s], &l4[s], sizeof(EvLineDev))) return 301 + s;
   return 0;
 }
 

@@ -55,15 +55,28 @@ def test_sextet_miller(sx, case):
     assert sx.sxe_miller29(p1, p2, q2, qf) == 0  # the carry-free f-chain of the device kernel
 
 
-@pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar"])
+@pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar", "all_zero", "madd_doubling", "madd_cancel"])
 def test_sextet_g2_lines(sx, case):
-    """G2 fixed-base combination + the 88 evaluated pair-2 lines, six lanes vs one."""
+    """G2 fixed-base combination + the 88 evaluated pair-2 lines, six lanes vs one, and
+    the split one-lane path with both part kernels (32-bit Jacobian and the carry-free
+    XYZZ form of dev/g2x29.h).  madd_doubling / madd_cancel make one part lane add a
+    table point equal to (minus) its running sum: with the emulation's 8-bit windows
+    (32 per base) part lane 0 takes window 4 of base 0 and then window 0 of base 1, and
+    B1 = +-2^32 B0 with k0 = d 2^32, k1 = d makes those two table points equal (opposite)."""
     rng = random.Random("g2" + case)
-    bases = b"".join(C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))) for _ in range(3))
-    p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "r_infinity" else bytes(64)
+    B = [C.g2_mul(C.G2_GEN, rng.randrange(1, C.R)) for _ in range(3)]
     ks = [rng.randrange(C.R) for _ in range(3)]
     if case == "zero_scalar":
         ks[1] = 0
+    if case == "all_zero":
+        ks = [0, 0, 0]
+    if case in ("madd_doubling", "madd_cancel"):
+        d = 77
+        B[1] = C.g2_mul(B[0], (1 << 32) if case == "madd_doubling" else C.R - (1 << 32))
+        ks[0] = d << 32
+        ks[1] = d
+    bases = b"".join(C.g2_bytes(b) for b in B)
+    p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "r_infinity" else bytes(64)
     scal = b"".join(k.to_bytes(32, "big") for k in ks)
     assert sx.sxe_g2lines(bases, p2, scal) == 0
 
