@@ -1,16 +1,16 @@
 // Fixed-base G2 partial sums (k_g2_part) on the carry-free balanced form of the
-// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_prod1): the XYZZ mixed
+// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_redc): the XYZZ mixed
 // addition (madd-2008-s, 8M + 2S) over Fp2 instead of the 32-bit Jacobian one
-// (madd-2007-bl, 7M + 4S, curve.h).  One Fp2 product is w29_prod1 -- three
-// 81-MAD limb-product rows folded by columns into the two rows the balanced
-// reductions need -- against three 32-bit Montgomery products with a carry add
-// per MAD.  The partial leaves in Jacobian form through x2q_to_g2j, so
+// (madd-2007-bl, 7M + 4S, curve.h).  One Fp2 product is q2_mulb -- three
+// 81-MAD limb-product rows (Karatsuba) folded by columns into the two rows the
+// balanced reductions need, reduced while they are scanned -- against three
+// 32-bit Montgomery products with a carry add per MAD.  The partial leaves in Jacobian form through x2q_to_g2j, so
 // job_g2lines_parts (the one-lane line kernel) is unchanged; t' = the sum of
 // the four partials in affine form does not depend on their representatives,
 // so g2out and every line byte are identical to job_g2_part's.
 //
-// Bounds: coordinates between operations are balanced (w29_prod1 and f29_lin2 /
-// f29_lin4 outputs: limbs in [-2^28, 2^28], |value| <= p/2 + e); w29_prod1
+// Bounds: coordinates between operations are balanced (q2_mulb and f29_lin2 /
+// f29_lin4 outputs: limbs in [-2^28, 2^28], |value| <= p/2 + e); q2_mulb
 // takes operands with limbs within 2^29 (a difference of two balanced values),
 // q2_sqrb balanced ones.
 #pragma once
@@ -19,26 +19,88 @@
 
 namespace fts {
 
+// Product scanning: column k of both result rows is formed, the reduction's
+// multiples m_i p_j (i + j = k) of the digits already chosen are added, and
+// the column either yields the next balanced digit m_k (k < 9: the running sum
+// then divides exactly by 2^29) or the next output digit -- w29_redc's digits
+// and output, with two running sums and the 18 digits live instead of the
+// 34 columns of each row (a lone product here sits next to four coordinates).
+struct Scan2 {
+  int64_t ar, ai;
+  int32_t mr[9], mi[9];
+};
+FTS_HD void scan2_step(Scan2& s, int k, int64_t re, int64_t im, q2& r) {
+  s.ar += re;
+  s.ai += im;
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const int j = k - i;
+    if (i >= k || j < 0 || j > 8) continue;
+    s.ar += (int64_t)s.mr[i] * P29B[j];
+    s.ai += (int64_t)s.mi[i] * P29B[j];
+  }
+  if (k < 9) {
+    const uint32_t m0 = ((uint32_t)s.ar * P29_INV) & (uint32_t)F29_MASK;
+    const uint32_t m1 = ((uint32_t)s.ai * P29_INV) & (uint32_t)F29_MASK;
+    s.mr[k] = (int32_t)((m0 + (uint32_t)F29_HALF) & (uint32_t)F29_MASK) - F29_HALF;
+    s.mi[k] = (int32_t)((m1 + (uint32_t)F29_HALF) & (uint32_t)F29_MASK) - F29_HALF;
+    s.ar = (s.ar + (int64_t)s.mr[k] * P29B[0]) >> 29;  // a multiple of 2^29 now
+    s.ai = (s.ai + (int64_t)s.mi[k] * P29B[0]) >> 29;
+  } else {
+    r.c0.l[k - 9] = f29_bdigit(s.ar);
+    r.c1.l[k - 9] = f29_bdigit(s.ai);
+    s.ar = (s.ar + F29_HALF) >> 29;
+    s.ai = (s.ai + F29_HALF) >> 29;
+  }
+}
+// a b (limbs within 2^29): the Karatsuba columns of sx29.h w29_prod1, scanned
+FTS_HD q2 q2_mulb(const q2& a, const q2& b) {
+  FTS_COUNT_MAD(192);
+  FTS_SCHED_FENCE();
+  const f29 sa = f29_add(a.c0, a.c1), sb = f29_add(b.c0, b.c1);
+  Scan2 s;
+  s.ar = s.ai = 0;
+  q2 r;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t u = 0, v = 0, w = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 8) continue;
+      u += w29_p(a.c0.l[i], b.c0.l[j]);
+      v += w29_p(a.c1.l[i], b.c1.l[j]);
+      w += w29_p(sa.l[i], sb.l[j]);
+    }
+    scan2_step(s, k, (int64_t)(u - v), (int64_t)(w - (u + v)), r);
+  }
+  r.c0.l[8] = (int32_t)s.ar;
+  r.c1.l[8] = (int32_t)s.ai;
+  return r;
+}
 // a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u (a balanced): two limb-product rows
 FTS_HD q2 q2_sqrb(const q2& a) {
   FTS_COUNT_MAD(128);
   FTS_SCHED_FENCE();
-  const f29 s = f29_add(a.c0, a.c1), d = f29_sub(a.c0, a.c1), t = f29_add(a.c0, a.c0);
-  int64_t re[17], im[17];
+  const f29 s0 = f29_add(a.c0, a.c1), d = f29_sub(a.c0, a.c1), t = f29_add(a.c0, a.c0);
+  Scan2 s;
+  s.ar = s.ai = 0;
+  q2 r;
 #pragma unroll
-  for (int c = 0; c < 17; c++) {
-    int64_t r = 0, m = 0;
+  for (int k = 0; k < 17; k++) {
+    int64_t re = 0, im = 0;
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-      const int j = c - i;
+      const int j = k - i;
       if (j < 0 || j > 8) continue;
-      r += (int64_t)s.l[i] * d.l[j];
-      m += (int64_t)t.l[i] * a.c1.l[j];
+      re += (int64_t)s0.l[i] * d.l[j];
+      im += (int64_t)t.l[i] * a.c1.l[j];
     }
-    re[c] = r;
-    im[c] = m;
+    scan2_step(s, k, re, im, r);
   }
-  return {w29_redc(re), w29_redc(im)};
+  r.c0.l[8] = (int32_t)s.ar;
+  r.c1.l[8] = (int32_t)s.ai;
+  return r;
 }
 FTS_HD q2 q2_lin2b(const q2& a, int32_t ca, const q2& b, int32_t cb) {
   return {f29_lin2(a.c0, ca, b.c0, cb), f29_lin2(a.c1, ca, b.c1, cb)};
@@ -60,11 +122,11 @@ struct x2q {
 FTS_HD x2q x2q_dbl_aff(const q2& x, const q2& y) {
   const q2 U = q2_lin2b(y, 2, y, 0);
   const q2 V = q2_sqrb(U);
-  const q2 W = w29_prod1(U, V);
-  const q2 S = w29_prod1(x, V);
+  const q2 W = q2_mulb(U, V);
+  const q2 S = q2_mulb(x, V);
   const q2 M = q2_lin2b(q2_sqrb(x), 3, x, 0);
   const q2 X3 = q2_lin3b(q2_sqrb(M), 1, S, -2, S, 0);
-  const q2 Y3 = q2_lin2b(w29_prod1(M, q2_subr(S, X3)), 1, w29_prod1(W, y), -1);
+  const q2 Y3 = q2_lin2b(q2_mulb(M, q2_subr(S, X3)), 1, q2_mulb(W, y), -1);
   return {X3, Y3, V, W, false};
 }
 
@@ -76,8 +138,8 @@ FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
     const q2 one = q2_one_b();
     return {x2, y2, one, one, false};
   }
-  const q2 P = q2_lin2b(w29_prod1(x2, p.zz), 1, p.x, -1);
-  const q2 R = q2_lin2b(w29_prod1(y2, p.zzz), 1, p.y, -1);
+  const q2 P = q2_lin2b(q2_mulb(x2, p.zz), 1, p.x, -1);
+  const q2 R = q2_lin2b(q2_mulb(y2, p.zzz), 1, p.y, -1);
   if (q2_rzero(P)) {
     if (q2_rzero(R)) return x2q_dbl_aff(x2, y2);
     x2q o = p;
@@ -87,13 +149,13 @@ FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
   // ordered so that each input dies at its last use (the accumulator, the
   // operands and one product's 34 columns are live together)
   const q2 PP = q2_sqrb(P);
-  const q2 ZZ3 = w29_prod1(p.zz, PP);
-  const q2 PPP = w29_prod1(P, PP);
-  const q2 ZZZ3 = w29_prod1(p.zzz, PPP);
-  const q2 Q = w29_prod1(p.x, PP);
+  const q2 ZZ3 = q2_mulb(p.zz, PP);
+  const q2 PPP = q2_mulb(P, PP);
+  const q2 ZZZ3 = q2_mulb(p.zzz, PPP);
+  const q2 Q = q2_mulb(p.x, PP);
   const q2 X3 = q2_lin3b(q2_sqrb(R), 1, PPP, -1, Q, -2);
-  const q2 YP = w29_prod1(p.y, PPP);
-  const q2 Y3 = q2_lin2b(w29_prod1(R, q2_subr(Q, X3)), 1, YP, -1);
+  const q2 YP = q2_mulb(p.y, PPP);
+  const q2 Y3 = q2_lin2b(q2_mulb(R, q2_subr(Q, X3)), 1, YP, -1);
   return {X3, Y3, ZZ3, ZZZ3, false};
 }
 
@@ -102,9 +164,9 @@ FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
 FTS_HD g2j x2q_to_g2j(const x2q& p) {
   if (p.inf) return jac_inf<fp2>();
   const q2 t = q2_sqrb(p.zzz);
-  const q2 X = w29_prod1(w29_prod1(p.x, p.zz), t);
-  const q2 Y = w29_prod1(p.y, q2_sqrb(t));
-  const q2 Z = w29_prod1(p.zz, p.zzz);
+  const q2 X = q2_mulb(q2_mulb(p.x, p.zz), t);
+  const q2 Y = q2_mulb(p.y, q2_sqrb(t));
+  const q2 Z = q2_mulb(p.zz, p.zzz);
   return {q2_to_fp2(X), q2_to_fp2(Y), q2_to_fp2(Z)};
 }
 

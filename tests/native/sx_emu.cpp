@@ -153,6 +153,37 @@ int sxe_ops(uint32_t seed, int iters) {
   return bad;
 }
 
+// dev/g2x29.h's scanned products against sx29.h's column products: the same
+// columns and digits, so the same words.  Operands: random balanced values,
+// differences of two (limbs within 2^29), and all-extreme limbs; returns the
+// number of mismatches (1 mul, 2 sqr per failing case, summed)
+int sxe_q2_scan(uint32_t seed, int iters) {
+  uint32_t s = seed | 1;
+  auto bal = [&]() { return q2_from_fp2(fp2{rnd_fp(s), rnd_fp(s)}); };
+  auto edge = [&](int32_t v) {
+    q2 a;
+    for (int i = 0; i < 9; i++) a.c0.l[i] = a.c1.l[i] = (i < 8) ? v : (v < 0 ? -1 : 1);
+    return a;
+  };
+  int bad = 0;
+  for (int it = 0; it < iters; it++) {
+    q2 a = bal(), b = bal();
+    if (it % 3 == 1) a = q2_subr(a, bal());
+    if (it % 3 == 2) b = q2_subr(bal(), b);
+    if (it == 0) a = edge(1 << 29), b = edge(-(1 << 28));
+    if (it == 1) a = edge(-(1 << 29)), b = edge(-(1 << 28));
+    q2 x = q2_mulb(a, b), y = w29_prod1(a, b);
+    if (memcmp(&x, &y, sizeof(q2))) bad += 1;
+    q2 c = bal();
+    if (it == 2) c = edge(1 << 28);
+    if (it == 3) c = edge(-(1 << 28));
+    x = q2_sqrb(c);
+    y = w29_prod1(c, c);
+    if (memcmp(&x, &y, sizeof(q2))) bad += 2;
+  }
+  return bad;
+}
+
 // final exponentiation of a random Fp12: sextet vs one-lane (GT bytes);
 // variant 0 = exact (k_fexp_exact), 1 = Fuentes (k_fexp)
 int sxe_fexp(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {

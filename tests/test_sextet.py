@@ -100,3 +100,10 @@ def test_g2_lines_carry_free(sx, case):
     gt = (ctypes.c_uint8 * 384)()
     assert sx.sxe_g2lines29(bases, p2, scal, p1, qf, gt) == 0
     assert sx.sxe_g2l29_consts() == 0
+
+
+def test_g2x29_scanned_products(sx):
+    """dev/g2x29.h q2_mulb / q2_sqrb (product scanning) return the words of sx29.h's
+    column product w29_prod1 for balanced operands, differences of two, and limbs at
+    the bounds (2^29 operand limbs against balanced 2^28 ones)."""
+    assert sx.sxe_q2_scan(12345, 400) == 0
