@@ -1,6 +1,7 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
+#include "dev/g2lines29.h"
 #include "dev/g2x29.h"
 #include "dev/jobs.h"
 #include "launch.h"
@@ -9,6 +10,9 @@ using namespace fts;
 
 #ifndef FTS_G2_PART_X29
 #define FTS_G2_PART_X29 1
+#endif
+#ifndef FTS_G2LINES_X29
+#define FTS_G2LINES_X29 1  // k_g2lines1's line chain on the carry-free form (dev/g2lines29.h)
 #endif
 
 #define JOB_KERNEL_PROLOGUE(n)                          \
@@ -51,7 +55,11 @@ __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob*
                                                  const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,
                                                  EvLineDev* lines) {
   JOB_KERNEL_PROLOGUE(n);
+#if FTS_G2LINES_X29
+  job_g2lines_parts_x29(g2[i], pr[i], part, g2out, pts, lines, i, n);
+#else
   job_g2lines_parts(g2[i], pr[i], part, g2out, pts, lines, i, n);
+#endif
 }
 
 // ---- wide-window G2 tables (C > 8), as k_tab_g1_bw / k_tab_g1_fill

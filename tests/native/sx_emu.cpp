@@ -13,7 +13,7 @@
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
 #include "g2l29.h"
-#include "../../fabric-token-sdk_amd/csrc/dev/g2x29.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/g2lines29.h"
 
 using namespace fts;
 
@@ -381,19 +381,27 @@ int sxe_g2lines29(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalar
   job_g2lines(g, j, scal, tab.data(), o1.data(), &pt, l1.data(), 0, 1);
   job_g2lines29<0>(g, j, scal, tab.data(), o2.data(), &pt, l2.data(), 0, 1);
   if (memcmp(o1.data(), o2.data(), sizeof(G2Dev))) return 1;
+  // the device's k_g2_part + k_g2lines1 (dev/g2x29.h, dev/g2lines29.h)
+  std::vector<G2PartDev> part(4);
+  for (int q = 0; q < 4; q++) job_g2_part_x29(g, q, scal, tab.data(), part[q]);
+  std::vector<G2Dev> o3(1);
+  std::vector<EvLineDev> l3(MILLER_LINES);
+  job_g2lines_parts_x29(g, j, part.data(), o3.data(), &pt, l3.data(), 0, 1);
+  if (memcmp(o1.data(), o3.data(), sizeof(G2Dev))) return 3;
   std::vector<LineCoef> ql(MILLER_LINES);
   precompute_lines(ql.data(), ld_g2(qfix));
   std::vector<LineCoef29> ql29(MILLER_LINES);
   for (int i = 0; i < MILLER_LINES; i++) ql29[i] = linecoef29(ql[i]);
   g1a P1 = ld_g1(p1);
-  uint8_t out[2][384];
-  for (int v = 0; v < 2; v++) {
-    const EvLineDev* l = v ? l2.data() : l1.data();
+  uint8_t out[3][384];
+  for (int v = 0; v < 3; v++) {
+    const EvLineDev* l = v == 2 ? l3.data() : (v ? l2.data() : l1.data());
     fp2 got[6];
     run6q([&](const SqH& x) { got[x.k] = q2_to_fp2(sq_miller_f(x, ql29.data(), P1, l, 0, 1)); });
     f12_to_bytes(out[v], final_exp(from_coefs(got), 0));
   }
   memcpy(gt, out[1], 384);
+  if (memcmp(out[0], out[2], 384)) return 4;
   return memcmp(out[0], out[1], 384) ? 2 : 0;
 }
 

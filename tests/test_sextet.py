@@ -83,9 +83,10 @@ def test_sextet_g2_lines(sx, case):
 
 @pytest.mark.parametrize("case", ["random", "r_infinity", "zero_scalar", "all_zero", "p1_infinity"])
 def test_g2_lines_carry_free(sx, case):
-    """One-lane t' + pair-2 lines on the carry-free form (tests/native/g2l29.h): same t',
-    and the same GT after the Miller f-chain and the final exponentiation as the
-    32-bit one-lane lines (which test_sextet_g2_lines pins to the sextet ones)."""
+    """One-lane t' + pair-2 lines on the carry-free form -- tests/native/g2l29.h, and the
+    device's k_g2_part + k_g2lines1 (dev/g2x29.h, dev/g2lines29.h): same t', and the same
+    GT after the Miller f-chain and the final exponentiation as the 32-bit one-lane lines
+    (which test_sextet_g2_lines pins to the sextet ones)."""
     rng = random.Random("g29" + case)
     bases = b"".join(C.g2_bytes(C.g2_mul(C.G2_GEN, rng.randrange(1, C.R))) for _ in range(3))
     p2 = C.g1_bytes(C.g1_mul(C.G1_GEN, rng.randrange(1, C.R))) if case != "r_infinity" else bytes(64)
