@@ -20,22 +20,31 @@
 
 namespace fts {
 
-// 3 b' (the twist's b' = 3 / (9 + u)) in the balanced R = 2^261 form, as
-// literals (scalar operands); tests/native/sx_emu.cpp sxe_g2l29_consts
-// re-derives them from dev/constants.h
-static constexpr int32_t G2L_B3[2][9] = {
-    {-253769606, 6731155, -156399417, 46225477, -175165556, 162336334, -209914092, -192467748, -1389658},
-    {31837202, -172120824, -128414024, 15984953, -118312780, 62914239, -210424777, 247765560, 1563920},
+// Constants of the line chain in the balanced R = 2^261 form (from
+// dev/constants.h by q2_from_fp2 / f29_breduce; tests/native/sx_emu.cpp
+// sxe_g2l29_consts re-derives them): 3 b' (b' = 3 / (9 + u)), the twist
+// Frobenius factors of pi(Q) and -pi^2(Q), one.  As literals they are scalar
+// operands, not lane VGPRs.
+static constexpr int32_t G2L29_CONST[9][9] = {
+  {-253769606, 6731155, -156399417, 46225477, -175165556, 162336334, -209914092, -192467748, -1389658},  // 3 b' c0
+  {31837202, -172120824, -128414024, 15984953, -118312780, 62914239, -210424777, 247765560, 1563920},  // 3 b' c1
+  {203985993, 99656738, 260427116, -196420981, 88012806, 31651349, 187173606, 203914975, -774555},  // TW_FROB_X c0
+  {-250335503, 187804872, -44558148, -133497832, -94169217, -176792772, -242256849, 104485019, 1269326},  // TW_FROB_X c1
+  {44173617, 40868432, -156996498, -175615513, 213596584, -200916108, -28519026, -208385841, -1252753},  // TW_FROB_Y c0
+  {-106543147, -100798548, -40739557, 220163168, 145517765, -5938662, -212924673, 161949719, 1410845},  // TW_FROB_Y c1
+  {-120801391, -145023941, 193189603, 244240497, -226312478, 69340805, -1834625, -184005301, 1478938},  // TW_FROB2_X
+  {176370655, 199481511, 128831276, -21759002, -178483129, 45989682, 237679608, -86689705, -903222},  // TW_FROB2_Y
+  {-176370655, -199481511, -128831276, 21759002, 178483129, -45989682, -237679608, 86689705, 903222},  // one
 };
-FTS_HD q2 g2l_b3() {
-  q2 r;
+enum { G2C_B3 = 0, G2C_FX = 2, G2C_FY = 4, G2C_F2X = 6, G2C_F2Y = 7, G2C_ONE = 8 };
+FTS_HD f29 g2c_f(int i) {
+  f29 r;
 #pragma unroll
-  for (int k = 0; k < 9; k++) {
-    r.c0.l[k] = G2L_B3[0][k];
-    r.c1.l[k] = G2L_B3[1][k];
-  }
+  for (int k = 0; k < 9; k++) r.l[k] = G2L29_CONST[i][k];
   return r;
 }
+FTS_HD q2 g2c_q(int i) { return {g2c_f(i), g2c_f(i + 1)}; }
+FTS_HD q2 q2_one29() { return {g2c_f(G2C_ONE), q2_zero().c1}; }
 
 FTS_HD q2 q2_scaleb(const q2& a, int32_t c) { return q2_lin2b(a, c, a, 0); }
 
@@ -63,35 +72,40 @@ FTS_HD q2 q2_mulfb(const q2& a, const f29& s) {
   return r;
 }
 
+// Each step hands its three evaluated coefficients to emit(c, value) (c = 0:
+// c0, 1: c3, 2: c4) as soon as they are formed, so that none of them stays live
+// through the rest of the step.
+//
 // T <- 4 (2T) = 2T; the line (-H, 3J, I) evaluated: c0 = -H yP, c3 = 3 X^2 xP,
 // c4 = E - B
-FTS_HD void g2l_dbl(q2& X, q2& Y, q2& Z, const f29& yP, const f29& xP, q2& c0, q2& c3, q2& c4) {
+template <class Emit>
+FTS_HD void g2l_dbl(q2& X, q2& Y, q2& Z, const f29& yP, const f29& xP, const Emit& emit) {
   const q2 B = q2_sqrb(Y);
   const q2 C = q2_sqrb(Z);
   const q2 H = q2_lin3b(q2_sqrb(q2_lin2b(Y, 1, Z, 1)), 1, B, -1, C, -1);  // 2 Y Z
-  const q2 XY = q2_mulb(X, Y);
-  const q2 E = q2_mulb(C, g2l_b3());  // 3 b' Z^2
-  c0 = q2_mulfb(q2_neg(H), yP);
-  c3 = q2_scaleb(q2_mulfb(q2_sqrb(X), xP), 3);
-  c4 = q2_lin2b(E, 1, B, -1);
-  X = q2_scaleb(q2_mulb(XY, q2_lin2b(B, 1, E, -3)), 2);
+  emit(0, q2_mulfb(q2_neg(H), yP));
+  emit(1, q2_scaleb(q2_mulfb(q2_sqrb(X), xP), 3));
+  const q2 E = q2_mulb(C, g2c_q(G2C_B3));  // 3 b' Z^2
+  emit(2, q2_lin2b(E, 1, B, -1));
+  X = q2_scaleb(q2_mulb(q2_mulb(X, Y), q2_lin2b(B, 1, E, -3)), 2);
   Y = q2_lin2b(q2_sqrb(q2_lin2b(B, 1, E, 3)), 1, q2_sqrb(E), -12);
   Z = q2_scaleb(q2_mulb(B, H), 4);
 }
 
 // T <- T + (Qx, Qy) (affine, balanced); the line (L, -O, Qx O - L Qy)
 // evaluated: c0 = L yP, c3 = -O xP, c4 = Qx O - L Qy
-FTS_HD void g2l_add(q2& X, q2& Y, q2& Z, const q2& Qx, const q2& Qy, const f29& yP, const f29& xP, q2& c0, q2& c3,
-                    q2& c4) {
+template <class Emit>
+FTS_HD void g2l_add(q2& X, q2& Y, q2& Z, const q2& Qx, const q2& Qy, const f29& yP, const f29& xP,
+                    const Emit& emit) {
   const q2 O = q2_lin2b(Y, 1, q2_mulb(Qy, Z), -1);
   const q2 L = q2_lin2b(X, 1, q2_mulb(Qx, Z), -1);
+  emit(0, q2_mulfb(L, yP));
+  emit(1, q2_mulfb(q2_neg(O), xP));
+  emit(2, q2_lin2b(q2_mulb(Qx, O), 1, q2_mulb(L, Qy), -1));
   const q2 D = q2_sqrb(L);
   const q2 E = q2_mulb(L, D);
   const q2 G = q2_mulb(X, D);
   const q2 H = q2_lin3b(E, 1, G, -2, q2_mulb(Z, q2_sqrb(O)), 1);
-  c0 = q2_mulfb(L, yP);
-  c3 = q2_mulfb(q2_neg(O), xP);
-  c4 = q2_lin2b(q2_mulb(Qx, O), 1, q2_mulb(L, Qy), -1);
   const q2 Y3 = q2_lin2b(q2_mulb(q2_subr(G, H), O), 1, q2_mulb(Y, E), -1);
   X = q2_mulb(L, H);
   Y = Y3;
@@ -121,35 +135,32 @@ FTS_HD void job_g2lines_parts_x29(const G2Job& g, const PairJob& j, const G2Part
   const bool use = !(P.inf || Q.inf);
   const f29 yP = f29_breduce(f29_from_fp(P.y)), xP = f29_breduce(f29_from_fp(P.x));
   const q2 Qx = q2_from_fp2(Q.x), Qy = q2_from_fp2(Q.y);
-  q2 X = Qx, Y = Qy, Z = q2_one_b();
-  const q2 one = q2_one_b();
+  q2 X = Qx, Y = Qy, Z = q2_one29();
 #pragma nounroll
   for (int s = 0; s < MILLER_LINES; s++) {
     const int t = MILLER_STEPS.t[s];
-    q2 c0, c3, c4;
+    // a pair with an infinity point contributes 1 (gnark's MillerLoop skips it)
+    auto emit = [&](int c, const q2& v) {
+      const q2 w = use ? v : (c == 0 ? q2_one29() : q2_zero());
+      evline_put_b(lines, (uint32_t)s, 2 * c, idx, njobs, w.c0);
+      evline_put_b(lines, (uint32_t)s, 2 * c + 1, idx, njobs, w.c1);
+    };
     if (t == STEP_DBL) {
-      g2l_dbl(X, Y, Z, yP, xP, c0, c3, c4);
+      g2l_dbl(X, Y, Z, yP, xP, emit);
     } else {
       q2 Ax = Qx, Ay = Qy;
       if (t == STEP_FROB1 || t == STEP_FROB2) {
-        const g2a A = t == STEP_FROB1 ? tw_frob(Q) : tw_frob2_neg(Q);
+        // t' re-read from the output just written (this lane's own store): no
+        // 32-bit copy of it stays live through the loop
+        const g2a Qr = g2_load(g2out[g.out]);
+        const g2a A = t == STEP_FROB1 ? tw_frob(Qr) : tw_frob2_neg(Qr);
         Ax = q2_from_fp2(A.x);
         Ay = q2_from_fp2(A.y);
       } else if (t == STEP_SUB) {
         Ay = q2_neg(Qy);
       }
-      g2l_add(X, Y, Z, Ax, Ay, yP, xP, c0, c3, c4);
+      g2l_add(X, Y, Z, Ax, Ay, yP, xP, emit);
     }
-    if (!use) {
-      c0 = one;
-      c3 = c4 = q2_zero();
-    }
-    evline_put_b(lines, (uint32_t)s, 0, idx, njobs, c0.c0);
-    evline_put_b(lines, (uint32_t)s, 1, idx, njobs, c0.c1);
-    evline_put_b(lines, (uint32_t)s, 2, idx, njobs, c3.c0);
-    evline_put_b(lines, (uint32_t)s, 3, idx, njobs, c3.c1);
-    evline_put_b(lines, (uint32_t)s, 4, idx, njobs, c4.c0);
-    evline_put_b(lines, (uint32_t)s, 5, idx, njobs, c4.c1);
   }
 }
 

@@ -25,6 +25,7 @@
 #pragma once
 #include "../../fabric-token-sdk_amd/csrc/dev/jobs.h"
 #include "../../fabric-token-sdk_amd/csrc/dev/sx29.h"
+#include "../../fabric-token-sdk_amd/csrc/dev/g2lines29.h"
 
 namespace fts {
 
@@ -57,30 +58,7 @@ FTS_HD q2 q2_sqr29(const q2& a) {
 }
 
 
-// Constants of phase B in the balanced form (generated from dev/constants.h by
-// the conversions below; tests/native/sx_emu.cpp sxe_g2l29_consts re-derives
-// them): 3 b', the twist Frobenius factors of pi(Q) and -pi^2(Q), one.  As
-// literals they live in scalar registers, not in the lane's VGPRs.
-static constexpr int32_t G2L29_CONST[9][9] = {
-  {-253769606, 6731155, -156399417, 46225477, -175165556, 162336334, -209914092, -192467748, -1389658},  // 3 b' c0
-  {31837202, -172120824, -128414024, 15984953, -118312780, 62914239, -210424777, 247765560, 1563920},  // 3 b' c1
-  {203985993, 99656738, 260427116, -196420981, 88012806, 31651349, 187173606, 203914975, -774555},  // TW_FROB_X c0
-  {-250335503, 187804872, -44558148, -133497832, -94169217, -176792772, -242256849, 104485019, 1269326},  // TW_FROB_X c1
-  {44173617, 40868432, -156996498, -175615513, 213596584, -200916108, -28519026, -208385841, -1252753},  // TW_FROB_Y c0
-  {-106543147, -100798548, -40739557, 220163168, 145517765, -5938662, -212924673, 161949719, 1410845},  // TW_FROB_Y c1
-  {-120801391, -145023941, 193189603, 244240497, -226312478, 69340805, -1834625, -184005301, 1478938},  // TW_FROB2_X
-  {176370655, 199481511, 128831276, -21759002, -178483129, 45989682, 237679608, -86689705, -903222},  // TW_FROB2_Y
-  {-176370655, -199481511, -128831276, 21759002, 178483129, -45989682, -237679608, 86689705, 903222},  // one
-};
-enum { G2C_B3 = 0, G2C_FX = 2, G2C_FY = 4, G2C_F2X = 6, G2C_F2Y = 7, G2C_ONE = 8 };
-FTS_HD f29 g2c_f(int i) {
-  f29 r;
-#pragma unroll
-  for (int k = 0; k < 9; k++) r.l[k] = G2L29_CONST[i][k];
-  return r;
-}
-FTS_HD q2 g2c_q(int i) { return {g2c_f(i), g2c_f(i + 1)}; }
-FTS_HD q2 q2_one29() { return {g2c_f(G2C_ONE), q2_zero().c1}; }
+// Constants of phase B (G2L29_CONST, g2c_f / g2c_q, q2_one29): dev/g2lines29.h
 
 // Jacobian point on the twist in this form (inf: the identity)
 struct j2q {
