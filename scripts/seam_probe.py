@@ -3,7 +3,9 @@
 per call): per-stage device time (HIP events, ftz_batch_stats) of a staged
 pass of n transfers, serial (every kernel on one stream) and as scheduled,
 plus the wall time of one ftz_batch_run and of one ftz_verify_transfers call.
-    python scripts/seam_probe.py [n ...]"""
+    python scripts/seam_probe.py [n ...]
+SEAM_LAYOUT=one_lane|sextet forces the t' + lines stage's layout (default: the
+engine's choice, sextet for small passes)."""
 import json
 import os
 import sys
@@ -17,6 +19,8 @@ from zkatdlog import workload as W  # noqa: E402
 
 g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
 ctx = zkatdlog.Context(g["pp"].encode(), device=0)
+if os.environ.get("SEAM_LAYOUT"):
+    ctx.set_layout("g2lines", os.environ["SEAM_LAYOUT"])
 valid = W.prove_distinct(ctx, 256, tag=b"seam-probe")
 for n in [int(a) for a in sys.argv[1:]] or [1, 16, 64]:
     job = W.mixed_job(valid, None, n)
