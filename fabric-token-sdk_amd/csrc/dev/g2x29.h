@@ -19,6 +19,10 @@
 
 namespace fts {
 
+#ifndef FTS_G2_PART_XYZZ
+#define FTS_G2_PART_XYZZ 0  // 1: the parts in XYZZ form (x2q_madd), 0: Jacobian (j2b_madd)
+#endif
+
 // Product scanning: column k of both result rows is formed, the reduction's
 // multiples m_i p_j (i + j = k) of the digits already chosen are added, and
 // the column either yields the next balanced digit m_k (k < 9: the running sum
@@ -170,12 +174,64 @@ FTS_HD g2j x2q_to_g2j(const x2q& p) {
   return {q2_to_fp2(X), q2_to_fp2(Y), q2_to_fp2(Z)};
 }
 
+// Jacobian form (X / Z^2, Y / Z^3): madd-2007-bl, 7M + 4S -- the same product
+// rows as the XYZZ addition with one coordinate fewer to keep live, which
+// brings the part kernel under the 256 registers of two waves per SIMD
+struct j2b {
+  q2 x, y, z;
+  bool inf;
+};
+// dbl-2009-l (a = 0), p not the identity
+FTS_HD j2b j2b_dbl(const j2b& p) {
+  const q2 A = q2_sqrb(p.x);
+  const q2 B = q2_sqrb(p.y);
+  const q2 C = q2_sqrb(B);
+  const q2 D = q2_lin3b(q2_sqrb(q2_lin2b(p.x, 1, B, 1)), 2, A, -2, C, -2);  // 2((X + B)^2 - A - C)
+  const q2 E = q2_lin2b(A, 3, A, 0);
+  const q2 X3 = q2_lin3b(q2_sqrb(E), 1, D, -2, D, 0);
+  const q2 Y3 = q2_lin2b(q2_mulb(E, q2_subr(D, X3)), 1, C, -8);
+  const q2 Z3 = q2_lin2b(q2_mulb(p.y, p.z), 2, p.y, 0);
+  return {X3, Y3, Z3, false};
+}
+// p + (x2, y2), (x2, y2) affine (balanced) and not the identity.  H = U2 - X
+// vanishes iff the x coordinates agree: a doubling (r = 0) or the identity.
+FTS_HD j2b j2b_madd(const j2b& p, const q2& x2, const q2& y2) {
+  if (p.inf) return {x2, y2, q2_one_b(), false};
+  const q2 Z1Z1 = q2_sqrb(p.z);
+  const q2 H = q2_lin2b(q2_mulb(x2, Z1Z1), 1, p.x, -1);
+  const q2 r = q2_lin2b(q2_mulb(y2, q2_mulb(p.z, Z1Z1)), 2, p.y, -2);  // 2 (S2 - Y)
+  if (q2_rzero(H)) {
+    if (q2_rzero(r)) return j2b_dbl({x2, y2, q2_one_b(), false});
+    j2b o = p;
+    o.inf = true;
+    return o;
+  }
+  const q2 HH = q2_sqrb(H);
+  const q2 Z3 = q2_lin3b(q2_sqrb(q2_lin2b(p.z, 1, H, 1)), 1, Z1Z1, -1, HH, -1);  // 2 Z H
+  const q2 I = q2_lin2b(HH, 4, HH, 0);
+  const q2 J = q2_mulb(H, I);
+  const q2 V = q2_mulb(p.x, I);
+  const q2 X3 = q2_lin3b(q2_sqrb(r), 1, J, -1, V, -2);
+  const q2 Y3 = q2_lin2b(q2_mulb(r, q2_subr(V, X3)), 1, q2_mulb(p.y, J), -2);
+  return {X3, Y3, Z3, false};
+}
+FTS_HD g2j j2b_to_g2j(const j2b& p) {
+  if (p.inf) return jac_inf<fp2>();
+  return {q2_to_fp2(p.x), q2_to_fp2(p.y), q2_to_fp2(p.z)};
+}
+
 // job_g2_part (dev/jobs.h) on this form: lane q of a job sums the table points
 // of the (base, window) positions q, q + 4, ...
 FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev& out) {
+#if FTS_G2_PART_XYZZ
   x2q acc;
   acc.inf = true;
   acc.x = acc.y = acc.zz = acc.zzz = q2_zero();
+#else
+  j2b acc;
+  acc.inf = true;
+  acc.x = acc.y = acc.z = q2_zero();
+#endif
 #pragma nounroll
   for (int p = q; p < 3 * G2TAB_WINDOWS; p += 4) {
     int f = p / G2TAB_WINDOWS, w = p % G2TAB_WINDOWS;
@@ -186,11 +242,19 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
         const q2 x2 = q2_from_fp2(T.x);
         q2 y2 = q2_from_fp2(T.y);
         if (d < 0) y2 = q2_neg(y2);
+#if FTS_G2_PART_XYZZ
         acc = x2q_madd(acc, x2, y2);
+#else
+        acc = j2b_madd(acc, x2, y2);
+#endif
       }
     }
   }
+#if FTS_G2_PART_XYZZ
   g2part_store(out, x2q_to_g2j(acc));
+#else
+  g2part_store(out, j2b_to_g2j(acc));
+#endif
 }
 
 }  // namespace fts

@@ -11,6 +11,9 @@ using namespace fts;
 #ifndef FTS_G2_PART_X29
 #define FTS_G2_PART_X29 1
 #endif
+#ifndef FTS_G2_PART_WAVES
+#define FTS_G2_PART_WAVES 1  // waves per SIMD k_g2_part is compiled for
+#endif
 #ifndef FTS_G2LINES_X29
 #define FTS_G2LINES_X29 1  // k_g2lines1's line chain on the carry-free form (dev/g2lines29.h)
 #endif
@@ -40,7 +43,7 @@ __global__ void __launch_bounds__(64, 2) k_g2lines(const G2Job* g2, const PairJo
 // (dev/g2x29.h), 0 in the 32-bit Jacobian one.
 // four lanes per job sum the table points (part-major, so every wave runs one
 // part), then one lane per job adds the partials and emits the lines.
-__global__ void __launch_bounds__(64) k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8],
+__global__ void __launch_bounds__(64, FTS_G2_PART_WAVES) k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8],
                                                 const G2Dev* tab, G2PartDev* part) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 4 * n) return;
