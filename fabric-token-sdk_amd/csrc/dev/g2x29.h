@@ -195,14 +195,23 @@ FTS_HD j2b j2b_dbl(const j2b& p) {
   return {X3, Y3, Z3, false};
 }
 // p + (x2, y2), (x2, y2) affine (balanced) and not the identity.  H = U2 - X
-// vanishes iff the x coordinates agree: a doubling (r = 0) or the identity.
-FTS_HD j2b j2b_madd(const j2b& p, const q2& x2, const q2& y2) {
+// vanishes iff the x coordinates agree: the identity (r != 0), or p equals the
+// point -- then *dbl is set and p returned unchanged (the caller doubles; the
+// part kernel redoes the lane in the 32-bit code, so that the doubling's
+// registers do not count against the loop's)
+FTS_HD j2b j2b_madd(const j2b& p, const q2& x2, const q2& y2, bool* dbl = nullptr) {
   if (p.inf) return {x2, y2, q2_one_b(), false};
   const q2 Z1Z1 = q2_sqrb(p.z);
   const q2 H = q2_lin2b(q2_mulb(x2, Z1Z1), 1, p.x, -1);
   const q2 r = q2_lin2b(q2_mulb(y2, q2_mulb(p.z, Z1Z1)), 2, p.y, -2);  // 2 (S2 - Y)
   if (q2_rzero(H)) {
-    if (q2_rzero(r)) return j2b_dbl({x2, y2, q2_one_b(), false});
+    if (q2_rzero(r)) {
+      if (dbl) {
+        *dbl = true;
+        return p;
+      }
+      return j2b_dbl({x2, y2, q2_one_b(), false});
+    }
     j2b o = p;
     o.inf = true;
     return o;
@@ -232,6 +241,7 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
   j2b acc;
   acc.inf = true;
   acc.x = acc.y = acc.z = q2_zero();
+  bool dbl = false;
 #endif
 #pragma nounroll
   for (int p = q; p < 3 * G2TAB_WINDOWS; p += 4) {
@@ -246,7 +256,8 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
 #if FTS_G2_PART_XYZZ
         acc = x2q_madd(acc, x2, y2);
 #else
-        acc = j2b_madd(acc, x2, y2);
+        acc = j2b_madd(acc, x2, y2, &dbl);
+        if (dbl) break;
 #endif
       }
     }
@@ -254,6 +265,10 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
 #if FTS_G2_PART_XYZZ
   g2part_store(out, x2q_to_g2j(acc));
 #else
+  if (dbl) {
+    job_g2_part(g, q, scal, tab, out);  // a running sum met its next table point
+    return;
+  }
   g2part_store(out, j2b_to_g2j(acc));
 #endif
 }
