@@ -20,6 +20,10 @@
 
 namespace fts {
 
+#ifndef FTS_G2L_FUSED
+#define FTS_G2L_FUSED 0  // 1: the addition step's two sums of two products with one reduction each (stage -2%, device-only -2.5% on one box: off)
+#endif
+
 // Constants of the line chain in the balanced R = 2^261 form (from
 // dev/constants.h by q2_from_fp2 / f29_breduce; tests/native/sx_emu.cpp
 // sxe_g2l29_consts re-derives them): 3 b' (b' = 3 / (9 + u)), the twist
@@ -101,12 +105,20 @@ FTS_HD void g2l_add(q2& X, q2& Y, q2& Z, const q2& Qx, const q2& Qy, const f29& 
   const q2 L = q2_lin2b(X, 1, q2_mulb(Qx, Z), -1);
   emit(0, q2_mulfb(L, yP));
   emit(1, q2_mulfb(q2_neg(O), xP));
+#if FTS_G2L_FUSED
+  emit(2, q2_mul2b(Qx, O, L, q2_neg(Qy)));
+#else
   emit(2, q2_lin2b(q2_mulb(Qx, O), 1, q2_mulb(L, Qy), -1));
+#endif
   const q2 D = q2_sqrb(L);
   const q2 E = q2_mulb(L, D);
   const q2 G = q2_mulb(X, D);
   const q2 H = q2_lin3b(E, 1, G, -2, q2_mulb(Z, q2_sqrb(O)), 1);
+#if FTS_G2L_FUSED
+  const q2 Y3 = q2_mul2b(q2_subr(G, H), O, Y, q2_neg(E));  // one reduction for the two products
+#else
   const q2 Y3 = q2_lin2b(q2_mulb(q2_subr(G, H), O), 1, q2_mulb(Y, E), -1);
+#endif
   X = q2_mulb(L, H);
   Y = Y3;
   Z = q2_mulb(E, Z);

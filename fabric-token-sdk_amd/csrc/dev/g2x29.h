@@ -83,6 +83,33 @@ FTS_HD q2 q2_mulb(const q2& a, const q2& b) {
   r.c1.l[8] = (int32_t)s.ai;
   return r;
 }
+// a b + c d with one reduction (a, c limbs within 2^29; b, d balanced): the
+// four rows' columns stay below 36 x 2^57 + the reduction's terms < 2^63
+FTS_HD q2 q2_mul2b(const q2& a, const q2& b, const q2& c, const q2& d) {
+  FTS_COUNT_MAD(384);
+  FTS_SCHED_FENCE();
+  const f29 sa = f29_add(a.c0, a.c1), sb = f29_add(b.c0, b.c1);
+  const f29 sc = f29_add(c.c0, c.c1), sd = f29_add(d.c0, d.c1);
+  Scan2 s;
+  s.ar = s.ai = 0;
+  q2 r;
+#pragma unroll
+  for (int k = 0; k < 17; k++) {
+    uint64_t u = 0, v = 0, w = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+      const int j = k - i;
+      if (j < 0 || j > 8) continue;
+      u += w29_p(a.c0.l[i], b.c0.l[j]) + w29_p(c.c0.l[i], d.c0.l[j]);
+      v += w29_p(a.c1.l[i], b.c1.l[j]) + w29_p(c.c1.l[i], d.c1.l[j]);
+      w += w29_p(sa.l[i], sb.l[j]) + w29_p(sc.l[i], sd.l[j]);
+    }
+    scan2_step(s, k, (int64_t)(u - v), (int64_t)(w - (u + v)), r);
+  }
+  r.c0.l[8] = (int32_t)s.ar;
+  r.c1.l[8] = (int32_t)s.ai;
+  return r;
+}
 // a^2 = (a0 + a1)(a0 - a1) + 2 a0 a1 u (a balanced): two limb-product rows
 FTS_HD q2 q2_sqrb(const q2& a) {
   FTS_COUNT_MAD(128);

@@ -36,5 +36,5 @@ if kern:
         for k, g, _, v in rows:
             agg[(k.split("(")[0], g)].append(v)
         for (k, g), vs in sorted(agg.items()):
-            if k in kern.split(",") and g > 100000:
+            if k in kern.split(",") and g > 30000:
                 print("%-6s %s grid %d: %.4g VALU/launch (%d)" % (n, k, g, sum(vs) / len(vs), len(vs)))
