@@ -20,6 +20,11 @@ for r in range(1, rounds + 1):
             print(n, r, "missing")
             continue
         rf = d.get("roofline") or {}
+        if d.get("msm"):
+            print("%-6s r%d msm %s resident %s" % (n, r, [(m["n"], m["ms"], m.get("ms_host_scalars")) for m in d["msm"]],
+                                                 [(m["n"], m["ms"]) for m in d.get("msm_resident") or []]))
+        if not rf.get("serial_ms"):
+            continue
         print("%-6s r%d value %9.0f dev %9.0f | %s" % (
             n, r, d["value"], (d.get("device_only") or {}).get("transfers_per_s", 0),
             " ".join("%s %.3f/%.3f" % (k, rf["serial_ms"][k], rf["per_kernel_frac"][k])
