@@ -506,10 +506,7 @@ FTS_HD j29 j29_madd(const j29& p, const f29& x2, const f29& y2) {
 // add-2007-bl full Jacobian addition p + q: 11M + 5S, inputs normalised with
 // B <= 2 (products or f29_reduce outputs).  Same exceptional handling as
 // j29_madd: Z3 = ((Z1 + Z2)^2 - Z1Z1 - Z2Z2) H = 2 Z1 Z2 H vanishes iff H does.
-// dbl: where the caller has a slow path for it, p == q sets *dbl and returns p
-// instead of doubling inline (the doubling's registers then stay out of the
-// caller's loop)
-FTS_HD j29 j29_add(const j29& p, const j29& q, bool* dbl = nullptr) {
+FTS_HD j29 j29_add(const j29& p, const j29& q) {
   if (p.inf) return q;
   if (q.inf) return p;
   f29 Z1Z1 = f29_sqr(p.z);                         // (2, 1)
@@ -532,13 +529,7 @@ FTS_HD j29 j29_add(const j29& p, const j29& q, bool* dbl = nullptr) {
   f29 ZZ = f29_sqr(f29_norm(f29_add(p.z, q.z)));   // 16: (2, 1)
   f29 Z3 = f29_reduce(f29_mul(f29_norm(f29_sub(f29_sub(ZZ, Z1Z1), Z2Z2)), H));  // 6 x 4: (2, 1) -> (1.5, 1)
   if (f29_reduced_zero(Z3)) {
-    if (f29_is_zero(rr)) {  // p == q
-      if (dbl) {
-        *dbl = true;
-        return p;
-      }
-      return j29_dbl(p);
-    }
+    if (f29_is_zero(rr)) return j29_dbl(p);  // p == q
     j29 o = p;
     o.inf = true;
     return o;

@@ -335,67 +335,36 @@ FTS_HD j29 j29_ld(const G1JDev& d) { return j29_from(g1j_load(d)); }
 // addition per window.  The lanes of a wave take different k, so a per-bit
 // conditional addition ran in every bit position for the wave (16 doublings +
 // 16 additions for 16-bit k); windows halve the additions
-// d p for d in 1..3 as a value: limb-wise selects (a conditional lvalue would
-// take the three points' addresses and put them in scratch memory)
-FTS_HD j29 j29_sel3(uint32_t d, const j29& p, const j29& p2, const j29& p3) {
-  j29 r;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {
-    r.x.l[i] = d == 1 ? p.x.l[i] : (d == 2 ? p2.x.l[i] : p3.x.l[i]);
-    r.y.l[i] = d == 1 ? p.y.l[i] : (d == 2 ? p2.y.l[i] : p3.y.l[i]);
-    r.z.l[i] = d == 1 ? p.z.l[i] : (d == 2 ? p2.z.l[i] : p3.z.l[i]);
-  }
-  r.inf = d == 1 ? p.inf : (d == 2 ? p2.inf : p3.inf);
-  return r;
-}
-FTS_HD j29 j29_mul_small(const j29& p, uint32_t k, bool* dbl = nullptr) {
+FTS_HD j29 j29_mul_small(const j29& p, uint32_t k) {
   if (!k) return j29_inf();
-  const j29 p2 = j29_dbl(p), p3 = j29_add(p2, p, dbl);
+  const j29 p2 = j29_dbl(p), p3 = j29_add(p2, p);
   const int top = 31 - __builtin_clz(k), w = top >> 1;
   uint32_t d = (k >> (2 * w)) & 3u;
-  j29 acc = j29_sel3(d, p, p2, p3);
+  j29 acc = d == 1 ? p : (d == 2 ? p2 : p3);
   for (int i = w - 1; i >= 0; i--) {
     acc = j29_dbl(j29_dbl(acc));
     d = (k >> (2 * i)) & 3u;
-    if (d) acc = j29_add(acc, j29_sel3(d, p, p2, p3), dbl);
+    if (d) acc = j29_add(acc, d == 1 ? p : (d == 2 ? p2 : p3));
   }
   return acc;
 }
-// the segment in the 32-bit code: the slow path for a sum that meets an equal
-// point (jac_add_inl doubles inline)
-FTS_HD g1j msm_segment_fp(uint32_t lo, uint32_t hi, uint32_t bl, const uint32_t* owner, const G1JDev* slot_sum) {
-  g1j run = jac_inf<fp>(), acc = jac_inf<fp>();
-  for (uint32_t j = hi; j > lo; j--) {
-    run = jac_add_inl(run, g1j_load(slot_sum[j - 1]));
-    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = jac_add_inl(acc, run);
-  }
-  g1j m = jac_inf<fp>();
-  for (int b = 31; b >= 0; b--) {
-    m = jac_dbl(m);
-    if ((bl >> b) & 1) m = jac_add_inl(m, run);
-  }
-  return jac_add_inl(acc, m);
-}
+
+// Segment s of window w: slots [lo, hi) of the window's slot range, covering
+// consecutive buckets bl..bh (every bucket owns >= 1 slot).  Returns
+//   sum_slots (b + 1) P_slot = sum (b - bl + 1) P + bl sum P,
+// the first term by the running-sum trick from the top slot down.
 FTS_HD g1j msm_job_segment(const MsmPlan& p, uint32_t w, uint32_t s, const uint32_t* wlo, const uint32_t* whi,
                            const uint32_t* owner, const G1JDev* slot_sum) {
   uint32_t lo = wlo[w] + s * p.seg_len, hi = lo + p.seg_len;
   if (hi > whi[w]) hi = whi[w];
   if (lo >= hi) return jac_inf<fp>();
-  const uint32_t bl = owner[lo] - w * p.buckets;
   j29 run = j29_inf(), acc = j29_inf();
-  bool dbl = false;
-  for (uint32_t j = hi; j > lo && !dbl; j--) {
-    run = j29_add(run, j29_ld(slot_sum[j - 1]), &dbl);
-    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = j29_add(acc, run, &dbl);
+  for (uint32_t j = hi; j > lo; j--) {
+    run = j29_add(run, j29_ld(slot_sum[j - 1]));
+    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) acc = j29_add(acc, run);
   }
-  if (!dbl) {
-    const j29 m = j29_mul_small(run, bl, &dbl);
-    if (!dbl) {
-      const j29 r = j29_add(acc, m, &dbl);
-      if (!dbl) return j29_to(r);
-    }
-  }
-  return msm_segment_fp(lo, hi, bl, owner, slot_sum);
+  uint32_t bl = owner[lo] - w * p.buckets;
+  return j29_to(j29_add(acc, j29_mul_small(run, bl)));
 }
 
 // Decode one 64-byte gnark RawBytes G1 point (uncompressed, big-endian; the
