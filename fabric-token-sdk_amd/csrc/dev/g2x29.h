@@ -21,7 +21,7 @@
 namespace fts {
 
 #ifndef FTS_G2_PART_XYZZ
-#define FTS_G2_PART_XYZZ 0  // 1: the parts in XYZZ form (x2q_madd), 0: Jacobian (j2b_madd)
+#define FTS_G2_PART_XYZZ 1  // 1: the parts in XYZZ form (x2q_madd), 0: Jacobian (j2b_madd)
 #endif
 
 // Product scanning: column k of both result rows is formed, the reduction's
@@ -165,7 +165,7 @@ FTS_HD x2q x2q_dbl_aff(const q2& x, const q2& y) {
 // p + (x2, y2), (x2, y2) affine (balanced) and not the identity: madd-2008-s.
 // P = U2 - X vanishes iff the x coordinates agree: the sum is then a doubling
 // (R = 0) or the identity.
-FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
+FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2, bool* dbl = nullptr) {
   if (p.inf) {
     const q2 one = q2_one_b();
     return {x2, y2, one, one, false};
@@ -173,7 +173,13 @@ FTS_HD x2q x2q_madd(const x2q& p, const q2& x2, const q2& y2) {
   const q2 P = q2_lin2b(q2_mulb(x2, p.zz), 1, p.x, -1);
   const q2 R = q2_lin2b(q2_mulb(y2, p.zzz), 1, p.y, -1);
   if (q2_rzero(P)) {
-    if (q2_rzero(R)) return x2q_dbl_aff(x2, y2);
+    if (q2_rzero(R)) {
+      if (dbl) {  // as j2b_madd: the caller redoes the lane in the 32-bit code
+        *dbl = true;
+        return p;
+      }
+      return x2q_dbl_aff(x2, y2);
+    }
     x2q o = p;
     o.inf = true;
     return o;
@@ -264,6 +270,7 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
   x2q acc;
   acc.inf = true;
   acc.x = acc.y = acc.zz = acc.zzz = q2_zero();
+  bool dbl = false;
 #else
   j2b acc;
   acc.inf = true;
@@ -281,7 +288,8 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
         q2 y2 = q2_from_fp2(T.y);
         if (d < 0) y2 = q2_neg(y2);
 #if FTS_G2_PART_XYZZ
-        acc = x2q_madd(acc, x2, y2);
+        acc = x2q_madd(acc, x2, y2, &dbl);
+        if (dbl) break;
 #else
         acc = j2b_madd(acc, x2, y2, &dbl);
         if (dbl) break;
@@ -289,13 +297,13 @@ FTS_HD void job_g2_part_x29(const G2Job& g, int q, const uint32_t (*scal)[8], co
       }
     }
   }
-#if FTS_G2_PART_XYZZ
-  g2part_store(out, x2q_to_g2j(acc));
-#else
   if (dbl) {
     job_g2_part(g, q, scal, tab, out);  // a running sum met its next table point
     return;
   }
+#if FTS_G2_PART_XYZZ
+  g2part_store(out, x2q_to_g2j(acc));
+#else
   g2part_store(out, j2b_to_g2j(acc));
 #endif
 }
