@@ -1,8 +1,10 @@
 // Fixed-base G2 partial sums (k_g2_part) on the carry-free balanced form of the
-// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_redc): the Jacobian mixed
-// addition (madd-2007-bl, 7M + 4S; j2b_madd) over balanced Fp2 values instead
-// of the 32-bit one of curve.h (the XYZZ form, madd-2008-s, x2q_madd, is the
-// FTS_G2_PART_XYZZ option: measured the same).  One Fp2 product is q2_mulb -- three
+// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_redc): the XYZZ mixed
+// addition (madd-2008-s, 8M + 2S; x2q_madd) over balanced Fp2 values instead
+// of the 32-bit Jacobian one of curve.h (a Jacobian q2 form, j2b_madd, is the
+// FTS_G2_PART_XYZZ=0 option: 8 % more VALU).  The rare doubling case (a
+// running sum equal to its next table point) redoes the lane in the 32-bit
+// code, so that its registers stay out of the loop (two waves per SIMD).  One Fp2 product is q2_mulb -- three
 // 81-MAD limb-product rows (Karatsuba) folded by columns into the two rows the
 // balanced reductions need, reduced while they are scanned -- against three
 // 32-bit Montgomery products with a carry add per MAD.  The partial leaves in Jacobian form through x2q_to_g2j, so
