@@ -1,16 +1,18 @@
 // Fixed-base G2 partial sums (k_g2_part) on the carry-free balanced form of the
-// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_redc): the XYZZ mixed
-// addition (madd-2008-s, 8M + 2S; x2q_madd) over balanced Fp2 values instead
-// of the 32-bit Jacobian one of curve.h (a Jacobian q2 form, j2b_madd, is the
-// FTS_G2_PART_XYZZ=0 option: 8 % more VALU).  The rare doubling case (a
-// running sum equal to its next table point) redoes the lane in the 32-bit
-// code, so that its registers stay out of the loop (two waves per SIMD).  One Fp2 product is q2_mulb -- three
-// 81-MAD limb-product rows (Karatsuba) folded by columns into the two rows the
-// balanced reductions need, reduced while they are scanned -- against three
-// 32-bit Montgomery products with a carry add per MAD.  The partial leaves in Jacobian form through x2q_to_g2j, so
-// job_g2lines_parts (the one-lane line kernel) is unchanged; t' = the sum of
-// the four partials in affine form does not depend on their representatives,
-// so g2out and every line byte are identical to job_g2_part's.
+// sextet kernels (dev/fp29.h q2, dev/sx29.h w29_redc): the XYZZ mixed addition
+// (madd-2008-s, 8M + 2S; x2q_madd) over balanced Fp2 values instead of the
+// 32-bit Jacobian one of curve.h (a Jacobian q2 form, j2b_madd, is the
+// FTS_G2_PART_XYZZ=0 option: 8 % more VALU).  The rare doubling case (a running
+// sum equal to its next table point) redoes the lane in the 32-bit code, so
+// that its registers stay out of the loop (two waves per SIMD).
+//
+// One Fp2 product is q2_mulb: three 81-MAD limb-product rows (Karatsuba) folded
+// by columns into the two rows the balanced reductions need, reduced while they
+// are scanned -- against three 32-bit Montgomery products with a carry add per
+// MAD.  The partial leaves in 32-bit Jacobian form, so job_g2lines_parts (the
+// one-lane line kernel) reads it unchanged; t' = the sum of the four partials
+// in affine form does not depend on their representatives, so g2out and every
+// line byte are identical to job_g2_part's.
 //
 // Bounds: coordinates between operations are balanced (q2_mulb and f29_lin2 /
 // f29_lin4 outputs: limbs in [-2^28, 2^28], |value| <= p/2 + e); q2_mulb
