@@ -235,34 +235,38 @@ FTS_HD fp12 f12_load(const F12Dev& d) {
   return f;
 }
 
+// the standard base64 alphabet (A-Z a-z 0-9 + /) by arithmetic: a per-lane
+// table lookup is a divergent memory load per character
+FTS_HD uint8_t b64_char(uint32_t v) {
+  const uint32_t c = v < 26 ? 'A' + v : (v < 52 ? 'a' + (v - 26) : (v < 62 ? '0' + (v - 52) : (v == 62 ? '+' : '/')));
+  return (uint8_t)c;
+}
 FTS_HD void b64_encode_64(uint8_t* out, const uint8_t* in) {
-  const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
   int o = 0;
   for (int k = 0; k < 63; k += 3) {
     uint32_t v = ((uint32_t)in[k] << 16) | ((uint32_t)in[k + 1] << 8) | in[k + 2];
-    out[o++] = a[v >> 18];
-    out[o++] = a[(v >> 12) & 63];
-    out[o++] = a[(v >> 6) & 63];
-    out[o++] = a[v & 63];
+    out[o++] = b64_char(v >> 18);
+    out[o++] = b64_char((v >> 12) & 63);
+    out[o++] = b64_char((v >> 6) & 63);
+    out[o++] = b64_char(v & 63);
   }
   uint32_t v = (uint32_t)in[63] << 16;
-  out[o++] = a[v >> 18];
-  out[o++] = a[(v >> 12) & 63];
+  out[o++] = b64_char(v >> 18);
+  out[o++] = b64_char((v >> 12) & 63);
   out[o++] = '=';
   out[o++] = '=';
 }
 
 // standard base64 (with '=' padding) of the 3-byte group g of in[0..len)
 FTS_HD void b64_group(uint8_t* out, const uint8_t* in, uint32_t len, uint32_t g) {
-  const char* a = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
   uint32_t k = 3 * g, rem = len - k;
   uint32_t v = (uint32_t)in[k] << 16;
   if (rem > 1) v |= (uint32_t)in[k + 1] << 8;
   if (rem > 2) v |= in[k + 2];
-  out[0] = a[v >> 18];
-  out[1] = a[(v >> 12) & 63];
-  out[2] = rem > 1 ? a[(v >> 6) & 63] : '=';
-  out[3] = rem > 2 ? a[v & 63] : '=';
+  out[0] = b64_char(v >> 18);
+  out[1] = b64_char((v >> 12) & 63);
+  out[2] = rem > 1 ? b64_char((v >> 6) & 63) : '=';
+  out[3] = rem > 2 ? b64_char(v & 63) : '=';
 }
 FTS_HD void b64_encode(uint8_t* out, const uint8_t* in, uint32_t len) {
   for (uint32_t g = 0; 3 * g < len; g++) b64_group(out + 4 * g, in, len, g);
