@@ -411,6 +411,22 @@ struct Park {
       (base + (size_t)(slot * 18 + 9 + i) * stride)[lane] = a.c1.l[i];
     }
   }
+  // an Fp value (8 words of the 32-bit form) in the first 8 planes of a slot,
+  // at lane `at` (the batched inversion's per-job values, see sq_fexp_easy_a)
+  FTS_HD void put_fp(int slot, uint32_t at, const fp& v) const {
+    if (!on) return;
+#pragma unroll
+    for (int i = 0; i < 8; i++) (base + (size_t)(slot * 18 + i) * stride)[at] = (int32_t)v.v[i];
+  }
+  FTS_HD fp get_fp(int slot, uint32_t at) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::: "memory");
+#endif
+    fp v;
+#pragma unroll
+    for (int i = 0; i < 8; i++) v.v[i] = on ? (uint32_t)(base + (size_t)(slot * 18 + i) * stride)[at] : 0u;
+    return v;
+  }
   FTS_HD q2 get(int slot) const {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" ::: "memory");  // reload here: the value must not stay in registers since put()
@@ -444,6 +460,67 @@ FTS_HD q2 sq_fexp_easy(const X& x, const fp2& f) {
   q2 m = sq_mulv(x, sq_conj(k, F), sq_inv(x, F));
   return sq_mulv(x, sq_frob2(k, m), m);
 }
+// The easy part with its one Fp inversion batched over the whole launch (the
+// device path; sq_fexp_easy above is the same value in one piece).  The
+// inversion f^-1 = conj(f) / N(f) needs the inverse of an Fp norm n per job:
+// inverted lane by lane (binary extended Euclid, data-dependent loops) it was
+// 80 % of the easy part's instructions (measured by a build without it).
+//   sq_fexp_easy_a: the Fp6 norm's terms tk (per lane, slot 4), the Fp2 value D
+//     (slot 5) and n = N(D) (lane 0 of the job's sextet, slot 9 planes 0..7);
+//   k_fexp_binv: every n of the launch inverted together (product tree per
+//     256 jobs, one Euclid per tree), written back in place (n = 0 -> 0, as
+//     fp_inv_var);
+//   sq_fexp_easy_b: f^-1 from tk, D and n^-1, then m as sq_fexp_easy.
+// Slots 4, 5 and 9 are free until the x-powers run.
+static constexpr int FEXP_EASY_TK = 4, FEXP_EASY_D = 5, FEXP_EASY_N = 9;
+template <class X, class P>
+FTS_HD void sq_fexp_easy_a(const X& x, const fp2& f, const P& pk, uint32_t lane0) {
+  const int k = x.k;
+  q2 F = q2_from_fp2(f);
+  q2 fc = sq_conj(k, F);
+  q2 d = sq_mulv(x, fc, F);  // lanes 0, 2, 4: d0, d1, d2; odd lanes 0
+  sq_pub(x, SX_A, d);
+  x.sync();
+  W29 w;
+  w29_init(w);
+#pragma nounroll
+  for (int t = 0; t < 2; t++) {
+    uint32_t e = term_at(SX_INV_TAB[t], k);
+    q2 u = x.get(e & 63), v = x.get((e >> 6) & 63);
+    v = q2_sel((e & TM_NEG) != 0, q2_neg(v), v);
+    w29_mac(w, q2_sel((e & TM_ZERO) != 0, q2_zero(), u), v);
+  }
+  q2 t = w29_reduce(w);
+  x.put(SX_P + k, t);
+  x.sync();
+  W29 v;
+  w29_init(v);
+#pragma nounroll
+  for (int s = 0; s < 3; s++) w29_mac(v, x.get(s == 0 ? SX_A + 0 : (s == 1 ? SX_AX + 4 : SX_AX + 2)), x.get(SX_P + s));
+  q2 tk = x.get(SX_P + (k >> 1));
+  x.sync();
+  const q2 D = w29_reduce(v);
+  pk.put(FEXP_EASY_TK, tk);
+  pk.put(FEXP_EASY_D, D);
+  if (k == 0) {
+    const fp2 Df = q2_to_fp2(D);
+    pk.put_fp(FEXP_EASY_N, lane0, fe_sqr(Df.c0) + fe_sqr(Df.c1));
+  }
+}
+template <class X, class P>
+FTS_HD q2 sq_fexp_easy_b(const X& x, const fp2& f, const P& pk, uint32_t lane0) {
+  const int k = x.k;
+  q2 F = q2_from_fp2(f);
+  q2 fc = sq_conj(k, F);
+  const q2 tk = pk.get(FEXP_EASY_TK);
+  const fp2 Df = q2_to_fp2(pk.get(FEXP_EASY_D));
+  const fp ni = pk.get_fp(FEXP_EASY_N, lane0);
+  const fp2 di = {Df.c0 * ni, fe_neg(Df.c1 * ni)};  // D^-1, as f2_inv_inl
+  q2 inv6 = q2_sel((k & 1) == 0, q2_mul(tk, q2_from_fp2(di)), q2_zero());
+  q2 m = sq_mulv(x, sq_conj(k, F), sq_mulv(x, fc, inv6));
+  return sq_mulv(x, sq_frob2(k, m), m);
+}
+
 // hard part from the four parked powers: y0 y1^2 y2^6 y3^12 y4^18 y5^30 y6^36 as
 //   t0 = y6^2 y4 y5,  t1 = y3 y5 t0,  t0 <- t0 y2,  t1 <- (t1^2 t0)^2,
 //   result = (t1 y1)^2 (t1 y0)

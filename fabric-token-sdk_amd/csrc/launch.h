@@ -83,8 +83,16 @@ __global__ void k_miller_n(const PairJob* jobs, uint32_t n, const LineCoef29* ql
                            const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
 __global__ void k_miller_f3(const PairJob* jobs, uint32_t n, const LineCoef29* qlines_n, const LineCoef29* pklines_n,
                             const G1Dev* g1out, const G1Dev* pnorm, F12Dev* fbuf);
-// final exponentiation phases (k_fexp.hip); park: fexp_park_bytes(n) of scratch (dev/sx29.h Park)
+// final exponentiation phases (k_fexp.hip); park: fexp_park_bytes(n) of scratch (dev/sx29.h Park).
+// FTS_FEXP_EASY_BATCH (default 1): the easy part in three launches with the
+// launch's Fp inversions batched (k_fexp_easy_a, k_fexp_binv, k_fexp_easy_b)
+#ifndef FTS_FEXP_EASY_BATCH
+#define FTS_FEXP_EASY_BATCH 1
+#endif
 __global__ void k_fexp_easy(uint32_t n, const F12Dev* fbuf, int32_t* park);
+__global__ void k_fexp_easy_a(uint32_t n, const F12Dev* fbuf, int32_t* park);
+__global__ void k_fexp_easy_b(uint32_t n, const F12Dev* fbuf, int32_t* park);
+__global__ void k_fexp_binv(uint32_t n, int32_t* park, uint32_t stride);
 __global__ void k_fexp_expt(uint32_t n, int32_t* park, int src, int dst, int ps);
 __global__ void k_fexp_hard(const PairJob* jobs, uint32_t n, uint8_t* arena, int32_t* park);
 __global__ void k_fexp_fc_mid1(uint32_t n, int32_t* park);
@@ -99,7 +107,13 @@ inline void launch_fexp(bool exact, const PairJob* jobs, uint32_t n, const F12De
                         int32_t* park, hipStream_t s) {
   if (!n) return;
   const uint32_t nb = (n + SX_JOBS_PER_WAVE - 1) / SX_JOBS_PER_WAVE;
+#if FTS_FEXP_EASY_BATCH
+  k_fexp_easy_a<<<nb, 64, 0, s>>>(n, fbuf, park);
+  k_fexp_binv<<<(n + 255) / 256, 256, 0, s>>>(n, park, nb * 64);
+  k_fexp_easy_b<<<nb, 64, 0, s>>>(n, fbuf, park);
+#else
   k_fexp_easy<<<nb, 64, 0, s>>>(n, fbuf, park);
+#endif
   if (exact) {
     for (int e = 0; e < 3; e++) k_fexp_expt<<<nb, 64, 0, s>>>(n, park, e, e + 1, 4);
     k_fexp_hard<<<nb, 64, 0, s>>>(jobs, n, arena, park);

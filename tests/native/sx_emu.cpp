@@ -198,6 +198,36 @@ int sxe_fexp(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
 }
 
 // the same with the carry-free sextet final exponentiation (dev/sx29.h)
+// the device's easy part in three phases (sq_fexp_easy_a, the batched
+// inversion -- here fp_inv_var of the parked n, as k_fexp_binv computes it --
+// and sq_fexp_easy_b) against sq_fexp_easy in one piece: the same m words.
+// zero_norm forces the n = 0 branch (n^-1 = 0 in both).
+int sxe_fexp_easy_split(uint32_t seed) {
+  uint32_t s = seed | 1;
+  int bad = 0;
+  for (int it = 0; it < 4; it++) {
+    fp12 f = rnd_f12(s);
+    std::vector<int32_t> park(6 * FEXP_PARK_SLOTS * 18, 0);
+    q2 one[6], split[6];
+    run6q([&](const SqH& x) { one[x.k] = sq_fexp_easy(x, f12_coef(f, x.k)); });
+    run6q([&](const SqH& x) {
+      Park pk{park.data(), (uint32_t)x.k, 6, true};
+      sq_fexp_easy_a(x, f12_coef(f, x.k), pk, 0u);
+    });
+    {
+      Park pk{park.data(), 0, 6, true};
+      pk.put_fp(FEXP_EASY_N, 0, fp_inv_var(pk.get_fp(FEXP_EASY_N, 0)));
+    }
+    run6q([&](const SqH& x) {
+      Park pk{park.data(), (uint32_t)x.k, 6, true};
+      split[x.k] = sq_fexp_easy_b(x, f12_coef(f, x.k), pk, 0u);
+    });
+    for (int k = 0; k < 6; k++)
+      if (memcmp(&one[k], &split[k], sizeof(q2))) bad++;
+  }
+  return bad;
+}
+
 int sxe_fexp29(uint32_t seed, int variant, uint8_t* out_sx, uint8_t* out_ref) {
   uint32_t s = seed | 1;
   fp12 f = rnd_f12(s);

@@ -108,3 +108,9 @@ def test_g2x29_scanned_products(sx):
     column product w29_prod1 for balanced operands, differences of two, and limbs at
     the bounds (2^29 operand limbs against balanced 2^28 ones)."""
     assert sx.sxe_q2_scan(12345, 400) == 0
+
+
+def test_fexp_easy_split(sx):
+    """The device's easy part in three launches (dev/sx29.h sq_fexp_easy_a, the batched
+    inversion of k_fexp_binv, sq_fexp_easy_b) gives sq_fexp_easy's m word for word."""
+    assert sx.sxe_fexp_easy_split(777) == 0
