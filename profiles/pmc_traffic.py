@@ -38,7 +38,8 @@ def main(fetch_db, write_db, valu_db=None):
         out["g1p"] = kb(("k_g1_part", part[0])) + kb(("k_g1_combine", comb[0]))
     # "3*k" = three launches of k per pass (the final exponentiation's x-powers)
     for key, names in (("miller", ("k_miller_n", "k_miller")),
-                       ("fexp", ("k_fexp_easy+3*k_fexp_expt+k_fexp_hard", "k_fexp_exact", "k_fexp")),
+                       ("fexp", ("k_fexp_easy_a+k_fexp_binv+k_fexp_easy_b+3*k_fexp_expt+k_fexp_hard",
+                                 "k_fexp_easy+3*k_fexp_expt+k_fexp_hard", "k_fexp_exact", "k_fexp")),
                        ("g2", ("k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
         for name in names:
             parts = [(int(p.split("*")[0]), p.split("*")[1]) if "*" in p else (1, p) for p in name.split("+")]
