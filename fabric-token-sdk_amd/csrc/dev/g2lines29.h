@@ -131,16 +131,46 @@ FTS_HD void evline_put_b(EvLineDev* base, uint32_t s, int c, uint32_t idx, uint3
   o[9] = 0;
 }
 
-// job_g2lines_parts (dev/jobs.h) with the line chain on this form: the four
-// partial sums of t' are added and normalised in the 32-bit code (the G2
-// output), then the lines
-FTS_HD void job_g2lines_parts_x29(const G2Job& g, const PairJob& j, const G2PartDev* part, G2Dev* g2out,
-                                  const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+// The four partial sums of t' added in the 32-bit Jacobian form and written
+// over part 0, and the norm N(Z) = Z0^2 + Z1^2 of the sum (in Fp, zero only
+// for Z = 0: -1 is not a square mod p) parked in part 1's first eight words,
+// for the launch's batched inversion (k_g2_sum, k_g2_binv, dev/binv.h)
+FTS_HD void job_g2_sum(G2PartDev* part, uint32_t idx, uint32_t njobs) {
   g2j acc = g2part_load(part[idx]);
 #pragma nounroll
   for (int q = 1; q < 4; q++) acc = jac_add_inl(acc, g2part_load(part[(size_t)q * njobs + idx]));
+  g2part_store(part[idx], acc);
+  const fp nz = fe_sqr(acc.z.c0) + fe_sqr(acc.z.c1);
+#pragma unroll
+  for (int i = 0; i < 8; i++) part[njobs + idx].w[i] = nz.v[i];
+}
+// t' in affine form from the sum and N(Z)^-1 (part 1 after k_g2_binv):
+// Z^-1 = conj(Z) N(Z)^-1, as f2_inv_inl, then jac_to_aff_inl's products
+FTS_HD g2a g2_sum_aff(const G2PartDev* part, uint32_t idx, uint32_t njobs) {
+  const g2j acc = g2part_load(part[idx]);
+  g2a r;
+  if (is_zero(acc.z)) {
+    r.x = zero_of<fp2>();
+    r.y = zero_of<fp2>();
+    r.inf = true;
+    return r;
+  }
+  fp ni;
+#pragma unroll
+  for (int i = 0; i < 8; i++) ni.v[i] = part[njobs + idx].w[i];
+  const fp2 zi = {acc.z.c0 * ni, fe_neg(acc.z.c1 * ni)};
+  const fp2 zi2 = sqr(zi);
+  r.x = acc.x * zi2;
+  r.y = acc.y * zi2 * zi;
+  r.inf = false;
+  return r;
+}
+
+// job_g2lines_parts (dev/jobs.h) with the line chain on this form: t' (Q,
+// affine) is written to the G2 output, then the lines
+FTS_HD void g2lines_chain_x29(const g2a& Q, const G2Job& g, const PairJob& j, G2Dev* g2out, const G1Dev* pts,
+                              EvLineDev* lines, uint32_t idx, uint32_t njobs) {
   G2Dev d;
-  const g2a Q = jac_to_aff_inl(acc);
   g2_store(d, Q);
   g2out[g.out] = d;
   const g1a P = g1_load(pts[j.p2]);
@@ -174,6 +204,20 @@ FTS_HD void job_g2lines_parts_x29(const G2Job& g, const PairJob& j, const G2Part
       g2l_add(X, Y, Z, Ax, Ay, yP, xP, emit);
     }
   }
+}
+// the four partial sums added and normalised in the 32-bit code (one
+// inversion per lane), then the chain
+FTS_HD void job_g2lines_parts_x29(const G2Job& g, const PairJob& j, const G2PartDev* part, G2Dev* g2out,
+                                  const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+  g2j acc = g2part_load(part[idx]);
+#pragma nounroll
+  for (int q = 1; q < 4; q++) acc = jac_add_inl(acc, g2part_load(part[(size_t)q * njobs + idx]));
+  g2lines_chain_x29(jac_to_aff_inl(acc), g, j, g2out, pts, lines, idx, njobs);
+}
+// the same after job_g2_sum and the batched inversion
+FTS_HD void job_g2lines_summed_x29(const G2Job& g, const PairJob& j, const G2PartDev* part, G2Dev* g2out,
+                                   const G1Dev* pts, EvLineDev* lines, uint32_t idx, uint32_t njobs) {
+  g2lines_chain_x29(g2_sum_aff(part, idx, njobs), g, j, g2out, pts, lines, idx, njobs);
 }
 
 }  // namespace fts

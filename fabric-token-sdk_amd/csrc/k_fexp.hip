@@ -1,6 +1,7 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
+#include "dev/binv.h"
 #include "dev/jobs.h"
 #include "dev/sx29.h"
 #include "launch.h"
@@ -49,55 +50,16 @@ __global__ void __launch_bounds__(64, 2) k_fexp_easy_b(uint32_t n, const F12Dev*
   pk.put(0, sq_fexp_easy_b(x, fexp_load(fbuf, jc, x.k), pk, blockIdx.x * 64 + sx_ * 6));
 }
 // n^-1 for the n of every job of the launch (slot FEXP_EASY_N, lane 0 of the
-// job's sextet; stride = the fexp launches' lane count): a product tree over
-// 256 jobs per workgroup in LDS, one inversion of the root, and the inverses
-// handed down the tree (inv(a) = inv(ab) b); a zero n stays zero
+// job's sextet; stride = the fexp launches' lane count), 256 jobs per
+// workgroup (dev/binv.h); a zero n stays zero
 __global__ void __launch_bounds__(256) k_fexp_binv(uint32_t n, int32_t* park, uint32_t stride) {
   __shared__ uint32_t tree[512][8];
-  const uint32_t t = threadIdx.x, j = blockIdx.x * 256 + t;
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   const uint32_t lane0 = (j / SX_JOBS_PER_WAVE) * 64 + (j % SX_JOBS_PER_WAVE) * 6;
   const Park pk{park, 0, stride, true};
-  fp v = fe_one<ModP>();
-  bool zero = false;
-  if (j < n) {
-    v = pk.get_fp(FEXP_EASY_N, lane0);
-    zero = fe_is_zero(v);
-    if (zero) v = fe_one<ModP>();
-  }
-  auto st = [&](uint32_t i, const fp& a) {
-#pragma unroll
-    for (int q = 0; q < 8; q++) tree[i][q] = a.v[q];
-  };
-  auto ld = [&](uint32_t i) {
-    fp a;
-#pragma unroll
-    for (int q = 0; q < 8; q++) a.v[q] = tree[i][q];
-    return a;
-  };
-  st(256 + t, v);  // heap order: root 1, node i's children 2i, 2i + 1, leaves 256..511
-  __syncthreads();
-  for (uint32_t w = 128; w >= 1; w >>= 1) {
-    if (t < w) st(w + t, ld(2 * (w + t)) * ld(2 * (w + t) + 1));
-    __syncthreads();
-  }
-  if (t == 0) st(1, fp_inv_var(ld(1)));
-  __syncthreads();
-  for (uint32_t w = 1; w <= 128; w <<= 1) {
-    fp ia, ib;
-    if (t < w) {
-      const uint32_t p = w + t;
-      const fp ip = ld(p), a = ld(2 * p), b = ld(2 * p + 1);
-      ia = ip * b;
-      ib = ip * a;
-    }
-    __syncthreads();
-    if (t < w) {
-      st(2 * (w + t), ia);
-      st(2 * (w + t) + 1, ib);
-    }
-    __syncthreads();
-  }
-  if (j < n) pk.put_fp(FEXP_EASY_N, lane0, zero ? fe_zero<ModP>() : ld(256 + t));
+  binv_tree256(
+      tree, threadIdx.x, j < n, [&] { return pk.get_fp(FEXP_EASY_N, lane0); },
+      [&](const fp& v) { pk.put_fp(FEXP_EASY_N, lane0, v); });
 }
 
 // phase 2 (three launches): slot dst = (slot src)^x, a^3, a^5, a^7 parked

@@ -1,6 +1,7 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
+#include "dev/binv.h"
 #include "dev/g2lines29.h"
 #include "dev/g2x29.h"
 #include "dev/jobs.h"
@@ -13,9 +14,6 @@ using namespace fts;
 #endif
 #ifndef FTS_G2_PART_WAVES
 #define FTS_G2_PART_WAVES 1  // waves per SIMD k_g2_part is compiled for
-#endif
-#ifndef FTS_G2LINES_X29
-#define FTS_G2LINES_X29 1  // k_g2lines1's line chain on the carry-free form (dev/g2lines29.h)
 #endif
 
 #define JOB_KERNEL_PROLOGUE(n)                          \
@@ -54,11 +52,37 @@ __global__ void __launch_bounds__(64, FTS_G2_PART_WAVES) k_g2_part(const G2Job* 
   job_g2_part(g2[job], (int)q, scal, tab, part[i]);
 #endif
 }
+// FTS_G2_BINV (default 1): the partial sums added in k_g2_sum and the
+// launch's inversions batched (k_g2_binv) before k_g2lines1, instead of one
+// inversion per lane inside it (X29 line chain only)
+__global__ void __launch_bounds__(64) k_g2_sum(uint32_t n, G2PartDev* part) {
+  JOB_KERNEL_PROLOGUE(n);
+  job_g2_sum(part, i, n);
+}
+__global__ void __launch_bounds__(256) k_g2_binv(uint32_t n, G2PartDev* part) {
+  __shared__ uint32_t tree[512][8];
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  uint32_t* w = part[n + (j < n ? j : 0)].w;
+  binv_tree256(
+      tree, threadIdx.x, j < n,
+      [&] {
+        fp v;
+#pragma unroll
+        for (int q = 0; q < 8; q++) v.v[q] = w[q];
+        return v;
+      },
+      [&](const fp& v) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) w[q] = v.v[q];
+      });
+}
 __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n,
                                                  const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,
                                                  EvLineDev* lines) {
   JOB_KERNEL_PROLOGUE(n);
-#if FTS_G2LINES_X29
+#if FTS_G2LINES_X29 && FTS_G2_BINV
+  job_g2lines_summed_x29(g2[i], pr[i], part, g2out, pts, lines, i, n);
+#elif FTS_G2LINES_X29
   job_g2lines_parts_x29(g2[i], pr[i], part, g2out, pts, lines, i, n);
 #else
   job_g2lines_parts(g2[i], pr[i], part, g2out, pts, lines, i, n);

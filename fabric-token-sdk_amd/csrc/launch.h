@@ -71,6 +71,14 @@ __global__ void k_g2(const G2Job* jobs, uint32_t n, const uint32_t (*scal)[8], c
 __global__ void k_g2lines(const G2Job* g2, const PairJob* pr, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab,
                           G2Dev* g2out, const G1Dev* pts, EvLineDev* lines);
 __global__ void k_g2_part(const G2Job* g2, uint32_t n, const uint32_t (*scal)[8], const G2Dev* tab, G2PartDev* part);
+#ifndef FTS_G2LINES_X29
+#define FTS_G2LINES_X29 1  // k_g2lines1's line chain on the carry-free form (dev/g2lines29.h)
+#endif
+#ifndef FTS_G2_BINV
+#define FTS_G2_BINV 1  // k_g2_sum + k_g2_binv before k_g2lines1 (k_g2.hip)
+#endif
+__global__ void k_g2_sum(uint32_t n, G2PartDev* part);
+__global__ void k_g2_binv(uint32_t n, G2PartDev* part);
 __global__ void k_g2lines1(const G2Job* g2, const PairJob* pr, uint32_t n, const G2PartDev* part, G2Dev* g2out,
                            const G1Dev* pts, EvLineDev* lines);
 __global__ void k_tab_g2(const G2Dev* bases, uint32_t n, G2Dev* tab);

@@ -674,6 +674,10 @@ static void launch_g2lines(ftz_ctx* c, const SlotPtrs& p, const G1Dev* pts, hipS
   if (!prover && !c->g2lanes_set && p.n_g2 <= c->opt.small_pass) layout = FTZ_LAYOUT_SEXTET;
   if (layout == FTZ_LAYOUT_ONE_LANE) {
     k_g2_part<<<blocks_for(4 * p.n_g2, 64), 64, 0, s>>>(p.g2, p.n_g2, p.scal, c->g2tab.p, p.part2);
+#if FTS_G2_BINV && FTS_G2LINES_X29
+    k_g2_sum<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.n_g2, p.part2);
+    k_g2_binv<<<blocks_for(p.n_g2, 256), 256, 0, s>>>(p.n_g2, p.part2);
+#endif
     k_g2lines1<<<blocks_for(p.n_g2, 64), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.part2, p.g2out, pts, p.lines2);
   } else {
     k_g2lines<<<blocks_for(p.n_g2, SX_JOBS_PER_WAVE), 64, 0, s>>>(p.g2, p.pr, p.n_g2, p.scal, c->g2tab.p, p.g2out, pts,

@@ -418,6 +418,22 @@ int sxe_g2lines29(const uint8_t* bases, const uint8_t* p2, const uint8_t* scalar
   std::vector<EvLineDev> l3(MILLER_LINES);
   job_g2lines_parts_x29(g, j, part.data(), o3.data(), &pt, l3.data(), 0, 1);
   if (memcmp(o1.data(), o3.data(), sizeof(G2Dev))) return 3;
+  // the device default: k_g2_sum, the batched inversion of N(Z) (one job
+  // here: its inverse), k_g2lines1 from the sum -- the same bytes
+  {
+    std::vector<G2PartDev> ps(part);
+    job_g2_sum(ps.data(), 0, 1);
+    fp nz;
+    for (int i = 0; i < 8; i++) nz.v[i] = ps[1].w[i];
+    nz = fe_is_zero(nz) ? fe_zero<ModP>() : fp_inv_var(nz);
+    for (int i = 0; i < 8; i++) ps[1].w[i] = nz.v[i];
+    std::vector<G2Dev> o5(1);
+    std::vector<EvLineDev> l5(MILLER_LINES);
+    job_g2lines_summed_x29(g, j, ps.data(), o5.data(), &pt, l5.data(), 0, 1);
+    if (memcmp(o3.data(), o5.data(), sizeof(G2Dev))) return 5;
+    for (int s = 0; s < MILLER_LINES; s++)
+      if (memcmp(&l3[s], &l5[s], sizeof(EvLineDev))) return 6;
+  }
   std::vector<LineCoef> ql(MILLER_LINES);
   precompute_lines(ql.data(), ld_g2(qfix));
   std::vector<LineCoef29> ql29(MILLER_LINES);
