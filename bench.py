@@ -489,7 +489,7 @@ def roofline(ctx, job, batch, device, tx_per_s, keep_serial=False, pp_key="pp_a"
     peak = madpeak(device)
     opc = json.load(open(os.path.join(ROOT, "profiles", "opcounts.json")))[pp_key]
     names = {"g1": "k_g1_part+k_g1_combine (side stream)", "g1p": "k_g1_part+k_g1_combine (pairing inputs)",
-             "g2": "k_g2_part+k_g2lines1 (t' + pair-2 lines)", "miller": "k_miller", "fexp": "k_fexp_easy_a+k_fexp_binv+k_fexp_easy_b+k_fexp_expt x3+k_fexp_hard",
+             "g2": "k_g2_part+k_g2_sum+k_g2_binv+k_g2lines1 (t' + pair-2 lines)", "miller": "k_miller", "fexp": "k_fexp_easy_a+k_fexp_binv+k_fexp_easy_b+k_fexp_expt x3+k_fexp_hard",
              "hash": "k_hash", "decode": "k_decode"}
     mjob = dict(opc["m_per_job"])
     mjob["g1p"] = mjob["g1"]  # the pairing-input G1 jobs run the same job code

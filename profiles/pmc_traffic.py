@@ -40,7 +40,7 @@ def main(fetch_db, write_db, valu_db=None):
     for key, names in (("miller", ("k_miller_n", "k_miller")),
                        ("fexp", ("k_fexp_easy_a+k_fexp_binv+k_fexp_easy_b+3*k_fexp_expt+k_fexp_hard",
                                  "k_fexp_easy+3*k_fexp_expt+k_fexp_hard", "k_fexp_exact", "k_fexp")),
-                       ("g2", ("k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
+                       ("g2", ("k_g2_part+k_g2_sum+k_g2_binv+k_g2lines1", "k_g2_part+k_g2lines1", "k_g2lines")), ("decode", ("k_decode",))):
         for name in names:
             parts = [(int(p.split("*")[0]), p.split("*")[1]) if "*" in p else (1, p) for p in name.split("+")]
             gs = [grids(n) for _, n in parts]
