@@ -1,8 +1,13 @@
 // Kernel translation unit (one per kernel family keeps hipcc builds parallel).
 #include <hip/hip_runtime.h>
 
+#include "dev/binv.h"
 #include "dev/jobs.h"
 #include "launch.h"
+
+#ifndef FTS_COMBINE_PRIO
+#define FTS_COMBINE_PRIO FTS_BINV_PRIO  // wave priority of the block inversion's Euclid (dev/binv.h)
+#endif
 
 using namespace fts;
 
@@ -59,7 +64,9 @@ __device__ fp block_batch_inv(fp x, uint32_t (*pre)[NT], uint32_t (*suf)[NT], ui
     fp all;
 #pragma unroll
     for (int k = 0; k < 8; k++) all.v[k] = pre[k][NT - 1];
+    __builtin_amdgcn_s_setprio(FTS_COMBINE_PRIO);  // the block waits on this wave
     fp ia = fp_inv_var(all);  // public values; one wave, one value: no divergence
+    __builtin_amdgcn_s_setprio(0);
     if (t == 0)
 #pragma unroll
       for (int k = 0; k < 8; k++) tot[k] = ia.v[k];
