@@ -5,6 +5,9 @@
 #include "dev/jobs.h"
 #include "launch.h"
 
+#ifndef FTS_G1PART_PRIO
+#define FTS_G1PART_PRIO 0  // wave priority of k_g1_part (A/B)
+#endif
 #ifndef FTS_COMBINE_PRIO
 #define FTS_COMBINE_PRIO FTS_BINV_PRIO  // wave priority of the block inversion's Euclid (dev/binv.h)
 #endif
@@ -22,6 +25,9 @@ __global__ void __launch_bounds__(128) k_g1_part(const G1Job* jobs, uint32_t n, 
                                                  G1Dev* vtab) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= 4 * n) return;
+#if FTS_G1PART_PRIO
+  __builtin_amdgcn_s_setprio(FTS_G1PART_PRIO);
+#endif
   job_g1_part(jobs, n, i, vt, pts, scal, tab, part, vtab);
 }
 

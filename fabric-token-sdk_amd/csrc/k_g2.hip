@@ -16,6 +16,10 @@ using namespace fts;
 #define FTS_G2_PART_WAVES 1  // waves per SIMD k_g2_part is compiled for
 #endif
 
+#ifndef FTS_G2LINES_PRIO
+#define FTS_G2LINES_PRIO 0  // wave priority of k_g2lines1 (A/B)
+#endif
+
 #define JOB_KERNEL_PROLOGUE(n)                          \
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; \
   if (i >= (n)) return;
@@ -80,6 +84,9 @@ __global__ void __launch_bounds__(64) k_g2lines1(const G2Job* g2, const PairJob*
                                                  const G2PartDev* part, G2Dev* g2out, const G1Dev* pts,
                                                  EvLineDev* lines) {
   JOB_KERNEL_PROLOGUE(n);
+#if FTS_G2LINES_PRIO
+  __builtin_amdgcn_s_setprio(FTS_G2LINES_PRIO);
+#endif
 #if FTS_G2LINES_X29 && FTS_G2_BINV
   job_g2lines_summed_x29(g2[i], pr[i], part, g2out, pts, lines, i, n);
 #elif FTS_G2LINES_X29
