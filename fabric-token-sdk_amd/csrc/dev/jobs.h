@@ -97,6 +97,9 @@ struct VTerm {
 // P_{e-1}, ..., P_0, each weight = b, computed as V = b V + P_t (PP-B range
 // equality: 15 x (4 doublings + 1 addition) instead of 16 64-bit multiples)
 static constexpr uint32_t VT_HORNER = 1;
+// The term is subtracted (weight -w): the digit weight int64(math.Pow(b, i)) =
+// -2^63 once b^i reaches 2^63 (range/proof.go:428), given as w = 2^63 | VT_NEG
+static constexpr uint32_t VT_NEG = 2;
 
 struct G1Job {
   uint32_t fscal[3];
@@ -779,7 +782,7 @@ FTS_HD g1j g1_var_point(const G1Job& j, const VTerm* vterms, const G1Dev* pts) {
   const VTerm& v0 = vterms[j.vstart];
   const uint64_t b = vterm_w(v0);
   const bool horner = (v0.flags & VT_HORNER) != 0;
-  if (j.vcount == 1 && (horner || b == 1)) return jac_from_aff(g1_load(pts[v0.pt]));
+  if (j.vcount == 1 && (horner || b == 1) && !(v0.flags & VT_NEG)) return jac_from_aff(g1_load(pts[v0.pt]));
   if (horner && (b & (b - 1)) == 0) {
     const int top = b ? 63 - __builtin_clzll(b) : 0;
     g1j V = jac_from_aff(g1_load(pts[v0.pt]));
@@ -809,7 +812,10 @@ FTS_HD g1j g1_var_point(const G1Job& j, const VTerm* vterms, const G1Dev* pts) {
     for (uint32_t t = j.vcount; t-- > 0;) {
       const VTerm& vt = vterms[j.vstart + t];
       const uint64_t w = horner ? c : vterm_w(vt);
-      if ((w >> q) & 1) V = jac_add_aff(V, g1_load(pts[vt.pt]));
+      if ((w >> q) & 1) {
+        const g1a P = g1_load(pts[vt.pt]);
+        V = jac_add_aff(V, (vt.flags & VT_NEG) ? aff_neg(P) : P);
+      }
       c *= b;
     }
   }

@@ -13,6 +13,7 @@
 // the GPU.  The planner only parses bytes (JSON, base64) and lays out jobs.
 #include "planner.h"
 
+#include <math.h>
 #include <string.h>
 
 #include <algorithm>
@@ -762,7 +763,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
       return;
     }
   for (uint32_t j = 0; j < n; j++)
-    if (r.mps[j].coms.size() != e || r.eq_cbf[j].nil()) {
+    if (pp.exponent <= 0 || r.mps[j].coms.size() != e || r.eq_cbf[j].nil()) {
       fail(E_MALFORMED);
       return;
     }
@@ -781,7 +782,12 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
       for (uint32_t i = e; i-- > 0;) terms.push_back(vterm(com_pt[j][i], pp.base));
       terms[0].flags = VT_HORNER;
     } else {
-      for (uint32_t i = 0; i < e; i++) terms.push_back(vterm(com_pt[j][i], pp.pow[i]));
+      // int64 weights; only -2^63 (math.Pow >= 2^63) is negative: weight 2^63, subtracted
+      for (uint32_t i = 0; i < e; i++) {
+        const int64_t w = (int64_t)pp.pow[i];
+        terms.push_back(vterm(com_pt[j][i], w < 0 ? 0 - (uint64_t)w : (uint64_t)w));
+        if (w < 0) terms.back().flags = VT_NEG;
+      }
     }
     g1job({{G1B_PED0, sv[j]}, {G1B_PED1, scb}}, terms, sc_rc, rg_bytes + 64 * (n + j));
   }
@@ -1678,6 +1684,85 @@ bool pp_sig_tables(const PPInfo& pp) {
   return true;
 }
 
+// Go math.Pow (src/math/pow.go, go1.18; amd64 runs this pure-Go path) for an
+// integer exponent: yf = 0, so ans = Ldexp(a1, ae) with a1 the product of the
+// mantissas x1^(2^k) of the set bits of n, each squared mantissa renormalised
+// to [0.5, 1).  Each step is one IEEE multiply or add; contraction into an FMA
+// would change the rounding, so it is off here.
+double go_pow_int(double x, int64_t n) {
+#pragma clang fp contract(off)
+  if (n == 0 || x == 1.0) return 1.0;
+  if (n == 1) return x;
+  double a1 = 1.0;
+  int64_t ae = 0;
+  int xe_i = 0;
+  double x1 = frexp(x, &xe_i);
+  int64_t xe = xe_i;
+  for (int64_t i = n; i != 0; i >>= 1) {
+    if (xe < -(1 << 12) || (1 << 12) < xe) {  // catastrophic overflow: Ldexp handles it
+      ae += xe;
+      break;
+    }
+    if (i & 1) {
+      a1 *= x1;
+      ae += xe;
+    }
+    x1 *= x1;
+    xe <<= 1;
+    if (x1 < .5) {
+      x1 += x1;
+      xe--;
+    }
+  }
+  if (ae > 4096) return HUGE_VAL;  // Go's Ldexp overflows to +Inf (a1 in (0, 1])
+  return ldexp(a1, (int)ae);
+}
+
+// int64(f) on amd64 (CVTTSD2SQ): truncation when representable, else the
+// "integer indefinite" 0x8000000000000000.  [EXT] the Go spec leaves the
+// out-of-range result implementation-defined.
+int64_t go_int64(double f) {
+  if (!(f >= -9223372036854775808.0 && f < 9223372036854775808.0)) return INT64_MIN;
+  return (int64_t)f;
+}
+
+int64_t digit_weight(uint32_t base, int64_t i) { return go_int64(go_pow_int((double)base, i)); }
+
+int prover_digits(const PPInfo& pp, const uint8_t* be32, uint32_t* digits) {
+  const int64_t e = pp.exponent;
+  const uint32_t b = pp.base;
+  if (e <= 0 || b < 2 || pp.pow.size() != (size_t)e) return 1;
+  for (int k = 0; k < 24; k++)
+    if (be32[k]) return 1;
+  uint64_t u = 0;
+  for (int k = 24; k < 32; k++) u = (u << 8) | be32[k];
+  if (pp.pow_top == INT64_MIN) {
+    // [EXT] the reference refuses every value here; exact digits of v < b^e,
+    // valid for its verifier when every weight below e is b^i
+    if (!pp.pow_exact) return 1;
+    unsigned __int128 bound = 1;
+    for (int64_t i = 0; i < e && bound <= ((unsigned __int128)1 << 64); i++) bound *= b;
+    if ((unsigned __int128)u >= bound) return 1;
+    for (int64_t i = 0; i < e; i++) {
+      digits[i] = (uint32_t)(u % b);
+      u /= b;
+    }
+    return 0;
+  }
+  // Value.Int() (range/proof.go:299) fails above int64; then v >= int64(math.Pow(b, e)) (:303)
+  if (u >> 63 || (int64_t)u >= pp.pow_top) return 1;
+  int64_t v = (int64_t)u;
+  digits[0] = (uint32_t)(v % (int64_t)b);  // values[0] = v % Base on the original v (:307)
+  for (int64_t i = 0; i < e - 1; i++) {    // quotient / remainder by w_(e-1-i) (:308-311)
+    const int64_t w = (int64_t)pp.pow[e - 1 - i];
+    const int64_t q = v / w;
+    v = v % w;
+    if (q < 0 || q >= (int64_t)b) return 2;  // Signatures[values[i]] out of range (:326)
+    digits[e - 1 - i] = (uint32_t)q;
+  }
+  return 0;
+}
+
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out) {
   JDoc outer;
   if (!outer.parse(p, n)) return "invalid public parameters json";
@@ -1716,8 +1801,11 @@ std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out)
   for (int k = 0; k < 3; k++)
     if (!el(d.elem((uint32_t)spk, k), out.pk[k])) return "invalid range proof parameters: nil public key";
   if (!el(d.field((uint32_t)rpp, "Q"), out.q)) return "invalid range proof parameters: generator Q is nil";
-  if (dec_int(d, d.field((uint32_t)rpp, "Exponent"), out.exponent) != D_OK || out.exponent <= 0 ||
-      out.exponent > 64)
+  // RangeProofParams.Validate (setup.go:66-68) refuses only 0; a negative
+  // exponent is a PP on which every range proof is "not well formed"
+  // (range/proof.go:424-426).  Above MAX_EXPONENT the context is refused.
+  if (dec_int(d, d.field((uint32_t)rpp, "Exponent"), out.exponent) != D_OK || out.exponent == 0 ||
+      out.exponent > MAX_EXPONENT)
     return "invalid range proof parameters: exponent";
   int64_t sv = d.field((uint32_t)rpp, "SignedValues");
   if (sv < 0 || d.at((uint32_t)sv).type != J_ARR || d.len((uint32_t)sv) < 2)
@@ -1731,23 +1819,17 @@ std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out)
     if (!el(d.field(s, "R"), out.sig_r[k]) || !el(d.field(s, "S"), out.sig_s[k]))
       return "invalid range proof parameters: signed value is nil";
   }
-  // digit weights base^i (range/proof.go:428: int64(math.Pow(float64(base), i)))
+  // digit weights int64(math.Pow(float64(Base), float64(i))) (range/proof.go:428)
   out.pow.clear();
-  long double acc = 1;
-  for (int64_t i = 0; i < out.exponent; i++) {
-    double pw = 1.0;
-    for (int64_t k = 0; k < i; k++) pw *= (double)out.base;  // float64 math.Pow is exact below 2^53
-    (void)acc;
-    if (pw >= 9223372036854775808.0) return "range proof exponent overflows int64";
-    out.pow.push_back((uint64_t)(int64_t)pw);
-  }
+  for (int64_t i = 0; i < out.exponent; i++) out.pow.push_back((uint64_t)digit_weight(out.base, i));
+  out.pow_top = digit_weight(out.base, out.exponent > 0 ? out.exponent : 0);
   // the Horner form of sum_i pow[i] com_i needs pow[i] == base^i exactly
-  out.pow_exact = true;
+  out.pow_exact = out.exponent > 0;
   unsigned __int128 bi = 1;
   for (size_t i = 0; i < out.pow.size(); i++) {
     if (i) bi *= out.base;
-    if (bi >> 64 || (uint64_t)bi != out.pow[i]) out.pow_exact = false;
-    if (bi >> 64) break;
+    if (bi >> 63 || (uint64_t)bi != out.pow[i]) out.pow_exact = false;
+    if (bi >> 63) break;
   }
   out.fixed_pairs = pp_sig_tables(out) && g2_lines_normalisable(out.q) && g2_lines_normalisable(out.pk[1]) &&
                     g2_lines_normalisable(out.pk[2]);

@@ -33,7 +33,12 @@ struct PPInfo {
   int64_t exponent = 0;
   int64_t curve = 0;
   std::string label;
-  std::vector<uint64_t> pow;                      // base^i, i < exponent
+  // digit weights w_i = int64(math.Pow(float64(base), float64(i))), i < exponent,
+  // as the int64's bit pattern (range/proof.go:428; digit_weight below): base^i
+  // while that is a float64, the rounded float64 above 2^53, and INT64_MIN once
+  // it reaches 2^63
+  std::vector<uint64_t> pow;
+  int64_t pow_top = 0;                            // w_exponent: the prover's bound (range/proof.go:303)
   bool pow_exact = false;                         // every pow[i] is base^i exactly (float64 math.Pow was exact)
   // the prover's membership commitments as three fixed-G2 pairings (Q, PK1,
   // PK2; parse_pp: every line of the three normalisable and pp_sig_tables)
@@ -47,6 +52,23 @@ struct PPInfo {
 // signature point is the identity (64 zero bytes); else through the variable-
 // base path.  The runtime / host emulation build those tables on first use.
 bool pp_sig_tables(const PPInfo& pp);
+// Largest RangeProofParams.Exponent a context accepts (the reference bounds it
+// only by != 0; a range proof then holds 2 x Exponent membership proofs per token).
+static constexpr int64_t MAX_EXPONENT = 1024;
+// Go math.Pow(x, float64(n)) for an integer n >= 0 and finite x >= 2 (Go
+// src/math/pow.go, go1.18: Frexp, repeated mantissa squaring, Ldexp) and
+// int64(f) as amd64 converts it (out of range -> INT64_MIN, [EXT]).
+double go_pow_int(double x, int64_t n);
+int64_t go_int64(double f);
+// int64(math.Pow(float64(base), float64(i))): the weight of digit i
+int64_t digit_weight(uint32_t base, int64_t i);
+// The digits range.Prover.preProcess commits to (range/proof.go:297-311) for a
+// value given as 32 big-endian bytes; 0 on success, 1 when the value is
+// refused ("value of token outside authorized range"), 2 when the reference
+// would panic (a digit >= base indexes past Signatures, :326).  Where the
+// reference's bound int64(math.Pow(base, exponent)) overflows (PP-B) the
+// build's [EXT] extension proves v < base^exponent by exact digits.
+int prover_digits(const PPInfo& pp, const uint8_t* be32, uint32_t* digits);
 // Returns empty string on success, else an error message.
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out);
 // PublicParams.Validate (setup.go:238-273) on serialized PP: "" or the error text

@@ -303,7 +303,7 @@ struct PB {
   // rangeproof.Prover.Prove over tokens (output commitments at tok_bytes);
   // v[k], bf[k] witness scalars, vals[k] the integer values, h_type HashToZr(type)
   std::pair<uint32_t, uint32_t> range(uint32_t tok_bytes, uint32_t n, const std::vector<uint32_t>& v,
-                                      const std::vector<uint32_t>& bf, const std::vector<uint64_t>& vals,
+                                      const std::vector<uint32_t>& bf, const std::vector<uint32_t>& digs,
                                       uint32_t h_type, const std::string& tag);
   void transfer(const TransferWit& w, size_t idx);
   void issue(const IssueWit& w, size_t idx);
@@ -329,16 +329,27 @@ struct PB {
   }
 };
 
-static bool value_u64(const uint8_t* b, uint64_t& v) {
-  for (int k = 0; k < 24; k++)
-    if (b[k]) return false;
-  v = 0;
-  for (int k = 24; k < 32; k++) v = (v << 8) | b[k];
-  return true;
+// PB's value checks (transfer.go:100-107 / issue.go via range.Prover): every
+// output's digits (prover_digits), zero digits for a refused value; "" or the
+// error text of the first refused value
+static std::string range_digits(const PPInfo& pp, const uint8_t* vals, uint32_t n, size_t idx, uint32_t* digs) {
+  const uint32_t e = pp.exponent > 0 ? (uint32_t)pp.exponent : 0;
+  std::string err;
+  for (uint32_t k = 0; k < n; k++) {
+    int r = prover_digits(pp, vals + 32 * k, digs + (size_t)k * e);
+    if (r) {
+      memset(digs + (size_t)k * e, 0, sizeof(uint32_t) * e);
+      if (err.empty())
+        err = "proof " + std::to_string(idx) +
+              (r == 1 ? ": can't compute range proof: value of token outside authorized range"
+                      : ": can't compute range proof: digit index out of range (the reference panics)");
+    }
+  }
+  return err;
 }
 
 std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const std::vector<uint32_t>& v,
-                                        const std::vector<uint32_t>& bf, const std::vector<uint64_t>& vals,
+                                        const std::vector<uint32_t>& bf, const std::vector<uint32_t>& digs,
                                         uint32_t h_type, const std::string& tag) {
   const uint32_t e = (uint32_t)pp.exponent, base = pp.base;
   uint32_t coms = arena_alloc(64 * n * e);
@@ -348,12 +359,11 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
   };
   std::vector<std::vector<Dig>> dg(n, std::vector<Dig>(e));
   std::vector<uint32_t> cbf(n);
+  (void)base;
   for (uint32_t k = 0; k < n; k++) {
-    uint64_t x = vals[k];
     std::vector<uint32_t> parts;
     for (uint32_t i = 0; i < e; i++) {
-      uint32_t d = (uint32_t)(x % base);
-      x /= base;
+      uint32_t d = digs[k * e + i];  // prover_digits: preProcess's values[i] (range/proof.go:297-311)
       std::string mt = tag + "/mp/" + std::to_string(k) + "/" + std::to_string(i);
       uint32_t dbf = rnd(tag + "/digit/" + std::to_string(k) + "/" + std::to_string(i) + "/bf");
       uint32_t sd = zr_u64(d, SRC_DIGIT, k * e + i);
@@ -513,17 +523,13 @@ std::pair<uint32_t, uint32_t> PB::range(uint32_t tok_bytes, uint32_t n, const st
 
 void PB::transfer(const TransferWit& w, size_t idx) {
   const uint32_t ni = w.n_in, no = w.n_out;
-  unsigned __int128 bound = 1;  // base^e (2^64 for b = 16, e = 16)
-  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
-  std::vector<uint64_t> ov(no);
   bool need_range = !(ni == 1 && no == 1);
-  for (uint32_t k = 0; k < no; k++)
-    if (!value_u64(w.out_values + 32 * k, ov[k]) || (need_range && ov[k] >= bound)) {
-      if (err.empty())
-        err = "proof " + std::to_string(idx) +
-              ": can't compute range proof: value of token outside authorized range";
-      ov[k] = 0;
-    }
+  std::vector<uint32_t> ov;
+  if (need_range) {
+    ov.assign((size_t)no * (pp.exponent > 0 ? (size_t)pp.exponent : 0), 0);
+    std::string e = range_digits(pp, w.out_values, no, idx, ov.data());
+    if (err.empty()) err = e;
+  }
   begin(w.seed);
   uint32_t first_pt = pl.n_pts;
   // tokens: inputs then outputs, canonical RawBytes (hashed by both transcripts)
@@ -604,16 +610,11 @@ void PB::transfer(const TransferWit& w, size_t idx) {
 
 void PB::issue(const IssueWit& w, size_t idx) {
   const uint32_t n = w.n_out;
-  unsigned __int128 bound = 1;
-  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
-  std::vector<uint64_t> vv(n);
-  for (uint32_t k = 0; k < n; k++)
-    if (!value_u64(w.values + 32 * k, vv[k]) || vv[k] >= bound) {
-      if (err.empty())
-        err = "proof " + std::to_string(idx) +
-              ": can't compute range proof: value of token outside authorized range";
-      vv[k] = 0;
-    }
+  std::vector<uint32_t> vv((size_t)n * (pp.exponent > 0 ? (size_t)pp.exponent : 0), 0);
+  {
+    std::string e = range_digits(pp, w.values, n, idx, vv.data());
+    if (err.empty()) err = e;
+  }
   begin(w.seed);
   uint32_t first_pt = pl.n_pts;
   uint32_t tok = arena_alloc(64 * n);
@@ -676,38 +677,16 @@ struct ProofTpl {
   uint32_t img_arena = 0, img_out = 0;  // the piece's wire copies of p.arena / p.out
 };
 
-// PB's value checks (transfer.go:100-107 / issue.go via range.Prover): the
-// error text of the first failing proof, and the values its digits come from
-static bool range_values(const PPInfo& pp, const uint8_t* vals, uint32_t n, bool need_range, uint64_t* out) {
-  unsigned __int128 bound = 1;
-  for (int64_t i = 0; i < pp.exponent; i++) bound *= pp.base;
-  bool ok = true;
-  for (uint32_t k = 0; k < n; k++)
-    if (!value_u64(vals + 32 * k, out[k]) || (need_range && out[k] >= bound)) {
-      ok = false;
-      out[k] = 0;
-    }
-  return ok;
-}
-
 struct WitView {
   const uint8_t* seed;
   const uint8_t *in_pt, *out_pt, *in_val, *in_bf, *out_val, *out_bf;
   const char* type;
-  const uint64_t* vals;  // output values (digits)
+  const uint32_t* digs;  // output k's digit i at k * exponent + i (range_digits)
 };
 
-// digit i of v in base b the way PB::range decomposes it (repeated division):
-// not v / pp.pow[i], whose float64 math.Pow entries are inexact above 2^53
-static uint32_t digit_of(uint64_t v, uint32_t base, uint32_t i) {
-  for (uint32_t k = 0; k < i; k++) v /= base;
-  return (uint32_t)(v % base);
-}
-
 static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& o, const WitView& w, Plan& pl) {
-  const uint32_t e = (uint32_t)pp.exponent;
   for (const BasePatch& q : t.bpatches) {
-    uint32_t d = digit_of(w.vals[q.k / e], pp.base, q.k % e);
+    uint32_t d = w.digs[q.k];
     G1Job& j = q.g1p ? pl.g1p[o.sec[PS_G1P] + q.job] : pl.g1[o.sec[PS_G1] + q.job];
     j.fbase[q.slot] = (uint8_t)(G1B_SIG0 + 2 * d + q.s);
   }
@@ -715,7 +694,7 @@ static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& 
     const uint8_t* src = nullptr;
     uint8_t tmp[32];
     uint32_t d = 0;
-    if (q.kind >= SRC_SIG_R) d = digit_of(w.vals[q.k / e], pp.base, q.k % e);
+    if (q.kind >= SRC_SIG_R) d = w.digs[q.k];
     switch (q.kind) {
       case SRC_SEED: src = w.seed; break;
       case SRC_IN_PT: src = w.in_pt + 64 * q.k; break;
@@ -748,7 +727,7 @@ static void apply_patches(const PPInfo& pp, const ProofTpl& t, const PieceBase& 
 static bool tpl_ok(const PPInfo& pp) {
   for (uint32_t d = 0; d < pp.base; d++)
     if (pp.sig_r[d].size() != pp.sig_r[0].size() || pp.sig_s[d].size() != pp.sig_s[0].size()) return false;
-  return pp.base > 0 && pp.exponent > 0 && pp.exponent <= 64 && pp.pow.size() == (size_t)pp.exponent;
+  return pp.base > 0 && pp.exponent > 0 && pp.pow.size() == (size_t)pp.exponent;
 }
 
 struct TplCache {
@@ -775,16 +754,17 @@ static std::string key_of(const IssueWit& w) {
 static void plan_one(PB& b, const TransferWit& x, size_t i) { b.transfer(x, i); }
 static void plan_one(PB& b, const IssueWit& x, size_t i) { b.issue(x, i); }
 
-static bool tpl_values(const PPInfo& pp, const TransferWit& w, uint64_t* v) {
-  return range_values(pp, w.out_values, w.n_out, !(w.n_in == 1 && w.n_out == 1), v);
+static std::string tpl_digits(const PPInfo& pp, const TransferWit& w, size_t i, uint32_t* d) {
+  if (w.n_in == 1 && w.n_out == 1) return "";  // no range proof (transfer.go:100-107)
+  return range_digits(pp, w.out_values, w.n_out, i, d);
 }
-static bool tpl_values(const PPInfo& pp, const IssueWit& w, uint64_t* v) {
-  return range_values(pp, w.values, w.n_out, true, v);
+static std::string tpl_digits(const PPInfo& pp, const IssueWit& w, size_t i, uint32_t* d) {
+  return range_digits(pp, w.values, w.n_out, i, d);
 }
-static WitView view_of(const TransferWit& w, const uint64_t* v) {
+static WitView view_of(const TransferWit& w, const uint32_t* v) {
   return {w.seed, w.inputs, w.outputs, w.in_values, w.in_bfs, w.out_values, w.out_bfs, w.type, v};
 }
-static WitView view_of(const IssueWit& w, const uint64_t* v) {
+static WitView view_of(const IssueWit& w, const uint32_t* v) {
   return {w.seed, nullptr, w.outputs, nullptr, nullptr, w.values, w.bfs, w.type, v};
 }
 
@@ -808,7 +788,7 @@ std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& 
       return;
     }
     TplCache cache;
-    std::vector<uint64_t> vals;
+    std::vector<uint32_t> vals;
     for (size_t i = lo; i < hi; i++) {
       std::string key = key_of(w[i]);
       ProofTpl* t = cache.find(key);
@@ -828,9 +808,9 @@ std::string plan_prove_pieces(const PPInfo& pp, size_t n, const W* w, PlanWork& 
         t->img_out = (uint32_t)p.wire.size();
         p.wire.insert(p.wire.end(), t->p.out.begin(), t->p.out.end());
       }
-      vals.assign(w[i].n_out, 0);
-      if (!tpl_values(pp, w[i], vals.data()) && work.errs[c].empty())
-        work.errs[c] = "proof " + std::to_string(i) + ": can't compute range proof: value of token outside authorized range";
+      vals.assign((size_t)w[i].n_out * (size_t)pp.exponent, 0);
+      std::string de = tpl_digits(pp, w[i], i, vals.data());
+      if (!de.empty() && work.errs[c].empty()) work.errs[c] = de;
       PieceBase o = plan_append(p, t->p);
       p.cp.push_back({t->img_arena, (uint32_t)t->p.arena.size(), (uint32_t)o.sec[PS_ARENA], 0});
       p.cp.push_back({t->img_out, (uint32_t)t->p.out.size(), (uint32_t)o.sec[PS_OUT], 1});

@@ -440,13 +440,127 @@ def dec_membership(v):
 
 
 # ------------------------------------------------------------------ range proof
+INT64_MIN = -(1 << 63)
+
+# Counterfactual switch for the parity tests only: True weighs digit i by the
+# exact integer base**i instead of the reference's int64(math.Pow(...)).
+EXACT_WEIGHTS = False
+
+
+def go_pow(x, n):
+    """Go math.Pow(x, float64(n)) for an integer n >= 0 and a finite x >= 2
+    (Go standard library src/math/pow.go, go1.18 per the reference's go.mod:3;
+    amd64 has no assembly Pow, so this pure-Go path is what runs).  Special
+    cases y == 0 / x == 1 -> 1 and y == 1 -> x, then yi = n, yf = 0:
+    Frexp(x) = x1 * 2^xe, repeated squaring of the mantissa x1 (renormalised
+    back to [0.5, 1) after each square), the set bits of n multiplied into a1
+    with their exponents summed into ae, and Ldexp(a1, ae).  Every float64
+    operation here is a single IEEE-754 round-to-nearest multiply or add (Go
+    does not fuse them on amd64), which Python floats reproduce exactly."""
+    import math
+    x = float(x)
+    if n == 0 or x == 1.0:
+        return 1.0
+    if n == 1:
+        return x
+    a1, ae = 1.0, 0
+    x1, xe = math.frexp(x)
+    i = n
+    while i != 0:
+        if xe < -(1 << 12) or (1 << 12) < xe:
+            # catastrophic overflow: Ldexp handles it below
+            ae += xe
+            break
+        if i & 1:
+            a1 *= x1
+            ae += xe
+        x1 *= x1
+        xe <<= 1
+        if x1 < 0.5:
+            x1 += x1
+            xe -= 1
+        i >>= 1
+    try:
+        return math.ldexp(a1, ae)
+    except OverflowError:  # Go's Ldexp returns +Inf
+        return float("inf")
+
+
+def go_int64(f):
+    """int64(f) for a float64 f as Go compiles it on amd64 (CVTTSD2SQ): the
+    truncated value when it fits, else the "integer indefinite" 0x8000000000000000
+    (= -2^63) for NaN, +-Inf and every out-of-range value.  [EXT] the Go spec
+    leaves the out-of-range result implementation-defined; amd64 is the
+    platform the reference's peers run on."""
+    if f != f or not (-9223372036854775808.0 <= f < 9223372036854775808.0):
+        return INT64_MIN
+    return int(f)
+
+
+def digit_weight(base, i):
+    """The weight of digit i in the range proof: int64(math.Pow(float64(Base),
+    float64(i))) (range/proof.go:428 verifier, :327 prover).  Equal to base**i
+    only while base**i is a float64; e.g. 7^21 comes out as 7^21 + 25 and
+    base^i >= 2^63 as -2^63.  As a Zr it is taken mod r (NewZrFromInt keeps the
+    big.Int; scalar multiplication and ModMul/ModAdd reduce it mod r)."""
+    if EXACT_WEIGHTS:
+        return base ** i
+    return go_int64(go_pow(base, i))
+
+
+def _go_quo(a, b):
+    """Go int64 a / b (truncated toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def _go_rem(a, b):
+    """Go int64 a % b (sign of the dividend)."""
+    return a - _go_quo(a, b) * b
+
+
+def range_weights_exact(base, exponent):
+    """True when every verifier weight int64(math.Pow(base, i)), i < exponent, is base**i."""
+    return all(go_int64(go_pow(base, i)) == base ** i for i in range(max(exponent, 0)))
+
+
 def digits(v, base, exponent):
-    """range/proof.go:303-311 (exact integer form of the float64 math.Pow path,
-    identical whenever base^i < 2^53)."""
-    out = []
-    for _ in range(exponent):
-        out.append(v % base)
-        v //= base
+    """range/proof.go:297-311 preProcess: the digits the reference's prover
+    commits to.  v must be an int64 (Value.Int(), :299); v >= int64(math.Pow(
+    Base, Exponent)) is refused (:303-305); values[0] = v % Base on the
+    original v (:307), then for i = Exponent-1 .. 1 values[i] = v / w_i and
+    v = v % w_i with w_i = int64(math.Pow(Base, i)) (:308-311).  With inexact
+    weights the digits need not sum back to v (the reference's verifier then
+    rejects its own prover's proof), and a digit >= Base indexes past
+    Signatures (:326) -- a Go panic, raised here as ``Panic``.
+
+    [EXT] extension: where int64(math.Pow(Base, Exponent)) overflows (e.g.
+    PP-B, b = 16, e = 16: 2^64 -> -2^63) the reference refuses every value;
+    this build then proves v < Base^Exponent (up to 2^64 - 1) with the exact
+    base-Base digits, which the reference's verifier accepts whenever every
+    weight below Exponent is exact (else refused here)."""
+    if v < 0:
+        raise ValueError("can't compute range proof: value of token outside authorized range")
+    top = digit_weight(base, exponent)
+    if top == INT64_MIN and not EXACT_WEIGHTS:
+        if v >= base ** exponent or not range_weights_exact(base, exponent):
+            raise ValueError("can't compute range proof: value of token outside authorized range")
+        out = []
+        for _ in range(exponent):
+            out.append(v % base)
+            v //= base
+        return out
+    if v >= (1 << 63) or v >= top:
+        raise ValueError("can't compute range proof: value of token outside authorized range")
+    out = [0] * exponent
+    out[0] = _go_rem(v, base)
+    for i in range(exponent - 1):
+        w = digit_weight(base, exponent - 1 - i)
+        out[exponent - 1 - i] = _go_quo(v, w)
+        v = _go_rem(v, w)
+    for d in out:
+        if d >= base or d < 0:
+            raise Panic("index out of range [%d] with length %d" % (d, base))
     return out
 
 
@@ -459,14 +573,15 @@ def range_transcript(pp, tokens, com_tokens, com_values, coms):
     return data
 
 
-def range_prove(pp, rnd, tag, tokens, witnesses, ttype):
-    """range/proof.go:141-209 Prove.  witnesses: list of (value, bf)."""
+def range_prove(pp, rnd, tag, tokens, witnesses, ttype, digit_rows=None):
+    """range/proof.go:141-209 Prove.  witnesses: list of (value, bf).
+    digit_rows (test fixtures only): commit to these digits instead of
+    preProcess's (a crafted proof, e.g. one the reference's prover refuses to
+    make but its verifier accepts)."""
     base, e = pp.base, pp.exponent
     coms, mps, com_bfs = [], [], []
     for k, (v, bf) in enumerate(witnesses):
-        if v >= base ** e:
-            raise ValueError("can't compute range proof: value of token outside authorized range")
-        ds = digits(v, base, e)
+        ds = digits(v, base, e) if digit_rows is None else digit_rows[k]
         row, mrow, cbf = [], [], 0
         for i, d in enumerate(ds):
             dbf = rnd.zr("%s/digit/%d/%d/bf" % (tag, k, i))
@@ -474,7 +589,8 @@ def range_prove(pp, rnd, tag, tokens, witnesses, ttype):
             row.append(com)
             mrow.append(membership_prove(pp, rnd, "%s/mp/%d/%d" % (tag, k, i),
                                          pp.signed_values[d], d, dbf, com))
-            cbf = (cbf + dbf * base ** i) % R
+            # commitmentBlindingFactor += bf * pow mod r (:327-329)
+            cbf = (cbf + dbf * digit_weight(base, i)) % R
         coms.append(row)
         mps.append(mrow)
         com_bfs.append(cbf)
@@ -576,7 +692,7 @@ def range_verify(pp, tokens, raw):
         for i in range(pp.exponent):
             if cs[i] is None:
                 raise Panic("nil commitment")
-            com = C.g1_add(com, C.g1_mul(pt(cs[i]), pp.base ** i))
+            com = C.g1_add(com, C.g1_mul(pt(cs[i]), digit_weight(pp.base, i) % R))
         cvals.append(schnorr_recompute(pp.ped[:2], [eq["Value"][j], eq["CommitmentBlindingFactor"][j]],
                                        com, chal))
     coms = [[pt(c) for c in mps[j]["Commitments"]] for j in range(n)]
@@ -665,11 +781,12 @@ def wf_verify(pp, ins, outs, raw):
 
 
 # ------------------------------------------------------------------ transfer
-def transfer_prove(pp, rnd, ins, outs, in_w, out_w, ttype, tag="tx"):
-    """transfer/transfer.go:89-121 Prove -> json.Marshal(Proof{WF, Range})."""
+def transfer_prove(pp, rnd, ins, outs, in_w, out_w, ttype, tag="tx", digit_rows=None):
+    """transfer/transfer.go:89-121 Prove -> json.Marshal(Proof{WF, Range}).
+    digit_rows: see range_prove (crafted fixtures only)."""
     rc = None
     if not (len(ins) == 1 and len(outs) == 1):
-        rc = range_prove(pp, rnd, tag + "/range", outs, out_w, ttype)
+        rc = range_prove(pp, rnd, tag + "/range", outs, out_w, ttype, digit_rows)
     wf = wf_prove(pp, rnd, tag + "/wf", ins, outs, in_w, out_w, ttype)
     return J.enc_struct([("WellFormedness", J.enc_bytes(wf)),
                          ("RangeCorrectness", J.enc_bytes(rc))]).encode()
@@ -737,10 +854,10 @@ def issue_wf_prove(pp, rnd, tag, tokens, wit, ttype, anonymous=False):
     return J.enc_struct(fields).encode()
 
 
-def issue_prove(pp, rnd, tokens, wit, ttype, anonymous=False, tag="issue"):
-    """issue/issue.go:162-184 Prove."""
+def issue_prove(pp, rnd, tokens, wit, ttype, anonymous=False, tag="issue", digit_rows=None):
+    """issue/issue.go:162-184 Prove (digit_rows: see range_prove)."""
     wf = issue_wf_prove(pp, rnd, tag + "/wf", tokens, wit, ttype, anonymous)
-    rc = range_prove(pp, rnd, tag + "/range", tokens, wit, ttype)
+    rc = range_prove(pp, rnd, tag + "/range", tokens, wit, ttype, digit_rows)
     return J.enc_struct([("WellFormedness", J.enc_bytes(wf)),
                          ("RangeCorrectness", J.enc_bytes(rc))]).encode()
 

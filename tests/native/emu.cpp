@@ -80,7 +80,9 @@ int emu_g1_mul_glv(const uint8_t* p64, const uint8_t* k32, int which, uint8_t* o
   return g1_on_curve(r) ? 0 : 1;
 }
 // The variable part of one G1 job (job_g1_part, part 3): k (sum_t c_t P_t)
-// with c_t = base^(cnt-1-t) (horner) or w[t], negated when vneg.
+// with c_t = base^(cnt-1-t) (horner = 1) or w[t], negated when vneg.
+// horner = 2: w[t] are int64 weights, a negative one given to the job as its
+// magnitude with VT_NEG (the planner's -2^63 digit weight).
 int emu_g1_var_part(const uint8_t* pts64, const uint64_t* w, uint32_t cnt, int horner, int vneg,
                     const uint8_t* k32, uint8_t* out64) {
   std::vector<G1Dev> pts(cnt);
@@ -88,9 +90,11 @@ int emu_g1_var_part(const uint8_t* pts64, const uint64_t* w, uint32_t cnt, int h
   for (uint32_t t = 0; t < cnt; t++) {
     g1_store(pts[t], ld_g1(pts64 + 64 * t));
     vt[t].pt = t;
-    vt[t].w_lo = (uint32_t)w[t];
-    vt[t].w_hi = (uint32_t)(w[t] >> 32);
-    vt[t].flags = (horner && t == 0) ? VT_HORNER : 0;
+    const bool neg = horner == 2 && (int64_t)w[t] < 0;
+    const uint64_t m = neg ? 0 - w[t] : w[t];
+    vt[t].w_lo = (uint32_t)m;
+    vt[t].w_hi = (uint32_t)(m >> 32);
+    vt[t].flags = (horner == 1 && t == 0) ? VT_HORNER : (neg ? VT_NEG : 0);
   }
   G1Job j{};
   j.nfix = 0;

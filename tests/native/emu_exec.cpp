@@ -676,3 +676,16 @@ extern "C" int emu_f29_check(uint64_t seed, int iters) {
   }
   return bad;
 }
+
+// Range-proof digit weights and the prover's digits as the product computes
+// them (host/planner.cpp digit_weight / prover_digits), for the weight parity
+// tests (tests/test_weights.py)
+extern "C" int64_t emu_digit_weight(uint32_t base, int64_t i) { return ftsh::digit_weight(base, i); }
+extern "C" int emu_prover_digits(const uint8_t* pp_json, size_t pp_len, const uint8_t* be32, uint32_t* digits,
+                                 int64_t* weights) {
+  ftsh::PPInfo pp;
+  if (!ftsh::parse_pp(pp_json, pp_len, "zkatdlog", pp).empty()) return -1;
+  for (size_t i = 0; i < pp.pow.size(); i++) weights[i] = (int64_t)pp.pow[i];
+  weights[pp.pow.size()] = pp.pow_top;
+  return ftsh::prover_digits(pp, be32, digits);
+}

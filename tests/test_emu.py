@@ -167,10 +167,15 @@ def test_g1_variable_point_forms(emu):
         ([C.g1_neg(C.g1_mul(G, 100)), G], [100, 100], True),
         ([G, C.g1_neg(C.g1_mul(G, 100))], [100, 100], True),  # 100 G - 100 G = O
         ([G, G], [1, 1], False),  # doubling inside the sum
+        # signed int64 weights (horner = 2): int64(math.Pow) = -2^63 subtracts 2^63 P (range/proof.go:428)
+        (pts(3), [1, 1000, -(1 << 63)], 2),
+        (pts(2), [-(1 << 63), -(1 << 63)], 2),
+        ([G, G], [1 << 62, -(1 << 63)], 2),  # 2^62 G - 2^63 G
+        (pts(1), [-(1 << 63)], 2),
     ]
     for n, (P, w, horner) in enumerate(cases):
         cnt = len(P)
-        c = [w[0] ** (cnt - 1 - t) for t in range(cnt)] if horner else w
+        c = [w[0] ** (cnt - 1 - t) for t in range(cnt)] if horner is True else w
         V = None
         for Pt, ct in zip(P, c):
             V = C.g1_add(V, C.g1_mul(Pt, ct % C.R))
@@ -178,7 +183,7 @@ def test_g1_variable_point_forms(emu):
             k = rng.randrange(C.R) if n % 2 else C.R - 1
             want = C.g1_mul(C.g1_neg(V) if vneg else V, k)
             o = buf(64)
-            warr = (ctypes.c_uint64 * cnt)(*w)
+            warr = (ctypes.c_uint64 * cnt)(*[x % (1 << 64) for x in w])
             assert emu.emu_g1_var_part(b"".join(C.g1_bytes(p) for p in P), warr, cnt, int(horner), vneg,
                                        k.to_bytes(32, "big"), o) == 0
             assert o.raw == C.g1_bytes(want), (n, vneg)
