@@ -16,7 +16,9 @@ against its expected code.
 With N GPUs (torchrun, one process per GPU) the job is N x steps x batch
 transfers sharded contiguously by transaction (zkatdlog.dist.verify_shard,
 weak scaling: each rank verifies steps x batch); the only collective is the
-verdict-bitmap all-gather over RCCL (configs[3]).  Prints ONE JSON line.
+verdict-bitmap all-gather over RCCL (configs[3]).  Prints ONE JSON line (a
+compact summary, < 6 KB) and writes every leg in full to --detail-out
+(gpurun_out/bench_detail.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
@@ -747,6 +749,68 @@ def owner_signatures_curve(ctx, fixture, curve_id, curve_name, n, reps):
             "msg_bytes": len(base[0][1]), "all_accepted": ok, "curve": curve_name}
 
 
+def compact_line(line):
+    """The final stdout line: the contract's fields plus every leg's headline
+    numbers, without notes, per-kernel tables or MSM result bytes (those stay in
+    the detail file).  Kept under 6 KB."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "verdicts_bit_exact", "accepted", "setup_s", "library", "engine",
+            "cpu_baseline", "msm_split", "plan_upload_s_per_batch")
+    out = {k: line[k] for k in keep if k in line}
+    rf = line.get("roofline")
+    if rf:
+        out["roofline"] = {k: rf.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                                  "kernel_ms_serial", "jobs", "m_per_job", "serial_ms",
+                                                  "per_kernel_frac")}
+        iss = rf.get("issue") or {}
+        out["roofline"]["issue_frac"] = {k: v.get("frac") for k, v in (iss.get("per_kernel") or {}).items()}
+        out["roofline"]["pipeline_frac"] = (rf.get("pipeline") or {}).get("frac")
+
+    def msm_rows(rows):
+        if not rows:
+            return rows
+        return [{"n": r["n"], "ms": r["ms"], "device_ms": r.get("device_ms"), "ms_host_scalars": r.get("ms_host_scalars"),
+                 "window_bits": r.get("window_bits"), "frac": (r.get("roofline") or {}).get("frac"),
+                 "matches_variable_base": r.get("matches_variable_base")} for r in rows]
+    out["msm"] = msm_rows(line.get("msm"))
+    out["msm_resident"] = msm_rows(line.get("msm_resident"))
+    m20 = next((r for r in (line.get("msm") or []) if r["n"] == 1 << 20), None)
+    out["msm_2^20_latency_ms"] = m20["ms"] if m20 else None
+    out["msm_2^20_latency_ms_device"] = m20.get("device_ms") if m20 else None
+    out["msm_2^20_latency_ms_host_scalars"] = m20.get("ms_host_scalars") if m20 else None
+    if line.get("prover"):
+        out["prover"] = {k: line["prover"].get(k) for k in ("proofs_per_s", "ms_per_batch", "batch",
+                                                            "all_accepted_by_gpu_verifier")}
+    if line.get("pp_b"):
+        p = line["pp_b"]
+        out["pp_b"] = {k: p.get(k) for k in ("verify_transfers_per_s", "verdicts_bit_exact", "prove_proofs_per_s")}
+        out["pp_b"]["frac"] = (p.get("roofline") or {}).get("frac")
+    if line.get("device_only"):
+        d = line["device_only"]
+        out["device_only"] = {k: d.get(k) for k in ("transfers_per_s", "ms_per_batch", "batch_latency_ms",
+                                                    "verdicts_ok", "kernel_ms")}
+    if line.get("owner_signatures"):
+        out["owner_signatures"] = {k: v.get("signatures_per_s") for k, v in line["owner_signatures"].items()}
+    if line.get("token_requests"):
+        t = line["token_requests"]
+        out["token_requests"] = {"batched_transfers_per_s": (t.get("batched_get_states") or {}).get("transfers_per_s"),
+                                 "per_key_transfers_per_s": (t.get("per_key_get_state") or {}).get("transfers_per_s"),
+                                 "verdicts_bit_exact": all((t.get(k) or {}).get("verdicts_bit_exact", True)
+                                                           for k in ("batched_get_states", "per_key_get_state")),
+                                 "vs_verify_transfers": t.get("vs_verify_transfers")}
+    if line.get("seam"):
+        s = line["seam"]
+        out["seam"] = {"call_latency_ms_by_size": s.get("call_latency_ms_by_size"),
+                       "closed_loop_n1": [{k: r.get(k) for k in ("callers", "transfers_per_s", "p99_ms", "max_ms",
+                                                                 "verdict_mismatches")}
+                                          for r in s.get("closed_loop_n1") or []]}
+    if line.get("cpu_baselines"):
+        out["cpu_baselines"] = {k: (v.get("value") if isinstance(v, dict) and "value" in v else
+                                    v.get("ms") if isinstance(v, dict) else v)
+                                for k, v in line["cpu_baselines"].items()}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -770,6 +834,9 @@ def main():
                     help="profiling: every kernel on one stream for the whole run (ftz_ctx_set_serial), so that a "
                          "rocprofv3 kernel trace gives per-kernel durations without overlap")
     ap.add_argument("--opt", default="", help="A/B: extra ftz_options fields, e.g. 'pass_shaping=0,small_pass=0'")
+    ap.add_argument("--lib", default=None, help="A/B only: a variant build of libftsamd.so (build.py --variant)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="every leg in full (repo-relative path); the last stdout line is the compact summary")
     ap.add_argument("--layout", default=os.environ.get("FTZ_LAYOUT", ""),
                     help="kernel layouts, e.g. 'g2lines=sextet,pairing=one_lane' (ftz_ctx_set_layout)")
     args = ap.parse_args()
@@ -787,8 +854,11 @@ def main():
     import numpy as np
 
     import zkatdlog
+    from zkatdlog import _abi
     from zkatdlog import workload as W
     from zkatdlog.dist import bitmap_of, verify_shard
+    if args.lib:
+        _abi.use_library(args.lib)
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     pp_json = g["pp"].encode()
     extra_opt = {k: int(v) for k, v in (kv.split("=") for kv in filter(None, args.opt.split(",")))}
@@ -890,6 +960,7 @@ def main():
                        "batch_per_gpu": args.batch, "device_pass": db, "pp": "b=100,e=2", "fexp": "exact",
                        "parallelism": "tx-sharded x%d" % world},
             "verdicts_bit_exact": verdict_ok, "accepted": n_accept, "setup_s": round(t_setup, 2),
+            "library": os.path.relpath(_abi.loaded_path(), ROOT),
             "engine": {"batches": est["batches"], "max_in_flight": est["max_in_flight"],
                        "host_plan_ms_per_batch": round(est["plan_ms"] / max(1, est["batches"]), 3),
                        "enqueue_ms_per_batch": round(est["submit_ms"] / max(1, est["batches"]), 3),
@@ -902,7 +973,15 @@ def main():
             "msm_2^20_latency_ms": msm20, "msm": msm, "msm_resident": msm_res, "msm_split": msm_split, "prover": prover, "pp_b": ppb,
         }
         line.update(extras)
-        print(json.dumps(line), flush=True)
+        # every leg in full -> the detail file; the one stdout line (the driver
+        # keeps an 8 KB tail) is the compact summary of the same numbers
+        detail = os.path.join(ROOT, args.detail_out)
+        os.makedirs(os.path.dirname(detail), exist_ok=True)
+        with open(detail, "w") as f:
+            json.dump(line, f, indent=1)
+        summary = compact_line(line)
+        summary["detail"] = args.detail_out
+        print(json.dumps(summary), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -9,8 +9,9 @@ travels to the GPU box with the repo snapshot).
     python fabric-token-sdk_amd/build.py --variant NAME --defs "-DFTS_SX_KARA=0"
 
 --variant builds an A/B library with extra defines into zkatdlog/_lib/ab/
-libftsamd_NAME.so (objects in build/obj_NAME); FTS_LIB=<path> makes
-zkatdlog._abi load it instead of the default library (same-box A/B runs).
+libftsamd_NAME.so (objects in build/obj_NAME); `bench.py --lib <path>`
+(zkatdlog._abi.use_library) loads it instead of the default library for
+same-box A/B runs.
 """
 import argparse
 import glob

@@ -273,8 +273,6 @@ class Stats(ctypes.Structure):
 
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libftsamd.so")
-# same-box A/B runs load a variant build (build.py --variant) instead
-LIB_PATH = os.environ.get("FTS_LIB") or LIB_PATH
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
@@ -289,6 +287,23 @@ SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ct
            "ftz_prover_run", "ftz_prover_submit", "ftz_prover_wait", "ftz_prover_bytes", "ftz_prover_proofs", "ftz_prover_stats", "ftz_prover_destroy"]
 
 _lib = None
+
+
+def use_library(path):
+    """Bench / A/B entry points only (bench.py --lib): load the variant build at
+    `path` (build.py --variant) instead of the bundled library.  No environment
+    variable does this, so a deployment always runs the bundled build; must be
+    called before the first load()."""
+    global LIB_PATH
+    path = os.path.abspath(path)
+    if _lib is not None and path != LIB_PATH:
+        raise RuntimeError("libftsamd already loaded from %s" % LIB_PATH)
+    LIB_PATH = path
+
+
+def loaded_path():
+    """The path of the library this process loaded (None before load())."""
+    return LIB_PATH if _lib is not None else None
 
 
 def load():

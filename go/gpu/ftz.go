@@ -28,6 +28,7 @@ import (
 	"crypto/sha256"
 	"os"
 	"runtime"
+	"sort"
 	"strconv"
 	"sync"
 	"unsafe"
@@ -127,61 +128,157 @@ func newVerifierRaw(raw []byte, device int, o *Options) (*Verifier, error) {
 	return v, nil
 }
 
-// shared holds one (Verifier, OwnerVerifier) pair per device, keyed by the
-// SHA-256 of the serialized public parameters (Shared).
+// shared holds the process's (Verifier, OwnerVerifier) pairs, one per
+// (device, SHA-256 of the serialized public parameters): one process can run
+// several TMSs (one per network, channel and namespace; tms.go:294 ->
+// core.NewValidator), each with its own public parameters, on one device.
 var shared struct {
-	mu sync.Mutex
-	m  map[int]*sharedEntry
+	mu   sync.Mutex
+	m    map[sharedKey]*sharedEntry
+	tick uint64
+}
+
+type sharedKey struct {
+	device int
+	pp     [32]byte
 }
 
 type sharedEntry struct {
-	pp [32]byte
-	v  *Verifier
-	ov *OwnerVerifier // nil when SupportsIdemixCurve(pp.IdemixCurveID) is false
+	key      sharedKey
+	v        *Verifier
+	ov       *OwnerVerifier // nil when SupportsIdemixCurve(pp.IdemixCurveID) is false
+	refs     int            // live Handles
+	lastUsed uint64         // shared.tick when the last Handle was released
 }
 
-// Shared returns the process-wide Verifier and OwnerVerifier of (device, pp).
-// Driver.NewValidator runs per request on some paths (the Orion custodian:
-// services/network/orion/approval.go:100 -> token.NewServicesFromPublicParams
-// -> core.NewValidator), so a device context -- the PP's fixed-base tables in
-// HBM, streams, planning threads -- is built once per (device, PP) and reused
-// by every validator. New public parameters on a device close the previous
-// pair explicitly (Close waits for the calls in flight; a validator still
-// holding the old pair then fails with "gpu verifier closed"). ov is nil when
-// the library does not verify owner signatures on pp.IdemixCurveID.
-func Shared(pp *crypto.PublicParams, device int) (v *Verifier, ov *OwnerVerifier, err error) {
+// MaxIdleContexts bounds the contexts per device that no validator holds: the
+// least recently released beyond it are closed. A context a Handle holds is
+// never closed by the cache.
+var MaxIdleContexts = 2
+
+// Handle is one validator's hold on a shared (device, PP) context pair. Its
+// methods are the validator callbacks; a method value (h.VerifyIssue) keeps
+// the Handle, and so the pair, alive for as long as the validator holds it.
+// Release, or the finalizer once the Handle is unreachable, drops the hold.
+type Handle struct {
+	e    *sharedEntry
+	once sync.Once
+}
+
+// Shared returns a Handle on the process-wide Verifier and OwnerVerifier of
+// (device, pp). Driver.NewValidator runs per request on some paths (the Orion
+// custodian: services/network/orion/approval.go:100 ->
+// token.NewServicesFromPublicParams -> core.NewValidator), so a device context
+// -- the PP's fixed-base tables in HBM, streams, planning threads -- is built
+// once per (device, PP) and reused by every validator of that PP. Parameters
+// of different TMSs get their own contexts side by side; idle contexts beyond
+// MaxIdleContexts per device are closed outside the cache lock.
+func Shared(pp *crypto.PublicParams, device int) (*Handle, error) {
 	raw, err := pp.Serialize()
 	if err != nil {
-		return nil, nil, err
+		return nil, err
 	}
-	key := sha256.Sum256(raw)
+	key := sharedKey{device: device, pp: sha256.Sum256(raw)}
 	shared.mu.Lock()
-	defer shared.mu.Unlock()
 	if shared.m == nil {
-		shared.m = map[int]*sharedEntry{}
+		shared.m = map[sharedKey]*sharedEntry{}
 	}
-	if e := shared.m[device]; e != nil {
-		if e.pp == key {
-			return e.v, e.ov, nil
-		}
-		if e.ov != nil {
-			e.ov.Close()
-		}
-		e.v.Close()
-		delete(shared.m, device)
+	if e := shared.m[key]; e != nil {
+		e.refs++
+		shared.mu.Unlock()
+		return newHandle(e), nil
 	}
-	v, err = newVerifierRaw(raw, device, nil)
+	shared.mu.Unlock()
+	// build outside the lock (table construction takes a while); a racing
+	// Shared for the same key keeps the first entry and closes its own pair
+	v, err := newVerifierRaw(raw, device, nil)
 	if err != nil {
-		return nil, nil, err
+		return nil, err
 	}
+	var ov *OwnerVerifier
 	if SupportsIdemixCurve(pp.IdemixCurveID) {
 		if ov, err = v.NewOwnerVerifier(pp); err != nil {
 			v.Close()
-			return nil, nil, err
+			return nil, err
 		}
 	}
-	shared.m[device] = &sharedEntry{pp: key, v: v, ov: ov}
-	return v, ov, nil
+	shared.mu.Lock()
+	e := shared.m[key]
+	if e == nil {
+		e = &sharedEntry{key: key, v: v, ov: ov}
+		shared.m[key] = e
+		v, ov = nil, nil
+	}
+	e.refs++
+	shared.mu.Unlock()
+	closePair(v, ov)
+	return newHandle(e), nil
+}
+
+func newHandle(e *sharedEntry) *Handle {
+	h := &Handle{e: e}
+	runtime.SetFinalizer(h, (*Handle).Release)
+	return h
+}
+
+func closePair(v *Verifier, ov *OwnerVerifier) {
+	if ov != nil {
+		ov.Close()
+	}
+	if v != nil {
+		v.Close()
+	}
+}
+
+// Release drops this Handle's hold (idempotent). The pair stays cached; it is
+// closed only when more than MaxIdleContexts idle pairs share its device.
+func (h *Handle) Release() {
+	h.once.Do(func() {
+		runtime.SetFinalizer(h, nil)
+		var evict []*sharedEntry
+		shared.mu.Lock()
+		h.e.refs--
+		shared.tick++
+		h.e.lastUsed = shared.tick
+		var idle []*sharedEntry
+		for _, e := range shared.m {
+			if e.key.device == h.e.key.device && e.refs == 0 {
+				idle = append(idle, e)
+			}
+		}
+		sort.Slice(idle, func(i, j int) bool { return idle[i].lastUsed > idle[j].lastUsed })
+		for len(idle) > MaxIdleContexts {
+			e := idle[len(idle)-1]
+			idle = idle[:len(idle)-1]
+			delete(shared.m, e.key)
+			evict = append(evict, e)
+		}
+		shared.mu.Unlock()
+		for _, e := range evict { // Close waits for calls in flight: never under shared.mu
+			closePair(e.v, e.ov)
+		}
+	})
+}
+
+// Verifier is the shared context pair's zero-knowledge verifier.
+func (h *Handle) Verifier() *Verifier { return h.e.v }
+
+// OwnerVerifier is the pair's idemix owner-signature verifier, nil when the
+// library does not verify owner signatures on pp.IdemixCurveID.
+func (h *Handle) OwnerVerifier() *OwnerVerifier { return h.e.ov }
+
+// TransferZKProofValidate is Verifier.TransferZKProofValidate (validator_transfer.go:84-98).
+func (h *Handle) TransferZKProofValidate(ctx *validator.Context) error {
+	return h.e.v.TransferZKProofValidate(ctx)
+}
+
+// VerifyIssue is Verifier.VerifyIssue (validator.go:181-191).
+func (h *Handle) VerifyIssue(action *issue2.IssueAction) error { return h.e.v.VerifyIssue(action) }
+
+// TransferSignatureValidate is OwnerVerifier.TransferSignatureValidate
+// (validator_transfer.go:42-82); only for a Handle whose OwnerVerifier is not nil.
+func (h *Handle) TransferSignatureValidate(ctx *validator.Context) error {
+	return h.e.ov.TransferSignatureValidate(ctx)
 }
 
 // SharedContexts is the number of device contexts Shared holds (tests).

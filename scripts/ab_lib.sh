@@ -14,9 +14,9 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
   for s in "${SETS[@]}"; do
     name=${s%%=*}
     path=${s#*=}
-    if [ "$path" = "default" ]; then lib=""; else lib="$PWD/$path"; fi
+    if [ "$path" = "default" ]; then lib=""; else lib="--lib $PWD/$path"; fi
     log=gpurun_out/ablib_${name}_$r.log
-    FTS_LIB=$lib timeout -k 10 300 python -u bench.py $ARGS > $log 2>&1 || { echo "[$name] bench failed"; tail -30 $log; exit 4; }
+    timeout -k 10 300 python -u bench.py $ARGS $lib > $log 2>&1 || { echo "[$name] bench failed"; tail -30 $log; exit 4; }
     echo "[$name round $r]"
     tail -1 $log | python3 -c "
 import json,sys

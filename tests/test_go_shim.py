@@ -109,4 +109,24 @@ def test_owner_signature_precedence_logic():
     body = o[o.index("func transferSignatures"):]
     assert body.index("st.owner(") < body.index("st.signed(")
     t = _go_sources()["gpu_test.go"]
-    assert "func TestTransferSignaturePrecedence" in t and "func TestSharedContextReuse" in t
+    assert "func TestTransferSignaturePrecedence" in t and "func TestSharedContextsPerPP" in t
+
+
+def test_shared_contexts_keyed_per_pp():
+    """the process-wide context cache is keyed by (device,
+    SHA-256 of the PP), so two TMSs on one device keep their own contexts; a
+    Handle holds its pair (refcount, finalizer), idle pairs beyond
+    MaxIdleContexts are closed outside the cache lock; the driver patch binds
+    the validator callbacks to the Handle"""
+    f = _go_sources()["ftz.go"]
+    assert "type sharedKey struct" in f and "pp     [32]byte" in f and "device int" in f
+    assert "m    map[sharedKey]*sharedEntry" in f
+    rel = f[f.index("func (h *Handle) Release()"):f.index("// Verifier is the shared")]
+    assert rel.index("shared.mu.Unlock()") < rel.index("closePair(e.v, e.ov)")
+    assert "e.refs == 0" in rel
+    sh = f[f.index("func Shared("):f.index("func newHandle")]
+    assert "newVerifierRaw" in sh and sh.index("shared.mu.Unlock()") < sh.index("newVerifierRaw")
+    import os
+    patch = open(os.path.join(os.path.dirname(__file__), "..", "go", "patches",
+                              "0001-zkatdlog-gpu-validator.patch")).read()
+    assert "h, err := gpu.Shared(pp, device)" in patch and "h.TransferZKProofValidate" in patch
