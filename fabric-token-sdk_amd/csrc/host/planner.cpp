@@ -368,6 +368,8 @@ class Builder {
     (feeds_pairing ? pl.g1p : pl.g1).push_back(j);
     return j.out;
   }
+  // a verification transcript's HashToZr slot (debug_challenges plans only)
+  uint32_t dbg_scal() { return pp.debug_challenges ? pl.n_scal++ : NONE; }
   static VTerm vterm(uint32_t pt, uint64_t w = 1) {
     VTerm v;
     v.pt = pt;
@@ -743,7 +745,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
       seg(d.slot + 128, 384 + SIG_JSON_LEN);
       h.seg_count = 5;
       h.expect = sc_ch;
-      h.out_scal = NONE;
+      h.out_scal = dbg_scal();
       pl.hmain.push_back(h);
       check(CK_HASH, E_MEMBERSHIP, (uint32_t)pl.hmain.size() - 1);
     }
@@ -801,7 +803,7 @@ void Builder::range_part(const std::vector<uint8_t>& rc, bool rc_nil, uint32_t o
   seg(coms_bytes, 64 * ncoms);
   h.seg_count = 6;
   h.expect = sc_rc;
-  h.out_scal = NONE;
+  h.out_scal = dbg_scal();
   pl.hmain.push_back(h);
   check(CK_HASH, E_RANGE, (uint32_t)pl.hmain.size() - 1);
 }
@@ -887,7 +889,7 @@ void Builder::transfer(const TransferIn& t) {
           seg(in_bytes, 64 * (t.n_in + t.n_out));
           h.seg_count = 2;
           h.expect = s_chal;
-          h.out_scal = NONE;
+          h.out_scal = dbg_scal();
           pl.hmain.push_back(h);
           check(CK_HASH, E_WF, (uint32_t)pl.hmain.size() - 1);
         }
@@ -1059,7 +1061,7 @@ void Builder::issue(const IssueIn& t) {
   seg(tok_bytes, 64 * n);
   h.seg_count = 2;
   h.expect = s_chal;
-  h.out_scal = NONE;
+  h.out_scal = dbg_scal();
   pl.hmain.push_back(h);
   check(CK_HASH, E_WF, (uint32_t)pl.hmain.size() - 1);
   range_part(rcb, rc_nil, tok_pt, tok_bytes, n);
@@ -1682,6 +1684,25 @@ bool pp_sig_tables(const PPInfo& pp) {
   for (uint32_t d = 0; d < pp.base; d++)
     if (zero(pp.sig_r[d]) || zero(pp.sig_s[d])) return false;
   return true;
+}
+
+size_t proof_challenge_slots(const TxChecks& t, const Check* ck, const HashJob* hmain, int32_t* kinds,
+                             uint32_t* slots, size_t cap) {
+  size_t m = 0;
+  auto part = [&](uint32_t start, uint32_t count) {
+    for (uint32_t k = 0; k < count; k++) {
+      const Check& c = ck[start + k];
+      if (c.kind != CK_HASH) continue;
+      if (m < cap) {
+        kinds[m] = c.code;
+        slots[m] = hmain[c.a].out_scal;
+      }
+      m++;
+    }
+  };
+  part(t.wf_start, t.wf_count);
+  part(t.rg_start, t.rg_count);
+  return m;
 }
 
 // Go math.Pow (src/math/pow.go, go1.18; amd64 runs this pure-Go path) for an

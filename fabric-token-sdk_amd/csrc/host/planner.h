@@ -43,6 +43,10 @@ struct PPInfo {
   // the prover's membership commitments as three fixed-G2 pairings (Q, PK1,
   // PK2; parse_pp: every line of the three normalisable and pp_sig_tables)
   bool fixed_pairs = false;
+  // parity debugging (ftz_ctx_set_debug FTZ_DEBUG_CHALLENGES): every
+  // verification transcript hash also writes its HashToZr into a scalar slot of
+  // its own, which ftz_batch_challenges reads back (set before planning)
+  bool debug_challenges = false;
   // the runtime's copy for planning WITHOUT the prover's table set (not built:
   // ftz_options.prover_tables = 0, or its allocation failed): pp_sig_tables false
   bool no_sigtab = false;
@@ -69,6 +73,13 @@ int64_t digit_weight(uint32_t base, int64_t i);
 // reference's bound int64(math.Pow(base, exponent)) overflows (PP-B) the
 // build's [EXT] extension proves v < base^exponent by exact digits.
 int prover_digits(const PPInfo& pp, const uint8_t* be32, uint32_t* digits);
+// The recomputed challenges of one proof of a debug_challenges plan: its
+// CK_HASH checks in check order (well-formedness, then the range part: every
+// membership proof in (output, digit) order, then the range proof) as (class
+// code E_WF / E_MEMBERSHIP / E_RANGE, scalar slot holding the HashToZr).
+// Returns the number of such checks (entries beyond cap are not written).
+size_t proof_challenge_slots(const TxChecks& t, const Check* ck, const HashJob* hmain, int32_t* kinds,
+                             uint32_t* slots, size_t cap);
 // Returns empty string on success, else an error message.
 std::string parse_pp(const uint8_t* p, size_t n, const char* label, PPInfo& out);
 // PublicParams.Validate (setup.go:238-273) on serialized PP: "" or the error text

@@ -334,6 +334,13 @@ extern "C" int ftz_ctx_debug_poison(ftz_ctx* c, const uint8_t* proof) {
   return FTZ_SUCCESS;
 }
 
+extern "C" int ftz_ctx_set_debug(ftz_ctx* c, int flags) {
+  if (!c) return set_err(FTZ_E_INVALID, "null context");
+  if (flags & ~FTZ_DEBUG_CHALLENGES) return set_err(FTZ_E_INVALID, "unknown debug flag");
+  c->pp.debug_challenges = (flags & FTZ_DEBUG_CHALLENGES) != 0;
+  return FTZ_SUCCESS;
+}
+
 extern "C" int ftz_ctx_set_layout(ftz_ctx* c, int stage, int layout) {
   if (!c) return set_err(FTZ_E_INVALID, "null context");
   if (layout != FTZ_LAYOUT_ONE_LANE && layout != FTZ_LAYOUT_SEXTET) return set_err(FTZ_E_INVALID, "unknown layout");
@@ -896,6 +903,31 @@ extern "C" int ftz_batch_stats(const ftz_batch* b, ftz_stats* out) {
 }
 
 extern "C" size_t ftz_batch_size(const ftz_batch* b) { return b ? b->n : 0; }
+
+extern "C" int ftz_batch_challenges(ftz_batch* b, size_t i, int32_t* kinds, uint8_t* values, size_t cap,
+                                    size_t* count) {
+  if (!b || !count || (cap && (!kinds || !values))) return set_err(FTZ_E_INVALID, "null argument");
+  if (i >= b->n) return set_err(FTZ_E_INVALID, "proof index out of range");
+  int rc = slot_wait(b);
+  if (rc != FTZ_SUCCESS) return rc;
+  const FlatPlan& f = b->fp;
+  const TxChecks* tx = f.ptr<TxChecks>(b->h_blob.p, PS_TX);
+  const Check* ck = f.ptr<Check>(b->h_blob.p, PS_CK);
+  const HashJob* hm = f.ptr<HashJob>(b->h_blob.p, PS_HMAIN);
+  std::vector<int32_t> kd(cap);
+  std::vector<uint32_t> slot(cap);
+  size_t m = proof_challenge_slots(tx[i], ck, hm, kd.data(), slot.data(), cap);
+  *count = m;
+  HC(hipSetDevice(b->ctx->device));
+  for (size_t k = 0; k < std::min(m, cap); k++) {
+    if (slot[k] == NONE) return set_err(FTZ_E_INVALID, "batch not loaded with FTZ_DEBUG_CHALLENGES");
+    uint32_t h[8];
+    HC(hipMemcpy(h, b->d_scr.p + b->sl.scal + 32 * (size_t)slot[k], 32, hipMemcpyDeviceToHost));
+    kinds[k] = kd[k];
+    limbs_to_be32(values + 32 * k, h);
+  }
+  return FTZ_SUCCESS;
+}
 
 extern "C" void ftz_batch_destroy(ftz_batch* b) {
   if (!b) return;

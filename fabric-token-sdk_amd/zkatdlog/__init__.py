@@ -166,6 +166,11 @@ class Context:
     LAYOUTS = {"one_lane": 1, "sextet": 6}
     STAGES = {"g2lines": 0, "prover_g2lines": 1}
 
+    def set_debug(self, challenges=False):
+        """ftz_ctx_set_debug: keep every recomputed challenge of batches loaded
+        afterwards (Batch.challenges); set before planning on the context"""
+        _check(self._lib.ftz_ctx_set_debug(self._h, _abi.FTZ_DEBUG_CHALLENGES if challenges else 0), self._lib)
+
     def set_layout(self, stage, layout):
         """profiling: kernel layout of a pipeline stage (ftz_ctx_set_layout); stage 'g2lines'
         (verifier, default 'one_lane') or 'prover_g2lines' (default 'one_lane'), layout 'one_lane'
@@ -491,6 +496,17 @@ class Batch:
     def wait(self):
         """Block until the last submission finished (ftz_batch_wait)."""
         _check(self._lib.ftz_batch_wait(self._h), self._lib)
+
+    def challenges(self, i, cap=256):
+        """[(class code, 32-byte HashToZr)] recomputed for proof i (a batch
+        loaded after Context.set_debug(challenges=True); ftz_batch_challenges)"""
+        kinds = (ctypes.c_int32 * cap)()
+        vals = ctypes.create_string_buffer(32 * cap)
+        cnt = ctypes.c_size_t()
+        _check(self._lib.ftz_batch_challenges(self._h, i, kinds, vals, cap, ctypes.byref(cnt)), self._lib)
+        if cnt.value > cap:
+            return self.challenges(i, cnt.value)
+        return [(kinds[k], vals.raw[32 * k:32 * k + 32]) for k in range(cnt.value)]
 
     def codes(self):
         c = (ctypes.c_int32 * max(1, self.n))()

@@ -10,6 +10,7 @@ FTZ_ERR_RANGE = 4
 FTZ_ERR_MEMBERSHIP = 5
 FTZ_ERR_PANIC = 6
 FTZ_ERR_OPENING = 7
+FTZ_DEBUG_CHALLENGES = 1  # ftz_ctx_set_debug
 
 FTZ_SUCCESS = 0
 FTZ_E_INVALID = -1
@@ -276,11 +277,11 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 
 # every symbol include/ftsamd.h declares (checked by tests/test_abi.py)
 SYMBOLS = ["ftz_options_default", "ftz_ctx_create", "ftz_ctx_create_ex", "ftz_ctx_destroy", "ftz_last_error",
-           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_debug_poison", "ftz_ctx_set_layout", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
+           "ftz_ctx_set_threads", "ftz_ctx_set_serial", "ftz_ctx_debug_poison", "ftz_ctx_set_debug", "ftz_ctx_set_layout", "ftz_ctx_info", "ftz_ctx_options", "ftz_ctx_engine_stats", "ftz_pp_validate", "ftz_pp_setup",
            "ftz_commit_tokens", "ftz_audit_openings",
            "ftz_verify_transfers", "ftz_verify_issues", "ftz_batch_load_transfers", "ftz_batch_load_issues",
            "ftz_batch_run", "ftz_batch_submit", "ftz_batch_wait", "ftz_batch_codes", "ftz_batch_bitmap", "ftz_batch_stats", "ftz_batch_size",
-           "ftz_batch_destroy", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_run_scalars", "ftz_host_alloc", "ftz_host_free", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
+           "ftz_batch_destroy", "ftz_batch_challenges", "ftz_msm_g1", "ftz_msm_load", "ftz_msm_load_gen", "ftz_msm_run", "ftz_msm_set_scalars", "ftz_msm_run_scalars", "ftz_host_alloc", "ftz_host_free", "ftz_msm_info", "ftz_msm_destroy", "ftz_g1_sum",
            "ftz_token_request_decode", "ftz_verify_token_requests", "ftz_verify_token_requests_batched", "ftz_ctx_request_stats",
            "ftz_idemix_create", "ftz_verify_owner_signatures", "ftz_idemix_set_strict_nym", "ftz_idemix_destroy", "ftz_audit_owners",
            "ftz_prove_transfers", "ftz_prove_issues", "ftz_ctx_prover_stats", "ftz_prover_load_transfers", "ftz_prover_load_issues",
@@ -322,6 +323,7 @@ def load():
     lib.ftz_ctx_create_ex.argtypes = [ctypes.c_char_p, sz, ctypes.c_int, ctypes.POINTER(Options), ctypes.POINTER(vp)]
     lib.ftz_ctx_set_serial.argtypes = [vp, ctypes.c_int]
     lib.ftz_ctx_debug_poison.argtypes = [vp, ctypes.c_void_p]
+    lib.ftz_ctx_set_debug.argtypes = [vp, ctypes.c_int]
     lib.ftz_ctx_set_layout.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     lib.ftz_ctx_options.argtypes = [vp, ctypes.POINTER(Options)]
     lib.ftz_pp_validate.argtypes = [ctypes.c_char_p, sz]
@@ -351,6 +353,7 @@ def load():
     lib.ftz_batch_size.restype = sz
     lib.ftz_batch_destroy.argtypes = [vp]
     lib.ftz_batch_destroy.restype = None
+    lib.ftz_batch_challenges.argtypes = [vp, sz, ctypes.POINTER(i32), ctypes.c_char_p, sz, ctypes.POINTER(sz)]
     u8p = ctypes.POINTER(ctypes.c_uint8)
     lib.ftz_msm_g1.argtypes = [vp, sz, ctypes.c_char_p, ctypes.c_char_p, u8p]
     lib.ftz_msm_load.argtypes = [vp, sz, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(vp)]

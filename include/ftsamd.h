@@ -163,6 +163,14 @@ int ftz_ctx_set_serial(ftz_ctx* ctx, int serial);
  * then deliver that error to the one request holding the item and the right
  * codes to every other caller whose items shared the pass. */
 int ftz_ctx_debug_poison(ftz_ctx* ctx, const uint8_t* proof);
+/* parity debugging: with FTZ_DEBUG_CHALLENGES set, batches loaded afterwards
+ * (ftz_batch_load_*) keep every recomputed Fiat-Shamir challenge -- the
+ * HashToZr of each well-formedness, membership and range transcript
+ * (transfer/wellformedness.go, sigproof/membership.go:260-277,
+ * range/proof.go:371-389) -- whether or not it matches the proof's claim.  Set
+ * it before any call plans on the context; 0 clears it. */
+#define FTZ_DEBUG_CHALLENGES 1
+int ftz_ctx_set_debug(ftz_ctx* ctx, int flags);
 /* profiling: kernel layout of a pipeline stage (results are identical; only
  * speed differs).  stage FTZ_STAGE_G2LINES (the verifier's t' = c PK0 + v PK1
  * + h PK2 and its 88 pair-2 Miller lines; default one lane) or
@@ -253,6 +261,14 @@ int ftz_batch_bitmap(ftz_batch* b, uint8_t* bits);
 int ftz_batch_stats(const ftz_batch* b, ftz_stats* out);
 size_t ftz_batch_size(const ftz_batch* b);
 void ftz_batch_destroy(ftz_batch* b);
+/* the recomputed challenges of proof i of a batch loaded with
+ * FTZ_DEBUG_CHALLENGES, after ftz_batch_run: one per transcript the planner
+ * scheduled, in check order -- well-formedness (FTZ_ERR_WF), then every
+ * membership proof in (output, digit) order (FTZ_ERR_MEMBERSHIP), then the
+ * range proof (FTZ_ERR_RANGE) -- as kinds[k] and 32-byte big-endian values at
+ * values + 32 k.  *count = the number available (entries beyond cap are not
+ * written).  A proof rejected before its transcripts are planned has none. */
+int ftz_batch_challenges(ftz_batch* b, size_t i, int32_t* kinds, uint8_t* values, size_t cap, size_t* count);
 
 /* ---- token commitments and auditor opening checks.
  * A token opening is token.TokenDataWitness{Type, Value, BlindingFactor}

@@ -38,6 +38,18 @@ ERR_MEMBERSHIP = 5    # "invalid membership proof"
 ERR_PANIC = 6         # the reference would panic (nil dereference, foreign curve)
 
 
+# Parity tests only: a list here collects every challenge a verifier
+# recomputes, as (class, HashToZr) in the order the checks run (see
+# include/ftsamd.h ftz_batch_challenges for the device's side).
+CHALLENGE_TRACE = None
+
+
+def _traced(kind, h):
+    if CHALLENGE_TRACE is not None:
+        CHALLENGE_TRACE.append((kind, h))
+    return h
+
+
 class VerifyError(Exception):
     def __init__(self, code, msg):
         super().__init__(msg)
@@ -417,7 +429,7 @@ def membership_verify(pp, com_to_value, proof):
     if proof["Commitment"] is None:
         raise VerifyError(ERR_MALFORMED, "failed to marshal array of G1")
     data = membership_transcript(pp, pt(proof["Commitment"]), g1c, gt, Rw, Sw)
-    if C.hash_to_zr(data) != c:
+    if _traced(ERR_MEMBERSHIP, C.hash_to_zr(data)) != c:
         raise VerifyError(ERR_MEMBERSHIP, "invalid membership proof")
 
 
@@ -696,7 +708,7 @@ def range_verify(pp, tokens, raw):
         cvals.append(schnorr_recompute(pp.ped[:2], [eq["Value"][j], eq["CommitmentBlindingFactor"][j]],
                                        com, chal))
     coms = [[pt(c) for c in mps[j]["Commitments"]] for j in range(n)]
-    if C.hash_to_zr(range_transcript(pp, tokens, ctoks, cvals, coms)) != chal:
+    if _traced(ERR_RANGE, C.hash_to_zr(range_transcript(pp, tokens, ctoks, cvals, coms))) != chal:
         raise VerifyError(ERR_RANGE, "invalid range proof")
 
 
@@ -776,7 +788,7 @@ def wf_verify(pp, ins, outs, raw):
     cin = [schnorr_recompute(pp.ped, p, s, wf["Challenge"]) for p, s in zin]
     zout = parse_proof(outs, wf["OutputValues"], wf["OutputBlindingFactors"])
     cout = [schnorr_recompute(pp.ped, p, s, wf["Challenge"]) for p, s in zout]
-    if C.hash_to_zr(g1_array_bytes(cin + cout + ins + outs)) != wf["Challenge"]:
+    if _traced(ERR_WF, C.hash_to_zr(g1_array_bytes(cin + cout + ins + outs))) != wf["Challenge"]:
         raise VerifyError(ERR_WF, "invalid zero-knowledge transfer")
 
 
@@ -887,7 +899,7 @@ def issue_wf_verify(pp, tokens, anonymous, raw):
         raise VerifyError(ERR_MALFORMED, "well-formedness proof is not well formed: length mismatch")
     coms = [schnorr_recompute(pp.ped, [wf["Type"], vals[i], bfs[i]], tokens[i], c)
             for i in range(len(tokens))]
-    if C.hash_to_zr(g1_array_bytes(coms + tokens)) != c:
+    if _traced(ERR_WF, C.hash_to_zr(g1_array_bytes(coms + tokens))) != c:
         raise VerifyError(ERR_WF, "invalid well-formedness proof")
 
 

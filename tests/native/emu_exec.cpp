@@ -167,7 +167,7 @@ static void emu_ensure_sig_tables(EmuCtx* c) {
 void emu_ctx_set_fexp(void* c, int variant) { ((EmuCtx*)c)->fexp = variant; }
 void emu_set_threads(int t) { g_threads = t > 0 ? (unsigned)t : 0; }
 
-static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
+static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes, std::vector<uint32_t>* scal_out = nullptr) {
   memcpy(p.arena.data(), c->const_bytes.data(), C_SIZE);
   std::vector<uint8_t> wire = p.wire;
   wire.resize(wire.size() + 64, 0);
@@ -205,6 +205,7 @@ static void run_plan(EmuCtx* c, Plan& p, size_t n, int32_t* codes) {
   par_for((uint32_t)p.pr.size(), [&](uint32_t i) { job_fexp(p.pr[i], fbuf.data(), i, p.arena.data(), c->fexp); });
   par_for((uint32_t)p.hmain.size(), [&](uint32_t i) { hok[i] = job_hash(p.hmain[i], p.seg.data(), p.arena.data(), scal, canon.data()); });
   for (size_t i = 0; i < n; i++) codes[i] = job_verdict(p.tx[i], p.ck.data(), pt_ok.data(), hok.data());
+  if (scal_out) scal_out->swap(scalv);
 }
 
 #ifdef FTS_COUNT_OPS
@@ -465,6 +466,37 @@ int emu_verify_transfers(void* ctx, size_t n, const ftz_transfer* tx, int32_t* c
   Plan p;
   plan_transfers(c->pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
   run_plan(c, p, n, codes);
+  return 0;
+}
+
+// The recomputed challenges of every proof (ftz_batch_challenges on the host):
+// transfers (kind 0) or issues (kind 1) planned with debug_challenges; proof i's
+// at kinds / values + 32 * (i * cap), counts[i] of them.
+int emu_challenges(void* ctx, int kind, size_t n, const void* items, int32_t* codes, int32_t* kinds,
+                   uint8_t* values, size_t cap, size_t* counts) {
+  EmuCtx* c = (EmuCtx*)ctx;
+  PPInfo pp = c->pp;
+  pp.debug_challenges = true;
+  Plan p;
+  if (kind == 0) {
+    const ftz_transfer* tx = static_cast<const ftz_transfer*>(items);
+    std::vector<TransferIn> t(n);
+    for (size_t i = 0; i < n; i++)
+      t[i] = {tx[i].inputs, tx[i].n_in, tx[i].outputs, tx[i].n_out, tx[i].proof, tx[i].proof_len};
+    plan_transfers(pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
+  } else {
+    const ftz_issue* is = static_cast<const ftz_issue*>(items);
+    std::vector<IssueIn> t(n);
+    for (size_t i = 0; i < n; i++) t[i] = {is[i].outputs, is[i].n_out, is[i].proof, is[i].proof_len, is[i].anonymous};
+    plan_issues(pp, n, t.data(), p, g_threads ? (int)g_threads : 4);
+  }
+  std::vector<uint32_t> scal;
+  run_plan(c, p, n, codes, &scal);
+  std::vector<uint32_t> slot(cap);
+  for (size_t i = 0; i < n; i++) {
+    counts[i] = proof_challenge_slots(p.tx[i], p.ck.data(), p.hmain.data(), kinds + i * cap, slot.data(), cap);
+    for (size_t k = 0; k < std::min(counts[i], cap); k++) limbs_to_be32(values + 32 * (i * cap + k), &scal[8 * (size_t)slot[k]]);
+  }
   return 0;
 }
 
