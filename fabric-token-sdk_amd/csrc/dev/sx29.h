@@ -869,13 +869,24 @@ FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const
   return f;
 }
 
-// LDS dwords per sextet region: NS slots of 18 dwords, padded so that the
-// regions of a wave's ten sextets start on distinct even banks (stride = 2 x odd
-// mod 64): the b64 reads of the ten sextets, each broadcast to its six lanes,
-// then never share a bank.
+// LDS dwords per sextet region: NS slots of 18 dwords, padded.  The operand
+// exchange is compiled to ds_read2_b64 / ds_read2_b32 / ds_write2_b64 /
+// ds_write2_b32, all of which bank on (a/4) mod 32 (MI355X_MICROARCH.md, LDS
+// table).  FTS_SQ_PAD (default 20): the region stride is = 20 mod 32 dwords,
+// which a model of the exchange's access patterns (broadcast gets, per-lane
+// slot gets, per-lane puts; 16-lane groups for b64, 32-lane for b32; lane =
+// 6 sextet + k) puts at 2.6x fewer conflict cycles than the previous rule;
+// FTS_SQ_PAD = 0: the previous rule, distinct even banks mod 64 (stride = 2 x
+// odd mod 64), which only the b64 reads' banking (mod 64) would favour.
+#ifndef FTS_SQ_PAD
+#define FTS_SQ_PAD 20
+#endif
 constexpr uint32_t sq_region_dwords(uint32_t ns) {
   uint32_t s = ns * 18;
-  while ((s % 64) % 4 != 2) s += 2;
+  if (FTS_SQ_PAD)
+    while (s % 32 != FTS_SQ_PAD) s += 2;
+  else
+    while ((s % 64) % 4 != 2) s += 2;
   return s;
 }
 

@@ -194,12 +194,13 @@ void Engine::dispatcher() {
     // A pass closes at B items, BATCH_PROOF_BYTES of proofs, or B * 4 pairing
     // jobs -- a PP-A pass of B 2-output transfers (e = 2): wider range proofs
     // (PP-B: e = 16, 8x the pairings per transfer) get proportionally fewer
-    // proofs per pass, so their passes cost what a PP-A pass costs.  (Smaller
-    // first / tail passes to shorten a job's fill and drain were measured:
-    // 420-442k vs 676-688k transfers/s on a 20-step job -- a pass's planning and
-    // kernel chain have a fixed latency that smaller passes do not shed.)
-    // the first pass of a job (nothing in flight) may be smaller: it reaches the
-    // device after a shorter planning step (ftz_options.first_pass)
+    // proofs per pass, so their passes cost what a PP-A pass costs.
+    // The first pass of a job (nothing in flight) may be smaller: it reaches the
+    // device after a shorter planning step (ftz_options.first_pass, default
+    // 4096 of the 8192-proof batch: +2.5 % on a 20-step job, profiles/r05/
+    // first_pass_ab.txt).  Passes much smaller than that throughout the job were
+    // slower (round 2: 420-442k vs 676-688k transfers/s): a pass's planning and
+    // kernel chain have a fixed latency that small passes do not shed.
     const size_t fp1 = ctx->opt.first_pass, ts = ctx->opt.tail_split;
     size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
     // the queue's last pass in two halves whose kernel chains overlap

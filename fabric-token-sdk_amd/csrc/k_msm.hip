@@ -202,8 +202,12 @@ __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, 
   uint32_t i = ch * 256 + t;
   s[t] = i < m ? j29_ld(in[(size_t)w * m + i]) : j29_inf();
   __syncthreads();
-  for (uint32_t o = 128; o > 0; o >>= 1) {
-    if (t < o) s[t] = j29_add(s[t], s[t + o]);
+  // only the levels the chunk's live parts need (a window's last tree level
+  // often holds a few dozen: 5 additions deep instead of 8)
+  uint32_t live = min(256u, m - ch * 256), o = 1;
+  while (2 * o < live) o *= 2;
+  for (; live > 1; live = o, o >>= 1) {
+    if (t < o && t + o < live) s[t] = j29_add(s[t], s[t + o]);
     __syncthreads();
   }
   if (t == 0) g1j_store(out[(size_t)w * chunks + ch], j29_to(s[0]));

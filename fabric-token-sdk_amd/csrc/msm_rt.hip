@@ -31,6 +31,13 @@ struct ftz_msm {
   hipEvent_t cev[RAW_CHUNKS + 1];
   bool cev_init = false;
   float last_ms = 0;
+  // ftz_msm_run's launch chain (keys .. Horner, ~25 kernels and memsets) as one
+  // graph, captured on the first run: the short launches of a 2^16 MSM ran
+  // behind the host's enqueue rate (15-18 us gaps); graph_state 0 = not tried,
+  // 1 = captured, -1 = capture failed (direct launches)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  int graph_state = 0;
   uint32_t radix_bits = 8;  // digit bits per radix-sort pass (8: rocPRIM's gfx950 default; 9: Radix9)
 };
 
@@ -234,9 +241,8 @@ extern "C" int ftz_msm_set_scalars(ftz_msm* m, const uint8_t* scalars) {
   return upload_scalars(m, scalars);
 }
 
-// the pipeline after the sort keys (stream s, event ev[0] already recorded)
-static int msm_after_keys(ftz_msm* m, uint8_t out[64]) {
-  hipStream_t s = m->ctx->stream;
+// the pipeline after the sort keys, enqueued on s
+static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
   const MsmPlan& p = m->p;
   size_t wb = (size_t)p.rw * p.buckets;
   size_t wn = (size_t)p.windows * p.nv;
@@ -277,6 +283,12 @@ static int msm_after_keys(ftz_msm* m, uint8_t out[64]) {
     cnt = chunks;
   }
   k_msm_horner<<<1, 64, 0, s>>>(p, p.rw, 0, in, cnt, m->hacc.p);
+  return FTZ_SUCCESS;
+}
+
+// the result after the enqueued pipeline (event ev[0] recorded at its start)
+static int msm_finish(ftz_msm* m, uint8_t out[64]) {
+  hipStream_t s = m->ctx->stream;
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
   G1JDev acc;
@@ -292,17 +304,54 @@ static int msm_after_keys(ftz_msm* m, uint8_t out[64]) {
   return FTZ_SUCCESS;
 }
 
+static int msm_enqueue_all(ftz_msm* m, hipStream_t s) {
+  const MsmPlan& p = m->p;
+  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
+  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
+  return msm_enqueue_tail(m, s);
+}
+
+// capture keys .. Horner once (relaxed mode: the context's other threads may
+// allocate meanwhile); on failure the handle keeps launching directly
+static void msm_capture(ftz_msm* m, hipStream_t s) {
+  m->graph_state = -1;
+  if (hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  int rc = msm_enqueue_all(m, s);
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(s, &g);
+  if (rc != FTZ_SUCCESS || e != hipSuccess || !g) {
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return;
+  }
+  if (hipGraphInstantiate(&m->graph_exec, g, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    m->graph_exec = nullptr;
+    return;
+  }
+  m->graph = g;
+  m->graph_state = 1;
+}
+
 extern "C" int ftz_msm_run(ftz_msm* m, uint8_t out[64]) {
   if (!m || !out) return set_err(FTZ_E_INVALID, "null argument");
   ftz_ctx* c = m->ctx;
   std::lock_guard<std::mutex> lk(c->mu);
   HC(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  const MsmPlan& p = m->p;
+  if (m->graph_state == 0 && c->opt.msm_graph) msm_capture(m, s);
   HC(hipEventRecord(m->ev[0], s));
-  const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
-  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
-  return msm_after_keys(m, out);
+  if (m->graph_state == 1) {
+    HC(hipGraphLaunch(m->graph_exec, s));
+  } else {
+    int rc = msm_enqueue_all(m, s);
+    if (rc != FTZ_SUCCESS) return rc;
+  }
+  return msm_finish(m, out);
 }
 
 // ftz_msm_run with the scalars copied from host memory in RAW_CHUNKS pieces on a
@@ -337,7 +386,9 @@ extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t o
     HC(hipStreamWaitEvent(s, m->cev[k], 0));
     k_msm_keys_raw<<<blocks(i1 - i0, 256), 256, 0, s>>>(p, i0, i1, m->raw.p, scal, m->key.p, m->val.p);
   }
-  return msm_after_keys(m, out);
+  int rc = msm_enqueue_tail(m, s);
+  if (rc != FTZ_SUCCESS) return rc;
+  return msm_finish(m, out);
 }
 
 extern "C" int ftz_host_alloc(size_t bytes, void** out) {
@@ -375,6 +426,8 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
     (void)hipStreamSynchronize(m->cstream);
     (void)hipStreamDestroy(m->cstream);
   }
+  if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  if (m->graph) (void)hipGraphDestroy(m->graph);
   delete m;
 }
 

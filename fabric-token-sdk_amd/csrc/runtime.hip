@@ -56,6 +56,7 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->first_pass = 4096;
   o->msm_glv = 1;
   o->prover_tables = 1;
+  o->msm_graph = 1;
 }
 
 extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {
@@ -76,8 +77,8 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     if (o.fexp != FTZ_FEXP_EXACT && o.fexp != FTZ_FEXP_FUENTES) return set_err(FTZ_E_INVALID, "unknown fexp variant");
     if (o.batch > (1u << 20) || o.slots > 64) return set_err(FTZ_E_INVALID, "batch / slots out of range");
     if (o.msm_window_bits > 24) return set_err(FTZ_E_INVALID, "msm_window_bits out of range (0..24)");
-    if (o.msm_glv > 1 || o.msm_precompute > 1 || o.prover_tables > 1)
-      return set_err(FTZ_E_INVALID, "msm_glv / msm_precompute / prover_tables must be 0 or 1");
+    if (o.msm_glv > 1 || o.msm_precompute > 1 || o.prover_tables > 1 || o.msm_graph > 1)
+      return set_err(FTZ_E_INVALID, "msm_glv / msm_precompute / prover_tables / msm_graph must be 0 or 1");
     if (o.msm_radix_bits && o.msm_radix_bits != 8 && o.msm_radix_bits != 9)
       return set_err(FTZ_E_INVALID, "msm_radix_bits must be 0, 8 or 9");
   }

@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
+#include "../dev/binv.h"
 #include "../dev/fp.h"
 
 using namespace fts;
@@ -102,4 +105,49 @@ extern "C" double ftz_fpbench(int device, int impl, int iters, int waves_per_sim
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return 2.0 * threads * blocks * (double)iters / (ms * 1e-3);
+}
+
+// The batched inversion of dev/binv.h (k_fexp_binv, k_g2_binv) over 256-lane
+// workgroups: n values, zero where zmask says so, lanes past n inactive (a
+// partial last block), each output against the lane's own fp_inv_var.  Returns
+// the number of mismatches (every active output and every untouched inactive
+// slot checked), -1 on a HIP error.
+__global__ void __launch_bounds__(256) k_binvcheck(uint32_t n, const uint8_t* zmask, uint32_t seed, fp* out,
+                                                   uint32_t* bad) {
+  __shared__ uint32_t tree[512][8];
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  uint32_t s = seed ^ (j + 1) * 2654435761u;
+  if (!s) s = 1;
+  fp v = rnd_fe<ModP>(s);
+  if (j < n && zmask[j]) v = fe_zero<ModP>();
+  binv_tree256(tree, threadIdx.x, j < n, [&] { return v; }, [&](const fp& r) { out[j] = r; });
+  if (j >= n) return;
+  const fp want = fe_is_zero(v) ? fe_zero<ModP>() : fp_inv_var(v);
+  if (!fe_eq(out[j], want)) atomicAdd(bad, 1u);
+}
+
+extern "C" int ftz_binvcheck(int device, uint32_t n, const uint8_t* zmask, uint32_t seed) {
+  if (hipSetDevice(device) != hipSuccess || n == 0) return -1;
+  const uint32_t blocks = (n + 255) / 256;
+  uint32_t* bad = nullptr;
+  uint8_t* dz = nullptr;
+  fp* out = nullptr;
+  int rc = -1;
+  if (hipMalloc(&bad, 4) == hipSuccess && hipMalloc(&dz, n) == hipSuccess &&
+      hipMalloc(&out, sizeof(fp) * (size_t)blocks * 256) == hipSuccess &&
+      hipMemset(bad, 0, 4) == hipSuccess && hipMemcpy(dz, zmask, n, hipMemcpyHostToDevice) == hipSuccess &&
+      hipMemset(out, 0xA5, sizeof(fp) * (size_t)blocks * 256) == hipSuccess) {
+    k_binvcheck<<<blocks, 256>>>(n, dz, seed, out, bad);
+    uint32_t h = 0;
+    std::vector<uint32_t> tail((size_t)(blocks * 256 - n) * 8);
+    if (hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost) == hipSuccess &&
+        (tail.empty() || hipMemcpy(tail.data(), out + n, tail.size() * 4, hipMemcpyDeviceToHost) == hipSuccess)) {
+      for (uint32_t w : tail) h += w != 0xA5A5A5A5u;  // inactive lanes write nothing
+      rc = (int)h;
+    }
+  }
+  (void)hipFree(bad);
+  (void)hipFree(dz);
+  (void)hipFree(out);
+  return rc;
 }

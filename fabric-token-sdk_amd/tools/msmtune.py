@@ -2,7 +2,8 @@
 """MSM plan sweep: device latency of ftz_msm_run for window bits C, slot cap T,
 slots per segment S, resident-point mode P and sort digit bits R (ftz_options
 msm_window_bits / msm_slot_cap / msm_seg_slots / msm_precompute /
-msm_radix_bits; 0 = the planner's choice / off).
+msm_radix_bits; 0 = the planner's choice / off) and graph replay G
+(ftz_options.msm_graph, default 1).
     python msmtune.py 20 "0,0,0 16,16,0 16,32,0 15,0,0 17,0,0,1 0,0,0,0,8"
 """
 import json
@@ -16,14 +17,15 @@ import numpy as np  # noqa: E402
 import zkatdlog  # noqa: E402
 
 lg = int(sys.argv[1])
-combos = [tuple(int(v) for v in (c + ",0,0").split(",")[:5]) for c in sys.argv[2].split()]
+combos = [tuple(int(v) for v in (c + ",0,0,0,0,1"[len(c.split(",")) * 2 - 2:]).split(",")[:6])
+          for c in sys.argv[2].split()]
 pp = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]["pp"].encode()
 scal = np.random.default_rng(lg).bytes(32 << lg)
 ref = None
 import time  # noqa: E402
-for c, t, s, pre, rb in combos:
+for c, t, s, pre, rb, gr in combos:
     ctx = zkatdlog.Context(pp, device=0, msm_window_bits=c, msm_slot_cap=t, msm_seg_slots=s, msm_precompute=pre,
-                           msm_radix_bits=rb)
+                           msm_radix_bits=rb, msm_graph=gr)
     t0 = time.perf_counter()
     m = zkatdlog.Msm(ctx, scalars=scal, gen_offset=1)
     load_s = time.perf_counter() - t0
@@ -33,7 +35,8 @@ for c, t, s, pre, rb in combos:
         assert m.run() == out
         ms.append(m.info()["last_ms"])
     ref = ref or out
-    print("n=2^%d C=%2d T=%3d S=%3d P=%d R=%d  %8.3f ms  load %.2f s  %s" % (
-        lg, m.info()["window_bits"], t, s, pre, rb, min(ms), load_s, "ok" if out == ref else "MISMATCH"), flush=True)
+    print("n=2^%d C=%2d T=%3d S=%3d P=%d R=%d G=%d  %8.3f ms  load %.2f s  %s" % (
+        lg, m.info()["window_bits"], t, s, pre, rb, gr, min(ms), load_s, "ok" if out == ref else "MISMATCH"),
+        flush=True)
     m.close()
     ctx.close()

@@ -137,6 +137,9 @@ typedef struct {
                            halves of at least this many proofs, whose kernel chains then
                            overlap: 0 (default) = off (measured no gain on the 20-step
                            job, profiles/r05/tail_split_ab.txt)                         */
+  uint32_t msm_graph;   /* 1 (default): ftz_msm_run replays its launch chain (keys, sort,
+                           bucket, segment, tree and Horner kernels) as one HIP graph
+                           captured on the handle's first run; 0: direct launches        */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);

@@ -149,3 +149,24 @@ def test_fp_multiplier_self_check():
                                    "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsfpcheck.so"))
     lib.ftz_fpcheck.argtypes = [ctypes.c_int, ctypes.c_uint32]
     assert lib.ftz_fpcheck(0, 12345) == 0
+
+
+def test_binv_tree_device_check():
+    """dev/binv.h binv_tree256 (the 256-job batched inversion of k_fexp_binv /
+    k_g2_binv) on the device against each lane's own fp_inv_var: random values,
+    zeros alone and in runs (a t' at infinity; every lane of a block zero),
+    and a partial last block whose inactive lanes write nothing"""
+    import ctypes
+    import os
+    import random
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsfpcheck.so"))
+    lib.ftz_binvcheck.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]
+    rng = random.Random(5)
+    for n in (256, 1000, 4096 + 37, 255, 1):
+        z = bytearray(n)
+        for _ in range(max(1, n // 50)):
+            z[rng.randrange(n)] = 1
+        if n >= 512:
+            z[256:512] = b"\x01" * 256  # a block of zeros only
+        assert lib.ftz_binvcheck(0, n, bytes(z), 1000 + n) == 0, n

@@ -127,6 +127,28 @@ def test_engine_chunks_and_mixes(ctx, valid_set, bad_set, golden):
     assert all(g == [c["expect"] for c in issues] for g in got_i)
 
 
+@pytest.mark.parametrize("opts", [{"first_pass": 1000}, {"first_pass": 0}, {"first_pass": 2048, "tail_split": 1024},
+                                  {"first_pass": 0, "tail_split": 3000}])
+def test_engine_first_pass_and_tail_split(zk, golden, valid_set, bad_set, opts):
+    """ftz_options.first_pass (the job's first pass smaller than the batch, so
+    one request's items straddle two passes) and tail_split (the queue's last
+    pass cut in two halves): every code at its row equals the single-pass
+    result and the expected code, for one request of 8192 + 777 rows and for
+    one just above a first pass"""
+    from zkatdlog import workload as W
+    pp = golden["pp_a"]["pp"].encode()
+    job = W.mixed_job(valid_set, bad_set, 8192 + 777, seed=31)
+    small = W.mixed_job(valid_set, bad_set, 1001, seed=32)
+    with zk.Context(pp, device=0, **opts) as c:
+        for j in (job, small):
+            codes = c.verify_transfers_packed(j.ptr(), j.n)
+            assert np.array_equal(codes, j.expect), opts
+        st = c.engine_stats(reset=True)
+        assert st["batches"] >= 2, st
+    with zk.Context(pp, device=0, first_pass=0, tail_split=0) as c:  # one pass per batch: the reference codes
+        assert np.array_equal(c.verify_transfers_packed(job.ptr(), job.n), job.expect)
+
+
 def test_engine_1m_transfer_job_sharded(ctx, valid_set, bad_set):
     """BASELINE configs[3] at N = 1 through the multi-GPU job path: a job of
     2^20 transfers cut with shard_range (world 1, and each half of world 2 run
