@@ -872,14 +872,19 @@ FTS_HD q2 sq_miller_f(const X& x, const LineCoef29* qlines, const g1a& P1, const
 // LDS dwords per sextet region: NS slots of 18 dwords, padded.  The operand
 // exchange is compiled to ds_read2_b64 / ds_read2_b32 / ds_write2_b64 /
 // ds_write2_b32, all of which bank on (a/4) mod 32 (MI355X_MICROARCH.md, LDS
-// table).  FTS_SQ_PAD (default 20): the region stride is = 20 mod 32 dwords,
-// which a model of the exchange's access patterns (broadcast gets, per-lane
-// slot gets, per-lane puts; 16-lane groups for b64, 32-lane for b32; lane =
-// 6 sextet + k) puts at 2.6x fewer conflict cycles than the previous rule;
-// FTS_SQ_PAD = 0: the previous rule, distinct even banks mod 64 (stride = 2 x
-// odd mod 64), which only the b64 reads' banking (mod 64) would favour.
+// table).  FTS_SQ_PAD (default 12): the region stride is = 12 mod 32 dwords.
+// A model of the exchange's access patterns (broadcast gets, per-lane slot
+// gets, per-lane puts; 16-lane groups for b64, 32-lane for b32; lane = 6
+// sextet + k; the x-power's cyclotomic squarings and products, the Miller
+// step's squaring, normalised fixed line and pair-2 line) puts the x-power at
+// 2.6x and the Miller step at 1.4x fewer conflict cycles than the previous
+// rule, the best of every stride mod 32 and of slot strides 18..30 (measured,
+// 20 mod 32: k_fexp_expt 9.97 -> 3.34 conflict cycles per LDS instruction,
+// 746 -> 728 us; profiles/r06/lds_pad.txt).  FTS_SQ_PAD = 0: the previous
+// rule, distinct even banks mod 64 (stride = 2 x odd mod 64), which only the
+// b64 reads' banking (mod 64) would favour.
 #ifndef FTS_SQ_PAD
-#define FTS_SQ_PAD 20
+#define FTS_SQ_PAD 12
 #endif
 constexpr uint32_t sq_region_dwords(uint32_t ns) {
   uint32_t s = ns * 18;

@@ -56,7 +56,7 @@ extern "C" void ftz_options_default(ftz_options* o) {
   o->first_pass = 4096;
   o->msm_glv = 1;
   o->prover_tables = 1;
-  o->msm_graph = 1;
+  o->msm_graph = 0;
 }
 
 extern "C" int ftz_ctx_create(const uint8_t* pp, size_t pp_len, int device, ftz_ctx** out) {

@@ -137,9 +137,11 @@ typedef struct {
                            halves of at least this many proofs, whose kernel chains then
                            overlap: 0 (default) = off (measured no gain on the 20-step
                            job, profiles/r05/tail_split_ab.txt)                         */
-  uint32_t msm_graph;   /* 1 (default): ftz_msm_run replays its launch chain (keys, sort,
-                           bucket, segment, tree and Horner kernels) as one HIP graph
-                           captured on the handle's first run; 0: direct launches        */
+  uint32_t msm_graph;   /* 1: ftz_msm_run replays its launch chain (keys, sort, bucket,
+                           segment, tree and Horner kernels) as one HIP graph captured on
+                           the handle's first run; 0 (default): direct launches (the
+                           graph measured the same: 2^16 0.92-0.93 ms either way,
+                           profiles/r06/msm_graph.txt)                                   */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
