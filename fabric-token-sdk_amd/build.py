@@ -29,8 +29,12 @@ FPCHECK = os.path.join(HERE, "zkatdlog", "_lib", "libftsfpcheck.so")
 CALLERS = os.path.join(HERE, "zkatdlog", "_lib", "libftscallers.so")  # bench: closed-loop n=1 callers
 ARCH = os.environ.get("FTS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-# 16-bit signed windows for the G1 fixed-base tables (dev/jobs.h FTS_G1TAB_C)
-DEFS = ["-DFTS_G1TAB_C=16", "-DFTS_G2TAB_C=13"]
+# 16-bit signed windows for the G1 fixed-base tables (dev/jobs.h FTS_G1TAB_C);
+# FTS_HOST64: the host side's Montgomery products (gnark SetBytes checks of the
+# request path, PP decoding, the MSM result's affine conversion) in 4 x 64-bit
+# limbs with 128-bit products -- bit-identical to the device's 8 x 32-bit ones
+# (dev/fp.h); the device code is unaffected
+DEFS = ["-DFTS_G1TAB_C=16", "-DFTS_G2TAB_C=13", "-DFTS_HOST64"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wno-unknown-pragmas", "--offload-arch=" + ARCH] + DEFS
 
 SOURCES = (sorted(glob.glob(os.path.join(CSRC, "k_*.hip")))
@@ -67,6 +71,7 @@ def build_variant(name, defs, jobs=8, force=False):
     lib = os.path.join(os.path.dirname(LIB), "ab", "libftsamd_%s.so" % name)
     os.makedirs(obj_dir, exist_ok=True)
     os.makedirs(os.path.dirname(lib), exist_ok=True)
+    force = flags_changed(obj_dir, defs) or force
     hdr_time = newest(headers())
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         results = list(ex.map(lambda s: compile_one(s, force, hdr_time, obj_dir, defs), SOURCES))
@@ -83,9 +88,23 @@ def build_variant(name, defs, jobs=8, force=False):
     return lib
 
 
+def flags_changed(obj_dir, extra=()):
+    """True (and the stamp rewritten) when the compile flags differ from the
+    ones the objects in obj_dir were built with: a define change rebuilds."""
+    stamp = os.path.join(obj_dir, ".flags")
+    want = " ".join([HIPCC] + FLAGS + list(extra))
+    have = open(stamp).read() if os.path.exists(stamp) else ""
+    if have == want:
+        return False
+    with open(stamp, "w") as f:
+        f.write(want)
+    return True
+
+
 def build(jobs=8, force=False, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    force = flags_changed(OBJ) or force
     hdr_time = newest(headers())
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         results = list(ex.map(lambda s: compile_one(s, force, hdr_time), SOURCES))

@@ -19,9 +19,12 @@ def main():
     ap.add_argument("--n", type=int, default=100000)
     ap.add_argument("--threads", default="16")
     ap.add_argument("--slots", default="4")
+    ap.add_argument("--lib", default=None, help="A/B: a variant build (build.py --variant)")
     a = ap.parse_args()
     import bench
     import zkatdlog
+    if a.lib:
+        zkatdlog._abi.use_library(a.lib)
     from zkatdlog import workload as W
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     for th in [int(x) for x in a.threads.split(",")]:
