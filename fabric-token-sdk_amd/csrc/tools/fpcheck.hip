@@ -7,6 +7,7 @@
 
 #include "../dev/binv.h"
 #include "../dev/fp.h"
+#include "../dev/row29.h"
 
 using namespace fts;
 
@@ -150,4 +151,103 @@ extern "C" int ftz_binvcheck(int device, uint32_t n, const uint8_t* zmask, uint3
   (void)hipFree(dz);
   (void)hipFree(out);
   return rc;
+}
+
+// ---- dev/row29.h against dev/fp29.h: every row of every wave multiplies,
+// normalises and reduces its own operands (limbs normalised, or signed within
+// 2^29) row-wide, every lane the same one-lane, and lane r compares limb r.
+__device__ f29 rnd_f29(uint32_t& s, bool sgn) {
+  f29 a;
+  for (int i = 0; i < 8; i++) {
+    uint32_t x = xorshift(s) & (uint32_t)F29_MASK;
+    a.l[i] = sgn ? (int32_t)(x >> 0) - (int32_t)(1u << 28) : (int32_t)x;
+  }
+  a.l[8] = (int32_t)(xorshift(s) & 0x3FFFFFu) - (sgn ? (1 << 21) : 0);
+  return a;
+}
+__global__ void __launch_bounds__(64) k_rowcheck(uint32_t seed, uint32_t* bad) {
+  const uint32_t r = row_lane(), q = row_index();
+  uint32_t s = seed ^ ((blockIdx.x * 4 + q) + 1) * 2654435761u;
+  if (!s) s = 1;
+  for (int it = 0; it < 16; it++) {
+    const bool sgn = (it & 1) != 0;
+    const f29 a = rnd_f29(s, sgn), b = rnd_f29(s, sgn);
+    const f29 want_m = f29_mul_c(a, b), want_n = f29_norm(f29_add(a, b)), want_r = f29_reduce(f29_sub(a, b));
+    const r29 ra = row_from(a), rb = row_from(b);
+    const r29 gm = row_mul(ra, rb), gn = row_norm(row_add(ra, rb)), gr = row_reduce(row_sub(ra, rb));
+    int32_t wm = 0, wn = 0, wr = 0;
+    for (int i = 0; i < 9; i++) {
+      wm = r == (uint32_t)i ? want_m.l[i] : wm;
+      wn = r == (uint32_t)i ? want_n.l[i] : wn;
+      wr = r == (uint32_t)i ? want_r.l[i] : wr;
+    }
+    if (gm.v != wm || gn.v != wn || gr.v != wr) atomicAdd(bad, 1u);
+    const bool z = row_is_zero(row_sub(ra, ra)), nz = row_is_zero(ra);
+    if (!z || nz != f29_is_zero(a)) atomicAdd(bad + 1, 1u);
+    // four different products at once through row_level, against the one-lane ones
+    r29 xa[4] = {ra, rb, gm, gn}, xb[4] = {rb, gm, gn, ra}, o[4];
+    row_level<4>(xa, xb, o);
+    const f29 fa[4] = {a, b, want_m, want_n}, fb[4] = {b, want_m, want_n, a};
+    for (int k = 0; k < 4; k++) {
+      const f29 w = f29_mul_c(fa[k], fb[k]);
+      int32_t wk = 0;
+      for (int i = 0; i < 9; i++) wk = r == (uint32_t)i ? w.l[i] : wk;
+      if (o[k].v != wk) atomicAdd(bad + 2, 1u);
+    }
+  }
+}
+
+extern "C" int ftz_rowcheck(int device, uint32_t seed, uint32_t* out3) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  uint32_t* bad;
+  if (hipMalloc(&bad, 12) != hipSuccess) return -1;
+  (void)hipMemset(bad, 0, 12);
+  k_rowcheck<<<1024, 64>>>(seed, bad);
+  uint32_t h[3] = {0, 0, 0};
+  hipError_t e = hipMemcpy(h, bad, 12, hipMemcpyDeviceToHost);
+  (void)hipFree(bad);
+  if (e != hipSuccess) return -1;
+  for (int k = 0; k < 3; k++) out3[k] = h[k];
+  return (int)(h[0] + h[1] + h[2]);
+}
+
+// one wave, a chain of n dependent products: row-wide (impl 1) or one-lane
+// f29_mul_c (impl 0); returns GPU clock cycles per product
+__global__ void __launch_bounds__(64) k_rowbench(int impl, int n, int32_t* io, uint64_t* cyc) {
+  f29 a, b;
+  for (int i = 0; i < 9; i++) {
+    a.l[i] = io[i] & F29_MASK;
+    b.l[i] = io[9 + i] & F29_MASK;
+  }
+  a.l[8] &= 0xFFFF;
+  b.l[8] &= 0xFFFF;
+  const uint64_t t0 = __builtin_readcyclecounter();
+  if (impl == 1) {
+    r29 x = row_from(a), y = row_from(b);
+    for (int k = 0; k < n; k++) x = row_mul(x, y);
+    a = row_to(x);
+  } else {
+    for (int k = 0; k < n; k++) a = f29_mul_c(a, b);
+  }
+  const uint64_t t1 = __builtin_readcyclecounter();
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 9; i++) io[18 + i] = a.l[i];
+    *cyc = (t1 - t0) / (uint64_t)n;
+  }
+}
+
+extern "C" long ftz_rowbench(int device, int impl, int n) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  int32_t* io;
+  uint64_t* cyc;
+  if (hipMalloc(&io, 27 * 4) != hipSuccess || hipMalloc(&cyc, 8) != hipSuccess) return -1;
+  int32_t h[27];
+  for (int i = 0; i < 27; i++) h[i] = 123456789 * (i + 1);
+  (void)hipMemcpy(io, h, sizeof h, hipMemcpyHostToDevice);
+  k_rowbench<<<1, 64>>>(impl, n, io, cyc);
+  uint64_t c = 0;
+  hipError_t e = hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(io);
+  (void)hipFree(cyc);
+  return e == hipSuccess ? (long)c : -1;
 }

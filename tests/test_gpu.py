@@ -170,3 +170,18 @@ def test_binv_tree_device_check():
         if n >= 512:
             z[256:512] = b"\x01" * 256  # a block of zeros only
         assert lib.ftz_binvcheck(0, n, bytes(z), 1000 + n) == 0, n
+
+
+def test_row29_device_check():
+    """dev/row29.h (one field element per 16-lane DPP row: the MSM Horner
+    chain's arithmetic) against dev/fp29.h on the device: products, carry
+    normalisation, reduction, zero tests and four products at once through
+    row_level, for normalised and signed-limb operands (1024 waves x 16 rounds
+    x 4 rows): every limb identical"""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsfpcheck.so"))
+    out = (ctypes.c_uint32 * 3)()
+    lib.ftz_rowcheck.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    assert lib.ftz_rowcheck(0, 777, out) == 0, list(out)
