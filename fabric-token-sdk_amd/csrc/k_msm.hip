@@ -3,6 +3,7 @@
 
 #include "dev/msm.h"
 #include "launch.h"
+#include "dev/row29.h"
 
 using namespace fts;
 
@@ -378,6 +379,117 @@ __device__ __forceinline__ void coop29_add(f29& X, f29& Y, f29& Z, bool& inf, co
   Z = Z3;
 }
 
+// ---- the same formulas on dev/row29.h: each element one DPP row, a level's
+// (up to four) products one per row (row_level), so a product is 18 row-wide
+// MADs instead of 162 one-lane ones; every limb identical to coop29_*.
+// FTS_MSM_ROW_HORNER (default 1) selects these for the Horner chain.
+#ifndef FTS_MSM_ROW_HORNER
+#define FTS_MSM_ROW_HORNER 1
+#endif
+__device__ __forceinline__ r29 rnorm(const r29& a) { return row_norm(a); }
+__device__ __forceinline__ r29 rred(const r29& a) { return row_reduce(a); }
+
+__device__ __forceinline__ void row29_dbl(r29& X, r29& Y, r29& Z) {
+  r29 A, Bq, Z3, C, T2, F, Y3a;
+  {
+    r29 a[4] = {X, Y, rnorm(row_add(Y, Z)), Z}, o[4];
+    row_level<4>(a, a, o);
+    A = o[0];
+    Bq = o[1];
+    Z3 = rred(row_sub(row_sub(o[2], o[1]), o[3]));
+  }
+  r29 E = rnorm(row_add(row_add(A, A), A));
+  {
+    r29 t = rnorm(row_add(X, Bq));
+    r29 a[3] = {Bq, t, E}, o[3];
+    row_level<3>(a, a, o);
+    C = o[0];
+    T2 = o[1];
+    F = o[2];
+  }
+  r29 D1 = rnorm(row_sub(row_sub(T2, A), C));
+  r29 D = row_add(D1, D1);
+  r29 X3 = rred(row_sub(rnorm(row_sub(F, D)), D));
+  {
+    r29 a[1] = {E}, b[1] = {rnorm(row_sub(D, X3))}, o[1];
+    row_level<1>(a, b, o);
+    Y3a = o[0];
+  }
+  r29 C2 = row_add(C, C);
+  r29 C4 = rnorm(row_add(C2, C2));
+  X = X3;
+  Y = rred(row_sub(Y3a, row_add(C4, C4)));
+  Z = Z3;
+}
+
+__device__ __forceinline__ void row29_add(r29& X, r29& Y, r29& Z, bool& inf, const r29& qx, const r29& qy,
+                                          const r29& qz, bool qinf) {
+  if (qinf) return;
+  if (inf) {
+    X = qx;
+    Y = qy;
+    Z = qz;
+    inf = false;
+    return;
+  }
+  r29 Z1Z1, Z2Z2, ZZ, U1, U2, t1, t2, S1, S2, I, J, V, R2, Z3p, Y3a, SJ;
+  {
+    r29 zs = rnorm(row_add(Z, qz));
+    r29 a[3] = {Z, qz, zs}, o[3];
+    row_level<3>(a, a, o);
+    Z1Z1 = o[0];
+    Z2Z2 = o[1];
+    ZZ = o[2];
+  }
+  {
+    r29 a[4] = {X, qx, qz, Z}, b[4] = {Z2Z2, Z1Z1, Z2Z2, Z1Z1}, o[4];
+    row_level<4>(a, b, o);
+    U1 = o[0];
+    U2 = o[1];
+    t1 = o[2];
+    t2 = o[3];
+  }
+  r29 H = rnorm(row_sub(U2, U1));
+  r29 H2 = rnorm(row_add(H, H));
+  {
+    r29 a[3] = {Y, qy, H2}, b[3] = {t1, t2, H2}, o[3];
+    row_level<3>(a, b, o);
+    S1 = o[0];
+    S2 = o[1];
+    I = o[2];
+  }
+  r29 rr = row_sub(S2, S1);
+  r29 r2 = rnorm(row_add(rr, rr));
+  {
+    r29 zd = rnorm(row_sub(row_sub(ZZ, Z1Z1), Z2Z2));
+    r29 a[4] = {H, U1, r2, zd}, b[4] = {I, I, r2, H}, o[4];
+    row_level<4>(a, b, o);
+    J = o[0];
+    V = o[1];
+    R2 = o[2];
+    Z3p = o[3];
+  }
+  r29 X3 = rred(row_sub(row_sub(row_sub(R2, J), V), V));
+  {
+    r29 a[2] = {r2, S1}, b[2] = {rnorm(row_sub(V, X3)), J}, o[2];
+    row_level<2>(a, b, o);
+    Y3a = o[0];
+    SJ = o[1];
+  }
+  r29 Y3 = rred(row_sub(row_sub(Y3a, SJ), SJ));
+  r29 Z3 = rred(Z3p);
+  if (row_zero_reduced(Z3)) {  // H == 0: p == q (a doubling) or p == -q (infinity)
+    if (row_is_zero(rr))
+      row29_dbl(X, Y, Z);
+    else
+      inf = true;
+    return;
+  }
+  X = X3;
+  Y = Y3;
+  Z = Z3;
+}
+
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
 // on one wave with the 4-lane cooperative carry-free point ops, the Jacobian
 // result in acc_buf.  W_w arrives as `per` partial sums (wparts[w per + k], the
@@ -402,6 +514,19 @@ __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uin
   }
   __syncthreads();
   j29 a0 = w_hi == p.rw ? j29_inf() : j29_ld(*acc_buf);
+#if FTS_MSM_ROW_HORNER
+  r29 X = row_from(a0.x), Y = row_from(a0.y), Z = row_from(a0.z);
+  bool inf = a0.inf;
+  for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
+    if (w != (int)p.rw - 1 && !inf)
+      for (uint32_t q = 0; q < p.c; q++) row29_dbl(X, Y, Z);
+    const j29& q = ws[w - (int)w_lo];
+    row29_add(X, Y, Z, inf, row_from(q.x), row_from(q.y), row_from(q.z), q.inf);
+  }
+  const j29 res = {row_to(X), row_to(Y), row_to(Z), inf};
+  if (threadIdx.x != 0) return;
+  g1j_store(*acc_buf, j29_to(res));
+#else
   f29 X = a0.x, Y = a0.y, Z = a0.z;
   bool inf = a0.inf;
   for (int w = (int)w_hi - 1; w >= (int)w_lo; w--) {
@@ -411,6 +536,7 @@ __global__ void __launch_bounds__(64) k_msm_horner(MsmPlan p, uint32_t w_hi, uin
   }
   if (threadIdx.x != 0) return;
   g1j_store(*acc_buf, j29_to({X, Y, Z, inf}));
+#endif
 }
 
 // test points with known logs: P_i = (i + off) G from the generator's fixed-base

@@ -4,7 +4,7 @@ slots per segment S, resident-point mode P and sort digit bits R (ftz_options
 msm_window_bits / msm_slot_cap / msm_seg_slots / msm_precompute /
 msm_radix_bits; 0 = the planner's choice / off) and graph replay G
 (ftz_options.msm_graph, default 1).
-    python msmtune.py 20 "0,0,0 16,16,0 16,32,0 15,0,0 17,0,0,1 0,0,0,0,8"
+    python msmtune.py 20 "0,0,0 16,16,0 16,32,0 15,0,0 17,0,0,1 0,0,0,0,8" [variant.so]
 """
 import json
 import os
@@ -15,6 +15,9 @@ sys.path.insert(0, os.path.join(ROOT, "fabric-token-sdk_amd"))
 import numpy as np  # noqa: E402
 
 import zkatdlog  # noqa: E402
+
+if len(sys.argv) > 3:  # A/B: a variant build (build.py --variant)
+    zkatdlog._abi.use_library(sys.argv[3])
 
 lg = int(sys.argv[1])
 combos = [tuple(int(v) for v in (c + ",0,0,0,0,1"[len(c.split(",")) * 2 - 2:]).split(",")[:6])
