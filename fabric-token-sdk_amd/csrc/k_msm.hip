@@ -382,9 +382,13 @@ __device__ __forceinline__ void coop29_add(f29& X, f29& Y, f29& Z, bool& inf, co
 // ---- the same formulas on dev/row29.h: each element one DPP row, a level's
 // (up to four) products one per row (row_level), so a product is 18 row-wide
 // MADs instead of 162 one-lane ones; every limb identical to coop29_*.
-// FTS_MSM_ROW_HORNER (default 1) selects these for the Horner chain.
+// FTS_MSM_ROW_HORNER=1 selects these for the Horner chain.  Measured (round 6,
+// profiles/r06/msm_row.txt): the rows' products are 2.36x faster than one-lane
+// f29_mul_c in a dependent chain, but the whole MSM is 3-4% SLOWER than with
+// the quad-cooperative coop29_* chain below (the normalisation rounds and the
+// bpermute exchange eat the MAD saving), so the default stays 0.
 #ifndef FTS_MSM_ROW_HORNER
-#define FTS_MSM_ROW_HORNER 1
+#define FTS_MSM_ROW_HORNER 0
 #endif
 __device__ __forceinline__ r29 rnorm(const r29& a) { return row_norm(a); }
 __device__ __forceinline__ r29 rred(const r29& a) { return row_reduce(a); }

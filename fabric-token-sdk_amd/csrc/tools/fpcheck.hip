@@ -184,10 +184,18 @@ __global__ void __launch_bounds__(64) k_rowcheck(uint32_t seed, uint32_t* bad) {
     if (gm.v != wm || gn.v != wn || gr.v != wr) atomicAdd(bad, 1u);
     const bool z = row_is_zero(row_sub(ra, ra)), nz = row_is_zero(ra);
     if (!z || nz != f29_is_zero(a)) atomicAdd(bad + 1, 1u);
-    // four different products at once through row_level, against the one-lane ones
-    r29 xa[4] = {ra, rb, gm, gn}, xb[4] = {rb, gm, gn, ra}, o[4];
+    // four different products at once through row_level (operands common to
+    // the wave's rows, as in the Horner chain: row 0's here), against the one-lane ones
+    f29 c0 = a, c1 = b;
+    for (int i = 0; i < 9; i++) {
+      c0.l[i] = __builtin_amdgcn_readlane(a.l[i], 0);
+      c1.l[i] = __builtin_amdgcn_readlane(b.l[i], 0);
+    }
+    const f29 cm = f29_mul_c(c0, c1), cn = f29_norm(f29_add(c0, c1));
+    const r29 r0 = row_from(c0), r1 = row_from(c1), rm = row_from(cm), rn = row_from(cn);
+    r29 xa[4] = {r0, r1, rm, rn}, xb[4] = {r1, rm, rn, r0}, o[4];
     row_level<4>(xa, xb, o);
-    const f29 fa[4] = {a, b, want_m, want_n}, fb[4] = {b, want_m, want_n, a};
+    const f29 fa[4] = {c0, c1, cm, cn}, fb[4] = {c1, cm, cn, c0};
     for (int k = 0; k < 4; k++) {
       const f29 w = f29_mul_c(fa[k], fb[k]);
       int32_t wk = 0;

@@ -10,8 +10,8 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu.py tests/test_msm.py -m gpu
 echo tests ok
 for r in 1 2; do
   for lg in 16 20 24; do
-    timeout -k 10 200 python -u fabric-token-sdk_amd/tools/msmtune.py $lg "0,0,0 0,0,0,0,0,0,1" >> gpurun_out/r06g_msm_row.log 2>&1 || { echo "msmtune row $lg failed"; exit 5; }
-    timeout -k 10 200 python -u fabric-token-sdk_amd/tools/msmtune.py $lg "0,0,0" fabric-token-sdk_amd/zkatdlog/_lib/ab/libftsamd_hq.so >> gpurun_out/r06g_msm_hq.log 2>&1 || { echo "msmtune hq $lg failed"; exit 6; }
+    timeout -k 10 200 python -u fabric-token-sdk_amd/tools/msmtune.py $lg "0,0,0,0,0,0" >> gpurun_out/r06g_msm_row.log 2>&1 || { echo "msmtune row $lg failed"; exit 5; }
+    timeout -k 10 200 python -u fabric-token-sdk_amd/tools/msmtune.py $lg "0,0,0,0,0,0" fabric-token-sdk_amd/zkatdlog/_lib/ab/libftsamd_hq.so >> gpurun_out/r06g_msm_hq.log 2>&1 || { echo "msmtune hq $lg failed"; exit 6; }
   done
 done
 echo row; grep "n=2" gpurun_out/r06g_msm_row.log; echo old; grep "n=2" gpurun_out/r06g_msm_hq.log
