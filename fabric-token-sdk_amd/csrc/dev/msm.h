@@ -55,6 +55,26 @@ struct MsmPlan {
   uint64_t nv_magic;   // floor(2^32 / nv) + 1: the window of an entry t without a division
 };
 
+// k_msm_tree: parts per block (quad-cooperative additions: 128, one lane each: 256)
+#ifndef FTS_MSM_QUAD_TREE
+#define FTS_MSM_QUAD_TREE 1
+#endif
+static constexpr uint32_t MSM_TREE_CHUNK = FTS_MSM_QUAD_TREE ? 128u : 256u;
+// k_msm_segment: one quad per segment (64 per 256-lane block) or one lane each
+// (default: the quads measured slower, 2^16 segment stage 264 against 188 us,
+// 2^20 523 against 282, profiles/r06/msm_tail.txt)
+#ifndef FTS_MSM_QUAD_SEG
+#define FTS_MSM_QUAD_SEG 0
+#endif
+static constexpr uint32_t MSM_SEG_THREADS = FTS_MSM_QUAD_SEG ? 256u : 128u;
+static constexpr uint32_t MSM_SEG_PER_BLOCK = FTS_MSM_QUAD_SEG ? 64u : 128u;
+
+// the window combination (Horner) on the host from the read-back window sums
+// (msm_rt.hip msm_horner_host); 0: on one wave of the device (k_msm_horner)
+#ifndef FTS_MSM_HOST_HORNER
+#define FTS_MSM_HOST_HORNER 1
+#endif
+
 // window bits for n (virtual) points: floor(log2 n / 2) + 7 clamped to [8, 20]
 // (measured on MI355X with GLV: 2^17 -> 15, 2^21 -> 17, 2^25 -> 19; the
 // latency-bound reduction favours fewer windows than the usual log2 n - 4)

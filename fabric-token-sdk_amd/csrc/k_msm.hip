@@ -185,34 +185,6 @@ __global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* w
   g1j_store(slot_sum[j], msm_job_slot(p, j, owner, soff, start, count, perm, pts));
 }
 
-__global__ void __launch_bounds__(128) k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1, const uint32_t* wlo,
-                                                     const uint32_t* whi, const uint32_t* owner,
-                                                     const G1JDev* slot_sum, G1JDev* part) {
-  uint32_t i = w0 * p.segs + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= w1 * p.segs) return;
-  uint32_t w = i / p.segs, s = i - w * p.segs;
-  g1j_store(part[i], msm_job_segment(p, w, s, wlo, whi, owner, slot_sum));
-}
-
-// tree sum of m consecutive parts per window in chunks of 256: out[w][ceil(m/256)]
-// (carry-free form in LDS: one conversion in, one out)
-__global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out) {
-  __shared__ j29 s[256];
-  uint32_t chunks = (m + 255) / 256;
-  uint32_t w = blockIdx.x / chunks, ch = blockIdx.x - w * chunks, t = threadIdx.x;
-  uint32_t i = ch * 256 + t;
-  s[t] = i < m ? j29_ld(in[(size_t)w * m + i]) : j29_inf();
-  __syncthreads();
-  // only the levels the chunk's live parts need (a window's last tree level
-  // often holds a few dozen: 5 additions deep instead of 8)
-  uint32_t live = min(256u, m - ch * 256), o = 1;
-  while (2 * o < live) o *= 2;
-  for (; live > 1; live = o, o >>= 1) {
-    if (t < o && t + o < live) s[t] = j29_add(s[t], s[t + o]);
-    __syncthreads();
-  }
-  if (t == 0) g1j_store(out[(size_t)w * chunks + ch], j29_to(s[0]));
-}
 
 // ---- 4-lane cooperative point arithmetic for the serial Horner chain.  A
 // wave issues a one-lane product at the cost of a 64-lane one, so the chain's
@@ -492,6 +464,114 @@ __device__ __forceinline__ void row29_add(r29& X, r29& Y, r29& Z, bool& inf, con
   X = X3;
   Y = Y3;
   Z = Z3;
+}
+
+// k P (k < 2^32) on the quad: j29_mul_small's 2-bit windows from the top one
+// with coop29_dbl / coop29_add (k is quad-uniform; m P != O for 0 < m < 2^32)
+__device__ __forceinline__ void coop29_mul_small(f29& X, f29& Y, f29& Z, bool& inf, uint32_t k) {
+  if (inf) return;
+  if (!k) {
+    inf = true;
+    return;
+  }
+  const j29 p1 = {X, Y, Z, false};
+  f29 X2 = X, Y2 = Y, Z2 = Z;
+  coop29_dbl(X2, Y2, Z2);
+  const j29 p2 = {X2, Y2, Z2, false};
+  bool i3 = false;
+  f29 X3 = X2, Y3 = Y2, Z3 = Z2;
+  coop29_add(X3, Y3, Z3, i3, p1);
+  const j29 p3 = {X3, Y3, Z3, false};
+  const int top = 31 - __builtin_clz(k), w = top >> 1;
+  uint32_t d = (k >> (2 * w)) & 3u;
+  const j29& a0 = d == 1 ? p1 : (d == 2 ? p2 : p3);
+  X = a0.x;
+  Y = a0.y;
+  Z = a0.z;
+  for (int i = w - 1; i >= 0; i--) {
+    coop29_dbl(X, Y, Z);
+    coop29_dbl(X, Y, Z);
+    d = (k >> (2 * i)) & 3u;
+    if (d) coop29_add(X, Y, Z, inf, d == 1 ? p1 : (d == 2 ? p2 : p3));
+  }
+}
+
+// Segment sums (dev/msm.h msm_job_segment).  FTS_MSM_QUAD_SEG=1: one
+// quad per segment, the running sums and the bl multiple (j29_mul_small: ~13
+// doublings + 7 additions at 2^14) on coop29_*, 64 segments per 256-lane block;
+// the stage is a latency-bound chain per segment (2^16 points: 55k segments, a
+// single-lane chain of ~16 additions + 13 doublings).  0 (default, measured
+// faster: the one-lane chains interleave their independent products and need
+// a quarter of the waves): one lane per segment.
+__global__ void __launch_bounds__(MSM_SEG_THREADS) k_msm_segment(MsmPlan p, uint32_t w0, uint32_t w1,
+                                                                 const uint32_t* wlo, const uint32_t* whi,
+                                                                 const uint32_t* owner, const G1JDev* slot_sum,
+                                                                 G1JDev* part) {
+#if FTS_MSM_QUAD_SEG
+  const uint32_t i = w0 * p.segs + blockIdx.x * MSM_SEG_PER_BLOCK + (threadIdx.x >> 2);
+  if (i >= w1 * p.segs) return;  // quad-uniform
+  const uint32_t w = i / p.segs, sg = i - w * p.segs;
+  const bool lead = (threadIdx.x & 3) == 0;
+  const uint32_t lo = wlo[w] + sg * p.seg_len;
+  uint32_t hi = lo + p.seg_len;
+  if (hi > whi[w]) hi = whi[w];
+  if (lo >= hi) {
+    if (lead) g1j_store(part[i], jac_inf<fp>());
+    return;
+  }
+  f29 RX{}, RY{}, RZ{}, AX{}, AY{}, AZ{};
+  bool rinf = true, ainf = true;
+  for (uint32_t j = hi; j > lo; j--) {
+    coop29_add(RX, RY, RZ, rinf, j29_ld(slot_sum[j - 1]));
+    if (j - 1 == lo || owner[j - 2] != owner[j - 1]) coop29_add(AX, AY, AZ, ainf, {RX, RY, RZ, rinf});
+  }
+  coop29_mul_small(RX, RY, RZ, rinf, owner[lo] - w * p.buckets);
+  coop29_add(AX, AY, AZ, ainf, {RX, RY, RZ, rinf});
+  if (lead) g1j_store(part[i], j29_to({AX, AY, AZ, ainf}));
+#else
+  uint32_t i = w0 * p.segs + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= w1 * p.segs) return;
+  uint32_t w = i / p.segs, s = i - w * p.segs;
+  g1j_store(part[i], msm_job_segment(p, w, s, wlo, whi, owner, slot_sum));
+#endif
+}
+
+// tree sum of m consecutive parts per window in chunks of MSM_TREE_CHUNK:
+// out[w][ceil(m / chunk)].  FTS_MSM_QUAD_TREE (default 1): a block of 256 lanes
+// is 64 quads, each addition of a level runs on one quad (coop29_add: 5 product
+// levels instead of one lane's 16 dependent products), a chunk of 128 parts is
+// 7 levels.  0: one lane per addition, chunks of 256 (8 levels).  Only the
+// levels the chunk's live parts need (a window's last level often holds a few
+// dozen).  Carry-free form in LDS: one conversion in, one out.
+__global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, G1JDev* out) {
+  constexpr uint32_t CH = MSM_TREE_CHUNK;
+  __shared__ j29 s[CH];
+  const uint32_t chunks = (m + CH - 1) / CH;
+  const uint32_t w = blockIdx.x / chunks, ch = blockIdx.x - w * chunks, t = threadIdx.x;
+  const uint32_t i = ch * CH + t;
+  if (t < CH) s[t] = i < m ? j29_ld(in[(size_t)w * m + i]) : j29_inf();
+  __syncthreads();
+  uint32_t live = min(CH, m - ch * CH), o = 1;
+  while (2 * o < live) o *= 2;
+#if FTS_MSM_QUAD_TREE
+  const uint32_t q = t >> 2;  // quad-uniform branches: the 4 lanes hold the same point
+  for (; live > 1; live = o, o >>= 1) {
+    if (q < o && q + o < live) {
+      const j29 a = s[q], b = s[q + o];
+      f29 X = a.x, Y = a.y, Z = a.z;
+      bool inf = a.inf;
+      coop29_add(X, Y, Z, inf, b);
+      if ((t & 3) == 0) s[q] = {X, Y, Z, inf};
+    }
+    __syncthreads();
+  }
+#else
+  for (; live > 1; live = o, o >>= 1) {
+    if (t < o && t + o < live) s[t] = j29_add(s[t], s[t + o]);
+    __syncthreads();
+  }
+#endif
+  if (t == 0) g1j_store(out[(size_t)w * chunks + ch], j29_to(s[0]));
 }
 
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,

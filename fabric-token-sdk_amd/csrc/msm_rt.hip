@@ -20,6 +20,7 @@ struct ftz_msm {
   uint32_t key_bits = 0;
   DBuf<G1JDev> slot_sum, part, tree;
   DBuf<G1JDev> hacc;
+  G1JDev* hwin = nullptr;  // page-locked: the window sums read back for the host Horner
   DBuf<uint8_t> ok;
   hipEvent_t ev[2];
   bool ev_init = false;
@@ -89,8 +90,9 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->lenhist.alloc(1024));
   HC(m->lencur.alloc(1024));
   HC(m->part.alloc((size_t)p.rw * p.segs));
-  HC(m->tree.alloc((size_t)p.rw * ((p.segs + 255) / 256) * 2));
+  HC(m->tree.alloc((size_t)p.rw * ((p.segs + MSM_TREE_CHUNK - 1) / MSM_TREE_CHUNK) * 2));
   HC(m->hacc.alloc(1));
+  HC(hipHostMalloc(reinterpret_cast<void**>(&m->hwin), (size_t)p.rw * sizeof(G1JDev), hipHostMallocDefault));
   HC(m->ok.alloc(n));
   for (int k = 0; k < 2; k++) HC(hipEventCreate(&m->ev[k]));
   m->ev_init = true;
@@ -265,25 +267,53 @@ static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
                                                      m->lenhist.p, m->order.p);
   k_msm_bucket<<<blocks(sl, 128), 128, 0, s>>>(p, m->whi.p, m->order.p, m->owner.p, m->soff.p, m->start.p,
                                                m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
-  k_msm_segment<<<blocks((size_t)p.rw * p.segs, 128), 128, 0, s>>>(p, 0, p.rw, m->wlo.p, m->whi.p,
+  k_msm_segment<<<blocks((size_t)p.rw * p.segs, MSM_SEG_PER_BLOCK), MSM_SEG_THREADS, 0, s>>>(p, 0, p.rw, m->wlo.p, m->whi.p,
                                                                        m->owner.p, m->slot_sum.p, m->part.p);
-  // tree passes: segs -> ceil(segs/256) -> ... until at most HORNER_PARTS per
-  // window, which the Horner wave adds up itself (quads in parallel)
-  const uint32_t HORNER_PARTS = 8;
-  G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.rw * ((p.segs + 255) / 256)};
+  // tree passes: segs -> ceil(segs / chunk) -> ... until one part per window
+  // (host Horner) or at most HORNER_PARTS, which the Horner wave adds up itself
+  // (quads in parallel)
+  const uint32_t HORNER_PARTS = FTS_MSM_HOST_HORNER ? 1 : 8;
+  G1JDev* bufs[2] = {m->tree.p, m->tree.p + (size_t)p.rw * ((p.segs + MSM_TREE_CHUNK - 1) / MSM_TREE_CHUNK)};
   const G1JDev* in = m->part.p;
   uint32_t cnt = p.segs;
   int which = 0;
   while (cnt > HORNER_PARTS) {
-    uint32_t chunks = (cnt + 255) / 256;
+    uint32_t chunks = (cnt + MSM_TREE_CHUNK - 1) / MSM_TREE_CHUNK;
     G1JDev* out = bufs[which];
     k_msm_tree<<<p.rw * chunks, 256, 0, s>>>(in, cnt, out);
     in = out;
     which ^= 1;
     cnt = chunks;
   }
+#if FTS_MSM_HOST_HORNER
+  HC(hipMemcpyAsync(m->hwin, in, (size_t)p.rw * sizeof(G1JDev), hipMemcpyDeviceToHost, s));
+#else
   k_msm_horner<<<1, 64, 0, s>>>(p, p.rw, 0, in, cnt, m->hacc.p);
+#endif
   return FTZ_SUCCESS;
+}
+
+// The window combination sum_w 2^(c w) W_w on the host, from the rw window sums
+// the pipeline read back (rw * 96 bytes): c (rw - 1) dependent doublings (120 at
+// 2^16 and 2^20) are one serial chain whatever the device does, and a host core
+// runs a doubling in 4x64-bit Montgomery limbs (FTS_HOST64) several times faster
+// than one wave's latency-bound chain (k_msm_horner: 284-298 us per MSM,
+// profiles/r06/msm_trace.txt) -- the split sppark's Pippenger also makes.  The
+// affine result is unique, so the bytes are those of the device chain.
+// Counted in last_ms.
+static fts::g1j msm_horner_host(const MsmPlan& p, const G1JDev* win) {
+  fts::g1j acc = fts::jac_inf<fts::fp>();
+  bool started = false;
+  for (int w = (int)p.rw - 1; w >= 0; w--) {
+    if (started)
+      for (uint32_t q = 0; q < p.c; q++) acc = fts::jac_dbl(acc);
+    const fts::g1j x = fts::g1j_load(win[w]);
+    if (!fts::is_zero(x.z)) {
+      acc = fts::jac_add(acc, x);
+      started = !fts::is_zero(acc.z);
+    }
+  }
+  return acc;
 }
 
 // the result after the enqueued pipeline (event ev[0] recorded at its start)
@@ -291,6 +321,11 @@ static int msm_finish(ftz_msm* m, uint8_t out[64]) {
   hipStream_t s = m->ctx->stream;
   HC(hipEventRecord(m->ev[1], s));
   HC(hipGetLastError());
+#if FTS_MSM_HOST_HORNER
+  HC(hipStreamSynchronize(s));
+  auto t0 = std::chrono::steady_clock::now();
+  fts::g1j_to_raw(msm_horner_host(m->p, m->hwin), out);
+#else
   G1JDev acc;
   HC(hipMemcpyAsync(&acc, m->hacc.p, sizeof(acc), hipMemcpyDeviceToHost, s));
   HC(hipStreamSynchronize(s));
@@ -298,6 +333,7 @@ static int msm_finish(ftz_msm* m, uint8_t out[64]) {
   // here, ~40k single-lane instructions on the device); counted in last_ms
   auto t0 = std::chrono::steady_clock::now();
   fts::g1j_to_raw(fts::g1j_load(acc), out);
+#endif
   double host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   HC(hipEventElapsedTime(&m->last_ms, m->ev[0], m->ev[1]));
   m->last_ms += (float)host_ms;
@@ -427,6 +463,7 @@ extern "C" void ftz_msm_destroy(ftz_msm* m) {
     (void)hipStreamDestroy(m->cstream);
   }
   if (m->graph_exec) (void)hipGraphExecDestroy(m->graph_exec);
+  if (m->hwin) (void)hipHostFree(m->hwin);
   if (m->graph) (void)hipGraphDestroy(m->graph);
   delete m;
 }
