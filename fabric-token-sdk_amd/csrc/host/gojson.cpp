@@ -570,10 +570,47 @@ struct Merger {
 
 }  // namespace
 
+// false when merging obj under sch changes nothing: no schema field occurs
+// twice, and none of the fields' values (struct, or a slice's object
+// elements) needs merging itself -- the canonical encoder's output.  Merger
+// then returns every node unchanged, so go_merge can skip it (and its
+// allocations).
+static bool needs_merge(const JDoc& d, uint32_t obj, const JField* sch) {
+  int nf = 0;
+  while (sch && sch[nf].name) nf++;
+  if (!nf) return false;
+  if (nf > 16) return true;
+  uint8_t cnt[16] = {};
+  uint32_t val[16] = {};
+  const JNode& o = d.nodes[obj];
+  for (uint32_t k = 0; k < o.count; k++) {
+    uint32_t key = d.kids[o.first + 2 * k];
+    for (int q = 0; q < nf; q++)
+      if (go_key_matches(d.str(key), d.nodes[key].count, sch[q].name, strlen(sch[q].name))) {
+        if (++cnt[q] > 1) return true;
+        val[q] = d.kids[o.first + 2 * k + 1];
+      }
+  }
+  for (int q = 0; q < nf; q++) {
+    if (!cnt[q] || !sch[q].sub || !sch[q].sub[0].name) continue;
+    const JNode& v = d.nodes[val[q]];
+    if (sch[q].kind == JF_STRUCT) {
+      if (v.type == J_OBJ && needs_merge(d, val[q], sch[q].sub)) return true;
+    } else if (v.type == J_ARR) {
+      for (uint32_t k = 0; k < v.count; k++) {
+        uint32_t e = d.kids[v.first + k];
+        if (d.nodes[e].type == J_OBJ && needs_merge(d, e, sch[q].sub)) return true;
+      }
+    }
+  }
+  return false;
+}
+
 void go_merge(JDoc& d, const JField* schema) {
   if (d.nodes.empty()) return;
   uint32_t root = d.root();
   if (d.at(root).type != J_OBJ) return;
+  if (!needs_merge(d, root, schema)) return;
   Merger m{d};
   uint32_t r = m.merge({root}, schema);
   if (r != d.root()) {
@@ -800,6 +837,27 @@ static DecStatus elem_fields(const JDoc& d, int64_t node, int64_t& elem) {
   elem = d.field((uint32_t)node, "element");
   if (elem >= 0 && d.at((uint32_t)elem).type != J_NULL && d.at((uint32_t)elem).type != J_STR) return D_ERR;
   return curve == 1 ? D_OK : D_PANIC;
+}
+
+DecStatus dec_bytes_append(const JDoc& d, int64_t node, std::vector<uint8_t>& out) {
+  if (node < 0 || d.at((uint32_t)node).type == J_NULL) return D_NIL;
+  if (d.at((uint32_t)node).type != J_STR) return D_ERR;
+  const char* s = d.str((uint32_t)node);
+  size_t n = d.len((uint32_t)node), mark = out.size();
+  if (b64_decode_strict_append(s, n, out)) return D_OK;
+  out.resize(mark);  // the strict decoder may have stopped part way
+  if (!b64_decode_append(s, n, out)) {
+    out.resize(mark);
+    return D_ERR;
+  }
+  return D_OK;
+}
+
+DecStatus dec_elem_append(const JDoc& d, int64_t node, std::vector<uint8_t>& out) {
+  int64_t el = -1;
+  DecStatus st = elem_fields(d, node, el);
+  if (st == D_NIL || st == D_ERR) return st;
+  return dec_bytes_append(d, el, out) == D_ERR ? D_ERR : st;
 }
 
 ElemBytes dec_elem(const JDoc& d, int64_t node) {

@@ -106,6 +106,11 @@ ElemBytes dec_elem(const JDoc& d, int64_t node);
 DecStatus dec_elem_into(const JDoc& d, int64_t node, std::vector<uint8_t>& dst, size_t& off, uint32_t& len);
 // []byte field
 DecStatus dec_bytes(const JDoc& d, int64_t node, std::vector<uint8_t>& out);
+// the same appended to `out` (left as it was unless D_OK)
+DecStatus dec_bytes_append(const JDoc& d, int64_t node, std::vector<uint8_t>& out);
+// dec_elem's status with the element bytes appended to `out` (D_OK / D_PANIC;
+// `out` unchanged otherwise) -- no ElemBytes allocation per element
+DecStatus dec_elem_append(const JDoc& d, int64_t node, std::vector<uint8_t>& out);
 // int field (Go: number without fraction/exponent)
 DecStatus dec_int(const JDoc& d, int64_t node, int64_t& out);
 // string field

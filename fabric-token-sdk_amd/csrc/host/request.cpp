@@ -25,8 +25,9 @@ struct Der {
   size_t n;
 };
 
-// header at off: identifier byte must be `want`; on success body = [off, off+len)
-std::string der_header(const Der& d, size_t& off, uint8_t want, size_t& len) {
+// header at off: identifier byte must be `want`; on success (nullptr) body =
+// [off, off+len), else the reason
+const char* der_header(const Der& d, size_t& off, uint8_t want, size_t& len) {
   if (off >= d.n) return "sequence truncated";
   uint8_t id = d.b[off++];
   if ((id & 0x1f) == 0x1f) {  // high-tag-number form: tags 4 and 16 cannot use it
@@ -52,26 +53,26 @@ std::string der_header(const Der& d, size_t& off, uint8_t want, size_t& len) {
   }
   if (L > d.n - off) return "data truncated";
   len = L;
-  return "";
+  return nullptr;
 }
 
 // SEQUENCE OF OCTET STRING at off (advances off past it)
-std::string der_seq_of_octets(const Der& d, size_t& off, std::vector<Slice>& out) {
+const char* der_seq_of_octets(const Der& d, size_t& off, std::vector<Slice>& out) {
   size_t len;
-  std::string e = der_header(d, off, 0x30, len);
-  if (!e.empty()) return e;
+  const char* e = der_header(d, off, 0x30, len);
+  if (e) return e;
   Der inner{d.b + off, len};
   size_t k = 0;
   out.clear();
   while (k < inner.n) {
     size_t el;
     e = der_header(inner, k, 0x04, el);
-    if (!e.empty()) return e == "tags don't match" ? "sequence tag mismatch" : e;
+    if (e) return strcmp(e, "tags don't match") == 0 ? "sequence tag mismatch" : e;
     out.push_back(Slice{inner.b + k, el});
     k += el;
   }
   off += len;
-  return "";
+  return nullptr;
 }
 
 }  // namespace
@@ -81,13 +82,13 @@ std::string der_token_request(const uint8_t* raw, size_t len, std::vector<Slice>
   if (len == 0) return "empty token request";
   Der d{raw, len};
   size_t off = 0, body;
-  std::string e = der_header(d, off, 0x30, body);
-  if (!e.empty()) return "failed to unmarshal token request: " + e;
+  const char* e = der_header(d, off, 0x30, body);
+  if (e) return std::string("failed to unmarshal token request: ") + e;
   Der inner{raw + off, body};
   size_t k = 0;
   for (int f = 0; f < 4; f++) {
     e = der_seq_of_octets(inner, k, out[f]);
-    if (!e.empty()) return "failed to unmarshal token request: " + e;
+    if (e) return std::string("failed to unmarshal token request: ") + e;
   }
   // bytes after the fourth field (inside the SEQUENCE) and after the SEQUENCE
   // are ignored, as Go's parseField and FromBytes do
@@ -109,18 +110,18 @@ DecStatus dec_bool(const JDoc& d, int64_t node, bool& out) {
 // the slot is zero).  A buffer too short for its flags fails SetBytes inside
 // UnmarshalJSON whatever the curve arithmetic says (`bad`).
 DecStatus dec_g1(const JDoc& d, int64_t node, ElemRef& r, std::vector<uint8_t>& pool) {
-  ElemBytes e = dec_elem(d, node);
-  r.st = e.st;
+  const size_t off = pool.size();
+  const DecStatus st = dec_elem_append(d, node, pool);  // the bytes land at off
+  r.st = st;
   r.bad = 0;
   r.off = 0;
-  if (e.st != D_OK && e.st != D_PANIC) return e.st;
-  size_t L = e.raw.size();
-  uint8_t m = L ? (e.raw[0] & 0xC0) : 0;
+  if (st != D_OK && st != D_PANIC) return st;
+  size_t L = pool.size() - off;
+  uint8_t m = L ? (pool[off] & 0xC0) : 0;
   if (L < 32 || (m == 0x00 && L < 64)) r.bad = 1;
-  r.off = pool.size();
-  pool.resize(r.off + 64, 0);
-  memcpy(pool.data() + r.off, e.raw.data(), L < 64 ? L : 64);
-  return e.st;
+  r.off = off;
+  pool.resize(off + 64, 0);  // the slot: the first 64 bytes, zero-padded
+  return st;
 }
 
 // OutputTokens: []*token.Token, each {"Owner": []byte, "Data": *math.G1}
@@ -130,7 +131,7 @@ std::string dec_outputs(const JDoc& d, int64_t node, ActionOut& o, std::vector<u
   if (node < 0 || d.at((uint32_t)node).type == J_NULL) return "";
   if (d.at((uint32_t)node).type != J_ARR) return "cannot unmarshal into []*token.Token";
   uint32_t cnt = d.len((uint32_t)node);
-  std::vector<uint8_t> tmp;
+  static thread_local std::vector<uint8_t> tmp;  // Owner: checked, not kept
   for (uint32_t k = 0; k < cnt; k++) {
     uint32_t t = d.elem((uint32_t)node, k);
     ElemRef r{D_NIL, 0, 0};
@@ -152,7 +153,7 @@ std::string check_metadata(const JDoc& d, int64_t node) {
   if (node < 0 || d.at((uint32_t)node).type == J_NULL) return "";
   if (d.at((uint32_t)node).type != J_OBJ) return "cannot unmarshal into map[string][]byte";
   const JNode& o = d.at((uint32_t)node);
-  std::vector<uint8_t> tmp;
+  static thread_local std::vector<uint8_t> tmp;
   for (uint32_t k = 0; k < o.count; k++)
     if (dec_bytes(d, d.kids[o.first + 2 * k + 1], tmp) == D_ERR) return "bad Metadata value";
   return "";
@@ -235,7 +236,7 @@ std::string dec_issue_action(const uint8_t* p, size_t n, IssueAct& a, std::vecto
   if (!top_object(d, p, n, err, is_null, ISSUE_F)) return err;
   if (is_null) return "";
   uint32_t root = d.root();
-  std::vector<uint8_t> tmp;
+  static thread_local std::vector<uint8_t> tmp;
   if (dec_bytes(d, d.field(root, "Issuer"), tmp) == D_ERR) return "bad Issuer";
   // OutputTokens carries the tag json:"outputs,omitempty" (issue.go:24)
   err = dec_outputs(d, d.field(root, "outputs"), a.out, pool);
@@ -253,7 +254,7 @@ std::string dec_token(const uint8_t* p, size_t n, ElemRef& data, std::vector<uin
   if (!top_object(d, p, n, err, is_null)) return err;
   if (is_null) return "";
   uint32_t root = d.root();
-  std::vector<uint8_t> tmp;
+  static thread_local std::vector<uint8_t> tmp;
   if (dec_bytes(d, d.field(root, "Owner"), tmp) == D_ERR) return "bad Owner";
   if (dec_g1(d, d.field(root, "Data"), data, pool) == D_ERR) return "bad Data";
   if (data.st == D_OK && data.bad) return "bad Data";
@@ -343,20 +344,26 @@ void prefix(std::vector<size_t>& v) {
   for (size_t i = 1; i < v.size(); i++) v[i] += v[i - 1];
 }
 
-// steps 1-4 of a chunk and the start of its ZK verification.  Every per-request
-// stage runs on h.par (a request's state is written by one thread); the
-// calling thread does the prefix sums, the device checks and the ledger
-// callbacks.
-int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::string& err) {
-  const size_t m = c.r1 - c.r0;
-  StageClock clk{h.stats};
-  c.st.resize(m);
+// Steps 1-4 of a chunk and the start of its ZK verification: decode_chunk
+// (steps 1-2, decoding and the unmarshal checks), then ledger_chunk (the
+// ledger callbacks on the calling thread, token decoding, checks, the
+// verification hand-off).  Every per-request stage runs on h.par (a request's
+// state is written by one thread).  Decoding chunk k+1 on a thread of its own
+// beside chunk k's ledger phase measured the same (674k against 675k
+// transfers/s, six alternating runs, profiles/r06/req_decode.txt): the leg is
+// bound by the device work and the planning threads, not the calling thread.
+void par_each(const RequestHooks& h, size_t m, const std::function<void(size_t)>& f) {
   constexpr size_t PIECE = 32;
-  auto each = [&](const std::function<void(size_t)>& f) {
-    run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
-      for (size_t r = p * PIECE; r < m && r < (p + 1) * PIECE; r++) f(r);
-    });
-  };
+  run_par(h, (m + PIECE - 1) / PIECE, [&](size_t p) {
+    for (size_t r = p * PIECE; r < m && r < (p + 1) * PIECE; r++) f(r);
+  });
+}
+
+int decode_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, RequestStats* stats, std::string& err) {
+  const size_t m = c.r1 - c.r0;
+  StageClock clk{stats};
+  c.st.resize(m);
+  auto each = [&](const std::function<void(size_t)>& f) { par_each(h, m, f); };
   std::vector<size_t> cnt(m + 1, 0);
   // 1. decode: ASN.1, then every issue action, then every transfer action
   //    (validator.go unmarshalIssueActions / unmarshalTransferActions);
@@ -364,7 +371,7 @@ int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::s
   each([&](size_t i) {
     ReqState& s = c.st[i];
     const ftz_bytes& q = reqs[c.r0 + i];
-    std::vector<Slice> f[4];
+    static thread_local std::vector<Slice> f[4];  // cleared by der_token_request
     std::string e = der_token_request(q.p, q.len, f);
     if (e.empty()) {
       s.is.resize(f[0].size());
@@ -408,6 +415,14 @@ int prepare_chunk(const ftz_bytes* reqs, const RequestHooks& h, Chunk& c, std::s
     });
   }
   clk.mark(&RequestStats::check);
+  return FTZ_SUCCESS;
+}
+
+int ledger_chunk(const RequestHooks& h, Chunk& c, std::string& err) {
+  const size_t m = c.r1 - c.r0;
+  StageClock clk{h.stats};
+  auto each = [&](const std::function<void(size_t)>& f) { par_each(h, m, f); };
+  std::vector<size_t> cnt(m + 1, 0);
   // 3. ledger inputs of every transfer (TransferSignatureValidate's loads,
   //    validator_transfer.go:42-81) through the callbacks on the calling thread
   std::vector<size_t> kat(m + 1, 0);  // the request's first key index
@@ -641,7 +656,21 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
   const size_t CH = h.chunk ? h.chunk : 8192, IN = h.inflight ? h.inflight : 1;
   std::deque<std::unique_ptr<Chunk>> fly;
   int rc = FTZ_SUCCESS;
-  for (size_t r0 = 0; r0 < n && rc == FTZ_SUCCESS; r0 += CH) {
+  // the first chunks are smaller (CH/8, CH/4, CH/2, then CH): the device gets
+  // its first verification work after an eighth of a chunk's decoding
+#ifndef FTS_REQ_RAMP
+#define FTS_REQ_RAMP 8
+#endif
+  size_t ch = std::max<size_t>(CH / FTS_REQ_RAMP, 1), r0 = 0;
+  auto make = [&]() {
+    std::unique_ptr<Chunk> c(new Chunk());
+    c->r0 = r0;
+    c->r1 = std::min(n, r0 + ch);
+    r0 = c->r1;
+    ch = std::min(CH, 2 * ch);
+    return c;
+  };
+  for (; r0 < n && rc == FTZ_SUCCESS;) {
     StageClock clk{h.stats};
     while (fly.size() >= IN) {  // bound the memory held by chunks in flight
       rc = finish_chunk(*fly.front(), codes, failed, err);
@@ -650,11 +679,9 @@ int verify_token_requests(size_t n, const ftz_bytes* reqs, const RequestHooks& h
     }
     clk.mark(&RequestStats::drain);
     if (rc != FTZ_SUCCESS) break;
-    fly.emplace_back(new Chunk());
-    Chunk& c = *fly.back();
-    c.r0 = r0;
-    c.r1 = std::min(n, r0 + CH);
-    rc = prepare_chunk(reqs, h, c, err);
+    fly.push_back(make());
+    rc = decode_chunk(reqs, h, *fly.back(), h.stats, err);
+    if (rc == FTZ_SUCCESS) rc = ledger_chunk(h, *fly.back(), err);
   }
   // drain (also after an error: every helper thread is joined before returning)
   StageClock clk{h.stats};

@@ -39,13 +39,17 @@ int verify_requests(ftz_ctx* ctx, size_t n, const ftz_bytes* reqs, ftz_get_state
   WorkPool* pool;
   {
     std::lock_guard<std::mutex> lk(ctx->req_mu);
-    if (!ctx->req_pool) ctx->req_pool = new WorkPool((int)std::max<uint32_t>(4, ctx->opt.threads));
+    if (!ctx->req_pool)
+      ctx->req_pool = new WorkPool((int)std::max<uint32_t>(
+          4, ctx->opt.request_threads ? ctx->opt.request_threads : ctx->opt.threads));
     pool = ctx->req_pool;
   }
   ftsh::RequestHooks h;
   // gnark SetBytes checks: uncompressed and infinity-flag encodings on the host
   // threads (a few field products each), compressed ones -- a square root each,
-  // rare on the wire -- in one device pass
+  // rare on the wire -- in one device pass (all of them on the device measured
+  // slower: the calling thread then waits on each chunk's check pass,
+  // profiles/r06/req_decode.txt)
   h.check = [ctx, pool](size_t m, const uint8_t* slots, uint8_t* ok) {
     std::atomic<size_t> ncomp{0};
     pool->run((m + 255) / 256, [&](size_t p) {

@@ -79,6 +79,7 @@ extern "C" int ftz_ctx_create_ex(const uint8_t* pp, size_t pp_len, int device, c
     if (o.msm_window_bits > 24) return set_err(FTZ_E_INVALID, "msm_window_bits out of range (0..24)");
     if (o.msm_glv > 1 || o.msm_precompute > 1 || o.prover_tables > 1 || o.msm_graph > 1)
       return set_err(FTZ_E_INVALID, "msm_glv / msm_precompute / prover_tables / msm_graph must be 0 or 1");
+    if (o.request_threads > 1024) return set_err(FTZ_E_INVALID, "request_threads out of range (0..1024)");
     if (o.msm_radix_bits && o.msm_radix_bits != 8 && o.msm_radix_bits != 9)
       return set_err(FTZ_E_INVALID, "msm_radix_bits must be 0, 8 or 9");
   }

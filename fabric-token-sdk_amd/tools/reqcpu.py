@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--n", type=int, default=100000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--rthreads", type=int, default=None, help="ftz_options.request_threads")
     a = ap.parse_args()
     import numpy as np
     import zkatdlog
@@ -34,7 +35,8 @@ def main():
     from zkatdlog import workload as W
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "zkatdlog_golden.json")))["pp_a"]
     i32 = ctypes.POINTER(ctypes.c_int32)
-    with zkatdlog.Context(g["pp"].encode(), device=0, threads=a.threads) as ctx:
+    opts = {} if a.rthreads is None else {"request_threads": a.rthreads}
+    with zkatdlog.Context(g["pp"].encode(), device=0, threads=a.threads, **opts) as ctx:
         valid = W.prove_distinct(ctx, 16384, tag=b"reqcpu")
         rs = W.RequestSet(valid, a.n, per=2)
         led = zkatdlog.NativeLedger(rs.ledger)

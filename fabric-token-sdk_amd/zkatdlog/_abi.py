@@ -100,7 +100,8 @@ class Options(ctypes.Structure):
                 ("msm_seg_slots", ctypes.c_uint32), ("msm_glv", ctypes.c_uint32),
                 ("msm_precompute", ctypes.c_uint32), ("prover_tables", ctypes.c_uint32),
                 ("msm_radix_bits", ctypes.c_uint32), ("first_pass", ctypes.c_uint32),
-                ("tail_split", ctypes.c_uint32), ("msm_graph", ctypes.c_uint32)]
+                ("tail_split", ctypes.c_uint32), ("msm_graph", ctypes.c_uint32),
+                ("request_threads", ctypes.c_uint32)]
 
 
 HOLD_NEVER = 0xFFFFFFFF

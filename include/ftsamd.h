@@ -142,6 +142,9 @@ typedef struct {
                            the handle's first run; 0 (default): direct launches (the
                            graph measured the same: 2^16 0.92-0.93 ms either way,
                            profiles/r06/msm_graph.txt)                                   */
+  uint32_t request_threads; /* threads decoding token requests (ftz_verify_token_requests*;
+                           0 = threads): they share the host's cores with the planning
+                           threads that feed the device                                  */
 } ftz_options;
 #define FTZ_HOLD_NEVER 0xFFFFFFFFu
 void ftz_options_default(ftz_options* opt);
