@@ -87,6 +87,27 @@ FTS_HD uint32_t msm_window_bits(uint64_t n) {
   return c;
 }
 
+// variable base with the host window combination (round 6; msmtune sweeps in
+// profiles/r06/msm_plan.txt, 2^14 .. 2^24 points): up to 2^19 virtual points
+// 13-bit windows with slots of <= 16 points and 4-slot segments (2^17 points:
+// 0.77 ms against 1.11 at c = 16; 2^18: 1.17 against 1.37); above, the
+// round-5 rule except where it picks c = 18, whose top window of the 129-bit
+// halves keeps 3 bits (2^21 points: 4.21 ms at 17 against 5.37 at 18; 2^22:
+// 7.67 at 19 against 9.13).
+static constexpr uint32_t MSM_SMALL_LG = 19;
+FTS_HD uint32_t msm_lg(uint64_t n) {
+  uint32_t lg = 0;
+  while ((1ull << (lg + 1)) <= n) lg++;
+  return lg;
+}
+FTS_HD uint32_t msm_window_bits_var(uint64_t nv) {
+  const uint32_t lg = msm_lg(nv);
+  if (lg <= MSM_SMALL_LG) return 13;
+  if (lg == 22) return 17;
+  if (lg == 23) return 19;
+  return msm_window_bits(nv);
+}
+
 // resident-point mode: the bucket reduction runs once (not per window), and
 // the sort keys are c - 1 bits.  Up to 2^22 virtual points the variable-base
 // width (<= 17: keys of <= 16 bits, two radix passes); above, the bucket
@@ -109,7 +130,8 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   p.n = (uint32_t)n;
   p.glv = glv ? 1 : 0;
   p.nv = glv ? 2 * p.n : p.n;
-  p.c = c ? c : (pre ? msm_window_bits_pre(p.nv, glv) : msm_window_bits(p.nv));
+  p.c = c ? c : (pre ? msm_window_bits_pre(p.nv, glv) : msm_window_bits_var(p.nv));
+  const bool small = !pre && msm_lg(p.nv) <= MSM_SMALL_LG;
   uint32_t bits = glv ? 129 : 255;  // magnitude bits + 1 for the signed-digit carry
   p.windows = (bits + p.c - 1) / p.c;
   p.buckets = 1u << (p.c - 1);
@@ -120,6 +142,7 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
   p.nv_magic = (1ull << 32) / p.nv + 1;
   // the default cap keeps the per-window mean (about as many bucket lanes per
   // point as without pre)
+  if (!slot_cap && small) slot_cap = 16;
   if (!slot_cap) {
     uint64_t mean = (p.nv + p.buckets - 1) / p.buckets;
     slot_cap = (uint32_t)(2 * mean < 4 ? 4 : 2 * mean);
@@ -135,6 +158,7 @@ inline MsmPlan msm_make_plan(uint64_t n, uint32_t c = 0, uint32_t slot_cap = 0, 
     seg_len = 4;
     while (seg_len < 64 && p.max_slots / seg_len > 24576) seg_len *= 2;
   }
+  if (!seg_len && small) seg_len = 4;
   if (!seg_len) {
     uint64_t tot = (uint64_t)p.rw * p.max_slots;
     seg_len = 4;

@@ -79,12 +79,19 @@ def test_emu_pre_identity_points(emu):
     assert emu_msm(emu, pts, [0] * len(pts), 5, 2, 2, 1, 1) == C.g1_bytes(None)
 
 
+def window_bits_var(nv):
+    """dev/msm.h msm_window_bits_var: the variable-base planner's window bits for
+    nv virtual points (GLV: 2n) -- 13 up to 2^19, then floor(log2 nv / 2) + 7
+    clamped to [8, 20] except 17 at 2^22 and 19 at 2^23 (round-6 sweeps)."""
+    lg = nv.bit_length() - 1
+    if lg <= 19:
+        return 13
+    return {22: 17, 23: 19}.get(lg, min(20, max(8, lg // 2 + 7)))
+
+
 def test_window_plan():
-    # msm_window_bits: floor(log2(virtual points) / 2) + 7 clamped to [8, 20] (dev/msm.h); GLV doubles the points
-    def bits(n):
-        lg = n.bit_length() - 1
-        return min(20, max(8, lg // 2 + 7))
-    assert [bits(2 << k) for k in (10, 16, 20, 24, 28)] == [12, 15, 17, 19, 21 if False else 20]
+    assert [window_bits_var(2 << k) for k in (10, 16, 18, 19, 20, 21, 22, 23, 28)] == \
+        [13, 13, 13, 17, 17, 17, 19, 19, 20]
 
 
 @pytest.fixture(scope="module")
@@ -217,7 +224,7 @@ def test_gpu_msm_known_logs(ctx, lg, bits):
     want = C.g1_mul(C.G1_GEN, sum(k * (i + off) for i, k in enumerate(ks)) % C.R)
     assert got == C.g1_bytes(want)
     assert again == got
-    assert info["window_bits"] == (lg + 1) // 2 + 7 and info["last_ms"] > 0
+    assert info["window_bits"] == window_bits_var(2 << lg) and info["last_ms"] > 0
 
 
 @pytest.mark.gpu
