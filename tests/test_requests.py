@@ -135,13 +135,28 @@ def gctx(fx):
     c.close()
 
 
+def pipeline_chunks(n, ch=4096, ramp=8):
+    """chunks of host/request.cpp verify_token_requests: ch/8, ch/4, ch/2, then ch"""
+    k, c = 0, max(ch // ramp, 1)
+    while n > 0:
+        n -= c
+        k += 1
+        c = min(ch, 2 * c)
+    return k
+
+
+def test_pipeline_chunks():
+    assert [pipeline_chunks(n) for n in (0, 1, 512, 513, 3584, 3585, 20043)] == [0, 1, 1, 2, 3, 4, 8]
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("batched", [False, True])
 def test_gpu_requests_native_ledger_tiled(gctx, fx, batched):
     """ftz_verify_token_requests(_batched) with a native ledger callback over the
     fixture tiled past several 8192-request pipeline chunks: every verdict and
     failing index at its position, and every key looked up on the calling
-    thread (one callback per 4096-request chunk when batched)"""
+    thread (one callback per pipeline chunk when batched: 512, 1024, 2048, then
+    4096 requests)"""
     import zkatdlog
     rq = fx["requests"] * (20000 // len(fx["requests"]) + 1)
     led = zkatdlog.NativeLedger(fx["ledger_b"])
@@ -152,7 +167,7 @@ def test_gpu_requests_native_ledger_tiled(gctx, fx, batched):
         led.close()
     assert list(zip(codes, failed)) == [(r["expect"], r["failed_action"]) for r in rq]
     if batched:
-        assert calls <= (len(rq) + 4095) // 4096
+        assert calls <= pipeline_chunks(len(rq))
     else:
         assert calls == keys
 
