@@ -91,8 +91,14 @@ struct RequestHooks {
   void* user = nullptr;
   // parallel for over [0, k) (decoding); unset: serial on the calling thread
   std::function<void(size_t k, const std::function<void(size_t)>& f)> par;
-  size_t chunk = 4096;  // requests decoded per pipeline step
-  size_t inflight = 8;  // chunks whose ZK verification may be in flight at once
+#ifndef FTS_REQ_CHUNK
+#define FTS_REQ_CHUNK 4096
+#endif
+#ifndef FTS_REQ_INFLIGHT
+#define FTS_REQ_INFLIGHT 8
+#endif
+  size_t chunk = FTS_REQ_CHUNK;        // requests decoded per pipeline step
+  size_t inflight = FTS_REQ_INFLIGHT;  // chunks whose ZK verification may be in flight at once
   RequestStats* stats = nullptr;
 };
 
