@@ -45,24 +45,51 @@ __global__ void __launch_bounds__(256) k_msm_load_scal(uint32_t n, const uint8_t
   fe_to_int(scal[i], fe_from_int<ModR>(k));
 }
 
-// one lane per point: sort keys + values of every window (dev/msm.h msm_job_keys)
+// point i's entries (every window, both GLV halves) counted into their
+// (window, bucket) group: the counting sort of small plans (msm_rt.hip)
+__device__ __forceinline__ void msm_count_point(const MsmPlan& p, uint32_t i, const uint32_t* key, uint32_t* cnt) {
+  const uint32_t halves = p.glv ? 2u : 1u;
+  for (uint32_t w = 0; w < p.windows; w++)
+    for (uint32_t h = 0; h < halves; h++) atomicAdd(&cnt[w * p.buckets + key[(size_t)w * p.nv + i + h * p.n]], 1u);
+}
+
+// one lane per point: sort keys + values of every window (dev/msm.h
+// msm_job_keys); cnt != nullptr: also the group counts
 __global__ void __launch_bounds__(256) k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key,
-                                                  uint32_t* val) {
+                                                  uint32_t* val, uint32_t* cnt) {
   LANE_PROLOGUE(p.n);
   msm_job_keys(p, i, scal, key, val);
+  if (cnt) msm_count_point(p, i, key, cnt);
+}
+
+// counting sort, second half: entry t of group g lands at start[g] + its rank
+// among the group's entries (an atomic decrement of the count: any order in a
+// bucket gives the same sum); one lane per point, every window
+__global__ void __launch_bounds__(256) k_msm_scatter(MsmPlan p, const uint32_t* key, const uint32_t* val,
+                                                     const uint32_t* start, uint32_t* cnt, uint32_t* perm) {
+  LANE_PROLOGUE(p.n);
+  const uint32_t halves = p.glv ? 2u : 1u;
+  for (uint32_t w = 0; w < p.windows; w++)
+    for (uint32_t h = 0; h < halves; h++) {
+      const size_t t = (size_t)w * p.nv + i + h * p.n;
+      const uint32_t g = w * p.buckets + key[t];
+      perm[start[g] + atomicSub(&cnt[g], 1u) - 1u] = val[t];
+    }
 }
 
 // the same from 32-byte big-endian scalars in HBM for points [i0, i1) (the
 // chunk a host copy has delivered): reduce mod r, keep the limbs for later runs,
 // and write the sort keys -- k_msm_load_scal and k_msm_keys in one pass
 __global__ void __launch_bounds__(256) k_msm_keys_raw(MsmPlan p, uint32_t i0, uint32_t i1, const uint8_t* raw,
-                                                      uint32_t (*scal)[8], uint32_t* key, uint32_t* val) {
+                                                      uint32_t (*scal)[8], uint32_t* key, uint32_t* val,
+                                                      uint32_t* cnt) {
   uint32_t i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= i1) return;
   uint32_t k[8];
   be32_to_limbs_g(k, raw + 32 * (size_t)i);
   fe_to_int(scal[i], fe_from_int<ModR>(k));
   msm_job_keys(p, i, scal, key, val);
+  if (cnt) msm_count_point(p, i, key, cnt);
 }
 
 // one lane per sorted entry: bucket ranges
@@ -73,11 +100,12 @@ __global__ void __launch_bounds__(256) k_msm_bounds(MsmPlan p, uint64_t total, c
   msm_job_bounds(p, t, total, skey, sval, start, end);
 }
 
-// count[g] = end[g] - start[g] and the bucket's slot count
+// count[g] = end[g] - start[g] (start = nullptr: end holds the counts) and the
+// bucket's slot count
 __global__ void __launch_bounds__(256) k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end,
                                                     uint32_t* count, uint32_t* m) {
   LANE_PROLOGUE(p.rw * p.buckets);
-  uint32_t c = end[i] - start[i];
+  uint32_t c = start ? end[i] - start[i] : end[i];
   count[i] = c;
   m[i] = msm_bucket_slots(p, c);
 }

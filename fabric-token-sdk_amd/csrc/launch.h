@@ -146,9 +146,11 @@ __global__ void k_msm_load_pts(uint32_t n, const uint8_t* raw_pts, G1Dev* pts, u
 __global__ void k_g1_sum(uint32_t n, const uint8_t* raw, uint8_t* out, uint32_t* status);
 __global__ void k_g1_check(uint32_t n, const uint8_t* slots, uint8_t* ok);
 __global__ void k_msm_load_scal(uint32_t n, const uint8_t* raw_scal, uint32_t (*scal)[8]);
-__global__ void k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val);
+__global__ void k_msm_keys(MsmPlan p, const uint32_t (*scal)[8], uint32_t* key, uint32_t* val, uint32_t* cnt);
+__global__ void k_msm_scatter(MsmPlan p, const uint32_t* key, const uint32_t* val, const uint32_t* start,
+                              uint32_t* cnt, uint32_t* perm);
 __global__ void k_msm_keys_raw(MsmPlan p, uint32_t i0, uint32_t i1, const uint8_t* raw, uint32_t (*scal)[8],
-                               uint32_t* key, uint32_t* val);
+                               uint32_t* key, uint32_t* val, uint32_t* cnt);
 __global__ void k_msm_bounds(MsmPlan p, uint64_t total, const uint32_t* skey, const uint32_t* sval, uint32_t* start,
                              uint32_t* end);
 __global__ void k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end, uint32_t* count, uint32_t* m);

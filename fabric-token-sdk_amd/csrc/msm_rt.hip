@@ -40,6 +40,15 @@ struct ftz_msm {
   hipGraphExec_t graph_exec = nullptr;
   int graph_state = 0;
   uint32_t radix_bits = 8;  // digit bits per radix-sort pass (8: rocPRIM's gfx950 default; 9: Radix9)
+  // FTS_MSM_CSORT=1, small plans (dev/msm.h MSM_SMALL_LG): a counting sort
+  // instead of rocPRIM's radix sort -- the keys kernel counts each (window,
+  // bucket) group with an atomic, a scan gives the group starts, one scatter
+  // places the values by returning atomics (end[] holds the counts).  It
+  // saves ~9 of the radix sort's and bounds pass's ~5 us dependent launches
+  // but measured slower from 2^16 points up (2^16 0.71 against 0.61-0.64 ms,
+  // 2^18 1.66 against 1.16-1.19: the scatter's 1.3M returning atomics take
+  // 95 us), faster only at 2^14 (0.51 against 0.56), profiles/r06/msm_csort.txt
+  bool csort = false;
 };
 
 static int blocks(uint64_t n, int bs) { return (int)((n + bs - 1) / bs); }
@@ -73,6 +82,10 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->start.alloc(wb));
   HC(m->end.alloc(wb));
   m->key_bits = msm_key_bits(p);
+#ifndef FTS_MSM_CSORT
+#define FTS_MSM_CSORT 0
+#endif
+  m->csort = FTS_MSM_CSORT && !p.pre && msm_lg(p.nv) <= MSM_SMALL_LG;
   // 9-bit digits where they save a pass (17-18 bits: two passes instead of three)
   if (p.rw > 32) return set_err(FTZ_E_INVALID, "MSM plan has more than 32 windows");
   const uint32_t rb = m->ctx->opt.msm_radix_bits;
@@ -248,14 +261,23 @@ static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
   const MsmPlan& p = m->p;
   size_t wb = (size_t)p.rw * p.buckets;
   size_t wn = (size_t)p.windows * p.nv;
-  // (window, bucket)-sorted point lists: stable radix sort, bucket ranges
-  size_t tb = m->sort_tmp_bytes;
-  HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
-  HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
-  HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
-  k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start.p, m->end.p);
-  k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start.p, m->end.p, m->count.p, m->nsl.p);
-  int rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
+  int rc;
+  if (m->csort) {
+    // counting sort: end[] = the group counts from the keys kernel
+    rc = scan(m->end.p, m->start.p, wb, m->tot.p, s);
+    if (rc != FTZ_SUCCESS) return rc;
+    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, nullptr, m->end.p, m->count.p, m->nsl.p);
+    k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->val.p, m->start.p, m->end.p, m->perm.p);
+  } else {
+    // (window, bucket)-sorted point lists: stable radix sort, bucket ranges
+    size_t tb = m->sort_tmp_bytes;
+    HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
+    HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
+    HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
+    k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start.p, m->end.p);
+    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start.p, m->end.p, m->count.p, m->nsl.p);
+  }
+  rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
   // bucket slots in length order, then one lane per slot
@@ -343,7 +365,8 @@ static int msm_finish(ftz_msm* m, uint8_t out[64]) {
 static int msm_enqueue_all(ftz_msm* m, hipStream_t s) {
   const MsmPlan& p = m->p;
   const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
-  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p);
+  if (m->csort) HC(hipMemsetAsync(m->end.p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
+  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p, m->csort ? m->end.p : nullptr);
   return msm_enqueue_tail(m, s);
 }
 
@@ -412,6 +435,7 @@ extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t o
   HC(hipStreamWaitEvent(m->cstream, m->cev[ftz_msm::RAW_CHUNKS], 0));
   HC(hipEventRecord(m->ev[0], m->cstream));
   uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(m->scal.p);
+  if (m->csort) HC(hipMemsetAsync(m->end.p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
   const uint32_t per = (p.n + ftz_msm::RAW_CHUNKS - 1) / ftz_msm::RAW_CHUNKS;
   for (int k = 0; k < ftz_msm::RAW_CHUNKS; k++) {
     uint32_t i0 = k * per, i1 = std::min<uint32_t>(p.n, i0 + per);
@@ -420,7 +444,8 @@ extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t o
                       hipMemcpyHostToDevice, m->cstream));
     HC(hipEventRecord(m->cev[k], m->cstream));
     HC(hipStreamWaitEvent(s, m->cev[k], 0));
-    k_msm_keys_raw<<<blocks(i1 - i0, 256), 256, 0, s>>>(p, i0, i1, m->raw.p, scal, m->key.p, m->val.p);
+    k_msm_keys_raw<<<blocks(i1 - i0, 256), 256, 0, s>>>(p, i0, i1, m->raw.p, scal, m->key.p, m->val.p,
+                                                        m->csort ? m->end.p : nullptr);
   }
   int rc = msm_enqueue_tail(m, s);
   if (rc != FTZ_SUCCESS) return rc;
