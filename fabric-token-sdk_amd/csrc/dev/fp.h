@@ -496,7 +496,11 @@ FTS_HD fp fp_inv(const fp& a) { return fe_pow<ModP>(a, P_MINUS_2); }
 // halvings and ~log2 p subtractions of 8-limb integers, about 5x fewer
 // instructions than the Fermat chain.  For latency-bound single-lane code on
 // public values only (MSM Horner); the data-dependent loop diverges in a wave.
-FTS_HD fp fp_inv_var(const fp& am) {
+}  // namespace fts
+#include "safegcd.h"
+namespace fts {
+
+FTS_HD fp fp_inv_eea(const fp& am) {
   if (fe_is_zero(am)) return am;
   uint32_t u[8], v[8], x1[8], x2[8], pm[8], t[8];
 #pragma unroll
@@ -538,6 +542,22 @@ FTS_HD fp fp_inv_var(const fp& am) {
   for (int i = 0; i < 8; i++) x.v[i] = from_u ? x1[i] : x2[i];
   fp r2 = fe_const<ModP>(P_R2);
   return (x * r2) * r2;
+}
+// the same inverse by Bernstein-Yang divsteps (dev/safegcd.h; checked against
+// fp_inv_eea on the device and the host); FTS_INV_EEA = 1 keeps the Euclid
+#ifndef FTS_INV_EEA
+#define FTS_INV_EEA 0
+#endif
+FTS_HD fp fp_inv_var(const fp& am) {
+#if FTS_INV_EEA
+  return fp_inv_eea(am);
+#else
+  if (fe_is_zero(am)) return am;
+  fp x;
+  sg_inv_int(am.v, x.v);  // (a R)^-1 as a plain integer; the Montgomery form of a^-1 is x R^2
+  fp r2 = fe_const<ModP>(P_R2);
+  return (x * r2) * r2;
+#endif
 }
 FTS_HD fr fr_inv(const fr& a) { return fe_pow<ModR>(a, R_MINUS_2); }
 

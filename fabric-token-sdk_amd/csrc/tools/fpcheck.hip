@@ -259,3 +259,70 @@ extern "C" long ftz_rowbench(int device, int impl, int n) {
   (void)hipFree(cyc);
   return e == hipSuccess ? (long)c : -1;
 }
+
+// ---- dev/safegcd.h (fp_inv_var) against the binary Euclid (fp_inv_eea): one
+// random Montgomery element per lane plus the edge values 1, 2, p - 1 in the
+// first lanes; inverse * value must also be one.  Returns the mismatches.
+__global__ void __launch_bounds__(256) k_invcheck(uint32_t seed, uint32_t* bad) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  uint32_t s = seed ^ (j + 1) * 2654435761u;
+  if (!s) s = 1;
+  fp v = rnd_fe<ModP>(s);
+  if (j < 3) {
+    uint32_t k[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (j < 2) {
+      k[0] = j + 1;
+    } else {
+      for (int i = 0; i < 8; i++) k[i] = P_MOD[i];
+      k[0] -= 1;
+    }
+    v = fe_from_int<ModP>(k);
+  }
+  const fp a = fp_inv_var(v), b = fp_inv_eea(v);
+  if (!fe_eq(a, b) || !fe_eq(a * v, fe_one<ModP>())) atomicAdd(bad, 1u);
+}
+
+extern "C" int ftz_invcheck(int device, uint32_t blocks, uint32_t seed) {
+  if (hipSetDevice(device) != hipSuccess || blocks == 0) return -1;
+  uint32_t* bad = nullptr;
+  int rc = -1;
+  if (hipMalloc(&bad, 4) == hipSuccess && hipMemset(bad, 0, 4) == hipSuccess) {
+    k_invcheck<<<blocks, 256>>>(seed, bad);
+    uint32_t h = 0;
+    if (hipMemcpy(&h, bad, 4, hipMemcpyDeviceToHost) == hipSuccess) rc = (int)h;
+  }
+  (void)hipFree(bad);
+  return rc;
+}
+
+// one lane, a chain of n dependent inversions: safegcd (impl 1) or the binary
+// Euclid (impl 0); returns GPU clock cycles per inversion
+__global__ void __launch_bounds__(64) k_invbench(int impl, int n, fp* io, uint64_t* cyc) {
+  if (threadIdx.x != 0) return;
+  fp a = io[0];
+  const fp one = fe_one<ModP>();
+  const uint64_t t0 = __builtin_readcyclecounter();
+  for (int k = 0; k < n; k++) a = (impl == 1 ? fp_inv_var(a) : fp_inv_eea(a)) + one;
+  const uint64_t t1 = __builtin_readcyclecounter();
+  io[1] = a;
+  *cyc = (t1 - t0) / (uint64_t)n;
+}
+
+extern "C" long ftz_invbench(int device, int impl, int n) {
+  if (hipSetDevice(device) != hipSuccess) return -1;
+  fp* io;
+  uint64_t* cyc;
+  if (hipMalloc(&io, 2 * sizeof(fp)) != hipSuccess || hipMalloc(&cyc, 8) != hipSuccess) return -1;
+  uint32_t s = 12345;
+  fp h[2];
+  for (int i = 0; i < 8; i++) h[0].v[i] = 0;
+  h[0].v[0] = 7;
+  (void)s;
+  (void)hipMemcpy(io, h, sizeof h, hipMemcpyHostToDevice);
+  k_invbench<<<1, 64>>>(impl, n, io, cyc);
+  uint64_t c = 0;
+  hipError_t e = hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+  (void)hipFree(io);
+  (void)hipFree(cyc);
+  return e == hipSuccess ? (long)c : -1;
+}

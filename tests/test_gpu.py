@@ -185,3 +185,15 @@ def test_row29_device_check():
     out = (ctypes.c_uint32 * 3)()
     lib.ftz_rowcheck.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
     assert lib.ftz_rowcheck(0, 777, out) == 0, list(out)
+
+
+def test_safegcd_inverse_device_check():
+    """dev/safegcd.h (fp_inv_var: Bernstein-Yang divsteps) against the binary
+    Euclid fp_inv_eea on the device: 262,144 random Montgomery elements plus
+    1, 2 and p - 1, each inverse equal and times its value one"""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                   "fabric-token-sdk_amd", "zkatdlog", "_lib", "libftsfpcheck.so"))
+    lib.ftz_invcheck.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32]
+    assert lib.ftz_invcheck(0, 1024, 4242) == 0
