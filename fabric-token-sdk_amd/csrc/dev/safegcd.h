@@ -11,8 +11,10 @@
 // k_g1_combine end in ONE inversion run by one lane, on the latency path of
 // every pass; the 8 x 32-bit binary Euclid (fp_inv_eea) issues ~40k dependent
 // instructions there.  Here ~10 rounds of 62 divsteps on 64-bit words plus a
-// 2x2 matrix applied to 5-limb numbers.  tools/fpcheck.hip (ftz_invcheck)
-// and tests/native (emu_inv_check) compare it with fp_inv_eea.
+// 2x2 matrix applied to 5-limb numbers.  tools/fpcheck.hip (ftz_invcheck,
+// tests/test_gpu.py) compares it with fp_inv_eea on 262k values on the device;
+// the host build runs it in every host-emulated job that normalises a point
+// (tests/native, against the oracle's bytes).
 #pragma once
 // (included by fp.h, after its FTS_HD definitions)
 #include <stdint.h>

@@ -203,6 +203,9 @@ void Engine::dispatcher() {
     // kernel chain have a fixed latency that small passes do not shed.
     const size_t fp1 = ctx->opt.first_pass, ts = ctx->opt.tail_split;
     size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
+    // (doubling passes from fp1 while few are in flight -- fp1, 2 fp1, ... --
+    // measured 0.43-0.55M against 0.76-0.80M transfers/s on the 20-step job,
+    // profiles/r06/engine_ramp.txt: the small passes' fixed latency again)
     // the queue's last pass in two halves whose kernel chains overlap
     // (ftz_options.tail_split)
     if (ts && !tail_split_done && !inflight.empty() && pending <= Bp && pending >= 2 * (size_t)ts) {
