@@ -548,15 +548,29 @@ FTS_HD fp fp_inv_eea(const fp& am) {
 #ifndef FTS_INV_EEA
 #define FTS_INV_EEA 0
 #endif
+// divsteps on 30-bit limbs (default) or 62-bit limbs (FTS_INV_SG30 = 0)
+#ifndef FTS_INV_SG30
+#define FTS_INV_SG30 1
+#endif
+template <int LIMBS>
+FTS_HD fp fp_inv_sg(const fp& am) {
+  if (fe_is_zero(am)) return am;
+  fp x;
+  // (a R)^-1 as a plain integer; the Montgomery form of a^-1 is x R^2
+  if (LIMBS == 30)
+    sg30_inv_int(am.v, x.v);
+  else
+    sg_inv_int(am.v, x.v);
+  fp r2 = fe_const<ModP>(P_R2);
+  return (x * r2) * r2;
+}
 FTS_HD fp fp_inv_var(const fp& am) {
 #if FTS_INV_EEA
   return fp_inv_eea(am);
+#elif FTS_INV_SG30
+  return fp_inv_sg<30>(am);
 #else
-  if (fe_is_zero(am)) return am;
-  fp x;
-  sg_inv_int(am.v, x.v);  // (a R)^-1 as a plain integer; the Montgomery form of a^-1 is x R^2
-  fp r2 = fe_const<ModP>(P_R2);
-  return (x * r2) * r2;
+  return fp_inv_sg<62>(am);
 #endif
 }
 FTS_HD fr fr_inv(const fr& a) { return fe_pow<ModR>(a, R_MINUS_2); }

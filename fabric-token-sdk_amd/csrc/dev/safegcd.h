@@ -229,4 +229,199 @@ FTS_HD void sg_inv_int(const uint32_t x[8], uint32_t out[8]) {
   }
 }
 
+
+// ---- the same with 30-bit limbs and 30-divstep batches (libsecp256k1's
+// modinv32 layout): every product is 32 x 32 -> 64 bits (v_mad_i64_i32) and the
+// divstep loop runs on 32-bit words, where the 62-bit form spends two VALU
+// instructions on every 64-bit operation and emulates its 128-bit products.
+struct Sg30 {
+  int32_t v[9];
+};
+struct SgTrans30 {
+  int32_t u, v, q, r;
+};
+static constexpr uint32_t SG_M30 = 0x3FFFFFFFu;
+FTS_HD Sg30 sg30_modulus() {
+  return {{0x187cfd47, 0x3082305b, 0x71ca8d3, 0x205aa45a, 0x1585d97, 0x116da06, 0x1a029b85, 0x139cb84c, 0x3064}};
+}
+static constexpr uint32_t SG_P_INV30 = 0x1b799c77u;
+
+FTS_HD int32_t sg_divsteps_30_var(int32_t eta, uint32_t f0, uint32_t g0, SgTrans30& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  uint32_t f = f0, g = g0, m, w;
+  int i = 30, limit, zeros;
+  for (;;) {
+    zeros = (int)__builtin_ctz(g | (~0u << i));  // a sentinel bit: at most i zeros
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    if (eta < 0) {
+      uint32_t tmp;
+      eta = -eta;
+      tmp = f;
+      f = g;
+      g = 0u - tmp;
+      tmp = u;
+      u = q;
+      q = 0u - tmp;
+      tmp = v;
+      v = r;
+      r = 0u - tmp;
+      limit = (eta + 1) > i ? i : (eta + 1);
+      m = (~0u >> (32 - limit)) & 63u;
+      w = (f * g * (f * f - 2)) & m;
+    } else {
+      limit = (eta + 1) > i ? i : (eta + 1);
+      m = (~0u >> (32 - limit)) & 15u;
+      w = f + (((f + 1) & 4) << 1);
+      w = (0u - w * g) & m;
+    }
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+
+FTS_HD void sg30_update_de(Sg30& d, Sg30& e, const SgTrans30& t) {
+  const Sg30 P = sg30_modulus();
+  const int32_t u = t.u, v = t.v, q = t.q, r = t.r;
+  const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+  int32_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
+  int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0];
+  int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0];
+  md -= (int32_t)((SG_P_INV30 * (uint32_t)cd + (uint32_t)md) & SG_M30);
+  me -= (int32_t)((SG_P_INV30 * (uint32_t)ce + (uint32_t)me) & SG_M30);
+  cd += (int64_t)P.v[0] * md;
+  ce += (int64_t)P.v[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    cd += (int64_t)u * d.v[k] + (int64_t)v * e.v[k] + (int64_t)P.v[k] * md;
+    ce += (int64_t)q * d.v[k] + (int64_t)r * e.v[k] + (int64_t)P.v[k] * me;
+    d.v[k - 1] = (int32_t)((uint32_t)cd & SG_M30);
+    e.v[k - 1] = (int32_t)((uint32_t)ce & SG_M30);
+    cd >>= 30;
+    ce >>= 30;
+  }
+  d.v[8] = (int32_t)cd;
+  e.v[8] = (int32_t)ce;
+}
+
+FTS_HD void sg30_update_fg(int len, Sg30& f, Sg30& g, const SgTrans30& t) {
+  const int32_t u = t.u, v = t.v, q = t.q, r = t.r;
+  int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
+  int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int k = 1; k < 9; k++) {
+    if (k < len) {
+      cf += (int64_t)u * f.v[k] + (int64_t)v * g.v[k];
+      cg += (int64_t)q * f.v[k] + (int64_t)r * g.v[k];
+      f.v[k - 1] = (int32_t)((uint32_t)cf & SG_M30);
+      g.v[k - 1] = (int32_t)((uint32_t)cg & SG_M30);
+      cf >>= 30;
+      cg >>= 30;
+    }
+  }
+#pragma unroll
+  for (int k = 1; k <= 9; k++)
+    if (k == len) {
+      f.v[k - 1] = (int32_t)cf;
+      g.v[k - 1] = (int32_t)cg;
+    }
+}
+
+FTS_HD void sg30_normalize(Sg30& r, int32_t sign) {
+  const Sg30 P = sg30_modulus();
+  int32_t c = r.v[8] >> 31;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.v[k] += P.v[k] & c;
+  const int32_t neg = sign >> 31;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.v[k] = (r.v[k] ^ neg) - neg;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    r.v[k + 1] += r.v[k] >> 30;
+    r.v[k] &= (int32_t)SG_M30;
+  }
+  c = r.v[8] >> 31;
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.v[k] += P.v[k] & c;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    r.v[k + 1] += r.v[k] >> 30;
+    r.v[k] &= (int32_t)SG_M30;
+  }
+}
+
+FTS_HD void sg30_inv_int(const uint32_t x[8], uint32_t out[8]) {
+  Sg30 g;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const int b = 30 * k, l = b >> 5, o = b & 31;
+    uint64_t lo = l < 8 ? x[l] : 0u, hi = l + 1 < 8 ? x[l + 1] : 0u;
+    g.v[k] = (int32_t)((uint32_t)(((hi << 32) | lo) >> o) & SG_M30);
+  }
+  Sg30 f = sg30_modulus(), d = {{0, 0, 0, 0, 0, 0, 0, 0, 0}}, e = {{1, 0, 0, 0, 0, 0, 0, 0, 0}};
+  int32_t eta = -1;
+  int len = 9;
+  for (;;) {
+    SgTrans30 t;
+    eta = sg_divsteps_30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    sg30_update_de(d, e, t);
+    sg30_update_fg(len, f, g, t);
+    if (g.v[0] == 0) {
+      int32_t cond = 0;
+#pragma unroll
+      for (int k = 1; k < 9; k++)
+        if (k < len) cond |= g.v[k];
+      if (cond == 0) break;
+    }
+    int32_t fn = 0, gn = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++)
+      if (k == len - 1) {
+        fn = f.v[k];
+        gn = g.v[k];
+      }
+    int32_t cond = ((int32_t)len - 2) >> 31;
+    cond |= fn ^ (fn >> 31);
+    cond |= gn ^ (gn >> 31);
+    if (cond == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; k++)
+        if (k == len - 2) {
+          f.v[k] |= (int32_t)((uint32_t)fn << 30);
+          g.v[k] |= (int32_t)((uint32_t)gn << 30);
+        }
+      --len;
+    }
+  }
+  int32_t fs = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++)
+    if (k == len - 1) fs = f.v[k];
+  sg30_normalize(d, fs);
+  // 9 x 30-bit limbs (the top one < 2^14 for d < p) -> 8 x 32
+#pragma unroll
+  for (int k = 0; k < 8; k++) out[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    const int b = 30 * k, l = b >> 5, o = b & 31;
+    const uint64_t w = (uint64_t)(uint32_t)d.v[k] << o;
+    out[l] |= (uint32_t)w;
+    if (l + 1 < 8) out[l + 1] |= (uint32_t)(w >> 32);
+  }
+}
+
 }  // namespace fts

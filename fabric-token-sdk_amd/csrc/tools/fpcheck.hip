@@ -278,8 +278,9 @@ __global__ void __launch_bounds__(256) k_invcheck(uint32_t seed, uint32_t* bad) 
     }
     v = fe_from_int<ModP>(k);
   }
-  const fp a = fp_inv_var(v), b = fp_inv_eea(v);
-  if (!fe_eq(a, b) || !fe_eq(a * v, fe_one<ModP>())) atomicAdd(bad, 1u);
+  const fp a = fp_inv_sg<30>(v), a2 = fp_inv_sg<62>(v), b = fp_inv_eea(v);
+  if (!fe_eq(a, b) || !fe_eq(a2, b) || !fe_eq(a * v, fe_one<ModP>()) || !fe_eq(fp_inv_var(v), b))
+    atomicAdd(bad, 1u);
 }
 
 extern "C" int ftz_invcheck(int device, uint32_t blocks, uint32_t seed) {
@@ -295,14 +296,16 @@ extern "C" int ftz_invcheck(int device, uint32_t blocks, uint32_t seed) {
   return rc;
 }
 
-// one lane, a chain of n dependent inversions: safegcd (impl 1) or the binary
-// Euclid (impl 0); returns GPU clock cycles per inversion
+// one lane, a chain of n dependent inversions: divsteps on 30-bit limbs (impl
+// 2), on 62-bit limbs (impl 1) or the binary Euclid (impl 0); returns GPU clock
+// cycles per inversion
 __global__ void __launch_bounds__(64) k_invbench(int impl, int n, fp* io, uint64_t* cyc) {
   if (threadIdx.x != 0) return;
   fp a = io[0];
   const fp one = fe_one<ModP>();
   const uint64_t t0 = __builtin_readcyclecounter();
-  for (int k = 0; k < n; k++) a = (impl == 1 ? fp_inv_var(a) : fp_inv_eea(a)) + one;
+  for (int k = 0; k < n; k++)
+    a = (impl == 2 ? fp_inv_sg<30>(a) : impl == 1 ? fp_inv_sg<62>(a) : fp_inv_eea(a)) + one;
   const uint64_t t1 = __builtin_readcyclecounter();
   io[1] = a;
   *cyc = (t1 - t0) / (uint64_t)n;
