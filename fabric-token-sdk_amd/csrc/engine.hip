@@ -71,6 +71,7 @@ struct Engine {
   size_t pending = 0;        // proofs queued and not yet handed to a batch (under mu)
   bool disp_holding = false;  // the dispatcher is waiting out a window (under mu)
   bool tail_split_done = false;  // the queue's last pass was cut in two (under mu; reset by new requests)
+  uint32_t ramp_step = 0;        // passes since the engine was last idle (FTS_ENGINE_RAMP2)
   std::vector<ftz_batch*> slots;
   std::deque<ftz_batch*> free_slots, inflight;
   ftz_engine_stats st{};
@@ -202,10 +203,22 @@ void Engine::dispatcher() {
     // slower (round 2: 420-442k vs 676-688k transfers/s): a pass's planning and
     // kernel chain have a fixed latency that small passes do not shed.
     const size_t fp1 = ctx->opt.first_pass, ts = ctx->opt.tail_split;
+#ifndef FTS_ENGINE_RAMP2
+#define FTS_ENGINE_RAMP2 0
+#endif
     size_t Bp = (fp1 && fp1 < B && inflight.empty()) ? fp1 : B;
     // (doubling passes from fp1 while few are in flight -- fp1, 2 fp1, ... --
     // measured 0.43-0.55M against 0.76-0.80M transfers/s on the 20-step job,
     // profiles/r06/engine_ramp.txt: the small passes' fixed latency again)
+    // FTS_ENGINE_RAMP2: doubling from fp1 only for the passes that follow an
+    // idle engine (fp1, 2 fp1, ... up to B, then B until it is idle again);
+    // with first_pass 1024 it measured within noise of the default on two
+    // boxes (means 808k against 784k, medians 815k against 803k), so it is off
+    if (FTS_ENGINE_RAMP2 && fp1 && fp1 < B) {
+      if (inflight.empty() && ramp_step > 0 && (fp1 << std::min<uint32_t>(ramp_step, 20)) >= B) ramp_step = 0;
+      Bp = std::min(B, fp1 << std::min<uint32_t>(ramp_step, 20));
+      ramp_step++;
+    }
     // the queue's last pass in two halves whose kernel chains overlap
     // (ftz_options.tail_split)
     if (ts && !tail_split_done && !inflight.empty() && pending <= Bp && pending >= 2 * (size_t)ts) {
