@@ -13,8 +13,8 @@
 // instructions there.  Here ~10 rounds of 62 divsteps on 64-bit words plus a
 // 2x2 matrix applied to 5-limb numbers.  tools/fpcheck.hip (ftz_invcheck,
 // tests/test_gpu.py) compares it with fp_inv_eea on 262k values on the device;
-// the host build runs it in every host-emulated job that normalises a point
-// (tests/native, against the oracle's bytes).
+// tests/test_safegcd.py (tests/native/sg_check.cpp) checks both limb layouts
+// against Python on the host.
 #pragma once
 // (included by fp.h, after its FTS_HD definitions)
 #include <stdint.h>
