@@ -20,8 +20,10 @@
 //   bucket    one lane per slot: Jacobian sum of its <= T points
 //   segment   one lane per run of S consecutive slots of one window: running
 //             sums give sum (b+1) S_b restricted to the run
-//   window    tree sum of the segments through LDS
-//   final     Horner over the windows, affine, gnark RawBytes
+//   window    tree sum of the segments through LDS (quad-cooperative
+//             additions) down to one part per window
+//   final     the window sums read back; Horner over the windows, affine and
+//             gnark RawBytes on the host (msm_rt.hip msm_horner_host)
 //
 // Resident-point mode (MsmPlan.pre, ftz_options.msm_precompute): the points of
 // an ftz_msm handle stay on the device across runs (ftz_msm_set_scalars swaps

@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(128) k_msm_bucket(MsmPlan p, const uint32_t* w
 }
 
 
-// ---- 4-lane cooperative point arithmetic for the serial Horner chain.  A
+// ---- 4-lane cooperative point arithmetic (the tree's additions; the serial
+// Horner chain of FTS_MSM_HOST_HORNER=0 and the quad segments).  A
 // wave issues a one-lane product at the cost of a 64-lane one, so the chain's
 // latency is the number of dependent products times one product's latency:
 // every lane holds the same point, lane k (mod 4) computes the k-th independent
@@ -602,6 +603,8 @@ __global__ void __launch_bounds__(256) k_msm_tree(const G1JDev* in, uint32_t m, 
   if (t == 0) g1j_store(out[(size_t)w * chunks + ch], j29_to(s[0]));
 }
 
+// (FTS_MSM_HOST_HORNER=0 only: the default combines the windows on the host,
+// msm_rt.hip msm_horner_host.)
 // Horner steps for reduction windows w_hi-1 down to w_lo: acc = 2^c acc + W_w,
 // on one wave with the 4-lane cooperative carry-free point ops, the Jacobian
 // result in acc_buf.  W_w arrives as `per` partial sums (wparts[w per + k], the
