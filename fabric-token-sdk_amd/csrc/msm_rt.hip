@@ -14,7 +14,12 @@ struct ftz_msm {
   ftz_ctx* ctx = nullptr;
   MsmPlan p{};
   DBuf<G1Dev> pts;
-  DBuf<uint32_t> scal, key, skey, val, perm, count, start, end, tot, nsl, soff, owner, wlo, whi, order, lenhist, lencur;
+  DBuf<uint32_t> scal, key, skey, val, perm, count, tot, nsl, soff, owner, wlo, whi, order;
+  // start[wb], end[wb] and the slot-length histogram[1024] in one buffer: one
+  // memset clears the three before the bounds pass (nothing writes the
+  // histogram before k_msm_len_hist), two dependent launches fewer per run
+  DBuf<uint32_t> zb;
+  uint32_t *start_p = nullptr, *end_p = nullptr, *lenhist_p = nullptr;
   DBuf<uint8_t> sort_tmp;
   size_t sort_tmp_bytes = 0;
   uint32_t key_bits = 0;
@@ -79,8 +84,10 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->val.alloc(wn));
   HC(m->perm.alloc(wn));
   HC(m->count.alloc(wb));
-  HC(m->start.alloc(wb));
-  HC(m->end.alloc(wb));
+  HC(m->zb.alloc(2 * wb + 1024));
+  m->start_p = m->zb.p;
+  m->end_p = m->zb.p + wb;
+  m->lenhist_p = m->zb.p + 2 * wb;
   m->key_bits = msm_key_bits(p);
 #ifndef FTS_MSM_CSORT
 #define FTS_MSM_CSORT 0
@@ -100,8 +107,6 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(m->whi.alloc(p.rw));
   HC(m->slot_sum.alloc(ws));
   HC(m->order.alloc(ws));
-  HC(m->lenhist.alloc(1024));
-  HC(m->lencur.alloc(1024));
   HC(m->part.alloc((size_t)p.rw * p.segs));
   HC(m->tree.alloc((size_t)p.rw * ((p.segs + MSM_TREE_CHUNK - 1) / MSM_TREE_CHUNK) * 2));
   HC(m->hacc.alloc(1));
@@ -264,30 +269,29 @@ static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
   int rc;
   if (m->csort) {
     // counting sort: end[] = the group counts from the keys kernel
-    rc = scan(m->end.p, m->start.p, wb, m->tot.p, s);
+    rc = scan(m->end_p, m->start_p, wb, m->tot.p, s);
     if (rc != FTZ_SUCCESS) return rc;
-    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, nullptr, m->end.p, m->count.p, m->nsl.p);
-    k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->val.p, m->start.p, m->end.p, m->perm.p);
+    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, nullptr, m->end_p, m->count.p, m->nsl.p);
+    k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->val.p, m->start_p, m->end_p, m->perm.p);
   } else {
     // (window, bucket)-sorted point lists: stable radix sort, bucket ranges
     size_t tb = m->sort_tmp_bytes;
     HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
-    HC(hipMemsetAsync(m->start.p, 0, wb * sizeof(uint32_t), s));
-    HC(hipMemsetAsync(m->end.p, 0, wb * sizeof(uint32_t), s));
-    k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start.p, m->end.p);
-    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start.p, m->end.p, m->count.p, m->nsl.p);
+    HC(hipMemsetAsync(m->zb.p, 0, (2 * wb + 1024) * sizeof(uint32_t), s));  // start, end, histogram
+    k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start_p, m->end_p);
+    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start_p, m->end_p, m->count.p, m->nsl.p);
   }
   rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
   if (rc != FTZ_SUCCESS) return rc;
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
   // bucket slots in length order, then one lane per slot
   size_t sl = (size_t)p.rw * p.max_slots;
-  HC(hipMemsetAsync(m->lenhist.p, 0, 1024 * sizeof(uint32_t), s));
-  k_msm_len_hist<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p, m->lenhist.p);
-  k_msm_len_scan<<<1, 1024, 0, s>>>(p, m->lenhist.p);
+  if (m->csort) HC(hipMemsetAsync(m->lenhist_p, 0, 1024 * sizeof(uint32_t), s));
+  k_msm_len_hist<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p, m->lenhist_p);
+  k_msm_len_scan<<<1, 1024, 0, s>>>(p, m->lenhist_p);
   k_msm_len_scatter<<<blocks(sl, 256), 256, 0, s>>>(p, m->whi.p, m->owner.p, m->soff.p, m->count.p,
-                                                     m->lenhist.p, m->order.p);
-  k_msm_bucket<<<blocks(sl, 128), 128, 0, s>>>(p, m->whi.p, m->order.p, m->owner.p, m->soff.p, m->start.p,
+                                                     m->lenhist_p, m->order.p);
+  k_msm_bucket<<<blocks(sl, 128), 128, 0, s>>>(p, m->whi.p, m->order.p, m->owner.p, m->soff.p, m->start_p,
                                                m->count.p, m->perm.p, m->pts.p, m->slot_sum.p);
   k_msm_segment<<<blocks((size_t)p.rw * p.segs, MSM_SEG_PER_BLOCK), MSM_SEG_THREADS, 0, s>>>(p, 0, p.rw, m->wlo.p, m->whi.p,
                                                                        m->owner.p, m->slot_sum.p, m->part.p);
@@ -365,8 +369,8 @@ static int msm_finish(ftz_msm* m, uint8_t out[64]) {
 static int msm_enqueue_all(ftz_msm* m, hipStream_t s) {
   const MsmPlan& p = m->p;
   const uint32_t(*scal)[8] = reinterpret_cast<const uint32_t(*)[8]>(m->scal.p);
-  if (m->csort) HC(hipMemsetAsync(m->end.p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
-  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p, m->csort ? m->end.p : nullptr);
+  if (m->csort) HC(hipMemsetAsync(m->end_p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
+  k_msm_keys<<<blocks(p.n, 256), 256, 0, s>>>(p, scal, m->key.p, m->val.p, m->csort ? m->end_p : nullptr);
   return msm_enqueue_tail(m, s);
 }
 
@@ -435,7 +439,7 @@ extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t o
   HC(hipStreamWaitEvent(m->cstream, m->cev[ftz_msm::RAW_CHUNKS], 0));
   HC(hipEventRecord(m->ev[0], m->cstream));
   uint32_t(*scal)[8] = reinterpret_cast<uint32_t(*)[8]>(m->scal.p);
-  if (m->csort) HC(hipMemsetAsync(m->end.p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
+  if (m->csort) HC(hipMemsetAsync(m->end_p, 0, (size_t)p.rw * p.buckets * sizeof(uint32_t), s));
   const uint32_t per = (p.n + ftz_msm::RAW_CHUNKS - 1) / ftz_msm::RAW_CHUNKS;
   for (int k = 0; k < ftz_msm::RAW_CHUNKS; k++) {
     uint32_t i0 = k * per, i1 = std::min<uint32_t>(p.n, i0 + per);
@@ -445,7 +449,7 @@ extern "C" int ftz_msm_run_scalars(ftz_msm* m, const uint8_t* scalars, uint8_t o
     HC(hipEventRecord(m->cev[k], m->cstream));
     HC(hipStreamWaitEvent(s, m->cev[k], 0));
     k_msm_keys_raw<<<blocks(i1 - i0, 256), 256, 0, s>>>(p, i0, i1, m->raw.p, scal, m->key.p, m->val.p,
-                                                        m->csort ? m->end.p : nullptr);
+                                                        m->csort ? m->end_p : nullptr);
   }
   int rc = msm_enqueue_tail(m, s);
   if (rc != FTZ_SUCCESS) return rc;
