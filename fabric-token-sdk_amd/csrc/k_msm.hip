@@ -100,16 +100,6 @@ __global__ void __launch_bounds__(256) k_msm_bounds(MsmPlan p, uint64_t total, c
   msm_job_bounds(p, t, total, skey, sval, start, end);
 }
 
-// count[g] = end[g] - start[g] (start = nullptr: end holds the counts) and the
-// bucket's slot count
-__global__ void __launch_bounds__(256) k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end,
-                                                    uint32_t* count, uint32_t* m) {
-  LANE_PROLOGUE(p.rw * p.buckets);
-  uint32_t c = start ? end[i] - start[i] : end[i];
-  count[i] = c;
-  m[i] = msm_bucket_slots(p, c);
-}
-
 // exclusive scan, 1024 elements per workgroup; block totals to `tot`
 __global__ void __launch_bounds__(1024) k_scan_block(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tot) {
   __shared__ uint32_t s[1024];
@@ -125,6 +115,31 @@ __global__ void __launch_bounds__(1024) k_scan_block(const uint32_t* in, uint32_
   }
   if (i < n) out[i] = s[t] - v;
   if (t == 1023) tot[blockIdx.x] = s[1023];
+}
+
+// k_msm_counts fused with the first level of the slot-count scan: count[g] and
+// the bucket's slot count m_g, then the block-exclusive scan of m into soff and
+// the block totals into tot (the higher levels as in scan(), msm_rt.hip)
+__global__ void __launch_bounds__(1024) k_msm_counts_scan(MsmPlan p, const uint32_t* start, const uint32_t* end,
+                                                          uint32_t* count, uint32_t* soff, uint32_t* tot) {
+  __shared__ uint32_t sh[1024];
+  const uint32_t n = p.rw * p.buckets, t = threadIdx.x, i = blockIdx.x * 1024 + t;
+  uint32_t v = 0;
+  if (i < n) {
+    const uint32_t c = start ? end[i] - start[i] : end[i];
+    count[i] = c;
+    v = msm_bucket_slots(p, c);
+  }
+  sh[t] = v;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    uint32_t a = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += a;
+    __syncthreads();
+  }
+  if (i < n) soff[i] = sh[t] - v;
+  if (t == 1023) tot[blockIdx.x] = sh[1023];
 }
 
 __global__ void __launch_bounds__(1024) k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add) {

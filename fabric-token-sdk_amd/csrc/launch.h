@@ -153,9 +153,10 @@ __global__ void k_msm_keys_raw(MsmPlan p, uint32_t i0, uint32_t i1, const uint8_
                                uint32_t* key, uint32_t* val, uint32_t* cnt);
 __global__ void k_msm_bounds(MsmPlan p, uint64_t total, const uint32_t* skey, const uint32_t* sval, uint32_t* start,
                              uint32_t* end);
-__global__ void k_msm_counts(MsmPlan p, const uint32_t* start, const uint32_t* end, uint32_t* count, uint32_t* m);
 __global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* tot);
 __global__ void k_scan_add(uint32_t* out, uint32_t n, const uint32_t* add);
+__global__ void k_msm_counts_scan(MsmPlan p, const uint32_t* start, const uint32_t* end, uint32_t* count,
+                                  uint32_t* soff, uint32_t* tot);
 __global__ void k_msm_owner(MsmPlan p, const uint32_t* count, const uint32_t* soff, uint32_t* owner, uint32_t* wlo,
                             uint32_t* whi);
 __global__ void k_msm_phi(MsmPlan p, G1Dev* pts);

@@ -14,7 +14,7 @@ struct ftz_msm {
   ftz_ctx* ctx = nullptr;
   MsmPlan p{};
   DBuf<G1Dev> pts;
-  DBuf<uint32_t> scal, key, skey, val, perm, count, tot, nsl, soff, owner, wlo, whi, order;
+  DBuf<uint32_t> scal, key, skey, val, perm, count, tot, soff, owner, wlo, whi, order;
   // start[wb], end[wb] and the slot-length histogram[1024] in one buffer: one
   // memset clears the three before the bounds pass (nothing writes the
   // histogram before k_msm_len_hist), two dependent launches fewer per run
@@ -100,7 +100,6 @@ static int msm_alloc(ftz_msm* m, size_t n) {
   HC(msm_sort(m, nullptr, m->sort_tmp_bytes, wn, m->ctx->stream));
   HC(m->sort_tmp.alloc(m->sort_tmp_bytes ? m->sort_tmp_bytes : 1));
   HC(m->tot.alloc(2 * ((wb + 1023) / 1024) + 2048));
-  HC(m->nsl.alloc(wb));
   HC(m->soff.alloc(wb));
   HC(m->owner.alloc(ws));
   HC(m->wlo.alloc(p.rw));
@@ -271,7 +270,7 @@ static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
     // counting sort: end[] = the group counts from the keys kernel
     rc = scan(m->end_p, m->start_p, wb, m->tot.p, s);
     if (rc != FTZ_SUCCESS) return rc;
-    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, nullptr, m->end_p, m->count.p, m->nsl.p);
+    k_msm_counts_scan<<<blocks(wb, 1024), 1024, 0, s>>>(p, nullptr, m->end_p, m->count.p, m->soff.p, m->tot.p);
     k_msm_scatter<<<blocks(p.n, 256), 256, 0, s>>>(p, m->key.p, m->val.p, m->start_p, m->end_p, m->perm.p);
   } else {
     // (window, bucket)-sorted point lists: stable radix sort, bucket ranges
@@ -279,10 +278,16 @@ static int msm_enqueue_tail(ftz_msm* m, hipStream_t s) {
     HC(msm_sort(m, m->sort_tmp.p, tb, wn, s));
     HC(hipMemsetAsync(m->zb.p, 0, (2 * wb + 1024) * sizeof(uint32_t), s));  // start, end, histogram
     k_msm_bounds<<<blocks(wn, 256), 256, 0, s>>>(p, (uint64_t)wn, m->skey.p, m->perm.p, m->start_p, m->end_p);
-    k_msm_counts<<<blocks(wb, 256), 256, 0, s>>>(p, m->start_p, m->end_p, m->count.p, m->nsl.p);
+    k_msm_counts_scan<<<blocks(wb, 1024), 1024, 0, s>>>(p, m->start_p, m->end_p, m->count.p, m->soff.p, m->tot.p);
   }
-  rc = scan(m->nsl.p, m->soff.p, wb, m->tot.p, s);
-  if (rc != FTZ_SUCCESS) return rc;
+  // the slot-count scan's higher levels (its first level ran fused above)
+  const uint32_t nb = (uint32_t)((wb + 1023) / 1024);
+  if (nb > 1) {
+    uint32_t* sums = m->tot.p + nb;
+    rc = scan(m->tot.p, sums, nb, sums + nb + 1, s);
+    if (rc != FTZ_SUCCESS) return rc;
+    k_scan_add<<<nb, 1024, 0, s>>>(m->soff.p, (uint32_t)wb, sums);
+  }
   k_msm_owner<<<blocks(wb, 256), 256, 0, s>>>(p, m->count.p, m->soff.p, m->owner.p, m->wlo.p, m->whi.p);
   // bucket slots in length order, then one lane per slot
   size_t sl = (size_t)p.rw * p.max_slots;

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: one clear of start/end/histogram instead of three memsets (new) vs the previous tree (prev)
+# round 6: MSM counts fused with the slot-count scan (new) vs the previous tree (prev)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
